@@ -1,0 +1,556 @@
+// capi.hip -- extern "C" boundary (include/mi355x_groth16.h).  Host code only: translates the
+// wire formats, owns object lifetimes, serialises each context and turns C++ exceptions into
+// status codes + mi_last_error().  No CPU fallback exists: every compute entry point runs the
+// HIP kernels of this library or fails.
+#include <string.h>
+
+#include <string>
+
+#include "../../include/mi355x_groth16.h"
+#include "prover.h"
+
+struct mi_ctx {
+    mi::Ctx c;
+    hipStream_t normal = nullptr, high = nullptr;
+};
+struct mi_circuit {
+    mi::Circuit *p;
+    int device;
+};
+struct mi_srs {
+    mi::Srs *p;
+    int device;
+};
+struct mi_points {
+    void *dev;
+    uint64_t n;
+    int is_g2;
+    int owns;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+template <class Fn>
+int guard(Fn &&f) {
+    try {
+        f();
+        return MI_OK;
+    } catch (const mi::hip_error &e) {
+        g_err = e.what();
+        return MI_ERR_HIP;
+    } catch (const std::invalid_argument &e) {
+        g_err = e.what();
+        return MI_ERR_ARG;
+    } catch (const std::length_error &e) {
+        g_err = e.what();
+        return MI_ERR_SIZE;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return MI_ERR_INTERNAL;
+    } catch (...) {
+        g_err = "unknown error";
+        return MI_ERR_INTERNAL;
+    }
+}
+
+void need(bool cond, const char *msg) {
+    if (!cond) throw std::invalid_argument(msg);
+}
+
+struct CtxLock {
+    mi_ctx *ctx;
+    std::lock_guard<std::recursive_mutex> lk;
+    CtxLock(mi_ctx *c, int priority = 0) : ctx(c), lk(c->c.mu) {
+        MI_HIP(hipSetDevice(c->c.device));
+        c->c.stream = priority ? c->high : c->normal;
+    }
+};
+
+void proof_bytes(const mi::ProofPoints &pp, uint8_t *proof, uint8_t *raw) {
+    mi::g1_compress(pp.A, proof);
+    mi::g2_compress(pp.B, proof + 48);
+    mi::g1_compress(pp.C, proof + 144);
+    if (raw) {
+        mi::g1_encode(pp.A, raw);
+        mi::g2_encode(pp.B, raw + 96);
+        mi::g1_encode(pp.C, raw + 288);
+    }
+}
+
+mi::fr_t fr_checked(const uint8_t *b) {
+    mi::fr_t x = mi::fr_from_le(b);
+    need(!mi::geq_raw(x, mi::fr_t::modulus_raw()), "scalar is not canonical (>= r)");
+    return x;
+}
+
+// upload z (host) to a device scratch buffer and reduce it mod r
+mi::fr_t *upload_fr(mi::Ctx &c, int slot, const uint8_t *bytes, uint64_t n) {
+    mi::fr_t *d = c.scratch[slot].as<mi::fr_t>(n ? n : 1);
+    if (n) {
+        MI_HIP(hipMemcpyAsync(d, bytes, 32 * n, hipMemcpyHostToDevice, c.stream));
+        mi::fr_canonicalize(c, d, n);
+    }
+    return d;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *mi_last_error(void) { return g_err.c_str(); }
+
+int mi_device_count(int *out) {
+    return guard([&] {
+        need(out != nullptr, "null out");
+        int n = 0;
+        hipError_t e = hipGetDeviceCount(&n);
+        *out = e == hipSuccess ? n : 0;
+    });
+}
+
+int mi_ctx_create(int device, mi_ctx **out) {
+    int rc = guard([&] {
+        need(out != nullptr, "null out");
+        *out = nullptr;
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n == 0) throw std::runtime_error("no HIP device available");
+        need(device >= 0 && device < n, "device index out of range");
+        MI_HIP(hipSetDevice(device));
+        mi_ctx *c = new mi_ctx();
+        try {
+            c->c.device = device;
+            int lo = 0, hi = 0;
+            MI_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            MI_HIP(hipStreamCreateWithFlags(&c->normal, hipStreamNonBlocking));
+            MI_HIP(hipStreamCreateWithPriority(&c->high, hipStreamNonBlocking, hi));
+            c->c.stream = c->normal;
+            mi::ntt_init_tables(c->c);
+        } catch (...) {
+            if (c->normal) hipStreamDestroy(c->normal);
+            if (c->high) hipStreamDestroy(c->high);
+            delete c;
+            throw;
+        }
+        *out = c;
+    });
+    if (rc == MI_ERR_INTERNAL && g_err.find("no HIP device") != std::string::npos) return MI_ERR_NO_DEVICE;
+    return rc;
+}
+
+void mi_ctx_destroy(mi_ctx *ctx) {
+    if (!ctx) return;
+    hipSetDevice(ctx->c.device);
+    hipDeviceSynchronize();
+    mi::ntt_free_tables(ctx->c);
+    for (auto &b : ctx->c.scratch) b.release();
+    if (ctx->normal) hipStreamDestroy(ctx->normal);
+    if (ctx->high) hipStreamDestroy(ctx->high);
+    delete ctx;
+}
+
+int mi_ctx_stream(mi_ctx *ctx, void **stream_out) {
+    return guard([&] {
+        need(ctx && stream_out, "null argument");
+        *stream_out = (void *)ctx->normal;
+    });
+}
+
+int mi_ctx_synchronize(mi_ctx *ctx) {
+    return guard([&] {
+        need(ctx != nullptr, "null ctx");
+        CtxLock l(ctx);
+        MI_HIP(hipStreamSynchronize(ctx->normal));
+        MI_HIP(hipStreamSynchronize(ctx->high));
+        ctx->c.timer.resolve();
+    });
+}
+
+// ------------------------------------------------------------------------------------------
+int mi_circuit_load(mi_ctx *ctx, const mi_r1cs *cs, mi_circuit **out) {
+    return guard([&] {
+        need(ctx && cs && out, "null argument");
+        CtxLock l(ctx);
+        mi::R1csHost h;
+        h.n = cs->num_constraints;
+        h.n_in = cs->num_inputs;
+        h.n_aux = cs->num_aux;
+        for (int m = 0; m < 3; m++) {
+            need(cs->row_ptr[m] != nullptr, "null row_ptr");
+            h.row_ptr[m] = cs->row_ptr[m];
+            h.col[m] = cs->col[m];
+            h.coeff[m] = cs->coeff[m];
+            need(cs->row_ptr[m][cs->num_constraints] == 0 || (cs->col[m] && cs->coeff[m]), "null col/coeff");
+        }
+        mi::Circuit *p = mi::circuit_load(ctx->c, h);
+        *out = new mi_circuit{p, ctx->c.device};
+    });
+}
+
+int mi_circuit_info(const mi_circuit *c, uint64_t out[9]) {
+    return guard([&] {
+        need(c && out, "null argument");
+        const mi::Circuit &p = *c->p;
+        uint64_t v[9] = {p.n, p.n_in, p.n_aux, p.d, p.n_a, p.n_b, p.nnz[0], p.nnz[1], p.nnz[2]};
+        memcpy(out, v, sizeof v);
+    });
+}
+
+void mi_circuit_free(mi_circuit *c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    delete c->p;
+    delete c;
+}
+
+int mi_srs_load(mi_ctx *ctx, const mi_circuit *circ, const mi_srs_host *h, int checked, mi_srs **out) {
+    return guard([&] {
+        need(ctx && h && out, "null argument");
+        need(h->vk && (h->n_ic == 0 || h->ic) && h->h, "null query pointer");
+        CtxLock l(ctx);
+        mi::SrsHost sh;
+        sh.vk = h->vk;
+        sh.ic = h->ic;
+        sh.n_ic = h->n_ic;
+        sh.h = h->h;
+        sh.n_h = h->n_h;
+        sh.l = h->l;
+        sh.n_l = h->n_l;
+        sh.a = h->a;
+        sh.n_a = h->n_a;
+        sh.b_g1 = h->b_g1;
+        sh.n_b_g1 = h->n_b_g1;
+        sh.b_g2 = h->b_g2;
+        sh.n_b_g2 = h->n_b_g2;
+        mi::Srs *p = mi::srs_load(ctx->c, circ ? circ->p : nullptr, sh, checked != 0);
+        *out = new mi_srs{p, ctx->c.device};
+    });
+}
+
+int mi_srs_generate(mi_ctx *ctx, const mi_circuit *circ, const uint8_t toxic[160], mi_srs **out) {
+    return guard([&] {
+        need(ctx && circ && toxic && out, "null argument");
+        CtxLock l(ctx);
+        mi::fr_t t[5];
+        for (int i = 0; i < 5; i++) t[i] = fr_checked(toxic + 32 * i);
+        need(!t[3].is_zero() && !t[4].is_zero(), "gamma and delta must be non-zero");
+        mi::Srs *p = mi::srs_generate(ctx->c, *circ->p, t);
+        *out = new mi_srs{p, ctx->c.device};
+    });
+}
+
+int mi_srs_export_vk(const mi_srs *srs, uint8_t *vk, uint8_t *ic) {
+    return guard([&] {
+        need(srs != nullptr, "null srs");
+        const mi::Srs &s = *srs->p;
+        if (vk) {
+            mi::g1_encode(s.alpha_g1, vk);
+            mi::g1_encode(s.beta_g1, vk + 96);
+            mi::g2_encode(s.beta_g2, vk + 192);
+            mi::g2_encode(s.gamma_g2, vk + 384);
+            mi::g1_encode(s.delta_g1, vk + 576);
+            mi::g2_encode(s.delta_g2, vk + 672);
+        }
+        if (ic)
+            for (size_t i = 0; i < s.ic.size(); i++) mi::g1_encode(s.ic[i], ic + 96 * i);
+    });
+}
+
+int mi_srs_info(const mi_srs *srs, uint64_t out[6]) {
+    return guard([&] {
+        need(srs && out, "null argument");
+        const mi::Srs &s = *srs->p;
+        uint64_t v[6] = {s.d, s.n_h, s.n_l, s.n_a, s.n_b, s.n_ic};
+        memcpy(out, v, sizeof v);
+    });
+}
+
+int mi_srs_export_query(mi_ctx *ctx, const mi_srs *srs, int which, uint8_t *out, uint64_t cap) {
+    return guard([&] {
+        need(ctx && srs && out, "null argument");
+        CtxLock l(ctx);
+        const mi::Srs &s = *srs->p;
+        const void *src = nullptr;
+        uint64_t n = 0;
+        bool g2 = false;
+        switch (which) {
+            case 0: src = s.h_perm; n = s.n_h; break;
+            case 1: src = s.l; n = s.n_l; break;
+            case 2: src = s.a; n = s.n_a; break;
+            case 3: src = s.b_g1; n = s.n_b; break;
+            case 4: src = s.b_g2; n = s.n_b; g2 = true; break;
+            default: throw std::invalid_argument("which must be 0..4");
+        }
+        need(cap >= n, "output buffer too small");
+        if (!n) return;
+        if (g2) {
+            std::vector<mi::g2_affine_t> h(n);
+            MI_HIP(hipMemcpy(h.data(), src, sizeof(mi::g2_affine_t) * n, hipMemcpyDeviceToHost));
+            for (uint64_t i = 0; i < n; i++) mi::g2_encode(h[i], out + 192 * i);
+        } else {
+            std::vector<mi::g1_affine_t> h(n);
+            MI_HIP(hipMemcpy(h.data(), src, sizeof(mi::g1_affine_t) * n, hipMemcpyDeviceToHost));
+            for (uint64_t i = 0; i < n; i++) {
+                uint64_t dst = i;
+                if (which == 0 && s.log_d) dst = __builtin_bitreverse64(i) >> (64 - s.log_d);  // un-permute
+                mi::g1_encode(h[i], out + 96 * dst);
+            }
+        }
+    });
+}
+
+void mi_srs_free(mi_srs *s) {
+    if (!s) return;
+    hipSetDevice(s->device);
+    delete s->p;
+    delete s;
+}
+
+// ------------------------------------------------------------------------------------------
+static void prove_impl(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circ, const mi::fr_t *z_dev,
+                       const uint8_t r[32], const uint8_t s[32], uint8_t *proof, uint8_t *raw) {
+    mi::fr_t rr = fr_checked(r), ss = fr_checked(s);
+    mi::ProofPoints pp = mi::groth16_prove(ctx->c, *srs->p, *circ->p, z_dev, rr, ss);
+    proof_bytes(pp, proof, raw);
+}
+
+int mi_groth16_prove(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circ, const uint8_t *z, const uint8_t r[32],
+                     const uint8_t s[32], int priority, uint8_t *proof, uint8_t *raw) {
+    return guard([&] {
+        need(ctx && srs && circ && z && r && s && proof, "null argument");
+        CtxLock l(ctx, priority);
+        uint64_t nv = circ->p->n_in + circ->p->n_aux;
+        mi::fr_t *zd = upload_fr(ctx->c, 21, z, nv);
+        prove_impl(ctx, srs, circ, zd, r, s, proof, raw);
+    });
+}
+
+int mi_groth16_prove_dev(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circ, const void *z_dev,
+                         const uint8_t r[32], const uint8_t s[32], int priority, uint8_t *proof, uint8_t *raw) {
+    return guard([&] {
+        need(ctx && srs && circ && z_dev && r && s && proof, "null argument");
+        CtxLock l(ctx, priority);
+        prove_impl(ctx, srs, circ, (const mi::fr_t *)z_dev, r, s, proof, raw);
+    });
+}
+
+int mi_groth16_prove_batch(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circ, uint64_t count,
+                           const uint8_t *const *z, const uint8_t *rs, int priority, uint8_t *proofs_out) {
+    return guard([&] {
+        need(ctx && srs && circ && z && rs && proofs_out, "null argument");
+        CtxLock l(ctx, priority);
+        uint64_t nv = circ->p->n_in + circ->p->n_aux;
+        for (uint64_t k = 0; k < count; k++) {
+            need(z[k] != nullptr, "null witness");
+            mi::fr_t *zd = upload_fr(ctx->c, 21, z[k], nv);
+            prove_impl(ctx, srs, circ, zd, rs + 64 * k, rs + 64 * k + 32, proofs_out + 192 * k, nullptr);
+        }
+    });
+}
+
+int mi_groth16_trapdoor_dlogs(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circ, const void *z_dev,
+                              const uint8_t r[32], const uint8_t s[32], uint8_t out[96]) {
+    return guard([&] {
+        need(ctx && srs && circ && z_dev && r && s && out, "null argument");
+        CtxLock l(ctx);
+        mi::fr_t d[3];
+        mi::groth16_trapdoor_dlogs(ctx->c, *srs->p, *circ->p, (const mi::fr_t *)z_dev, fr_checked(r), fr_checked(s),
+                                   d);
+        for (int i = 0; i < 3; i++) mi::fr_to_le(d[i], out + 32 * i);
+    });
+}
+
+// ------------------------------------------------------------------------------------------
+static mi_points *points_upload(mi_ctx *ctx, const uint8_t *bytes, uint64_t n, bool g2) {
+    mi::Ctx &c = ctx->c;
+    const size_t esz = g2 ? 192 : 96, dsz = g2 ? sizeof(mi::g2_affine_t) : sizeof(mi::g1_affine_t);
+    void *dev = nullptr;
+    MI_HIP(hipMalloc(&dev, dsz * (n ? n : 1)));
+    int *bad = c.scratch[9].as<int>(4);
+    MI_HIP(hipMemsetAsync(bad, 0, sizeof(int), c.stream));
+    const uint64_t chunk = 1ull << 22;
+    uint8_t *stage = c.scratch[0].as<uint8_t>(esz * (n < chunk ? (n ? n : 1) : chunk));
+    for (uint64_t o = 0; o < n; o += chunk) {
+        uint64_t m = n - o < chunk ? n - o : chunk;
+        MI_HIP(hipMemcpyAsync(stage, bytes + esz * o, esz * m, hipMemcpyHostToDevice, c.stream));
+        if (g2)
+            mi::g2_decode_uncompressed(c, stage, (mi::g2_affine_t *)dev + o, m, bad);
+        else
+            mi::g1_decode_uncompressed(c, stage, (mi::g1_affine_t *)dev + o, m, bad);
+    }
+    int nbad = 0;
+    MI_HIP(hipMemcpyAsync(&nbad, bad, sizeof(int), hipMemcpyDeviceToHost, c.stream));
+    MI_HIP(hipStreamSynchronize(c.stream));
+    if (nbad) {
+        hipFree(dev);
+        throw std::invalid_argument("point encoding invalid (non-canonical or not on curve)");
+    }
+    return new mi_points{dev, n, g2 ? 1 : 0, 1};
+}
+
+int mi_points_upload_g1(mi_ctx *ctx, const uint8_t *b, uint64_t n, mi_points **out) {
+    return guard([&] {
+        need(ctx && (b || !n) && out, "null argument");
+        CtxLock l(ctx);
+        *out = points_upload(ctx, b, n, false);
+    });
+}
+int mi_points_upload_g2(mi_ctx *ctx, const uint8_t *b, uint64_t n, mi_points **out) {
+    return guard([&] {
+        need(ctx && (b || !n) && out, "null argument");
+        CtxLock l(ctx);
+        *out = points_upload(ctx, b, n, true);
+    });
+}
+int mi_points_from_srs(mi_ctx *ctx, const mi_srs *srs, int which, mi_points **out) {
+    return guard([&] {
+        need(ctx && srs && out, "null argument");
+        const mi::Srs &s = *srs->p;
+        switch (which) {
+            case 0: *out = new mi_points{s.h_perm, s.n_h, 0, 0}; break;
+            case 1: *out = new mi_points{s.l, s.n_l, 0, 0}; break;
+            case 2: *out = new mi_points{s.a, s.n_a, 0, 0}; break;
+            case 3: *out = new mi_points{s.b_g1, s.n_b, 0, 0}; break;
+            case 4: *out = new mi_points{s.b_g2, s.n_b, 1, 0}; break;
+            default: throw std::invalid_argument("which must be 0..4");
+        }
+    });
+}
+void mi_points_free(mi_points *p) {
+    if (!p) return;
+    if (p->owns && p->dev) hipFree(p->dev);
+    delete p;
+}
+uint64_t mi_points_count(const mi_points *p) { return p ? p->n : 0; }
+
+int mi_msm_g1_dev(mi_ctx *ctx, const mi_points *bases, const void *scalars_dev, uint64_t n, uint8_t out96[96]) {
+    return guard([&] {
+        need(ctx && bases && scalars_dev && out96, "null argument");
+        need(!bases->is_g2, "G2 bases passed to mi_msm_g1_dev");
+        need(n <= bases->n, "n exceeds the number of bases");
+        CtxLock l(ctx);
+        mi::g1_xyzz_t r;
+        mi::msm_g1(ctx->c, (const mi::g1_affine_t *)bases->dev, (const mi::fr_t *)scalars_dev, nullptr, n, &r);
+        mi::g1_encode(mi::xyzz_to_affine(r), out96);
+    });
+}
+int mi_msm_g2_dev(mi_ctx *ctx, const mi_points *bases, const void *scalars_dev, uint64_t n, uint8_t out192[192]) {
+    return guard([&] {
+        need(ctx && bases && scalars_dev && out192, "null argument");
+        need(bases->is_g2, "G1 bases passed to mi_msm_g2_dev");
+        need(n <= bases->n, "n exceeds the number of bases");
+        CtxLock l(ctx);
+        mi::g2_xyzz_t r;
+        mi::msm_g2(ctx->c, (const mi::g2_affine_t *)bases->dev, (const mi::fr_t *)scalars_dev, nullptr, n, &r);
+        mi::g2_encode(mi::xyzz_to_affine(r), out192);
+    });
+}
+
+int mi_msm_g1(mi_ctx *ctx, const uint8_t *bases96, const uint8_t *scalars32, uint64_t n, uint8_t out96[96]) {
+    return guard([&] {
+        need(ctx && (n == 0 || (bases96 && scalars32)) && out96, "null argument");
+        CtxLock l(ctx);
+        mi_points *p = points_upload(ctx, bases96, n, false);
+        try {
+            mi::fr_t *sd = upload_fr(ctx->c, 21, scalars32, n);
+            mi::g1_xyzz_t r;
+            mi::msm_g1(ctx->c, (const mi::g1_affine_t *)p->dev, sd, nullptr, n, &r);
+            mi::g1_encode(mi::xyzz_to_affine(r), out96);
+        } catch (...) {
+            mi_points_free(p);
+            throw;
+        }
+        mi_points_free(p);
+    });
+}
+int mi_msm_g2(mi_ctx *ctx, const uint8_t *bases192, const uint8_t *scalars32, uint64_t n, uint8_t out192[192]) {
+    return guard([&] {
+        need(ctx && (n == 0 || (bases192 && scalars32)) && out192, "null argument");
+        CtxLock l(ctx);
+        mi_points *p = points_upload(ctx, bases192, n, true);
+        try {
+            mi::fr_t *sd = upload_fr(ctx->c, 21, scalars32, n);
+            mi::g2_xyzz_t r;
+            mi::msm_g2(ctx->c, (const mi::g2_affine_t *)p->dev, sd, nullptr, n, &r);
+            mi::g2_encode(mi::xyzz_to_affine(r), out192);
+        } catch (...) {
+            mi_points_free(p);
+            throw;
+        }
+        mi_points_free(p);
+    });
+}
+
+static void ntt_impl(mi::Ctx &c, mi::fr_t *d, unsigned log_n, int inverse, int coset) {
+    uint64_t n = 1ull << log_n;
+    mi::fr_to_mont_inplace(c, d, n);
+    if (coset && !inverse) mi::coset_scale_natural(c, d, log_n, false, nullptr);
+    mi::ntt_dif(c, d, log_n, inverse != 0);
+    mi::bitrev_permute(c, d, log_n);
+    if (inverse) {
+        mi::fr_t dd = mi::fr_t::zero();
+        dd.v[0] = (uint32_t)n;
+        dd.v[1] = (uint32_t)(n >> 32);
+        mi::fr_t ninv = mi::inverse(mi::to_mont(dd));
+        if (coset)
+            mi::coset_scale_natural(c, d, log_n, true, &ninv);
+        else
+            mi::scale_all(c, d, n, ninv);
+    }
+    mi::fr_from_mont_inplace(c, d, n);
+}
+
+int mi_ntt_fr_dev(mi_ctx *ctx, void *data_dev, unsigned log_n, int inverse, int coset) {
+    return guard([&] {
+        need(ctx && data_dev, "null argument");
+        need(log_n <= 32, "log_n > 32 (Fr 2-adicity)");
+        CtxLock l(ctx);
+        mi::fr_canonicalize(ctx->c, (mi::fr_t *)data_dev, 1ull << log_n);
+        ntt_impl(ctx->c, (mi::fr_t *)data_dev, log_n, inverse, coset);
+    });
+}
+
+int mi_ntt_fr(mi_ctx *ctx, uint8_t *data32, unsigned log_n, int inverse, int coset) {
+    return guard([&] {
+        need(ctx && data32, "null argument");
+        need(log_n <= 32, "log_n > 32 (Fr 2-adicity)");
+        CtxLock l(ctx);
+        uint64_t n = 1ull << log_n;
+        mi::fr_t *d = upload_fr(ctx->c, 21, data32, n);
+        ntt_impl(ctx->c, d, log_n, inverse, coset);
+        MI_HIP(hipMemcpyAsync(data32, d, 32 * n, hipMemcpyDeviceToHost, ctx->c.stream));
+        MI_HIP(hipStreamSynchronize(ctx->c.stream));
+    });
+}
+
+// ------------------------------------------------------------------------------------------
+int mi_ctx_get_stats(mi_ctx *ctx, double out[21]) {
+    return guard([&] {
+        need(ctx && out, "null argument");
+        CtxLock l(ctx);
+        MI_HIP(hipStreamSynchronize(ctx->normal));
+        MI_HIP(hipStreamSynchronize(ctx->high));
+        ctx->c.timer.resolve();
+        const mi::Stats &s = ctx->c.stats;
+        const mi::KStat *ks[7] = {&s.accum_g1, &s.accum_g2, &s.msm_g1, &s.msm_g2, &s.sort, &s.ntt, &s.prove};
+        for (int i = 0; i < 7; i++) {
+            out[3 * i] = ks[i]->ms;
+            out[3 * i + 1] = (double)ks[i]->launches;
+            out[3 * i + 2] = (double)ks[i]->units;
+        }
+    });
+}
+int mi_ctx_reset_stats(mi_ctx *ctx) {
+    return guard([&] {
+        need(ctx != nullptr, "null ctx");
+        CtxLock l(ctx);
+        MI_HIP(hipStreamSynchronize(ctx->normal));
+        MI_HIP(hipStreamSynchronize(ctx->high));
+        ctx->c.timer.resolve();
+        ctx->c.stats = mi::Stats();
+    });
+}
+unsigned mi_msm_window_bits(uint64_t n) { return mi::msm_window_bits(n); }
+
+}  // extern "C"

@@ -1,0 +1,189 @@
+// ctx.h -- per-device context shared by the NTT, MSM and prover translation units.
+//
+// One mi_ctx per GPU: owns the stream, the twiddle tables and a grow-only
+// scratch arena, and is internally serialised by a mutex like the reference's
+// GROTH_PARAM_MEMORY_CACHE mutexes (libs/filecoin/include/nil/filecoin/proofs/caches.hpp:48-54).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "curve.h"
+#include "field.h"
+
+namespace mi {
+
+struct hip_error : std::runtime_error {
+    hipError_t code;
+    hip_error(hipError_t c, const std::string &what) : std::runtime_error(what), code(c) {}
+};
+
+#define MI_HIP(call)                                                                              \
+    do {                                                                                          \
+        hipError_t _e = (call);                                                                   \
+        if (_e != hipSuccess)                                                                     \
+            throw ::mi::hip_error(_e, std::string(#call) + " failed: " + hipGetErrorString(_e) + \
+                                          " at " + __FILE__ + ":" + std::to_string(__LINE__));    \
+    } while (0)
+
+// A device buffer that only grows (no hipMalloc inside the timed steady state).
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    void *get(size_t bytes) {
+        if (bytes > cap) {
+            if (p) MI_HIP(hipFree(p));
+            p = nullptr;
+            size_t want = bytes + bytes / 8;
+            MI_HIP(hipMalloc(&p, want));
+            cap = want;
+        }
+        return p;
+    }
+    template <class T>
+    T *as(size_t count) {
+        return (T *)get(count * sizeof(T));
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    ~DevBuf() { release(); }
+};
+
+// Twiddle tables for every power-of-two domain up to 2^32 (bellman: Fr::ROOT_OF_UNITY with
+// S = 32, multiplicative generator 7).  w^e for e < 2^32 = LO[e & 0xffff] * HI[e >> 16].
+struct NttTables {
+    fr_t *fw_lo = nullptr, *fw_hi = nullptr;  // powers of omega_{2^32}
+    fr_t *iv_lo = nullptr, *iv_hi = nullptr;  // powers of omega_{2^32}^-1
+    fr_t *g_lo = nullptr, *g_hi = nullptr;    // powers of the coset generator 7
+    fr_t *gi_lo = nullptr, *gi_hi = nullptr;  // powers of 7^-1
+};
+
+// Per-kernel-class device time from HIP events recorded on the launching stream.  Event pairs are
+// resolved lazily at the next point where the host synchronises anyway, so the timers stay on in
+// the timed region without adding synchronisation.
+struct KStat {
+    double ms = 0;
+    uint64_t launches = 0;
+    uint64_t units = 0;  // points (MSM) or elements (NTT) processed by the timed launches
+};
+struct Stats {
+    KStat accum_g1, accum_g2;  // k_accum_level0 (the bucket-accumulation hot loop)
+    KStat msm_g1, msm_g2;      // whole MSM (digits -> sort -> accumulate -> reduce)
+    KStat sort;                // digit extraction + radix sort + bucket bounds
+    KStat ntt;                 // NTT passes (all launches of one transform)
+    KStat prove;               // whole Groth16 prove (device part through host assembly)
+};
+
+struct Ctx;
+struct EventTimer {
+    struct Pending {
+        hipEvent_t a, b;
+        KStat *dst;
+        uint64_t units;
+    };
+    std::vector<hipEvent_t> pool;
+    std::vector<Pending> pending;
+    hipEvent_t get() {
+        if (pool.empty()) {
+            hipEvent_t e;
+            MI_HIP(hipEventCreate(&e));
+            return e;
+        }
+        hipEvent_t e = pool.back();
+        pool.pop_back();
+        return e;
+    }
+    // resolve every pending pair whose end event has completed (call after a stream sync)
+    void resolve() {
+        std::vector<Pending> keep;
+        for (auto &p : pending) {
+            if (hipEventQuery(p.b) != hipSuccess) {
+                keep.push_back(p);
+                continue;
+            }
+            float ms = 0;
+            hipEventElapsedTime(&ms, p.a, p.b);
+            p.dst->ms += ms;
+            p.dst->launches += 1;
+            p.dst->units += p.units;
+            pool.push_back(p.a);
+            pool.push_back(p.b);
+        }
+        pending.swap(keep);
+    }
+    ~EventTimer() {
+        for (auto &p : pending) {
+            hipEventDestroy(p.a);
+            hipEventDestroy(p.b);
+        }
+        for (auto e : pool) hipEventDestroy(e);
+    }
+};
+
+struct Ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::recursive_mutex mu;
+    NttTables tw;
+    DevBuf scratch[24];  // 0-15: MSM / NTT / upload temporaries, 20-21: prover vectors / staging
+    Stats stats;
+    EventTimer timer;
+};
+
+// Records a start event now and an end event at scope exit, on the ctx stream; no synchronisation.
+struct ScopedTimer {
+    Ctx &c;
+    KStat *dst;
+    uint64_t units;
+    hipEvent_t a;
+    ScopedTimer(Ctx &ctx, KStat *s, uint64_t u = 0) : c(ctx), dst(s), units(u) {
+        a = c.timer.get();
+        MI_HIP(hipEventRecord(a, c.stream));
+    }
+    ~ScopedTimer() {
+        hipEvent_t b = c.timer.get();
+        hipEventRecord(b, c.stream);
+        c.timer.pending.push_back({a, b, dst, units});
+    }
+};
+
+// ---- NTT (ntt.hip) ----
+void ntt_init_tables(Ctx &c);
+void ntt_free_tables(Ctx &c);
+// DIF: natural order in -> bit-reversed out (forward uses omega, inverse omega^-1, no 1/n)
+void ntt_dif(Ctx &c, fr_t *d, unsigned log_n, bool inverse);
+// DIT: bit-reversed in -> natural out
+void ntt_dit(Ctx &c, fr_t *d, unsigned log_n, bool inverse);
+void bitrev_permute(Ctx &c, fr_t *d, unsigned log_n);
+// d[pos] *= g^(±bitrev(pos)) * scale (scale may be null)
+void coset_scale_bitrev(Ctx &c, fr_t *d, unsigned log_n, bool inverse_gen, const fr_t *scale_host,
+                        bool to_canonical);
+void coset_scale_natural(Ctx &c, fr_t *d, unsigned log_n, bool inverse_gen, const fr_t *scale_host);
+void scale_all(Ctx &c, fr_t *d, uint64_t n, const fr_t &s);
+void fr_to_mont_inplace(Ctx &c, fr_t *d, uint64_t n);
+void fr_from_mont_inplace(Ctx &c, fr_t *d, uint64_t n);
+
+// ---- MSM (msm.hip) ----
+// result = sum_i scalar[idx ? idx[i] : i] * bases[i]; scalars canonical (raw) Fr.
+void msm_g1(Ctx &c, const g1_affine_t *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,
+            g1_xyzz_t *result_host);
+void msm_g2(Ctx &c, const g2_affine_t *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,
+            g2_xyzz_t *result_host);
+// host-side window-size heuristic (exposed for tests)
+unsigned msm_window_bits(uint64_t n);
+
+// ---- encodings (encode.hip) ----
+// zcash uncompressed big-endian -> device Montgomery affine; returns count of invalid points
+void g1_decode_uncompressed(Ctx &c, const uint8_t *dev_bytes, g1_affine_t *out, uint64_t n, int *bad_dev);
+void g2_decode_uncompressed(Ctx &c, const uint8_t *dev_bytes, g2_affine_t *out, uint64_t n, int *bad_dev);
+// canonical LE Fr bytes (already on device, 32B each) -> canonical, reduced mod r (in place)
+void fr_canonicalize(Ctx &c, fr_t *d, uint64_t n);
+
+}  // namespace mi

@@ -1,0 +1,154 @@
+// curve.h -- BLS12-381 G1 (over Fq) and G2 (over Fq2) group law for the MSM hot loop.
+//
+// Restates crypto3 algebra's curve arithmetic ([NOT IN TREE]: libs/crypto/algebra, g1_type /
+// g2_type of bls12<381>, core/crypto/scheme_params.hpp:40-41).  Buckets use XYZZ coordinates
+// (x = X/ZZ, y = Y/ZZZ, ZZ^3 = ZZZ^2): a mixed add costs 8M + 2S with no field inversion and no
+// doubling of Z, which is what the bucket loop does ~N * windows times.
+// Affine infinity is encoded as (0, 0) (not on the curve: 0 != 0 + b).
+#pragma once
+#include "field.h"
+
+namespace mi {
+
+template <class F>
+struct alignas(16) Affine {
+    F x, y;
+    MI_HD bool is_inf() const { return x.is_zero() && y.is_zero(); }
+    MI_HD static Affine inf() { return {F::zero(), F::zero()}; }
+};
+
+template <class F>
+struct alignas(16) XYZZ {
+    F X, Y, ZZ, ZZZ;
+    MI_HD static XYZZ inf() { return {F::one(), F::one(), F::zero(), F::zero()}; }
+    MI_HD bool is_inf() const { return ZZ.is_zero(); }
+};
+
+template <class F>
+MI_HD XYZZ<F> xyzz_from_affine(const Affine<F> &a) {
+    if (a.is_inf()) return XYZZ<F>::inf();
+    return {a.x, a.y, F::one(), F::one()};
+}
+
+template <class F>
+MI_HD Affine<F> affine_neg(const Affine<F> &a) {
+    return {a.x, -a.y};
+}
+
+template <class F>
+MI_HD XYZZ<F> xyzz_neg(const XYZZ<F> &p) {
+    return {p.X, -p.Y, p.ZZ, p.ZZZ};
+}
+
+// dbl-2008-s-1 (a = 0)
+template <class F>
+MI_NOINL XYZZ<F> xyzz_dbl(const XYZZ<F> &p) {
+    if (p.is_inf()) return p;
+    F U = dbl(p.Y);
+    F V = sqr(U);
+    F W = U * V;
+    F S = p.X * V;
+    F X2 = sqr(p.X);
+    F M = X2 + dbl(X2);
+    XYZZ<F> r;
+    r.X = sqr(M) - dbl(S);
+    r.Y = M * (S - r.X) - W * p.Y;
+    r.ZZ = V * p.ZZ;
+    r.ZZZ = W * p.ZZZ;
+    return r;
+}
+
+// mdbl-2008-s-1: double an affine point
+template <class F>
+MI_NOINL XYZZ<F> xyzz_dbl_affine(const Affine<F> &a) {
+    F U = dbl(a.y);
+    F V = sqr(U);
+    F W = U * V;
+    F S = a.x * V;
+    F X2 = sqr(a.x);
+    F M = X2 + dbl(X2);
+    XYZZ<F> r;
+    r.X = sqr(M) - dbl(S);
+    r.Y = M * (S - r.X) - W * a.y;
+    r.ZZ = V;
+    r.ZZZ = W;
+    return r;
+}
+
+// madd-2008-s: p (XYZZ) + q (affine, may be infinity)
+template <class F>
+MI_NOINL XYZZ<F> xyzz_add_affine(const XYZZ<F> &p, const Affine<F> &q) {
+    if (q.is_inf()) return p;
+    if (p.is_inf()) return xyzz_from_affine(q);
+    F U2 = q.x * p.ZZ;
+    F S2 = q.y * p.ZZZ;
+    F P = U2 - p.X;
+    F R = S2 - p.Y;
+    if (P.is_zero()) {
+        if (R.is_zero()) return xyzz_dbl_affine(q);
+        return XYZZ<F>::inf();
+    }
+    F PP = sqr(P);
+    F PPP = P * PP;
+    F Q = p.X * PP;
+    XYZZ<F> r;
+    r.X = sqr(R) - PPP - dbl(Q);
+    r.Y = R * (Q - r.X) - p.Y * PPP;
+    r.ZZ = p.ZZ * PP;
+    r.ZZZ = p.ZZZ * PPP;
+    return r;
+}
+
+// add-2008-s: p + q, both XYZZ
+template <class F>
+MI_NOINL XYZZ<F> xyzz_add(const XYZZ<F> &p, const XYZZ<F> &q) {
+    if (q.is_inf()) return p;
+    if (p.is_inf()) return q;
+    F U1 = p.X * q.ZZ;
+    F U2 = q.X * p.ZZ;
+    F S1 = p.Y * q.ZZZ;
+    F S2 = q.Y * p.ZZZ;
+    F P = U2 - U1;
+    F R = S2 - S1;
+    if (P.is_zero()) {
+        if (R.is_zero()) return xyzz_dbl(p);
+        return XYZZ<F>::inf();
+    }
+    F PP = sqr(P);
+    F PPP = P * PP;
+    F Q = U1 * PP;
+    XYZZ<F> r;
+    r.X = sqr(R) - PPP - dbl(Q);
+    r.Y = R * (Q - r.X) - S1 * PPP;
+    r.ZZ = p.ZZ * q.ZZ * PP;
+    r.ZZZ = p.ZZZ * q.ZZZ * PPP;
+    return r;
+}
+
+// host/device: XYZZ -> affine (one inversion)
+template <class F>
+MI_NOINL Affine<F> xyzz_to_affine(const XYZZ<F> &p) {
+    if (p.is_inf()) return Affine<F>::inf();
+    F izzz = inverse(p.ZZZ);
+    F izz_sq = sqr(p.ZZ * izzz);  // (ZZ/ZZZ)^2 = 1/ZZ  (ZZ^3 = ZZZ^2)
+    return {p.X * izz_sq, p.Y * izzz};
+}
+
+// scalar multiplication by a canonical little-endian word scalar (host / rare device use)
+template <class F>
+MI_NOINL XYZZ<F> xyzz_mul(const XYZZ<F> &p, const uint32_t *k, int nwords) {
+    XYZZ<F> r = XYZZ<F>::inf();
+    for (int i = nwords - 1; i >= 0; i--)
+        for (int b = 31; b >= 0; b--) {
+            r = xyzz_dbl(r);
+            if ((k[i] >> b) & 1) r = xyzz_add(r, p);
+        }
+    return r;
+}
+
+typedef Affine<fq_t> g1_affine_t;
+typedef Affine<fq2_t> g2_affine_t;
+typedef XYZZ<fq_t> g1_xyzz_t;
+typedef XYZZ<fq2_t> g2_xyzz_t;
+
+}  // namespace mi

@@ -1,0 +1,118 @@
+// encode.hip -- wire formats <-> device representation.
+//
+// Boundary formats follow the reference's data contracts:
+//   * points: zcash/bellman "uncompressed" big-endian encodings, the layout of the Groth params
+//     file the reference mmaps (core/crypto/mapped_scheme_params.hpp:43-84): G1 = x|y (96 B),
+//     G2 = x.c1|x.c0|y.c1|y.c0 (192 B); flag bits live in the top 3 bits of byte 0
+//     (0x40 = point at infinity).
+//   * scalars: Fr as 32-byte little-endian (core/fr32.hpp:36-52).
+// On device, coordinates are Montgomery 32-bit-limb little-endian; affine infinity is (0, 0).
+#include "ctx.h"
+
+namespace mi {
+
+namespace {
+
+__device__ __forceinline__ uint32_t be32(const uint8_t *p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
+}
+
+// 48 big-endian bytes -> raw limbs; returns false when >= p
+__device__ __forceinline__ bool fq_from_be48(const uint8_t *p, bool mask_flags, fq_t &out) {
+    MI_UNROLL for (int i = 0; i < 12; i++) {
+        uint32_t w = be32(p + 4 * (11 - i));
+        if (i == 11 && mask_flags) w &= 0x1fffffffu;
+        out.v[i] = w;
+    }
+    return !geq_raw(out, fq_t::modulus_raw());
+}
+
+__device__ bool g1_on_curve(const g1_affine_t &a) {
+    fq_t four = fq_t::zero();
+    four.v[0] = 4;
+    four = to_mont(four);
+    return sqr(a.y) == sqr(a.x) * a.x + four;
+}
+__device__ bool g2_on_curve(const g2_affine_t &a) {
+    fq_t four = fq_t::zero();
+    four.v[0] = 4;
+    four = to_mont(four);
+    fq2_t b = {four, four};
+    return sqr(a.y) == sqr(a.x) * a.x + b;
+}
+
+__global__ void k_g1_decode(const uint8_t *__restrict__ in, g1_affine_t *__restrict__ out, uint64_t n,
+                            int *__restrict__ bad) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t *p = in + 96 * i;
+    if (p[0] & 0x40) {
+        out[i] = g1_affine_t::inf();
+        return;
+    }
+    g1_affine_t a;
+    bool ok = fq_from_be48(p, true, a.x) & fq_from_be48(p + 48, false, a.y);
+    a.x = to_mont(a.x);
+    a.y = to_mont(a.y);
+    if (!ok || !g1_on_curve(a)) atomicAdd(bad, 1);
+    out[i] = a;
+}
+
+__global__ void k_g2_decode(const uint8_t *__restrict__ in, g2_affine_t *__restrict__ out, uint64_t n,
+                            int *__restrict__ bad) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t *p = in + 192 * i;
+    if (p[0] & 0x40) {
+        out[i] = g2_affine_t::inf();
+        return;
+    }
+    g2_affine_t a;
+    bool ok = fq_from_be48(p, true, a.x.c1) & fq_from_be48(p + 48, false, a.x.c0) &
+              fq_from_be48(p + 96, false, a.y.c1) & fq_from_be48(p + 144, false, a.y.c0);
+    a.x = to_mont(a.x);
+    a.y = to_mont(a.y);
+    if (!ok || !g2_on_curve(a)) atomicAdd(bad, 1);
+    out[i] = a;
+}
+
+// x mod r for x < 2^256 (at most two subtractions: 2^256 < 3r)
+__global__ void k_fr_canon(fr_t *__restrict__ d, uint64_t n) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fr_t x = d[i];
+    fr_t m = fr_t::modulus_raw();
+    MI_UNROLL for (int k = 0; k < 2; k++) {
+        if (geq_raw(x, m)) {
+            uint32_t borrow = 0;
+            MI_UNROLL for (int j = 0; j < 8; j++) {
+                uint64_t t = (uint64_t)x.v[j] - m.v[j] - borrow;
+                x.v[j] = (uint32_t)t;
+                borrow = (uint32_t)(t >> 63);
+            }
+        }
+    }
+    d[i] = x;
+}
+
+inline unsigned grid1(uint64_t n) { return (unsigned)((n + 255) / 256); }
+
+}  // namespace
+
+void g1_decode_uncompressed(Ctx &c, const uint8_t *dev_bytes, g1_affine_t *out, uint64_t n, int *bad_dev) {
+    if (!n) return;
+    k_g1_decode<<<grid1(n), 256, 0, c.stream>>>(dev_bytes, out, n, bad_dev);
+    MI_HIP(hipGetLastError());
+}
+void g2_decode_uncompressed(Ctx &c, const uint8_t *dev_bytes, g2_affine_t *out, uint64_t n, int *bad_dev) {
+    if (!n) return;
+    k_g2_decode<<<grid1(n), 256, 0, c.stream>>>(dev_bytes, out, n, bad_dev);
+    MI_HIP(hipGetLastError());
+}
+void fr_canonicalize(Ctx &c, fr_t *d, uint64_t n) {
+    if (!n) return;
+    k_fr_canon<<<grid1(n), 256, 0, c.stream>>>(d, n);
+    MI_HIP(hipGetLastError());
+}
+
+}  // namespace mi

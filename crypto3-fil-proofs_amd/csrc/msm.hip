@@ -1,0 +1,360 @@
+// msm.hip -- Pippenger multi-scalar multiplication on BLS12-381 G1 / G2 for CDNA4 (gfx950).
+//
+// Restates crypto3's multiexp ([NOT IN TREE]: libs/crypto/algebra, used by r1cs_gg_ppzksnark's
+// prover for the H, L, A, B_G1 (G1) and B_G2 (G2) queries -- SURVEY.md §8a rows a7/a8).
+//
+// Pipeline (one MSM):
+//   1. k_digits     : every scalar -> ceil(256/c) signed c-bit digits; one (bucket key, point
+//                     index | sign) pair per non-zero digit, laid out [window][point] (coalesced).
+//   2. radix sort   : rocPRIM onesweep over only the key bits in use (hipcub::DeviceRadixSort).
+//   3. k_bounds     : bucket start / end from the sorted keys.
+//   4. accumulation : buckets are cut into chunks of <= L sorted entries, one thread per chunk
+//                     (mixed XYZZ += affine adds, point gathered by index); chunk partials of
+//                     the same bucket are summed by the same kernel shape level by level until
+//                     every bucket is one point.  Work per thread is bounded by L whatever the
+//                     scalar distribution (boolean-heavy Filecoin witnesses put most entries in
+//                     bucket 1 of window 0).
+//   5. k_bucket_reduce: running-sum reduction sum_b (b+1) B_b over segments of buckets, each
+//                     segment's offset folded in with a small double-and-add.
+//   6. k_window_sum : per-window sum of segment results (LDS tree).
+//   7. host         : Horner over windows (c doublings each) on the CPU.
+#include <hipcub/hipcub.hpp>
+
+#include "ctx.h"
+
+namespace mi {
+
+namespace {
+
+constexpr uint32_t L0 = 32;  // sorted entries per chunk at level 0 (mixed adds)
+constexpr uint32_t L1 = 16;  // partials per chunk at levels >= 1 (full adds)
+
+MI_HD uint32_t word_of(const fr_t &s, unsigned k) {
+    uint32_t r = 0;
+    MI_UNROLL for (int j = 0; j < 8; j++) r = (k == (unsigned)j) ? s.v[j] : r;
+    return r;
+}
+
+__global__ void k_digits(const fr_t *__restrict__ scalars, const uint32_t *__restrict__ idx, uint32_t n,
+                         unsigned c, unsigned nwin, uint32_t invalid, uint32_t *__restrict__ keys,
+                         uint32_t *__restrict__ vals) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const fr_t s = scalars[idx ? idx[i] : i];
+    const uint32_t nbk = 1u << (c - 1);
+    const uint32_t mask = (1u << c) - 1;
+    uint32_t carry = 0;
+    for (unsigned w = 0; w < nwin; w++) {
+        unsigned bit = w * c, word = bit >> 5, sh = bit & 31;
+        uint32_t d = 0;
+        if (word < 8) {
+            d = word_of(s, word) >> sh;
+            if (sh + c > 32 && word + 1 < 8) d |= word_of(s, word + 1) << (32 - sh);
+        }
+        d = (d & mask) + carry;
+        uint32_t neg = 0;
+        if (d > nbk) {
+            d = (1u << c) - d;
+            neg = 1;
+            carry = 1;
+        } else {
+            carry = 0;
+        }
+        uint64_t o = (uint64_t)w * n + i;
+        keys[o] = d ? w * nbk + d - 1 : invalid;
+        vals[o] = i | (neg << 31);
+    }
+}
+
+__global__ void k_bounds(const uint32_t *__restrict__ keys, uint32_t np, uint32_t invalid,
+                         uint32_t *__restrict__ start, uint32_t *__restrict__ cnt) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= np) return;
+    uint32_t k = keys[i];
+    if (k == invalid) return;
+    if (i == 0 || keys[i - 1] != k) start[k] = i;
+    if (i == np - 1 || keys[i + 1] != k) cnt[k] = i + 1;  // end; converted to a count below
+}
+
+__global__ void k_end_to_cnt(const uint32_t *__restrict__ start, uint32_t *__restrict__ cnt, uint32_t nb) {
+    uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    uint32_t e = cnt[b];
+    cnt[b] = e ? e - start[b] : 0;
+}
+
+__global__ void k_chunk_count(const uint32_t *__restrict__ cnt, uint32_t nb, uint32_t L, uint32_t *__restrict__ ccnt) {
+    uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    ccnt[b] = (cnt[b] + L - 1) / L;
+}
+
+__global__ void k_chunk_heads(const uint32_t *__restrict__ ccnt, const uint32_t *__restrict__ coff, uint32_t nb,
+                              uint32_t *__restrict__ chunk_bucket) {
+    uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    if (ccnt[b]) chunk_bucket[coff[b]] = b;
+}
+
+struct MaxOp {
+    __device__ __host__ uint32_t operator()(uint32_t a, uint32_t b) const { return a > b ? a : b; }
+};
+
+template <class F>
+__global__ void __launch_bounds__(256) k_accum_level0(const uint32_t *__restrict__ chunk_bucket,
+                                                      const uint32_t *__restrict__ coff,
+                                                      const uint32_t *__restrict__ off,
+                                                      const uint32_t *__restrict__ cnt, uint32_t total,
+                                                      const uint32_t *__restrict__ vals,
+                                                      const Affine<F> *__restrict__ bases,
+                                                      XYZZ<F> *__restrict__ out) {
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= total) return;
+    uint32_t b = chunk_bucket[t];
+    uint32_t local = t - coff[b];
+    uint32_t beg = off[b] + local * L0;
+    uint32_t lim = local * L0 + L0 < cnt[b] ? local * L0 + L0 : cnt[b];
+    uint32_t end = off[b] + lim;
+    XYZZ<F> acc = XYZZ<F>::inf();
+    for (uint32_t p = beg; p < end; p++) {
+        uint32_t v = vals[p];
+        Affine<F> a = bases[v & 0x7fffffffu];
+        if (v >> 31) a.y = -a.y;
+        acc = xyzz_add_affine(acc, a);
+    }
+    out[t] = acc;
+}
+
+template <class F>
+__global__ void __launch_bounds__(256) k_accum_level(const uint32_t *__restrict__ chunk_bucket,
+                                                     const uint32_t *__restrict__ coff,
+                                                     const uint32_t *__restrict__ off,
+                                                     const uint32_t *__restrict__ cnt, uint32_t total,
+                                                     const XYZZ<F> *__restrict__ in,
+                                                     XYZZ<F> *__restrict__ out) {
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= total) return;
+    uint32_t b = chunk_bucket[t];
+    uint32_t local = t - coff[b];
+    uint32_t beg = off[b] + local * L1;
+    uint32_t lim = local * L1 + L1 < cnt[b] ? local * L1 + L1 : cnt[b];
+    uint32_t end = off[b] + lim;
+    XYZZ<F> acc = in[beg];
+    for (uint32_t p = beg + 1; p < end; p++) acc = xyzz_add(acc, in[p]);
+    out[t] = acc;
+}
+
+template <class F>
+MI_HD XYZZ<F> mul_small(const XYZZ<F> &p, uint32_t k) {
+    XYZZ<F> r = XYZZ<F>::inf();
+    for (int b = 31; b >= 0; b--) {
+        r = xyzz_dbl(r);
+        if ((k >> b) & 1) r = xyzz_add(r, p);
+    }
+    return r;
+}
+
+template <class F>
+__global__ void __launch_bounds__(256) k_bucket_reduce(const uint32_t *__restrict__ off,
+                                                       const uint32_t *__restrict__ cnt,
+                                                       const XYZZ<F> *__restrict__ P, unsigned nwin,
+                                                       unsigned nbk, unsigned seg_len,
+                                                       XYZZ<F> *__restrict__ segsum) {
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t nseg = nbk / seg_len;
+    if (t >= nwin * nseg) return;
+    uint32_t w = t / nseg, s = t % nseg;
+    uint32_t b0 = w * nbk + s * seg_len;
+    XYZZ<F> run = XYZZ<F>::inf(), acc = XYZZ<F>::inf();
+    for (int j = (int)seg_len - 1; j >= 0; j--) {
+        uint32_t b = b0 + j;
+        if (cnt[b]) run = xyzz_add(run, P[off[b]]);
+        acc = xyzz_add(acc, run);
+    }
+    uint32_t k = s * seg_len;
+    if (k && !run.is_inf()) {
+        // add k * run with a left-to-right double-and-add starting at k's top bit
+        XYZZ<F> m = run;
+        int top = 31 - __builtin_clz(k);
+        for (int bit = top - 1; bit >= 0; bit--) {
+            m = xyzz_dbl(m);
+            if ((k >> bit) & 1) m = xyzz_add(m, run);
+        }
+        acc = xyzz_add(acc, m);
+    }
+    segsum[t] = acc;
+}
+
+template <class F, int T>
+__global__ void __launch_bounds__(T) k_window_sum(const XYZZ<F> *__restrict__ segsum, unsigned nseg,
+                                                  XYZZ<F> *__restrict__ out) {
+    __shared__ XYZZ<F> sh[T];
+    unsigned w = blockIdx.x;
+    XYZZ<F> acc = XYZZ<F>::inf();
+    for (unsigned s = threadIdx.x; s < nseg; s += T) acc = xyzz_add(acc, segsum[(uint64_t)w * nseg + s]);
+    sh[threadIdx.x] = acc;
+    __syncthreads();
+    for (unsigned half = T / 2; half > 0; half >>= 1) {
+        if (threadIdx.x < half) sh[threadIdx.x] = xyzz_add(sh[threadIdx.x], sh[threadIdx.x + half]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[w] = sh[0];
+}
+
+inline unsigned grid_for(uint64_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
+
+}  // namespace
+
+unsigned msm_window_bits(uint64_t n) {
+    // minimise (mixed adds) + 1.4 x (bucket-reduction full adds) over c
+    unsigned best = 4;
+    double best_cost = 1e300;
+    for (unsigned c = 4; c <= 22; c++) {
+        unsigned nwin = (256 + c - 1) / c;
+        double cost = (double)n * nwin + 1.4 * 2.0 * nwin * (double)(1u << (c - 1)) + 64.0 * nwin * c;
+        if (cost < best_cost) {
+            best_cost = cost;
+            best = c;
+        }
+    }
+    return best;
+}
+
+template <class F>
+static void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,
+                    XYZZ<F> *result) {
+    if (n == 0) {
+        *result = XYZZ<F>::inf();
+        return;
+    }
+    hipStream_t st = c.stream;
+    ScopedTimer whole(c, sizeof(F) == sizeof(fq_t) ? &c.stats.msm_g1 : &c.stats.msm_g2, n);
+    const unsigned cb = msm_window_bits(n);
+    const unsigned nwin = (256 + cb - 1) / cb;
+    const uint32_t nbk = 1u << (cb - 1);
+    const uint64_t nb64 = (uint64_t)nwin * nbk;
+    const uint64_t np64 = (uint64_t)nwin * n;
+    if (np64 >= 0xffffffffull || nb64 >= 0x7fffffffull || n >= 0x80000000ull)
+        throw std::runtime_error("msm: instance too large for 32-bit sort indices");
+    const uint32_t nb = (uint32_t)nb64, np = (uint32_t)np64, invalid = nb;
+    unsigned key_bits = 1;
+    while ((1ull << key_bits) <= invalid) key_bits++;
+
+    uint32_t *keys = c.scratch[0].as<uint32_t>(np);
+    uint32_t *vals = c.scratch[1].as<uint32_t>(np);
+    uint32_t *keys_s = c.scratch[2].as<uint32_t>(np);
+    uint32_t *vals_s = c.scratch[3].as<uint32_t>(np);
+    uint32_t *offA = c.scratch[5].as<uint32_t>(nb);
+    uint32_t *cntA = c.scratch[6].as<uint32_t>(nb);
+    uint32_t *offB = c.scratch[7].as<uint32_t>(nb);
+    uint32_t *cntB = c.scratch[8].as<uint32_t>(nb);
+    uint32_t *dmax = c.scratch[9].as<uint32_t>(4);
+
+    {
+        ScopedTimer tsort(c, &c.stats.sort, n);
+        k_digits<<<grid_for(n, 256), 256, 0, st>>>(scalars, idx, (uint32_t)n, cb, nwin, invalid, keys, vals);
+        MI_HIP(hipGetLastError());
+        size_t tmp_bytes = 0;
+        MI_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys, keys_s, vals, vals_s, np, 0, key_bits,
+                                                  st));
+        void *tmp = c.scratch[4].get(tmp_bytes);
+        MI_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys, keys_s, vals, vals_s, np, 0, key_bits, st));
+        MI_HIP(hipMemsetAsync(offA, 0, sizeof(uint32_t) * nb, st));
+        MI_HIP(hipMemsetAsync(cntA, 0, sizeof(uint32_t) * nb, st));
+        k_bounds<<<grid_for(np, 256), 256, 0, st>>>(keys_s, np, invalid, offA, cntA);
+        k_end_to_cnt<<<grid_for(nb, 256), 256, 0, st>>>(offA, cntA, nb);
+        MI_HIP(hipGetLastError());
+    }
+
+    // largest bucket decides the number of accumulation levels
+    uint32_t maxcnt = 0;
+    {
+        size_t tmp_bytes = 0;
+        MI_HIP(hipcub::DeviceReduce::Max(nullptr, tmp_bytes, cntA, dmax, nb, st));
+        void *tmp = c.scratch[4].get(tmp_bytes);
+        MI_HIP(hipcub::DeviceReduce::Max(tmp, tmp_bytes, cntA, dmax, nb, st));
+        MI_HIP(hipMemcpyAsync(&maxcnt, dmax, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        MI_HIP(hipStreamSynchronize(st));
+    }
+
+    XYZZ<F> *Pcur = nullptr;
+    int pbuf = 10;
+    bool level0 = true;
+    uint32_t *off = offA, *cnt = cntA, *coff = offB, *ccnt = cntB;
+    {
+        while (level0 || maxcnt > 1) {
+            uint32_t L = level0 ? L0 : L1;
+            k_chunk_count<<<grid_for(nb, 256), 256, 0, st>>>(cnt, nb, L, ccnt);
+            size_t tmp_bytes = 0;
+            MI_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, ccnt, coff, nb, st));
+            void *tmp = c.scratch[4].get(tmp_bytes);
+            MI_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, ccnt, coff, nb, st));
+            uint32_t tail[2];
+            MI_HIP(hipMemcpyAsync(&tail[0], coff + nb - 1, 4, hipMemcpyDeviceToHost, st));
+            MI_HIP(hipMemcpyAsync(&tail[1], ccnt + nb - 1, 4, hipMemcpyDeviceToHost, st));
+            MI_HIP(hipStreamSynchronize(st));
+            uint32_t total = tail[0] + tail[1];
+            if (total == 0) {  // every scalar is zero
+                *result = XYZZ<F>::inf();
+                return;
+            }
+            uint32_t *heads = c.scratch[15].as<uint32_t>(total + 1);
+            uint32_t *chunk_bucket = c.scratch[13].as<uint32_t>(total + 1);
+            MI_HIP(hipMemsetAsync(heads, 0, sizeof(uint32_t) * (total + 1), st));
+            k_chunk_heads<<<grid_for(nb, 256), 256, 0, st>>>(ccnt, coff, nb, heads);
+            tmp_bytes = 0;
+            MI_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tmp_bytes, heads, chunk_bucket, MaxOp(), total, st));
+            tmp = c.scratch[4].get(tmp_bytes);
+            MI_HIP(hipcub::DeviceScan::InclusiveScan(tmp, tmp_bytes, heads, chunk_bucket, MaxOp(), total, st));
+            XYZZ<F> *Pnext = c.scratch[pbuf].as<XYZZ<F>>(total);
+            if (level0) {
+                ScopedTimer tacc(c, sizeof(F) == sizeof(fq_t) ? &c.stats.accum_g1 : &c.stats.accum_g2, n);
+                k_accum_level0<F><<<grid_for(total, 256), 256, 0, st>>>(chunk_bucket, coff, off, cnt, total, vals_s,
+                                                                         bases, Pnext);
+                maxcnt = (maxcnt + L0 - 1) / L0;
+            } else {
+                k_accum_level<F><<<grid_for(total, 256), 256, 0, st>>>(chunk_bucket, coff, off, cnt, total, Pcur,
+                                                                        Pnext);
+                maxcnt = (maxcnt + L1 - 1) / L1;
+            }
+            MI_HIP(hipGetLastError());
+            Pcur = Pnext;
+            pbuf = pbuf == 10 ? 11 : 10;
+            std::swap(off, coff);
+            std::swap(cnt, ccnt);
+            level0 = false;
+        }
+    }
+
+    // bucket reduction
+    unsigned seg_len = 1;
+    while (seg_len < nbk && (uint64_t)nwin * (nbk / (seg_len * 2)) >= 16384) seg_len *= 2;
+    uint32_t nseg = nbk / seg_len;
+    XYZZ<F> *segsum = c.scratch[12].as<XYZZ<F>>((uint64_t)nwin * nseg);
+    k_bucket_reduce<F><<<grid_for((uint64_t)nwin * nseg, 256), 256, 0, st>>>(off, cnt, Pcur, nwin, nbk, seg_len,
+                                                                           segsum);
+    XYZZ<F> *wsum = c.scratch[14].as<XYZZ<F>>(nwin);
+    k_window_sum<F, 64><<<nwin, 64, 0, st>>>(segsum, nseg, wsum);
+    MI_HIP(hipGetLastError());
+    std::vector<XYZZ<F>> W(nwin);
+    MI_HIP(hipMemcpyAsync(W.data(), wsum, sizeof(XYZZ<F>) * nwin, hipMemcpyDeviceToHost, st));
+    MI_HIP(hipStreamSynchronize(st));
+    XYZZ<F> acc = W[nwin - 1];
+    for (int w = (int)nwin - 2; w >= 0; w--) {
+        for (unsigned i = 0; i < cb; i++) acc = xyzz_dbl(acc);
+        acc = xyzz_add(acc, W[w]);
+    }
+    *result = acc;
+    c.timer.resolve();
+}
+
+void msm_g1(Ctx &c, const g1_affine_t *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,
+            g1_xyzz_t *result_host) {
+    msm_run<fq_t>(c, bases, scalars, idx, n, result_host);
+}
+void msm_g2(Ctx &c, const g2_affine_t *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,
+            g2_xyzz_t *result_host) {
+    msm_run<fq2_t>(c, bases, scalars, idx, n, result_host);
+}
+
+}  // namespace mi

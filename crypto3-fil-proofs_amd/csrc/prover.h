@@ -1,0 +1,85 @@
+// prover.h -- device-resident circuit / SRS objects and the Groth16 prover (bellman layout).
+#pragma once
+#include <stdint.h>
+
+#include <vector>
+
+#include "ctx.h"
+
+namespace mi {
+
+// R1CS resident on the device (crypto3 keeps the constraint system inside the proving key;
+// bellperson re-synthesises it -- here it is uploaded once per circuit shape, like the SRS).
+struct Circuit {
+    uint64_t n = 0, n_in = 0, n_aux = 0, d = 0;
+    unsigned log_d = 0;
+    uint64_t nnz[3] = {0, 0, 0};
+    uint64_t *row_ptr[3] = {nullptr, nullptr, nullptr};
+    uint32_t *col[3] = {nullptr, nullptr, nullptr};
+    fr_t *coeff[3] = {nullptr, nullptr, nullptr};  // Montgomery
+    // density index lists into z (bellman a_aux_density / b_input_density / b_aux_density)
+    uint32_t *idx_a = nullptr, *idx_b = nullptr;
+    uint64_t n_a = 0, n_b = 0, n_b_in = 0;
+    ~Circuit();
+};
+
+// Groth16 proving key resident on the device (scheme_params{vk,h,l,a,b_g1,b_g2},
+// core/crypto/scheme_params.hpp:46-66).  h is stored bit-reversed (h_perm[pos] = h[bitrev(pos)])
+// so the H coefficients can be consumed in the NTT's natural bit-reversed output order.
+struct Srs {
+    uint64_t d = 0;
+    unsigned log_d = 0;
+    uint64_t n_h = 0, n_l = 0, n_a = 0, n_b = 0, n_ic = 0;
+    g1_affine_t *h_perm = nullptr, *l = nullptr, *a = nullptr, *b_g1 = nullptr;
+    g2_affine_t *b_g2 = nullptr;
+    g1_affine_t alpha_g1, beta_g1, delta_g1;
+    g2_affine_t beta_g2, gamma_g2, delta_g2;
+    std::vector<g1_affine_t> ic;
+    // trapdoor evaluations (only when generated from known toxic waste): per-variable u,v,w(tau)
+    fr_t *at = nullptr, *bt = nullptr, *ct = nullptr;
+    fr_t toxic[5];
+    bool has_trapdoor = false;
+    ~Srs();
+};
+
+struct R1csHost {
+    uint64_t n, n_in, n_aux;
+    const uint64_t *row_ptr[3];
+    const uint32_t *col[3];
+    const uint8_t *coeff[3];
+};
+
+Circuit *circuit_load(Ctx &c, const R1csHost &cs);
+
+struct SrsHost {
+    const uint8_t *vk;  // 864 bytes
+    const uint8_t *ic;
+    uint64_t n_ic;
+    const uint8_t *h, *l, *a, *b_g1, *b_g2;
+    uint64_t n_h, n_l, n_a, n_b_g1, n_b_g2;
+};
+Srs *srs_load(Ctx &c, const Circuit *circ, const SrsHost &h, bool checked);
+Srs *srs_generate(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5]);
+
+struct ProofPoints {
+    g1_affine_t A, C;
+    g2_affine_t B;
+};
+// z_dev: (n_in + n_aux) canonical Fr on the device (z[0] must be ONE).  r, s canonical.
+ProofPoints groth16_prove(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, const fr_t &r,
+                          const fr_t &s);
+// trapdoor dlogs of the unique proof for (z, r, s) (requires srs.has_trapdoor): A, B, C in Fr (canonical)
+void groth16_trapdoor_dlogs(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, const fr_t &r,
+                            const fr_t &s, fr_t out[3]);
+
+// encodings (host)
+void g1_compress(const g1_affine_t &a, uint8_t out[48]);
+void g2_compress(const g2_affine_t &a, uint8_t out[96]);
+void g1_encode(const g1_affine_t &a, uint8_t out[96]);
+void g2_encode(const g2_affine_t &a, uint8_t out[192]);
+bool g1_decode_host(const uint8_t in[96], g1_affine_t &out);
+bool g2_decode_host(const uint8_t in[192], g2_affine_t &out);
+fr_t fr_from_le(const uint8_t in[32]);  // canonical raw (not Montgomery)
+void fr_to_le(const fr_t &raw, uint8_t out[32]);
+
+}  // namespace mi

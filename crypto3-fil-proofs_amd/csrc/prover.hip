@@ -1,0 +1,759 @@
+// prover.hip -- Groth16 prove (bellman/crypto3 r1cs_gg_ppzksnark semantics) on one MI355X.
+//
+// The reference boundary is the crypto3 prover call inside compound_proof::circuit_proofs /
+// prove (libs/storage/include/nil/filecoin/storage/proofs/core/proof/compound_proof.hpp:89-95,
+// 127-137; bodies are stubs in the reference and the prover itself is [NOT IN TREE]).  This file
+// restates that prover:
+//   witness map (bellman ProvingAssignment / libsnark r1cs_to_qap_witness_map):
+//     a_j, b_j, c_j = <A_j,z>, <B_j,z>, <C_j,z> for the n circuit rows, then one row "x_i * 0 = 0"
+//     per public input (a = x_i), zero padded to d = 2^ceil(log2(n + n_in));
+//     a,b,c <- coset_fft(ifft(.)); h_ev = (a*b - c) / (g^d - 1); H = icoset_fft(h_ev)[0..d-2]
+//   multiexps: H (h query), L (aux), A (inputs + aux with A-density), B_G1 / B_G2 (B-density)
+//   A = alpha + sum_A + r delta1; B = beta2 + sum_B2 + s delta2;
+//   C = rs delta1 + s alpha + r beta1 + s sum_A + r sum_B1 + H + L.
+// Proof wire format: compressed A (48) | B (96) | C (48) = 192 bytes (proofs/constants.hpp:93).
+#include <hipcub/hipcub.hpp>
+
+#include <string.h>
+
+#include "prover.h"
+
+namespace mi {
+
+namespace {
+
+inline unsigned grid1(uint64_t n) { return (unsigned)((n + 255) / 256); }
+
+fr_t fr_small_mont(uint32_t v) {
+    fr_t r = fr_t::zero();
+    r.v[0] = v;
+    return to_mont(r);
+}
+
+// ------------------------------------------------------------------------------ witness map
+__global__ void k_eval_rows(const uint64_t *__restrict__ rp0, const uint32_t *__restrict__ c0,
+                            const fr_t *__restrict__ k0, const uint64_t *__restrict__ rp1,
+                            const uint32_t *__restrict__ c1, const fr_t *__restrict__ k1,
+                            const uint64_t *__restrict__ rp2, const uint32_t *__restrict__ c2,
+                            const fr_t *__restrict__ k2, const fr_t *__restrict__ zm, uint64_t n, uint64_t n_in,
+                            uint64_t d, fr_t *__restrict__ a, fr_t *__restrict__ b, fr_t *__restrict__ c) {
+    uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= d) return;
+    fr_t va = fr_t::zero(), vb = fr_t::zero(), vc = fr_t::zero();
+    if (j < n) {
+        for (uint64_t e = rp0[j]; e < rp0[j + 1]; e++) va = va + k0[e] * zm[c0[e]];
+        for (uint64_t e = rp1[j]; e < rp1[j + 1]; e++) vb = vb + k1[e] * zm[c1[e]];
+        for (uint64_t e = rp2[j]; e < rp2[j + 1]; e++) vc = vc + k2[e] * zm[c2[e]];
+    } else if (j < n + n_in) {
+        va = zm[j - n];
+    }
+    a[j] = va;
+    b[j] = vb;
+    c[j] = vc;
+}
+
+__global__ void k_qap_divide(fr_t *__restrict__ a, const fr_t *__restrict__ b, const fr_t *__restrict__ c,
+                             uint64_t d, fr_t zinv) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= d) return;
+    a[i] = (a[i] * b[i] - c[i]) * zinv;
+}
+
+__global__ void k_copy_to_mont(const fr_t *__restrict__ in, fr_t *__restrict__ out, uint64_t n) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = to_mont(in[i]);
+}
+
+// h_perm[pos] = h[bitrev(pos)], pos < d - 1
+__global__ void k_permute_h(const g1_affine_t *__restrict__ h, g1_affine_t *__restrict__ hp, unsigned L,
+                            uint64_t m) {
+    uint64_t pos = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (pos >= m) return;
+    uint64_t r = L ? (__builtin_bitreverse64(pos) >> (64 - L)) : 0;
+    hp[pos] = h[r];
+}
+
+// ------------------------------------------------------------------------------ param generation
+// powers: out[i] = LO[i & 0xffff] * HI[i >> 16]
+__global__ void k_powers(const fr_t *__restrict__ lo, const fr_t *__restrict__ hi, uint64_t n, fr_t *__restrict__ out) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = lo[i & 0xffff] * hi[i >> 16];
+}
+// h scalars in bit-reversed position order: hs[pos] = pw[bitrev(pos)] * coeff (canonical out)
+__global__ void k_h_scalars(const fr_t *__restrict__ pw, unsigned L, uint64_t m, fr_t coeff, fr_t *__restrict__ hs) {
+    uint64_t pos = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (pos >= m) return;
+    uint64_t r = L ? (__builtin_bitreverse64(pos) >> (64 - L)) : 0;
+    hs[pos] = from_mont(pw[r] * coeff);
+}
+__global__ void k_entry_rows(const uint64_t *__restrict__ rp, uint64_t n, uint32_t *__restrict__ rows) {
+    uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    for (uint64_t e = rp[j]; e < rp[j + 1]; e++) rows[e] = (uint32_t)j;
+}
+__global__ void k_iota(uint32_t *__restrict__ x, uint64_t n) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) x[i] = (uint32_t)i;
+}
+__global__ void k_col_bounds(const uint32_t *__restrict__ cols, uint64_t nnz, uint32_t *__restrict__ start,
+                             uint32_t *__restrict__ end) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nnz) return;
+    uint32_t k = cols[i];
+    if (i == 0 || cols[i - 1] != k) start[k] = (uint32_t)i;
+    if (i == nnz - 1 || cols[i + 1] != k) end[k] = (uint32_t)i + 1;
+}
+// out[v] = sum over entries e of column v: coeff[e] * lag[row[e]]   (Montgomery)
+__global__ void k_col_sums(const uint32_t *__restrict__ start, const uint32_t *__restrict__ end,
+                           const uint32_t *__restrict__ perm, const uint32_t *__restrict__ rows,
+                           const fr_t *__restrict__ coeff, const fr_t *__restrict__ lag, uint64_t nv,
+                           fr_t *__restrict__ out) {
+    uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= nv) return;
+    fr_t acc = fr_t::zero();
+    for (uint32_t p = start[v]; p < end[v]; p++) {
+        uint32_t e = perm[p];
+        acc = acc + coeff[e] * lag[rows[e]];
+    }
+    out[v] = acc;
+}
+__global__ void k_add_input_rows(fr_t *__restrict__ at, const fr_t *__restrict__ lag, uint64_t n, uint64_t n_in) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n_in) at[i] = at[i] + lag[n + i];
+}
+// ext[v] = (beta at + alpha bt + ct) * inv  -> canonical
+__global__ void k_lc_scalars(const fr_t *__restrict__ at, const fr_t *__restrict__ bt, const fr_t *__restrict__ ct,
+                             uint64_t off, uint64_t n, fr_t alpha, fr_t beta, fr_t inv, fr_t *__restrict__ out) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t v = off + i;
+    out[i] = from_mont((beta * at[v] + alpha * bt[v] + ct[v]) * inv);
+}
+__global__ void k_gather_canon(const fr_t *__restrict__ src, const uint32_t *__restrict__ idx, uint64_t n,
+                               fr_t *__restrict__ out) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = from_mont(src[idx[i]]);
+}
+
+template <class F>
+MI_HD uint32_t byte_of(const fr_t &s, unsigned j) {
+    uint32_t w = 0;
+    MI_UNROLL for (int q = 0; q < 8; q++) w = (j >> 2) == (unsigned)q ? s.v[q] : w;
+    return (w >> (8 * (j & 3))) & 0xff;
+}
+
+// table[j*255 + m-1] = (m * 2^(8j)) * G, affine
+template <class F>
+__global__ void k_fb_table(Affine<F> G, Affine<F> *__restrict__ table) {
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 32 * 255) return;
+    uint32_t j = t / 255, m = t % 255 + 1;
+    uint32_t k[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned bit = 8 * j;
+    k[bit / 32] |= m << (bit % 32);
+    if (bit % 32 > 24 && bit / 32 + 1 < 9) k[bit / 32 + 1] |= m >> (32 - bit % 32);
+    XYZZ<F> p = xyzz_mul(xyzz_from_affine(G), k, 8);
+    table[t] = xyzz_to_affine(p);
+}
+
+template <class F>
+__global__ void __launch_bounds__(256) k_fixed_base(const fr_t *__restrict__ k, uint64_t n,
+                                                    const Affine<F> *__restrict__ table, XYZZ<F> *__restrict__ out) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const fr_t s = k[i];
+    XYZZ<F> acc = XYZZ<F>::inf();
+#pragma unroll 1
+    for (unsigned j = 0; j < 32; j++) {
+        uint32_t m = byte_of<F>(s, j);
+        if (m) acc = xyzz_add_affine(acc, table[j * 255 + m - 1]);
+    }
+    out[i] = acc;
+}
+
+// batch XYZZ -> affine with Montgomery's trick over K consecutive points per thread
+template <class F, int K>
+__global__ void __launch_bounds__(256) k_batch_affine(const XYZZ<F> *__restrict__ in, uint64_t n,
+                                                      F *__restrict__ pre, Affine<F> *__restrict__ out) {
+    uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t beg = t * K;
+    if (beg >= n) return;
+    uint64_t end = beg + K < n ? beg + K : n;
+    F prod = F::one();
+    for (uint64_t i = beg; i < end; i++) {
+        pre[i] = prod;
+        XYZZ<F> p = in[i];
+        if (!p.is_inf()) prod = prod * p.ZZZ;
+    }
+    F inv = inverse(prod);
+    for (uint64_t i = end; i-- > beg;) {
+        XYZZ<F> p = in[i];
+        if (p.is_inf()) {
+            out[i] = Affine<F>::inf();
+            continue;
+        }
+        F izzz = inv * pre[i];
+        inv = inv * p.ZZZ;
+        F izz = sqr(p.ZZ * izzz);
+        out[i] = {p.X * izz, p.Y * izzz};
+    }
+}
+
+// block-level partial dot products sum z_i * e_i (z canonical -> montgomery on the fly)
+__global__ void k_dot(const fr_t *__restrict__ z, const fr_t *__restrict__ e, uint64_t off, uint64_t n,
+                      fr_t *__restrict__ partial) {
+    __shared__ fr_t sh[256];
+    fr_t acc = fr_t::zero();
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+        acc = acc + to_mont(z[off + i]) * e[off + i];
+    sh[threadIdx.x] = acc;
+    __syncthreads();
+    for (unsigned h = 128; h > 0; h >>= 1) {
+        if (threadIdx.x < h) sh[threadIdx.x] = sh[threadIdx.x] + sh[threadIdx.x + h];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = sh[0];
+}
+
+// ------------------------------------------------------------------------------ host helpers
+void fq_to_be48(const fq_t &mont, uint8_t *out) {
+    fq_t raw = from_mont(mont);
+    for (int i = 0; i < 12; i++) {
+        uint32_t w = raw.v[i];
+        uint8_t *p = out + 4 * (11 - i);
+        p[0] = (uint8_t)(w >> 24);
+        p[1] = (uint8_t)(w >> 16);
+        p[2] = (uint8_t)(w >> 8);
+        p[3] = (uint8_t)w;
+    }
+}
+bool fq_from_be48_host(const uint8_t *p, bool mask, fq_t &out) {
+    fq_t raw;
+    for (int i = 0; i < 12; i++) {
+        const uint8_t *q = p + 4 * (11 - i);
+        uint32_t w = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+        if (i == 11 && mask) w &= 0x1fffffffu;
+        raw.v[i] = w;
+    }
+    if (geq_raw(raw, fq_t::modulus_raw())) return false;
+    out = to_mont(raw);
+    return true;
+}
+bool fq_lex_largest(const fq_t &y) {
+    fq_t a = from_mont(y), b = from_mont(-y);
+    for (int i = 11; i >= 0; i--)
+        if (a.v[i] != b.v[i]) return a.v[i] > b.v[i];
+    return false;
+}
+
+template <class T>
+T *dalloc(uint64_t count) {
+    T *p = nullptr;
+    if (count) MI_HIP(hipMalloc(&p, sizeof(T) * count));
+    return p;
+}
+
+template <class F>
+Affine<F> host_mul_affine(const Affine<F> &p, const fr_t &k_raw) {
+    return xyzz_to_affine(xyzz_mul(xyzz_from_affine(p), k_raw.v, 8));
+}
+
+}  // namespace
+
+// ================================================================================ encodings
+void g1_encode(const g1_affine_t &a, uint8_t out[96]) {
+    if (a.is_inf()) {
+        memset(out, 0, 96);
+        out[0] = 0x40;
+        return;
+    }
+    fq_to_be48(a.x, out);
+    fq_to_be48(a.y, out + 48);
+}
+void g2_encode(const g2_affine_t &a, uint8_t out[192]) {
+    if (a.is_inf()) {
+        memset(out, 0, 192);
+        out[0] = 0x40;
+        return;
+    }
+    fq_to_be48(a.x.c1, out);
+    fq_to_be48(a.x.c0, out + 48);
+    fq_to_be48(a.y.c1, out + 96);
+    fq_to_be48(a.y.c0, out + 144);
+}
+void g1_compress(const g1_affine_t &a, uint8_t out[48]) {
+    if (a.is_inf()) {
+        memset(out, 0, 48);
+        out[0] = 0xc0;
+        return;
+    }
+    fq_to_be48(a.x, out);
+    out[0] |= 0x80;
+    if (fq_lex_largest(a.y)) out[0] |= 0x20;
+}
+void g2_compress(const g2_affine_t &a, uint8_t out[96]) {
+    if (a.is_inf()) {
+        memset(out, 0, 96);
+        out[0] = 0xc0;
+        return;
+    }
+    fq_to_be48(a.x.c1, out);
+    fq_to_be48(a.x.c0, out + 48);
+    out[0] |= 0x80;
+    bool largest = a.y.c1.is_zero() ? fq_lex_largest(a.y.c0) : fq_lex_largest(a.y.c1);
+    if (largest) out[0] |= 0x20;
+}
+bool g1_decode_host(const uint8_t in[96], g1_affine_t &out) {
+    if (in[0] & 0x40) {
+        out = g1_affine_t::inf();
+        return true;
+    }
+    return fq_from_be48_host(in, true, out.x) && fq_from_be48_host(in + 48, false, out.y);
+}
+bool g2_decode_host(const uint8_t in[192], g2_affine_t &out) {
+    if (in[0] & 0x40) {
+        out = g2_affine_t::inf();
+        return true;
+    }
+    return fq_from_be48_host(in, true, out.x.c1) && fq_from_be48_host(in + 48, false, out.x.c0) &&
+           fq_from_be48_host(in + 96, false, out.y.c1) && fq_from_be48_host(in + 144, false, out.y.c0);
+}
+fr_t fr_from_le(const uint8_t in[32]) {
+    fr_t r;
+    memcpy(r.v, in, 32);
+    return r;
+}
+void fr_to_le(const fr_t &raw, uint8_t out[32]) { memcpy(out, raw.v, 32); }
+
+// ================================================================================ objects
+Circuit::~Circuit() {
+    for (int m = 0; m < 3; m++) {
+        if (row_ptr[m]) hipFree(row_ptr[m]);
+        if (col[m]) hipFree(col[m]);
+        if (coeff[m]) hipFree(coeff[m]);
+    }
+    if (idx_a) hipFree(idx_a);
+    if (idx_b) hipFree(idx_b);
+}
+Srs::~Srs() {
+    void *ps[] = {h_perm, l, a, b_g1, b_g2, at, bt, ct};
+    for (void *p : ps)
+        if (p) hipFree(p);
+}
+
+Circuit *circuit_load(Ctx &c, const R1csHost &cs) {
+    if (cs.n_in < 1) throw std::invalid_argument("circuit must have at least the ONE input");
+    uint64_t nv = cs.n_in + cs.n_aux;
+    if (nv >= 0x80000000ull) throw std::invalid_argument("too many variables");
+    Circuit *C = new Circuit();
+    try {
+        C->n = cs.n;
+        C->n_in = cs.n_in;
+        C->n_aux = cs.n_aux;
+        uint64_t rows = cs.n + cs.n_in;
+        C->log_d = 0;
+        while ((1ull << C->log_d) < rows) C->log_d++;
+        C->d = 1ull << C->log_d;
+        if (C->log_d > 31) throw std::invalid_argument("domain too large");
+        std::vector<uint8_t> a_den(cs.n_aux, 0), b_in(cs.n_in, 0), b_aux(cs.n_aux, 0);
+        for (int m = 0; m < 3; m++) {
+            uint64_t nnz = cs.row_ptr[m][cs.n];
+            C->nnz[m] = nnz;
+            if (cs.row_ptr[m][0] != 0) throw std::invalid_argument("row_ptr[0] must be 0");
+            for (uint64_t j = 0; j < cs.n; j++)
+                if (cs.row_ptr[m][j + 1] < cs.row_ptr[m][j]) throw std::invalid_argument("row_ptr not monotone");
+            for (uint64_t e = 0; e < nnz; e++) {
+                uint32_t v = cs.col[m][e];
+                if (v >= nv) throw std::invalid_argument("column index out of range");
+                if (m == 0 && v >= cs.n_in) a_den[v - cs.n_in] = 1;
+                if (m == 1) {
+                    if (v < cs.n_in)
+                        b_in[v] = 1;
+                    else
+                        b_aux[v - cs.n_in] = 1;
+                }
+            }
+            C->row_ptr[m] = dalloc<uint64_t>(cs.n + 1);
+            MI_HIP(hipMemcpy(C->row_ptr[m], cs.row_ptr[m], 8 * (cs.n + 1), hipMemcpyHostToDevice));
+            if (nnz) {
+                C->col[m] = dalloc<uint32_t>(nnz);
+                C->coeff[m] = dalloc<fr_t>(nnz);
+                MI_HIP(hipMemcpy(C->col[m], cs.col[m], 4 * nnz, hipMemcpyHostToDevice));
+                MI_HIP(hipMemcpy(C->coeff[m], cs.coeff[m], 32 * nnz, hipMemcpyHostToDevice));
+                fr_canonicalize(c, C->coeff[m], nnz);
+                fr_to_mont_inplace(c, C->coeff[m], nnz);
+            }
+        }
+        std::vector<uint32_t> ia, ib;
+        for (uint64_t i = 0; i < cs.n_in; i++) ia.push_back((uint32_t)i);
+        for (uint64_t i = 0; i < cs.n_aux; i++)
+            if (a_den[i]) ia.push_back((uint32_t)(cs.n_in + i));
+        for (uint64_t i = 0; i < cs.n_in; i++)
+            if (b_in[i]) ib.push_back((uint32_t)i);
+        C->n_b_in = ib.size();
+        for (uint64_t i = 0; i < cs.n_aux; i++)
+            if (b_aux[i]) ib.push_back((uint32_t)(cs.n_in + i));
+        C->n_a = ia.size();
+        C->n_b = ib.size();
+        C->idx_a = dalloc<uint32_t>(ia.size());
+        MI_HIP(hipMemcpy(C->idx_a, ia.data(), 4 * ia.size(), hipMemcpyHostToDevice));
+        if (!ib.empty()) {
+            C->idx_b = dalloc<uint32_t>(ib.size());
+            MI_HIP(hipMemcpy(C->idx_b, ib.data(), 4 * ib.size(), hipMemcpyHostToDevice));
+        }
+        MI_HIP(hipStreamSynchronize(c.stream));
+    } catch (...) {
+        delete C;
+        throw;
+    }
+    return C;
+}
+
+template <class A>
+static A *upload_points(Ctx &c, const uint8_t *bytes, uint64_t n, bool is_g2, bool checked) {
+    if (!n) return nullptr;
+    const size_t esz = is_g2 ? 192 : 96;
+    A *out = dalloc<A>(n);
+    int *bad = c.scratch[9].as<int>(4);
+    MI_HIP(hipMemsetAsync(bad, 0, sizeof(int), c.stream));
+    // stream through a bounded staging buffer
+    const uint64_t chunk = 1ull << 22;
+    uint8_t *stage = c.scratch[0].as<uint8_t>(esz * (n < chunk ? n : chunk));
+    for (uint64_t o = 0; o < n; o += chunk) {
+        uint64_t m = n - o < chunk ? n - o : chunk;
+        MI_HIP(hipMemcpyAsync(stage, bytes + esz * o, esz * m, hipMemcpyHostToDevice, c.stream));
+        if (is_g2)
+            g2_decode_uncompressed(c, stage, (g2_affine_t *)out + o, m, bad);
+        else
+            g1_decode_uncompressed(c, stage, (g1_affine_t *)out + o, m, bad);
+    }
+    int nbad = 0;
+    MI_HIP(hipMemcpyAsync(&nbad, bad, sizeof(int), hipMemcpyDeviceToHost, c.stream));
+    MI_HIP(hipStreamSynchronize(c.stream));
+    if (nbad && checked) {
+        hipFree(out);
+        throw std::invalid_argument("SRS contains points that are not on the curve / not canonical");
+    }
+    if (nbad) {
+        hipFree(out);
+        throw std::invalid_argument("SRS contains non-canonical coordinates");
+    }
+    return out;
+}
+
+Srs *srs_load(Ctx &c, const Circuit *circ, const SrsHost &h, bool checked) {
+    Srs *S = new Srs();
+    try {
+        if (h.n_h < 1) throw std::invalid_argument("empty h query");
+        uint64_t d = h.n_h + 1;
+        if (d & (d - 1)) throw std::invalid_argument("|h| + 1 must be a power of two");
+        S->d = d;
+        while ((1ull << S->log_d) < d) S->log_d++;
+        if (circ) {
+            if (circ->d != d) throw std::invalid_argument("SRS domain does not match the circuit");
+            if (h.n_l != circ->n_aux) throw std::invalid_argument("|l| != number of aux variables");
+            if (h.n_a != circ->n_a) throw std::invalid_argument("|a| != A-density of the circuit");
+            if (h.n_b_g1 != circ->n_b || h.n_b_g2 != circ->n_b)
+                throw std::invalid_argument("|b_g1| / |b_g2| != B-density of the circuit");
+            if (h.n_ic != circ->n_in) throw std::invalid_argument("|ic| != number of inputs");
+        }
+        S->n_h = h.n_h;
+        S->n_l = h.n_l;
+        S->n_a = h.n_a;
+        S->n_b = h.n_b_g1;
+        if (h.n_b_g1 != h.n_b_g2) throw std::invalid_argument("|b_g1| != |b_g2|");
+        g1_affine_t *hnat = upload_points<g1_affine_t>(c, h.h, h.n_h, false, checked);
+        S->h_perm = dalloc<g1_affine_t>(h.n_h);
+        k_permute_h<<<grid1(h.n_h), 256, 0, c.stream>>>(hnat, S->h_perm, S->log_d, h.n_h);
+        MI_HIP(hipStreamSynchronize(c.stream));
+        hipFree(hnat);
+        S->l = upload_points<g1_affine_t>(c, h.l, h.n_l, false, checked);
+        S->a = upload_points<g1_affine_t>(c, h.a, h.n_a, false, checked);
+        S->b_g1 = upload_points<g1_affine_t>(c, h.b_g1, h.n_b_g1, false, checked);
+        S->b_g2 = upload_points<g2_affine_t>(c, h.b_g2, h.n_b_g2, true, checked);
+        bool ok = g1_decode_host(h.vk, S->alpha_g1) && g1_decode_host(h.vk + 96, S->beta_g1) &&
+                  g2_decode_host(h.vk + 192, S->beta_g2) && g2_decode_host(h.vk + 384, S->gamma_g2) &&
+                  g1_decode_host(h.vk + 576, S->delta_g1) && g2_decode_host(h.vk + 672, S->delta_g2);
+        if (!ok) throw std::invalid_argument("bad verifying key encoding");
+        S->n_ic = h.n_ic;
+        S->ic.resize(h.n_ic);
+        for (uint64_t i = 0; i < h.n_ic; i++)
+            if (!g1_decode_host(h.ic + 96 * i, S->ic[i])) throw std::invalid_argument("bad ic encoding");
+    } catch (...) {
+        delete S;
+        throw;
+    }
+    return S;
+}
+
+// ------------------------------------------------------------------------------ fixed-base helper
+template <class F>
+static void fixed_base_affine(Ctx &c, const Affine<F> *table, const fr_t *k_dev, uint64_t n, Affine<F> *out) {
+    if (!n) return;
+    const uint64_t chunk = 1ull << 24;
+    XYZZ<F> *tmp = c.scratch[10].as<XYZZ<F>>(n < chunk ? n : chunk);
+    F *pre = c.scratch[11].as<F>(n < chunk ? n : chunk);
+    for (uint64_t o = 0; o < n; o += chunk) {
+        uint64_t m = n - o < chunk ? n - o : chunk;
+        k_fixed_base<F><<<grid1(m), 256, 0, c.stream>>>(k_dev + o, m, table, tmp);
+        constexpr int K = 32;
+        k_batch_affine<F, K><<<grid1((m + K - 1) / K), 256, 0, c.stream>>>(tmp, m, pre, out + o);
+        MI_HIP(hipGetLastError());
+    }
+}
+
+Srs *srs_generate(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5]) {
+    Srs *S = new Srs();
+    hipStream_t st = c.stream;
+    try {
+        const uint64_t d = circ.d, n = circ.n, nv = circ.n_in + circ.n_aux;
+        const unsigned L = circ.log_d;
+        S->d = d;
+        S->log_d = L;
+        fr_t tau = to_mont(toxic_canonical[0]), alpha = to_mont(toxic_canonical[1]),
+             beta = to_mont(toxic_canonical[2]), gamma = to_mont(toxic_canonical[3]),
+             delta = to_mont(toxic_canonical[4]);
+        for (int i = 0; i < 5; i++) S->toxic[i] = toxic_canonical[i];
+        S->has_trapdoor = true;
+        // powers of tau via two 65536-entry tables
+        std::vector<fr_t> lo(65536), hi(65536);
+        lo[0] = fr_t::one();
+        for (int i = 1; i < 65536; i++) lo[i] = lo[i - 1] * tau;
+        fr_t t16 = lo[65535] * tau;
+        hi[0] = fr_t::one();
+        for (int i = 1; i < 65536; i++) hi[i] = hi[i - 1] * t16;
+        fr_t *dlo = c.scratch[12].as<fr_t>(65536 * 2), *dhi = dlo + 65536;
+        MI_HIP(hipMemcpyAsync(dlo, lo.data(), 32 * 65536, hipMemcpyHostToDevice, st));
+        MI_HIP(hipMemcpyAsync(dhi, hi.data(), 32 * 65536, hipMemcpyHostToDevice, st));
+        fr_t *pw = dalloc<fr_t>(d);
+        k_powers<<<grid1(d), 256, 0, st>>>(dlo, dhi, d, pw);
+        fr_t tau_d = pow_u64(tau, d);
+        fr_t t_tau = tau_d - fr_t::one();
+        fr_t delta_inv = inverse(delta), gamma_inv = inverse(gamma);
+        // h query scalars (bit-reversed order) -> points
+        fr_t *ks = dalloc<fr_t>(nv > d ? nv : d);
+        k_h_scalars<<<grid1(d - 1), 256, 0, st>>>(pw, L, d - 1, t_tau * delta_inv, ks);
+        // Lagrange coefficients L_j(tau) = ifft(powers)
+        ntt_dif(c, pw, L, true);
+        bitrev_permute(c, pw, L);
+        fr_t draw = fr_t::zero();
+        draw.v[0] = (uint32_t)d;
+        draw.v[1] = (uint32_t)(d >> 32);
+        fr_t dinv = inverse(to_mont(draw));
+        scale_all(c, pw, d, dinv);
+        fr_t *lag = pw;
+        // tables for fixed-base multiplication
+        g1_affine_t g1;
+        g2_affine_t g2;
+        {
+            static const uint8_t g1b[96] = {
+                0x17, 0xf1, 0xd3, 0xa7, 0x31, 0x97, 0xd7, 0x94, 0x26, 0x95, 0x63, 0x8c, 0x4f, 0xa9, 0xac, 0x0f,
+                0xc3, 0x68, 0x8c, 0x4f, 0x97, 0x74, 0xb9, 0x05, 0xa1, 0x4e, 0x3a, 0x3f, 0x17, 0x1b, 0xac, 0x58,
+                0x6c, 0x55, 0xe8, 0x3f, 0xf9, 0x7a, 0x1a, 0xef, 0xfb, 0x3a, 0xf0, 0x0a, 0xdb, 0x22, 0xc6, 0xbb,
+                0x08, 0xb3, 0xf4, 0x81, 0xe3, 0xaa, 0xa0, 0xf1, 0xa0, 0x9e, 0x30, 0xed, 0x74, 0x1d, 0x8a, 0xe4,
+                0xfc, 0xf5, 0xe0, 0x95, 0xd5, 0xd0, 0x0a, 0xf6, 0x00, 0xdb, 0x18, 0xcb, 0x2c, 0x04, 0xb3, 0xed,
+                0xd0, 0x3c, 0xc7, 0x44, 0xa2, 0x88, 0x8a, 0xe4, 0x0c, 0xaa, 0x23, 0x29, 0x46, 0xc5, 0xe7, 0xe1};
+            static const uint8_t g2b[192] = {
+                0x13, 0xe0, 0x2b, 0x60, 0x52, 0x71, 0x9f, 0x60, 0x7d, 0xac, 0xd3, 0xa0, 0x88, 0x27, 0x4f, 0x65,
+                0x59, 0x6b, 0xd0, 0xd0, 0x99, 0x20, 0xb6, 0x1a, 0xb5, 0xda, 0x61, 0xbb, 0xdc, 0x7f, 0x50, 0x49,
+                0x33, 0x4c, 0xf1, 0x12, 0x13, 0x94, 0x5d, 0x57, 0xe5, 0xac, 0x7d, 0x05, 0x5d, 0x04, 0x2b, 0x7e,
+                0x02, 0x4a, 0xa2, 0xb2, 0xf0, 0x8f, 0x0a, 0x91, 0x26, 0x08, 0x05, 0x27, 0x2d, 0xc5, 0x10, 0x51,
+                0xc6, 0xe4, 0x7a, 0xd4, 0xfa, 0x40, 0x3b, 0x02, 0xb4, 0x51, 0x0b, 0x64, 0x7a, 0xe3, 0xd1, 0x77,
+                0x0b, 0xac, 0x03, 0x26, 0xa8, 0x05, 0xbb, 0xef, 0xd4, 0x80, 0x56, 0xc8, 0xc1, 0x21, 0xbd, 0xb8,
+                0x06, 0x06, 0xc4, 0xa0, 0x2e, 0xa7, 0x34, 0xcc, 0x32, 0xac, 0xd2, 0xb0, 0x2b, 0xc2, 0x8b, 0x99,
+                0xcb, 0x3e, 0x28, 0x7e, 0x85, 0xa7, 0x63, 0xaf, 0x26, 0x74, 0x92, 0xab, 0x57, 0x2e, 0x99, 0xab,
+                0x3f, 0x37, 0x0d, 0x27, 0x5c, 0xec, 0x1d, 0xa1, 0xaa, 0xa9, 0x07, 0x5f, 0xf0, 0x5f, 0x79, 0xbe,
+                0x0c, 0xe5, 0xd5, 0x27, 0x72, 0x7d, 0x6e, 0x11, 0x8c, 0xc9, 0xcd, 0xc6, 0xda, 0x2e, 0x35, 0x1a,
+                0xad, 0xfd, 0x9b, 0xaa, 0x8c, 0xbd, 0xd3, 0xa7, 0x6d, 0x42, 0x9a, 0x69, 0x51, 0x60, 0xd1, 0x2c,
+                0x92, 0x3a, 0xc9, 0xcc, 0x3b, 0xac, 0xa2, 0x89, 0xe1, 0x93, 0x54, 0x86, 0x08, 0xb8, 0x28, 0x01};
+            g1_decode_host(g1b, g1);
+            g2_decode_host(g2b, g2);
+        }
+        g1_affine_t *t1 = dalloc<g1_affine_t>(32 * 255);
+        g2_affine_t *t2 = dalloc<g2_affine_t>(32 * 255);
+        k_fb_table<fq_t><<<grid1(32 * 255), 256, 0, st>>>(g1, t1);
+        k_fb_table<fq2_t><<<grid1(32 * 255), 256, 0, st>>>(g2, t2);
+        MI_HIP(hipGetLastError());
+        S->n_h = d - 1;
+        S->h_perm = dalloc<g1_affine_t>(d - 1);
+        fixed_base_affine<fq_t>(c, t1, ks, d - 1, S->h_perm);
+        // QAP evaluations per variable: column sums of coeff * L_row(tau)
+        S->at = dalloc<fr_t>(nv);
+        S->bt = dalloc<fr_t>(nv);
+        S->ct = dalloc<fr_t>(nv);
+        fr_t *outs[3] = {S->at, S->bt, S->ct};
+        for (int m = 0; m < 3; m++) {
+            uint64_t nnz = circ.nnz[m];
+            MI_HIP(hipMemsetAsync(outs[m], 0, 32 * nv, st));
+            if (!nnz) continue;
+            uint32_t *rows = c.scratch[0].as<uint32_t>(nnz);
+            uint32_t *perm_in = c.scratch[1].as<uint32_t>(nnz);
+            uint32_t *cols_s = c.scratch[2].as<uint32_t>(nnz);
+            uint32_t *perm = c.scratch[3].as<uint32_t>(nnz);
+            uint32_t *cstart = c.scratch[5].as<uint32_t>(nv);
+            uint32_t *cend = c.scratch[6].as<uint32_t>(nv);
+            k_entry_rows<<<grid1(n), 256, 0, st>>>(circ.row_ptr[m], n, rows);
+            k_iota<<<grid1(nnz), 256, 0, st>>>(perm_in, nnz);
+            unsigned bits = 1;
+            while ((1ull << bits) < nv) bits++;
+            size_t tb = 0;
+            MI_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, circ.col[m], cols_s, perm_in, perm, nnz, 0, bits,
+                                                      st));
+            void *tmp = c.scratch[4].get(tb);
+            MI_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tb, circ.col[m], cols_s, perm_in, perm, nnz, 0, bits, st));
+            MI_HIP(hipMemsetAsync(cstart, 0, 4 * nv, st));
+            MI_HIP(hipMemsetAsync(cend, 0, 4 * nv, st));
+            k_col_bounds<<<grid1(nnz), 256, 0, st>>>(cols_s, nnz, cstart, cend);
+            k_col_sums<<<grid1(nv), 256, 0, st>>>(cstart, cend, perm, rows, circ.coeff[m], lag, nv, outs[m]);
+            MI_HIP(hipGetLastError());
+        }
+        k_add_input_rows<<<grid1(circ.n_in), 256, 0, st>>>(S->at, lag, n, circ.n_in);
+        // l query: (beta at + alpha bt + ct) / delta over aux
+        S->n_l = circ.n_aux;
+        if (circ.n_aux) {
+            k_lc_scalars<<<grid1(circ.n_aux), 256, 0, st>>>(S->at, S->bt, S->ct, circ.n_in, circ.n_aux, alpha, beta,
+                                                            delta_inv, ks);
+            S->l = dalloc<g1_affine_t>(circ.n_aux);
+            fixed_base_affine<fq_t>(c, t1, ks, circ.n_aux, S->l);
+        }
+        // ic (host side, few points)
+        {
+            k_lc_scalars<<<grid1(circ.n_in), 256, 0, st>>>(S->at, S->bt, S->ct, 0, circ.n_in, alpha, beta, gamma_inv,
+                                                           ks);
+            std::vector<fr_t> ick(circ.n_in);
+            MI_HIP(hipMemcpyAsync(ick.data(), ks, 32 * circ.n_in, hipMemcpyDeviceToHost, st));
+            MI_HIP(hipStreamSynchronize(st));
+            S->n_ic = circ.n_in;
+            S->ic.resize(circ.n_in);
+            for (uint64_t i = 0; i < circ.n_in; i++) S->ic[i] = host_mul_affine(g1, ick[i]);
+        }
+        // a, b queries
+        S->n_a = circ.n_a;
+        k_gather_canon<<<grid1(circ.n_a), 256, 0, st>>>(S->at, circ.idx_a, circ.n_a, ks);
+        S->a = dalloc<g1_affine_t>(circ.n_a);
+        fixed_base_affine<fq_t>(c, t1, ks, circ.n_a, S->a);
+        S->n_b = circ.n_b;
+        if (circ.n_b) {
+            k_gather_canon<<<grid1(circ.n_b), 256, 0, st>>>(S->bt, circ.idx_b, circ.n_b, ks);
+            S->b_g1 = dalloc<g1_affine_t>(circ.n_b);
+            S->b_g2 = dalloc<g2_affine_t>(circ.n_b);
+            fixed_base_affine<fq_t>(c, t1, ks, circ.n_b, S->b_g1);
+            fixed_base_affine<fq2_t>(c, t2, ks, circ.n_b, S->b_g2);
+        }
+        MI_HIP(hipStreamSynchronize(st));
+        hipFree(ks);
+        hipFree(pw);
+        hipFree(t1);
+        hipFree(t2);
+        // verifying key
+        S->alpha_g1 = host_mul_affine(g1, toxic_canonical[1]);
+        S->beta_g1 = host_mul_affine(g1, toxic_canonical[2]);
+        S->delta_g1 = host_mul_affine(g1, toxic_canonical[4]);
+        S->beta_g2 = host_mul_affine(g2, toxic_canonical[2]);
+        S->gamma_g2 = host_mul_affine(g2, toxic_canonical[3]);
+        S->delta_g2 = host_mul_affine(g2, toxic_canonical[4]);
+    } catch (...) {
+        delete S;
+        throw;
+    }
+    return S;
+}
+
+// ================================================================================ prove
+ProofPoints groth16_prove(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, const fr_t &r,
+                          const fr_t &s) {
+    if (srs.d != circ.d || srs.n_l != circ.n_aux || srs.n_a != circ.n_a || srs.n_b != circ.n_b)
+        throw std::invalid_argument("SRS does not match circuit");
+    hipStream_t st = c.stream;
+    const uint64_t d = circ.d, nv = circ.n_in + circ.n_aux;
+    const unsigned L = circ.log_d;
+    ProofPoints out;
+    {
+    ScopedTimer whole(c, &c.stats.prove, circ.n);
+    fr_t *zm = c.scratch[20].as<fr_t>(nv + 3 * d);
+    fr_t *a = zm + nv, *b = a + d, *cc = b + d;
+    k_copy_to_mont<<<grid1(nv), 256, 0, st>>>(z_dev, zm, nv);
+    k_eval_rows<<<grid1(d), 256, 0, st>>>(circ.row_ptr[0], circ.col[0], circ.coeff[0], circ.row_ptr[1], circ.col[1],
+                                          circ.coeff[1], circ.row_ptr[2], circ.col[2], circ.coeff[2], zm, circ.n,
+                                          circ.n_in, d, a, b, cc);
+    MI_HIP(hipGetLastError());
+    fr_t dd = fr_t::zero();
+    dd.v[0] = (uint32_t)d;
+    dd.v[1] = (uint32_t)(d >> 32);
+    fr_t dinv = inverse(to_mont(dd));
+    fr_t *vecs[3] = {a, b, cc};
+    for (fr_t *x : vecs) {
+        ntt_dif(c, x, L, true);                         // ifft (bit-reversed coefficients)
+        coset_scale_bitrev(c, x, L, false, &dinv, false);  // * g^i / d
+        ntt_dit(c, x, L, false);                        // fft on the coset (natural order)
+    }
+    fr_t g = fr_small_mont(7);
+    fr_t zinv = inverse(pow_u64(g, d) - fr_t::one());
+    k_qap_divide<<<grid1(d), 256, 0, st>>>(a, b, cc, d, zinv);
+    ntt_dif(c, a, L, true);
+    coset_scale_bitrev(c, a, L, true, &dinv, true);  // icoset, canonical H (bit-reversed order)
+    g1_xyzz_t H, Lq, As, B1;
+    g2_xyzz_t B2;
+    msm_g1(c, srs.h_perm, a, nullptr, d - 1, &H);
+    msm_g1(c, srs.l, z_dev + circ.n_in, nullptr, circ.n_aux, &Lq);
+    msm_g1(c, srs.a, z_dev, circ.idx_a, circ.n_a, &As);
+    msm_g1(c, srs.b_g1, z_dev, circ.idx_b, circ.n_b, &B1);
+    msm_g2(c, srs.b_g2, z_dev, circ.idx_b, circ.n_b, &B2);
+    // assembly on the host
+    fr_t rs = from_mont(to_mont(r) * to_mont(s));
+    g1_xyzz_t A = xyzz_add(xyzz_add_affine(As, srs.alpha_g1), xyzz_mul(xyzz_from_affine(srs.delta_g1), r.v, 8));
+    g2_xyzz_t B = xyzz_add(xyzz_add_affine(B2, srs.beta_g2), xyzz_mul(xyzz_from_affine(srs.delta_g2), s.v, 8));
+    g1_xyzz_t C = xyzz_mul(xyzz_from_affine(srs.delta_g1), rs.v, 8);
+    C = xyzz_add(C, xyzz_mul(xyzz_from_affine(srs.alpha_g1), s.v, 8));
+    C = xyzz_add(C, xyzz_mul(xyzz_from_affine(srs.beta_g1), r.v, 8));
+    C = xyzz_add(C, xyzz_mul(As, s.v, 8));
+    C = xyzz_add(C, xyzz_mul(B1, r.v, 8));
+    C = xyzz_add(C, H);
+    C = xyzz_add(C, Lq);
+    out.A = xyzz_to_affine(A);
+    out.B = xyzz_to_affine(B);
+    out.C = xyzz_to_affine(C);
+    }
+    MI_HIP(hipStreamSynchronize(st));
+    c.timer.resolve();
+    return out;
+}
+
+static fr_t device_dot(Ctx &c, const fr_t *z, const fr_t *e, uint64_t off, uint64_t n) {
+    if (!n) return fr_t::zero();
+    unsigned blocks = (unsigned)((n + 255) / 256);
+    if (blocks > 1024) blocks = 1024;
+    fr_t *part = c.scratch[14].as<fr_t>(blocks);
+    k_dot<<<blocks, 256, 0, c.stream>>>(z, e, off, n, part);
+    std::vector<fr_t> h(blocks);
+    MI_HIP(hipMemcpyAsync(h.data(), part, 32 * blocks, hipMemcpyDeviceToHost, c.stream));
+    MI_HIP(hipStreamSynchronize(c.stream));
+    fr_t acc = fr_t::zero();
+    for (auto &x : h) acc = acc + x;
+    return acc;
+}
+
+void groth16_trapdoor_dlogs(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, const fr_t &r,
+                            const fr_t &s, fr_t out[3]) {
+    if (!srs.has_trapdoor) throw std::invalid_argument("SRS was not generated from known toxic waste");
+    uint64_t nv = circ.n_in + circ.n_aux;
+    fr_t alpha = to_mont(srs.toxic[1]), beta = to_mont(srs.toxic[2]), delta = to_mont(srs.toxic[4]);
+    fr_t u = device_dot(c, z_dev, srs.at, 0, nv);
+    fr_t v = device_dot(c, z_dev, srs.bt, 0, nv);
+    fr_t w = device_dot(c, z_dev, srs.ct, 0, nv);
+    fr_t ua = device_dot(c, z_dev, srs.at, circ.n_in, circ.n_aux);
+    fr_t va = device_dot(c, z_dev, srs.bt, circ.n_in, circ.n_aux);
+    fr_t wa = device_dot(c, z_dev, srs.ct, circ.n_in, circ.n_aux);
+    fr_t rm = to_mont(r), sm = to_mont(s);
+    fr_t Ad = alpha + u + rm * delta;
+    fr_t Bd = beta + v + sm * delta;
+    fr_t lsum = beta * ua + alpha * va + wa;
+    fr_t ht = u * v - w;
+    fr_t Cd = (lsum + ht) * inverse(delta) + sm * Ad + rm * Bd - rm * sm * delta;
+    out[0] = from_mont(Ad);
+    out[1] = from_mont(Bd);
+    out[2] = from_mont(Cd);
+}
+
+}  // namespace mi

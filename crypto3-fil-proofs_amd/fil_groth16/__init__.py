@@ -1,0 +1,12 @@
+"""fil_groth16 -- MI355X-native Groth16 proving core (BLS12-381) for Filecoin Seal / PoSt.
+
+Host-side mirror of the reference's prover interface over libfilgpu.so's C ABI
+(include/mi355x_groth16.h).  See DESIGN.md for the hot path and INTEGRATION.md for the
+reference-side binding.
+"""
+from ._lib import EXPORTS, LIB_PATH, FilGpuError, build, lib  # noqa: F401
+from .core import (FR_MODULUS, PROOF_BYTES, VK_BYTES, Circuit, Context, Points, ProvingKey,  # noqa: F401
+                   device_count, fr_bytes, generate_random_parameters, msm_window_bits, prove, prove_batch,
+                   trapdoor_dlogs)
+from .compound import (MultiProof, partition_count, get_partitions_for_window_post,  # noqa: F401
+                       circuit_proofs)

@@ -1,0 +1,110 @@
+"""Loads libfilgpu.so (the HIP kernels + C ABI of include/mi355x_groth16.h).
+
+There is no CPU fallback: if the library is missing or no GPU is present, the compute entry points
+raise.  Loading the library itself needs no GPU (symbols can be inspected on CPU-only hosts).
+"""
+import ctypes
+import os
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("FILGPU_LIB", os.path.join(_PKG_ROOT, "build", "libfilgpu.so"))
+
+# Every symbol declared in include/mi355x_groth16.h (checked by tests/test_abi.py)
+EXPORTS = [
+    "mi_device_count", "mi_ctx_create", "mi_ctx_destroy", "mi_last_error", "mi_ctx_stream", "mi_ctx_synchronize",
+    "mi_circuit_load", "mi_circuit_info", "mi_circuit_free",
+    "mi_srs_load", "mi_srs_generate", "mi_srs_export_vk", "mi_srs_export_query", "mi_srs_info", "mi_srs_free",
+    "mi_groth16_prove", "mi_groth16_prove_dev", "mi_groth16_prove_batch", "mi_groth16_trapdoor_dlogs",
+    "mi_msm_g1", "mi_msm_g2", "mi_ntt_fr",
+    "mi_points_upload_g1", "mi_points_upload_g2", "mi_points_from_srs", "mi_points_free", "mi_points_count",
+    "mi_msm_g1_dev", "mi_msm_g2_dev", "mi_ntt_fr_dev",
+    "mi_ctx_get_stats", "mi_ctx_reset_stats", "mi_msm_window_bits",
+    "mi_synth_generate", "mi_synth_r1cs", "mi_synth_witness", "mi_synth_free",
+]
+
+_lib = None
+
+
+class FilGpuError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"libfilgpu error {code}: {msg}")
+        self.code = code
+
+
+def build():
+    import subprocess
+
+    subprocess.check_call(["make", "-s", "-C", _PKG_ROOT, "-j8"])
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FileNotFoundError(
+            f"{LIB_PATH} not found: build it with `make -C {_PKG_ROOT}` (HIP extension is required; "
+            "there is no CPU fallback)")
+    # One HIP runtime per process: torch's libtorch_hip NEEDs "libamdhip64.so" while this library
+    # NEEDs "libamdhip64.so.7".  Loading torch first makes our dependency resolve to the runtime
+    # torch already mapped (same SONAME); the other order maps two HIP/HSA runtimes into one process
+    # and torch then reports "No HIP GPUs are available".
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u8p, u64, c_int = ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int
+    pp = ctypes.POINTER(ctypes.c_void_p)
+    sig = {
+        "mi_device_count": ([ctypes.POINTER(c_int)], c_int),
+        "mi_ctx_create": ([c_int, pp], c_int),
+        "mi_ctx_destroy": ([vp], None),
+        "mi_last_error": ([], ctypes.c_char_p),
+        "mi_ctx_stream": ([vp, pp], c_int),
+        "mi_ctx_synchronize": ([vp], c_int),
+        "mi_circuit_load": ([vp, vp, pp], c_int),
+        "mi_circuit_info": ([vp, vp], c_int),
+        "mi_circuit_free": ([vp], None),
+        "mi_srs_load": ([vp, vp, vp, c_int, pp], c_int),
+        "mi_srs_generate": ([vp, vp, u8p, pp], c_int),
+        "mi_srs_export_vk": ([vp, vp, vp], c_int),
+        "mi_srs_export_query": ([vp, vp, c_int, vp, u64], c_int),
+        "mi_srs_info": ([vp, vp], c_int),
+        "mi_srs_free": ([vp], None),
+        "mi_groth16_prove": ([vp, vp, vp, u8p, u8p, u8p, c_int, vp, vp], c_int),
+        "mi_groth16_prove_dev": ([vp, vp, vp, vp, u8p, u8p, c_int, vp, vp], c_int),
+        "mi_groth16_prove_batch": ([vp, vp, vp, u64, vp, u8p, c_int, vp], c_int),
+        "mi_groth16_trapdoor_dlogs": ([vp, vp, vp, vp, u8p, u8p, vp], c_int),
+        "mi_msm_g1": ([vp, u8p, u8p, u64, vp], c_int),
+        "mi_msm_g2": ([vp, u8p, u8p, u64, vp], c_int),
+        "mi_ntt_fr": ([vp, vp, ctypes.c_uint, c_int, c_int], c_int),
+        "mi_points_upload_g1": ([vp, u8p, u64, pp], c_int),
+        "mi_points_upload_g2": ([vp, u8p, u64, pp], c_int),
+        "mi_points_from_srs": ([vp, vp, c_int, pp], c_int),
+        "mi_points_free": ([vp], None),
+        "mi_points_count": ([vp], u64),
+        "mi_msm_g1_dev": ([vp, vp, vp, u64, vp], c_int),
+        "mi_msm_g2_dev": ([vp, vp, vp, u64, vp], c_int),
+        "mi_ntt_fr_dev": ([vp, vp, ctypes.c_uint, c_int, c_int], c_int),
+        "mi_ctx_get_stats": ([vp, vp], c_int),
+        "mi_ctx_reset_stats": ([vp], c_int),
+        "mi_msm_window_bits": ([u64], ctypes.c_uint),
+        "mi_synth_generate": ([ctypes.c_uint, u64, u64, pp], c_int),
+        "mi_synth_r1cs": ([vp, vp], c_int),
+        "mi_synth_witness": ([vp, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(u64)], c_int),
+        "mi_synth_free": ([vp], None),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != 0:
+        msg = lib().mi_last_error()
+        raise FilGpuError(rc, msg.decode() if msg else "")
+    return rc

@@ -1,0 +1,289 @@
+"""Python mirror of the prover-side reference interface, over the C ABI.
+
+Reference names kept (paths relative to the reference root):
+  * ``Context``      one per GPU -- the device-side counterpart of the process-wide Groth param
+                     cache (libs/filecoin/include/nil/filecoin/proofs/caches.hpp:48-67)
+  * ``Circuit``      the R1CS a compound proof synthesises (e.g. StackedCompound::circuit,
+                     libs/storage/.../porep/stacked/circuit/proof.hpp:271-299)
+  * ``ProvingKey``   r1cs_gg_ppzksnark_mapped_scheme_params / scheme_params{vk,h,l,a,b_g1,b_g2}
+                     (core/crypto/scheme_params.hpp:38-67, core/crypto/mapped_scheme_params.hpp:43-84)
+  * ``prove``        crypto3 r1cs_gg_ppzksnark prove(pk, primary_input, auxiliary_input) -> proof
+                     (called from compound_proof::circuit_proofs, core/proof/compound_proof.hpp:127-137)
+  * ``generate_random_parameters``   groth16::generate_random_parameters (core/parameter_cache.hpp:190)
+Errors raise ``FilGpuError`` (the reference asserts / throws: compound_proof.hpp:94).
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import check, lib
+
+FR_MODULUS = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+PROOF_BYTES = 192
+VK_BYTES = 864
+
+
+def fr_bytes(x) -> bytes:
+    """int -> 32-byte LE canonical; 32-byte values pass through unchanged (the library rejects
+    non-canonical blinding values rather than reducing them)."""
+    if isinstance(x, (bytes, bytearray)):
+        assert len(x) == 32
+        return bytes(x)
+    return int(x % FR_MODULUS).to_bytes(32, "little")
+
+
+def _ptr(b):
+    """(ctypes pointer, keepalive) for bytes / bytearray / numpy buffers."""
+    if isinstance(b, np.ndarray):
+        assert b.flags.c_contiguous
+        return ctypes.c_void_p(b.ctypes.data), b
+    if isinstance(b, (bytes, bytearray, memoryview)):
+        arr = np.frombuffer(bytes(b), dtype=np.uint8)
+        return ctypes.c_void_p(arr.ctypes.data), arr
+    raise TypeError(type(b))
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    check(lib().mi_device_count(ctypes.byref(n)))
+    return n.value
+
+
+class Context:
+    def __init__(self, device: int = 0):
+        self.h = ctypes.c_void_p()
+        check(lib().mi_ctx_create(device, ctypes.byref(self.h)))
+        self.device = device
+
+    def close(self):
+        if self.h:
+            lib().mi_ctx_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def synchronize(self):
+        check(lib().mi_ctx_synchronize(self.h))
+
+    def stream(self) -> int:
+        s = ctypes.c_void_p()
+        check(lib().mi_ctx_stream(self.h, ctypes.byref(s)))
+        return s.value or 0
+
+    # ---- device timers (HIP events inside the library; always on) ----
+    STAT_KEYS = ["accum_g1", "accum_g2", "msm_g1", "msm_g2", "sort", "ntt", "prove"]
+
+    def reset_stats(self):
+        check(lib().mi_ctx_reset_stats(self.h))
+
+    def stats(self) -> dict:
+        out = (ctypes.c_double * 21)()
+        check(lib().mi_ctx_get_stats(self.h, out))
+        v = list(out)
+        return {k: {"ms": v[3 * i], "launches": int(v[3 * i + 1]), "units": int(v[3 * i + 2])}
+                for i, k in enumerate(self.STAT_KEYS)}
+
+    # ---- building blocks ----
+    def msm_g1(self, bases96: bytes, scalars32: bytes) -> bytes:
+        n = len(scalars32) // 32
+        assert len(bases96) >= 96 * n
+        out = ctypes.create_string_buffer(96)
+        check(lib().mi_msm_g1(self.h, bytes(bases96), bytes(scalars32), n, out))
+        return out.raw
+
+    def msm_g2(self, bases192: bytes, scalars32: bytes) -> bytes:
+        n = len(scalars32) // 32
+        assert len(bases192) >= 192 * n
+        out = ctypes.create_string_buffer(192)
+        check(lib().mi_msm_g2(self.h, bytes(bases192), bytes(scalars32), n, out))
+        return out.raw
+
+    def ntt(self, data32: bytes, log_n: int, inverse=False, coset=False) -> bytes:
+        assert len(data32) == 32 << log_n
+        buf = ctypes.create_string_buffer(bytes(data32), len(data32))
+        check(lib().mi_ntt_fr(self.h, buf, log_n, int(inverse), int(coset)))
+        return buf.raw
+
+    def ntt_dev(self, data_ptr: int, log_n: int, inverse=False, coset=False):
+        check(lib().mi_ntt_fr_dev(self.h, ctypes.c_void_p(data_ptr), log_n, int(inverse), int(coset)))
+
+
+class Points:
+    """Device-resident MSM bases (uploaded once, like the resident SRS)."""
+
+    def __init__(self, ctx: Context, data: bytes = None, g2=False, _handle=None, n=None):
+        self.ctx, self.g2 = ctx, g2
+        if _handle is not None:
+            self.h = _handle
+        else:
+            self.h = ctypes.c_void_p()
+            esz = 192 if g2 else 96
+            n = len(data) // esz
+            f = lib().mi_points_upload_g2 if g2 else lib().mi_points_upload_g1
+            check(f(ctx.h, bytes(data), n, ctypes.byref(self.h)))
+        self.n = lib().mi_points_count(self.h)
+
+    def msm_dev(self, scalars_ptr: int, n: int) -> bytes:
+        out = ctypes.create_string_buffer(192 if self.g2 else 96)
+        f = lib().mi_msm_g2_dev if self.g2 else lib().mi_msm_g1_dev
+        check(f(self.ctx.h, self.h, ctypes.c_void_p(scalars_ptr), n, out))
+        return out.raw
+
+    def __del__(self):
+        try:
+            lib().mi_points_free(self.h)
+        except Exception:
+            pass
+
+
+class _R1CS(ctypes.Structure):
+    _fields_ = [
+        ("num_constraints", ctypes.c_uint64),
+        ("num_inputs", ctypes.c_uint64),
+        ("num_aux", ctypes.c_uint64),
+        ("row_ptr", ctypes.c_void_p * 3),
+        ("col", ctypes.c_void_p * 3),
+        ("coeff", ctypes.c_void_p * 3),
+    ]
+
+
+class Circuit:
+    """R1CS uploaded once per shape.  mats: 3 x (row_ptr u64[n+1], col u32[nnz], coeff u8[nnz*32])."""
+
+    def __init__(self, ctx: Context, num_constraints: int, num_inputs: int, num_aux: int, mats):
+        self.ctx = ctx
+        keep = [(np.ascontiguousarray(rp, dtype=np.uint64), np.ascontiguousarray(c, dtype=np.uint32),
+                 np.ascontiguousarray(k, dtype=np.uint8)) for rp, c, k in mats]
+        s = _R1CS()
+        s.num_constraints, s.num_inputs, s.num_aux = num_constraints, num_inputs, num_aux
+        for m, (rp, c, k) in enumerate(keep):
+            s.row_ptr[m] = rp.ctypes.data
+            s.col[m] = c.ctypes.data if len(c) else None
+            s.coeff[m] = k.ctypes.data if len(k) else None
+        self.h = ctypes.c_void_p()
+        check(lib().mi_circuit_load(ctx.h, ctypes.byref(s), ctypes.byref(self.h)))
+        info = (ctypes.c_uint64 * 9)()
+        check(lib().mi_circuit_info(self.h, info))
+        (self.num_constraints, self.num_inputs, self.num_aux, self.d, self.n_a, self.n_b,
+         *self.nnz) = list(info)
+
+    @property
+    def num_vars(self):
+        return self.num_inputs + self.num_aux
+
+    def __del__(self):
+        try:
+            lib().mi_circuit_free(self.h)
+        except Exception:
+            pass
+
+
+class _SrsHost(ctypes.Structure):
+    _fields_ = [("vk", ctypes.c_void_p), ("ic", ctypes.c_void_p), ("n_ic", ctypes.c_uint64),
+                ("h", ctypes.c_void_p), ("n_h", ctypes.c_uint64), ("l", ctypes.c_void_p), ("n_l", ctypes.c_uint64),
+                ("a", ctypes.c_void_p), ("n_a", ctypes.c_uint64), ("b_g1", ctypes.c_void_p),
+                ("n_b_g1", ctypes.c_uint64), ("b_g2", ctypes.c_void_p), ("n_b_g2", ctypes.c_uint64)]
+
+
+class ProvingKey:
+    """Device-resident Groth16 proving key (bellman layout)."""
+
+    def __init__(self, ctx: Context, handle):
+        self.ctx, self.h = ctx, handle
+        info = (ctypes.c_uint64 * 6)()
+        check(lib().mi_srs_info(self.h, info))
+        self.d, self.n_h, self.n_l, self.n_a, self.n_b, self.n_ic = list(info)
+
+    @classmethod
+    def load(cls, ctx: Context, circuit, vk, ic, h, l, a, b_g1, b_g2, checked=False):
+        keep = []
+
+        def p(b):
+            ptr, k = _ptr(b) if len(b) else (None, None)
+            keep.append(k)
+            return ptr
+
+        s = _SrsHost()
+        s.vk, s.ic, s.n_ic = p(vk), p(ic), len(ic) // 96
+        s.h, s.n_h = p(h), len(h) // 96
+        s.l, s.n_l = p(l), len(l) // 96
+        s.a, s.n_a = p(a), len(a) // 96
+        s.b_g1, s.n_b_g1 = p(b_g1), len(b_g1) // 96
+        s.b_g2, s.n_b_g2 = p(b_g2), len(b_g2) // 192
+        hd = ctypes.c_void_p()
+        check(lib().mi_srs_load(ctx.h, circuit.h if circuit is not None else None, ctypes.byref(s), int(checked),
+                                ctypes.byref(hd)))
+        return cls(ctx, hd)
+
+    def verifying_key(self):
+        vk = ctypes.create_string_buffer(VK_BYTES)
+        ic = ctypes.create_string_buffer(96 * self.n_ic)
+        check(lib().mi_srs_export_vk(self.h, vk, ic))
+        return vk.raw, ic.raw
+
+    def query(self, which: int) -> bytes:
+        n = {0: self.n_h, 1: self.n_l, 2: self.n_a, 3: self.n_b, 4: self.n_b}[which]
+        esz = 192 if which == 4 else 96
+        out = ctypes.create_string_buffer(max(1, esz * n))
+        check(lib().mi_srs_export_query(self.ctx.h, self.h, which, out, n))
+        return out.raw[: esz * n]
+
+    def points(self, which: int) -> Points:
+        hd = ctypes.c_void_p()
+        check(lib().mi_points_from_srs(self.ctx.h, self.h, which, ctypes.byref(hd)))
+        p = Points(self.ctx, g2=(which == 4), _handle=hd)
+        p._srs = self  # keep the key alive while the borrowed points live
+        return p
+
+    def __del__(self):
+        try:
+            lib().mi_srs_free(self.h)
+        except Exception:
+            pass
+
+
+def generate_random_parameters(ctx: Context, circuit: Circuit, toxic) -> ProvingKey:
+    """GPU groth16::generate_random_parameters with known toxic waste (tau, alpha, beta, gamma, delta)."""
+    tb = b"".join(fr_bytes(t) for t in toxic)
+    hd = ctypes.c_void_p()
+    check(lib().mi_srs_generate(ctx.h, circuit.h, tb, ctypes.byref(hd)))
+    return ProvingKey(ctx, hd)
+
+
+def prove(ctx: Context, pk: ProvingKey, circuit: Circuit, z, r: int, s: int, priority=False, want_raw=False):
+    """One Groth16 proof. z: bytes (num_vars x 32 LE) or a device pointer (int) to the same layout."""
+    proof = ctypes.create_string_buffer(PROOF_BYTES)
+    raw = ctypes.create_string_buffer(384) if want_raw else None
+    if isinstance(z, int):
+        check(lib().mi_groth16_prove_dev(ctx.h, pk.h, circuit.h, ctypes.c_void_p(z), fr_bytes(r), fr_bytes(s),
+                                         int(priority), proof, raw))
+    else:
+        assert len(z) == 32 * circuit.num_vars, "witness length must be (num_inputs + num_aux) * 32"
+        check(lib().mi_groth16_prove(ctx.h, pk.h, circuit.h, bytes(z), fr_bytes(r), fr_bytes(s), int(priority),
+                                     proof, raw))
+    return (proof.raw, raw.raw) if want_raw else proof.raw
+
+
+def prove_batch(ctx: Context, pk: ProvingKey, circuit: Circuit, zs, rs, priority=False):
+    """count independent partition proofs -> list of 192-byte proofs."""
+    count = len(zs)
+    arr = (ctypes.c_char_p * count)(*[bytes(z) for z in zs])
+    rsb = b"".join(fr_bytes(r) + fr_bytes(s) for r, s in rs)
+    out = ctypes.create_string_buffer(PROOF_BYTES * count)
+    check(lib().mi_groth16_prove_batch(ctx.h, pk.h, circuit.h, count, arr, rsb, int(priority), out))
+    return [out.raw[i * PROOF_BYTES:(i + 1) * PROOF_BYTES] for i in range(count)]
+
+
+def trapdoor_dlogs(ctx: Context, pk: ProvingKey, circuit: Circuit, z_dev_ptr: int, r: int, s: int):
+    out = ctypes.create_string_buffer(96)
+    check(lib().mi_groth16_trapdoor_dlogs(ctx.h, pk.h, circuit.h, ctypes.c_void_p(z_dev_ptr), fr_bytes(r),
+                                          fr_bytes(s), out))
+    return [int.from_bytes(out.raw[32 * i:32 * i + 32], "little") for i in range(3)]
+
+
+def msm_window_bits(n: int) -> int:
+    return lib().mi_msm_window_bits(n)

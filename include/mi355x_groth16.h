@@ -1,0 +1,184 @@
+/*
+ * mi355x_groth16.h -- C ABI of the MI355X-native Groth16 proving core (libfilgpu.so).
+ *
+ * Drop-in boundary for the crypto3 prover call that NilFoundation/crypto3-fil-proofs makes inside
+ * its compound-proof partition loop.  Every entry point below names the reference interface it
+ * replaces (paths relative to the reference root; the crypto3 prover itself lives in the empty
+ * libs/crypto/zk submodule, .gitmodules:19-21, and is marked [NOT IN TREE]):
+ *
+ *   mi_groth16_prove        <- crypto3::zk::snark::prove<r1cs_gg_ppzksnark<bls12<381>>>(pk, primary, aux)
+ *                              as called per partition by compound_proof::circuit_proofs / prove
+ *                              (libs/storage/include/nil/filecoin/storage/proofs/core/proof/
+ *                               compound_proof.hpp:89-95,127-137); proof bytes are the 192-byte
+ *                              SINGLE_PARTITION_PROOF_LEN record (libs/filecoin/include/nil/filecoin/
+ *                              proofs/constants.hpp:93) written by seal_commit_phase2
+ *                              (libs/filecoin/include/nil/filecoin/proofs/api/seal.hpp:306-308)
+ *   mi_srs_load             <- the proving key behind r1cs_gg_ppzksnark_mapped_scheme_params /
+ *                              scheme_params{vk,h,l,a,b_g1,b_g2}
+ *                              (core/crypto/scheme_params.hpp:38-67, core/crypto/mapped_scheme_params.hpp:43-84)
+ *                              memoised by GROTH_PARAM_MEMORY_CACHE (proofs/caches.hpp:48-67)
+ *   mi_srs_generate         <- groth16::generate_random_parameters (core/parameter_cache.hpp:185-200),
+ *                              "used for testing only, or where parameters are otherwise unavailable"
+ *                              (compound_proof.hpp:171-186)
+ *   mi_circuit_load         <- the constraint system held by the crypto3 proving key
+ *                              (r1cs_gg_ppzksnark_proving_key::constraint_system, [NOT IN TREE]),
+ *                              synthesised by e.g. StackedCompound::circuit (porep/stacked/circuit/proof.hpp:271-299)
+ *   mi_msm_g1 / mi_msm_g2   <- crypto3 algebra multiexp ([NOT IN TREE], libs/crypto/algebra)
+ *   mi_ntt_fr               <- crypto3 math evaluation_domain fft/ifft/coset ([NOT IN TREE], libs/crypto/math)
+ *
+ * Conventions
+ *   Fr scalars      : 32 bytes little-endian canonical (< r)    (core/fr32.hpp:36-52)
+ *   G1 / G2 points  : zcash/bellman "uncompressed" big-endian, 96 / 192 bytes,
+ *                     G2 as x.c1|x.c0|y.c1|y.c0, flag 0x40 in byte 0 = infinity
+ *   proofs          : compressed A (48) | B (96) | C (48) = 192 bytes
+ *   variables       : z = inputs (z[0] = ONE) ++ aux, the crypto3 primary/auxiliary split
+ *   status codes    : 0 = OK, < 0 = error (see MI_ERR_*); mi_last_error() has the message
+ *                     (thread-local).  The C++ wrapper rethrows these as exceptions, matching the
+ *                     reference's assert/throw style (compound_proof.hpp:94).
+ *   threading       : a context is internally serialised (one mutex); drive one context per GPU
+ *                     from one host thread each for multi-GPU.
+ */
+#ifndef MI355X_GROTH16_H
+#define MI355X_GROTH16_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MI_OK 0
+#define MI_ERR_ARG (-1)
+#define MI_ERR_HIP (-2)
+#define MI_ERR_INVALID_POINT (-3)
+#define MI_ERR_SIZE (-4)
+#define MI_ERR_INTERNAL (-5)
+#define MI_ERR_NO_DEVICE (-6)
+
+#define MI_PROOF_BYTES 192
+#define MI_VK_BYTES 864 /* alpha_g1 | beta_g1 | beta_g2 | gamma_g2 | delta_g1 | delta_g2 (uncompressed) */
+
+typedef struct mi_ctx mi_ctx;         /* one per GPU: stream, twiddle tables, scratch */
+typedef struct mi_circuit mi_circuit; /* device-resident R1CS (one per circuit shape) */
+typedef struct mi_srs mi_srs;         /* device-resident proving key (one per circuit shape) */
+typedef struct mi_points mi_points;   /* device-resident MSM bases */
+
+/* R1CS in CSR form over variables z = inputs ++ aux (num_inputs includes ONE). */
+typedef struct {
+    uint64_t num_constraints;
+    uint64_t num_inputs;
+    uint64_t num_aux;
+    const uint64_t *row_ptr[3]; /* A, B, C: num_constraints + 1 offsets each */
+    const uint32_t *col[3];     /* variable index per entry */
+    const uint8_t *coeff[3];    /* Fr coefficient per entry, 32 B LE */
+} mi_r1cs;
+
+/* Proving key in the bellman/filecoin params layout (uncompressed points). */
+typedef struct {
+    const uint8_t *vk; /* MI_VK_BYTES */
+    const uint8_t *ic;
+    uint64_t n_ic; /* == num_inputs */
+    const uint8_t *h;
+    uint64_t n_h; /* d - 1 */
+    const uint8_t *l;
+    uint64_t n_l; /* num_aux */
+    const uint8_t *a;
+    uint64_t n_a; /* inputs + aux with A-density */
+    const uint8_t *b_g1;
+    uint64_t n_b_g1; /* inputs/aux with B-density */
+    const uint8_t *b_g2; /* 192-byte points */
+    uint64_t n_b_g2;
+} mi_srs_host;
+
+/* ---- context ---- */
+int mi_device_count(int *out);
+int mi_ctx_create(int device, mi_ctx **out);
+void mi_ctx_destroy(mi_ctx *ctx);
+const char *mi_last_error(void);
+/* stream handle (hipStream_t) the context launches on; external work may be ordered against it */
+int mi_ctx_stream(mi_ctx *ctx, void **stream_out);
+int mi_ctx_synchronize(mi_ctx *ctx);
+
+/* ---- circuits and proving keys ---- */
+int mi_circuit_load(mi_ctx *ctx, const mi_r1cs *cs, mi_circuit **out);
+/* out: num_constraints, num_inputs, num_aux, d, |a|, |b|, nnz(A), nnz(B), nnz(C) */
+int mi_circuit_info(const mi_circuit *c, uint64_t out[9]);
+void mi_circuit_free(mi_circuit *c);
+
+/* checked != 0 additionally verifies every point is on its curve (mapped_scheme_params::checked) */
+int mi_srs_load(mi_ctx *ctx, const mi_circuit *circuit_or_null, const mi_srs_host *host, int checked,
+                mi_srs **out);
+/* toxic waste tau, alpha, beta, gamma, delta: 5 x 32 B LE canonical; generators = standard G1/G2 */
+int mi_srs_generate(mi_ctx *ctx, const mi_circuit *circuit, const uint8_t toxic[160], mi_srs **out);
+/* vk (MI_VK_BYTES) and ic (num_inputs x 96 B) of a loaded / generated key */
+int mi_srs_export_vk(const mi_srs *srs, uint8_t *vk_out, uint8_t *ic_out);
+/* download one query in the wire format: which = 0 h (natural order), 1 l, 2 a, 3 b_g1, 4 b_g2 */
+int mi_srs_export_query(mi_ctx *ctx, const mi_srs *srs, int which, uint8_t *out, uint64_t cap_points);
+/* sizes: d, |h|, |l|, |a|, |b|, |ic| */
+int mi_srs_info(const mi_srs *srs, uint64_t out[6]);
+void mi_srs_free(mi_srs *srs);
+
+/* ---- Groth16 ---- */
+/* z: (num_inputs + num_aux) x 32 B, z[0] = ONE.  r, s: injected blinding (tests / parity);
+ * priority != 0 runs on the context's high-priority stream (post_config.priority,
+ * libs/filecoin/include/nil/filecoin/proofs/types/post_config.hpp:41-42).
+ * raw_out (optional, may be NULL): uncompressed A (96) | B (192) | C (96). */
+int mi_groth16_prove(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circuit, const uint8_t *z,
+                     const uint8_t r[32], const uint8_t s[32], int priority, uint8_t proof_out[MI_PROOF_BYTES],
+                     uint8_t *raw_out);
+/* same with z already resident in device memory (32 B LE canonical per variable) */
+int mi_groth16_prove_dev(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circuit, const void *z_dev,
+                         const uint8_t r[32], const uint8_t s[32], int priority, uint8_t proof_out[MI_PROOF_BYTES],
+                         uint8_t *raw_out);
+/* count independent partitions (compound_proof::circuit_proofs loop); proofs_out = count x 192 B */
+int mi_groth16_prove_batch(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circuit, uint64_t count,
+                           const uint8_t *const *z, const uint8_t *rs /* count x 64 B: r | s */, int priority,
+                           uint8_t *proofs_out);
+/* discrete logs (canonical Fr, 3 x 32 B) of the unique valid A, B, C for (z, r, s) under a key
+ * produced by mi_srs_generate -- the size-independent trapdoor check used by the tests */
+int mi_groth16_trapdoor_dlogs(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circuit, const void *z_dev,
+                              const uint8_t r[32], const uint8_t s[32], uint8_t out[96]);
+
+/* ---- building blocks ---- */
+int mi_msm_g1(mi_ctx *ctx, const uint8_t *bases96, const uint8_t *scalars32, uint64_t n, uint8_t out96[96]);
+int mi_msm_g2(mi_ctx *ctx, const uint8_t *bases192, const uint8_t *scalars32, uint64_t n, uint8_t out192[192]);
+/* bellman EvaluationDomain semantics, natural order in and out: (inverse, coset) =
+ * (0,0) fft, (1,0) ifft, (0,1) coset_fft, (1,1) icoset_fft.  data: 2^log_n x 32 B, in place. */
+int mi_ntt_fr(mi_ctx *ctx, uint8_t *data32, unsigned log_n, int inverse, int coset);
+
+/* device-resident variants: bases uploaded once, scalars / data already in device memory */
+int mi_points_upload_g1(mi_ctx *ctx, const uint8_t *bases96, uint64_t n, mi_points **out);
+int mi_points_upload_g2(mi_ctx *ctx, const uint8_t *bases192, uint64_t n, mi_points **out);
+/* device copies of a generated key's queries (for MSM benchmarking on real SRS points) */
+int mi_points_from_srs(mi_ctx *ctx, const mi_srs *srs, int which, mi_points **out);
+void mi_points_free(mi_points *p);
+uint64_t mi_points_count(const mi_points *p);
+int mi_msm_g1_dev(mi_ctx *ctx, const mi_points *bases, const void *scalars_dev, uint64_t n, uint8_t out96[96]);
+int mi_msm_g2_dev(mi_ctx *ctx, const mi_points *bases, const void *scalars_dev, uint64_t n, uint8_t out192[192]);
+int mi_ntt_fr_dev(mi_ctx *ctx, void *data_dev, unsigned log_n, int inverse, int coset);
+
+/* ---- synthetic workload (BASELINE configs 3/4: "synthetic 2^k-constraint R1CS") ----
+ * Host-side, deterministic, multithreaded generator of a satisfiable R1CS with 2^log_rows - num_inputs
+ * rows (so the evaluation domain is exactly 2^log_rows) and its witness.  Stands in for circuit
+ * synthesis (StackedCircuit::synthesize, porep/stacked/circuit/proof.hpp:98-165), which is outside
+ * the prover boundary.  Pointers returned by mi_synth_r1cs / mi_synth_witness live until mi_synth_free. */
+typedef struct mi_synth mi_synth;
+int mi_synth_generate(unsigned log_rows, uint64_t num_inputs, uint64_t seed, mi_synth **out);
+int mi_synth_r1cs(const mi_synth *s, mi_r1cs *out);
+int mi_synth_witness(const mi_synth *s, const uint8_t **z, uint64_t *num_vars);
+void mi_synth_free(mi_synth *s);
+
+/* ---- device timers (HIP events on the launching stream, resolved at existing sync points, so they
+ * stay on inside timed regions).  out = 7 records x {ms, launches, units}:
+ *   0 k_accum_level0<G1> (units = points)   1 k_accum_level0<G2>   2 whole G1 MSM   3 whole G2 MSM
+ *   4 digits + sort + bucket bounds          5 NTT transforms (units = elements)   6 whole prove (units = constraints) */
+int mi_ctx_get_stats(mi_ctx *ctx, double out[21]);
+int mi_ctx_reset_stats(mi_ctx *ctx);
+/* msm window size chosen for n points (exposed for tests / reports) */
+unsigned mi_msm_window_bits(uint64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MI355X_GROTH16_H */

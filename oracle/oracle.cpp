@@ -1139,6 +1139,63 @@ or_params *or_groth16_keygen(const or_r1cs *cs, const uint8_t toxic[5 * 32]) {
     P->delta_g2 = v2[2];
     return P;
 }
+// Load a proving key produced elsewhere (bellman layout, wire encodings).  Densities come from the
+// R1CS (a variable is dense when it appears in the matrix), as in bellman's prover.  The trapdoor
+// fields stay empty: or_groth16_trapdoor_check must not be used on such params.
+or_params *or_params_from_queries(const or_r1cs *cs, const uint8_t *h, uint64_t n_h, const uint8_t *l,
+                                  const uint8_t *a, uint64_t n_a, const uint8_t *b_g1, const uint8_t *b_g2,
+                                  uint64_t n_b, const uint8_t *vk, const uint8_t *ic) {
+    or_params *P = new or_params();
+    P->n = cs->num_constraints;
+    P->n_in = cs->num_inputs;
+    P->n_aux = cs->num_aux;
+    P->log_d = domain_log(P->n + P->n_in);
+    P->d = 1ULL << P->log_d;
+    if (n_h != P->d - 1) {
+        delete P;
+        return nullptr;
+    }
+    P->a_aux_density.assign(P->n_aux, 0);
+    P->b_in_density.assign(P->n_in, 0);
+    P->b_aux_density.assign(P->n_aux, 0);
+    for (int m = 0; m < 2; m++)
+        for (uint64_t e = 0; e < cs->row_ptr[m][P->n]; e++) {
+            uint32_t v = cs->col[m][e];
+            if (m == 0 && v >= P->n_in) P->a_aux_density[v - P->n_in] = 1;
+            if (m == 1) {
+                if (v < P->n_in)
+                    P->b_in_density[v] = 1;
+                else
+                    P->b_aux_density[v - P->n_in] = 1;
+            }
+        }
+    P->h.resize(n_h);
+    P->l.resize(P->n_aux);
+    P->a.resize(n_a);
+    P->b_g1.resize(n_b);
+    P->b_g2.resize(n_b);
+    P->ic.resize(P->n_in);
+    bool ok = true;
+    int nt = nthreads();
+#pragma omp parallel for num_threads(nt) reduction(&& : ok)
+    for (int64_t i = 0; i < (int64_t)n_h; i++) ok = ok && g1_decode(h + 96 * i, &P->h[i]);
+#pragma omp parallel for num_threads(nt) reduction(&& : ok)
+    for (int64_t i = 0; i < (int64_t)P->n_aux; i++) ok = ok && g1_decode(l + 96 * i, &P->l[i]);
+#pragma omp parallel for num_threads(nt) reduction(&& : ok)
+    for (int64_t i = 0; i < (int64_t)n_a; i++) ok = ok && g1_decode(a + 96 * i, &P->a[i]);
+#pragma omp parallel for num_threads(nt) reduction(&& : ok)
+    for (int64_t i = 0; i < (int64_t)n_b; i++)
+        ok = ok && g1_decode(b_g1 + 96 * i, &P->b_g1[i]) && g2_decode(b_g2 + 192 * i, &P->b_g2[i]);
+    for (uint64_t i = 0; i < P->n_in; i++) ok = ok && g1_decode(ic + 96 * i, &P->ic[i]);
+    ok = ok && g1_decode(vk, &P->alpha_g1) && g1_decode(vk + 96, &P->beta_g1) && g2_decode(vk + 192, &P->beta_g2) &&
+         g2_decode(vk + 384, &P->gamma_g2) && g1_decode(vk + 576, &P->delta_g1) && g2_decode(vk + 672, &P->delta_g2);
+    if (!ok) {
+        delete P;
+        return nullptr;
+    }
+    return P;
+}
+
 void or_params_free(or_params *p) { delete p; }
 void or_params_sizes(const or_params *p, uint64_t out[6]) {
     out[0] = p->d;

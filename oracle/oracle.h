@@ -76,6 +76,10 @@ int or_msm_g1_naive(const uint8_t *bases96, const uint8_t *scalars32, size_t n, 
 typedef struct or_params or_params;   /* opaque: vk + h,l,a,b_g1,b_g2 + densities + trapdoor evals */
 or_params *or_groth16_keygen(const or_r1cs *cs, const uint8_t toxic[5 * 32]);
 void or_params_free(or_params *p);
+/* Load externally produced params (wire encodings; densities derived from the R1CS). NULL on error. */
+or_params *or_params_from_queries(const or_r1cs *cs, const uint8_t *h, uint64_t n_h, const uint8_t *l,
+                                  const uint8_t *a, uint64_t n_a, const uint8_t *b_g1, const uint8_t *b_g2,
+                                  uint64_t n_b, const uint8_t *vk, const uint8_t *ic);
 /* Sizes of the queries (number of points) */
 void or_params_sizes(const or_params *p, uint64_t out[6]); /* d, |h|, |l|, |a|, |b_g1|, |b_g2| */
 /* Export the bellman-layout queries: h,l,a,b_g1 as G1 96B, b_g2 as G2 192B, vk (see .cpp) */

@@ -33,6 +33,9 @@ def lib():
         L.or_groth16_keygen.restype = ctypes.c_void_p
         L.or_groth16_keygen.argtypes = [ctypes.c_void_p, u8p]
         L.or_params_free.argtypes = [ctypes.c_void_p]
+        L.or_params_from_queries.restype = ctypes.c_void_p
+        L.or_params_from_queries.argtypes = [ctypes.c_void_p, u8p, ctypes.c_uint64, u8p, u8p, ctypes.c_uint64, u8p,
+                                             u8p, ctypes.c_uint64, u8p, u8p]
         L.or_params_sizes.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.or_params_export.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 7
         L.or_groth16_prove.argtypes = [ctypes.c_void_p, ctypes.c_void_p, u8p, u8p, u8p, ctypes.c_void_p,
@@ -202,10 +205,19 @@ class OracleCircuit:
 
 
 class OracleParams:
-    def __init__(self, circ: OracleCircuit, toxic):
-        tb = b"".join(fr_bytes(t) for t in toxic)
+    def __init__(self, circ: OracleCircuit, toxic=None, queries=None):
+        """toxic: keygen from known toxic waste; queries: dict(h,l,a,b_g1,b_g2,vk,ic) wire bytes."""
         self.circ = circ
-        self.p = lib().or_groth16_keygen(circ.ptr, tb)
+        if queries is not None:
+            q = queries
+            self.p = lib().or_params_from_queries(circ.ptr, q["h"], len(q["h"]) // 96, q["l"], q["a"],
+                                                  len(q["a"]) // 96, q["b_g1"], q["b_g2"], len(q["b_g1"]) // 96,
+                                                  q["vk"], q["ic"])
+            if not self.p:
+                raise ValueError("oracle could not load the given params")
+        else:
+            tb = b"".join(fr_bytes(t) for t in toxic)
+            self.p = lib().or_groth16_keygen(circ.ptr, tb)
         sizes = (ctypes.c_uint64 * 6)()
         lib().or_params_sizes(self.p, sizes)
         self.d, self.nh, self.nl, self.na, self.nb1, self.nb2 = list(sizes)

@@ -1,0 +1,143 @@
+"""GPU parity for the full Groth16 prover (crypto3 r1cs_gg_ppzksnark / bellman semantics).
+
+* golden fixtures: the SRS from the oracle's keygen is loaded through mi_srs_load and the proof
+  must equal the fixture bytes (which the independent Python restatement produced and a pairing
+  check accepted);
+* GPU parameter generation (mi_srs_generate) must reproduce the oracle keygen query-for-query;
+* larger circuits: GPU proof == oracle proof, oracle pairing verifier accepts it;
+* BASELINE-size property: trapdoor discrete logs of (A, B, C) at 2^20 constraints.
+"""
+import numpy as np
+import pytest
+
+import circuits
+import fil_groth16 as fg
+
+pytestmark = pytest.mark.gpu
+
+
+def _circuit_from_name(name):
+    if name.startswith("random"):
+        _, seed, rows = name.split("_")
+        return circuits.random_circuit(int(seed), int(rows))
+    return circuits.toy_chain(1022)
+
+
+def _load(ctx, oracle, n_in, n_aux, rows, z):
+    mats = circuits.to_csr(rows)
+    oc = oracle.OracleCircuit(len(rows), n_in, n_aux, mats)
+    gc = fg.Circuit(ctx, len(rows), n_in, n_aux, mats)
+    return oc, gc
+
+
+@pytest.mark.parametrize("name", ["random_11_24", "random_12_60", "toy_chain_1022"])
+def test_groth16_golden_loaded_srs(ctx, oracle, golden, name):
+    g = golden["groth16"][name]
+    n_in, n_aux, rows, z = _circuit_from_name(name)
+    oc, gc = _load(ctx, oracle, n_in, n_aux, rows, z)
+    op = oracle.OracleParams(oc, circuits.toxic())
+    ex = op.export()
+    pk = fg.ProvingKey.load(ctx, gc, ex["vk"], ex["ic"], ex["h"], ex["l"], ex["a"], ex["b_g1"], ex["b_g2"],
+                            checked=True)
+    r, s = circuits.blinding()
+    proof, raw = fg.prove(ctx, pk, gc, circuits.z_bytes(z), r, s, want_raw=True)
+    assert proof.hex() == g["proof"]
+    assert raw.hex() == g["raw"]
+
+
+@pytest.mark.parametrize("name", ["random_11_24", "random_12_60", "toy_chain_1022"])
+def test_groth16_golden_generated_srs(ctx, oracle, golden, name):
+    g = golden["groth16"][name]
+    n_in, n_aux, rows, z = _circuit_from_name(name)
+    oc, gc = _load(ctx, oracle, n_in, n_aux, rows, z)
+    pk = fg.generate_random_parameters(ctx, gc, circuits.toxic())
+    op = oracle.OracleParams(oc, circuits.toxic())
+    ex = op.export()
+    assert [pk.n_h, pk.n_l, pk.n_a, pk.n_b, pk.n_b] == g["query_sizes"]
+    vk, ic = pk.verifying_key()
+    assert vk == ex["vk"] and ic == ex["ic"]
+    for which, key in enumerate(("h", "l", "a", "b_g1", "b_g2")):
+        assert pk.query(which) == ex[key], key
+    r, s = circuits.blinding()
+    assert fg.prove(ctx, pk, gc, circuits.z_bytes(z), r, s).hex() == g["proof"]
+
+
+def test_groth16_unsatisfied_witness_matches_oracle(ctx, oracle):
+    """Bit-exactness does not depend on satisfiability (the prover is a deterministic map)."""
+    n_in, n_aux, rows, z = circuits.random_circuit(21, 40)
+    z = list(z)
+    z[-1] = (z[-1] + 1) % fg.FR_MODULUS
+    oc, gc = _load(ctx, oracle, n_in, n_aux, rows, z)
+    op = oracle.OracleParams(oc, circuits.toxic())
+    pk = fg.generate_random_parameters(ctx, gc, circuits.toxic())
+    zb = circuits.z_bytes(z)
+    r, s = 5, 7
+    assert fg.prove(ctx, pk, gc, zb, r, s) == op.prove(zb, r, s)[0]
+
+
+@pytest.mark.parametrize("rows,seed", [(700, 31), (5000, 32), (16000, 33)])
+def test_groth16_random_vs_oracle_and_pairing(ctx, oracle, rows, seed):
+    n_in, n_aux, rws, z = circuits.random_circuit(seed, rows, n_in=6, n_free=32)
+    oc, gc = _load(ctx, oracle, n_in, n_aux, rws, z)
+    tox = circuits.toxic(seed)
+    pk = fg.generate_random_parameters(ctx, gc, tox)
+    op = oracle.OracleParams(oc, tox)
+    zb = circuits.z_bytes(z)
+    r, s = circuits.blinding(seed)
+    proof, raw = fg.prove(ctx, pk, gc, zb, r, s, want_raw=True)
+    oproof, oraw, _ = op.prove(zb, r, s)
+    assert proof == oproof and raw == oraw
+    vk, ic = pk.verifying_key()
+    assert oracle.groth16_verify(vk, ic, zb[:32 * n_in], raw)
+    assert op.trapdoor_check(zb, r, s, raw)
+    # zero blinding edge case (r = s = 0) still matches
+    assert fg.prove(ctx, pk, gc, zb, 0, 0) == op.prove(zb, 0, 0)[0]
+
+
+def test_prove_batch_and_priority(ctx, oracle):
+    n_in, n_aux, rws, z = circuits.random_circuit(41, 300)
+    oc, gc = _load(ctx, oracle, n_in, n_aux, rws, z)
+    pk = fg.generate_random_parameters(ctx, gc, circuits.toxic())
+    op = oracle.OracleParams(oc, circuits.toxic())
+    zb = circuits.z_bytes(z)
+    rs = [(1, 2), (3, 4), (5, 6)]
+    proofs = fg.prove_batch(ctx, pk, gc, [zb] * 3, rs, priority=True)
+    for p, (r, s) in zip(proofs, rs):
+        assert p == op.prove(zb, r, s)[0]
+    mp = fg.MultiProof(proofs)
+    assert fg.MultiProof.from_bytes(mp.to_bytes()).circuit_proofs == proofs
+
+
+def test_prove_rejects_mismatched_srs(ctx):
+    n_in, n_aux, rws, z = circuits.random_circuit(51, 30)
+    gc = fg.Circuit(ctx, len(rws), n_in, n_aux, circuits.to_csr(rws))
+    n_in2, n_aux2, rws2, z2 = circuits.random_circuit(52, 200)
+    gc2 = fg.Circuit(ctx, len(rws2), n_in2, n_aux2, circuits.to_csr(rws2))
+    pk2 = fg.generate_random_parameters(ctx, gc2, circuits.toxic())
+    with pytest.raises(fg.FilGpuError):
+        fg.prove(ctx, pk2, gc, circuits.z_bytes(z), 1, 2)
+    with pytest.raises(fg.FilGpuError):
+        fg.prove(ctx, pk2, gc2, circuits.z_bytes(z2), fg.FR_MODULUS.to_bytes(32, "little"), 2)  # r >= r_mod
+
+
+def test_groth16_trapdoor_2_20(ctx, oracle):
+    """BASELINE-size property check: a 2^20-row synthetic circuit (GPU keygen from known toxic
+    waste), checked by discrete logs: A == a*G1, B == b*G2, C == c*G1 where (a, b, c) follow
+    from the QAP identity u(tau) v(tau) - w(tau) = h(tau) t(tau)."""
+    import torch
+
+    from fil_groth16 import synth
+
+    sc = synth.SynthCircuit(log_rows=20, n_in=4, seed=9)
+    gc = sc.load(ctx)
+    pk = fg.generate_random_parameters(ctx, gc, circuits.toxic())
+    z = torch.from_numpy(np.frombuffer(sc.z_bytes(), dtype=np.uint8).copy()).cuda()
+    r, s = circuits.blinding(3)
+    proof, raw = fg.prove(ctx, pk, gc, z.data_ptr(), r, s, want_raw=True)
+    a, b, c = fg.trapdoor_dlogs(ctx, pk, gc, z.data_ptr(), r, s)
+    g1, g2 = oracle.g1_generator(), oracle.g2_generator()
+    assert raw[:96] == oracle.g1_mul(g1, a)
+    assert raw[96:288] == oracle.g2_mul(g2, b)
+    assert raw[288:] == oracle.g1_mul(g1, c)
+    vk, ic = pk.verifying_key()
+    assert oracle.groth16_verify(vk, ic, sc.z_bytes()[:32 * sc.n_in], raw)
