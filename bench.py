@@ -90,7 +90,7 @@ def main():
     ap.add_argument("--n-in", type=int, default=4)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--msm-reps", type=int, default=3, help="reps of the standalone 2^log-rows G1 MSM")
-    ap.add_argument("--cpu-log-rows", type=int, default=18)
+    ap.add_argument("--cpu-log-rows", type=int, default=21)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stats-json", default=None, help="write per-kernel timers here")
     args = ap.parse_args()

@@ -1,0 +1,41 @@
+"""One process per GPU: shard independent partition proofs, gather the 192-byte proofs to rank 0.
+
+Reference behaviour being distributed: compound_proof::circuit_proofs proves every partition of
+a PoRep (10 at 32 GiB, proofs/constants.hpp:70-73) or Window-PoSt batch (post.cpp:37-46)
+sequentially in-process and concatenates 192 x P bytes (api/seal.hpp:306-308).  Partitions are
+independent proofs over the same proving key, so there is no data-path collective: each rank
+proves partitions rank, rank + world, ... against its own resident key, and the only exchange is
+one all-gather of the finished proofs (RCCL over xGMI with backend "nccl"; gloo on CPU tests).
+"""
+import numpy as np
+
+from .compound import shard_partitions
+from .core import PROOF_BYTES
+
+
+def gather_multiproof(local_proofs, num_partitions: int, rank: int, world: int, device="cpu"):
+    """local_proofs: this rank's proofs, in the order of shard_partitions(num_partitions, rank, world).
+    Returns the P x 192-byte multi-proof (partition order) on every rank."""
+    import torch
+    import torch.distributed as dist
+
+    mine = shard_partitions(num_partitions, rank, world)
+    if len(local_proofs) != len(mine):
+        raise ValueError(f"rank {rank} holds {len(local_proofs)} proofs, expected {len(mine)}")
+    kmax = (num_partitions + world - 1) // world
+    buf = np.zeros((kmax, PROOF_BYTES), dtype=np.uint8)
+    for i, p in enumerate(local_proofs):
+        if len(p) != PROOF_BYTES:
+            raise ValueError("proofs are 192 bytes")
+        buf[i] = np.frombuffer(p, dtype=np.uint8)
+    t = torch.from_numpy(buf).to(device)
+    if world > 1:
+        bufs = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(bufs, t)
+        allp = [b.cpu().numpy() for b in bufs]
+    else:
+        allp = [t.cpu().numpy()]
+    out = bytearray()
+    for p in range(num_partitions):
+        out += allp[p % world][p // world].tobytes()
+    return bytes(out)
