@@ -147,12 +147,27 @@ struct ScopedTimer {
         a = c.timer.get();
         MI_HIP(hipEventRecord(a, c.stream));
     }
-    ~ScopedTimer() {
-        hipEvent_t b = c.timer.get();
-        hipEventRecord(b, c.stream);
+    ~ScopedTimer() {  // must not throw: runs during stack unwinding too
+        hipEvent_t b = nullptr;
+        if (!c.timer.pool.empty()) {
+            b = c.timer.pool.back();
+            c.timer.pool.pop_back();
+        } else if (hipEventCreate(&b) != hipSuccess) {
+            return;
+        }
+        if (hipEventRecord(b, c.stream) != hipSuccess) return;
         c.timer.pending.push_back({a, b, dst, units});
     }
 };
+
+// Opt-in launch checking (env MI_DEBUG_SYNC=1): synchronise after each launch and name the kernel
+// that faulted.  Off by default (no synchronisation in the hot path).
+void debug_sync(Ctx &c, const char *what);
+#define MI_LAUNCHED(ctx, name)          \
+    do {                                \
+        MI_HIP(hipGetLastError());      \
+        ::mi::debug_sync((ctx), (name)); \
+    } while (0)
 
 // ---- NTT (ntt.hip) ----
 void ntt_init_tables(Ctx &c);

@@ -42,7 +42,7 @@ MI_HD XYZZ<F> xyzz_neg(const XYZZ<F> &p) {
 
 // dbl-2008-s-1 (a = 0)
 template <class F>
-MI_NOINL XYZZ<F> xyzz_dbl(const XYZZ<F> &p) {
+MI_HD XYZZ<F> xyzz_dbl_inl(const XYZZ<F> &p) {
     if (p.is_inf()) return p;
     F U = dbl(p.Y);
     F V = sqr(U);
@@ -57,10 +57,14 @@ MI_NOINL XYZZ<F> xyzz_dbl(const XYZZ<F> &p) {
     r.ZZZ = W * p.ZZZ;
     return r;
 }
+template <class F>
+MI_NOINL XYZZ<F> xyzz_dbl(const XYZZ<F> &p) {
+    return xyzz_dbl_inl(p);
+}
 
 // mdbl-2008-s-1: double an affine point
 template <class F>
-MI_NOINL XYZZ<F> xyzz_dbl_affine(const Affine<F> &a) {
+MI_HD XYZZ<F> xyzz_dbl_affine_inl(const Affine<F> &a) {
     F U = dbl(a.y);
     F V = sqr(U);
     F W = U * V;
@@ -74,10 +78,17 @@ MI_NOINL XYZZ<F> xyzz_dbl_affine(const Affine<F> &a) {
     r.ZZZ = W;
     return r;
 }
+template <class F>
+MI_NOINL XYZZ<F> xyzz_dbl_affine(const Affine<F> &a) {
+    return xyzz_dbl_affine_inl(a);
+}
+
+// *_inl: force-inlined bodies for the hot kernels (no call ABI, no scratch); the plain names
+// are noinline wrappers for cold code (host assembly, table builds, reductions).
 
 // madd-2008-s: p (XYZZ) + q (affine, may be infinity)
 template <class F>
-MI_NOINL XYZZ<F> xyzz_add_affine(const XYZZ<F> &p, const Affine<F> &q) {
+MI_HD XYZZ<F> xyzz_add_affine_inl(const XYZZ<F> &p, const Affine<F> &q) {
     if (q.is_inf()) return p;
     if (p.is_inf()) return xyzz_from_affine(q);
     F U2 = q.x * p.ZZ;
@@ -85,7 +96,7 @@ MI_NOINL XYZZ<F> xyzz_add_affine(const XYZZ<F> &p, const Affine<F> &q) {
     F P = U2 - p.X;
     F R = S2 - p.Y;
     if (P.is_zero()) {
-        if (R.is_zero()) return xyzz_dbl_affine(q);
+        if (R.is_zero()) return xyzz_dbl_affine_inl(q);
         return XYZZ<F>::inf();
     }
     F PP = sqr(P);
@@ -98,10 +109,14 @@ MI_NOINL XYZZ<F> xyzz_add_affine(const XYZZ<F> &p, const Affine<F> &q) {
     r.ZZZ = p.ZZZ * PPP;
     return r;
 }
+template <class F>
+MI_NOINL XYZZ<F> xyzz_add_affine(const XYZZ<F> &p, const Affine<F> &q) {
+    return xyzz_add_affine_inl(p, q);
+}
 
 // add-2008-s: p + q, both XYZZ
 template <class F>
-MI_NOINL XYZZ<F> xyzz_add(const XYZZ<F> &p, const XYZZ<F> &q) {
+MI_HD XYZZ<F> xyzz_add_inl(const XYZZ<F> &p, const XYZZ<F> &q) {
     if (q.is_inf()) return p;
     if (p.is_inf()) return q;
     F U1 = p.X * q.ZZ;
@@ -111,7 +126,7 @@ MI_NOINL XYZZ<F> xyzz_add(const XYZZ<F> &p, const XYZZ<F> &q) {
     F P = U2 - U1;
     F R = S2 - S1;
     if (P.is_zero()) {
-        if (R.is_zero()) return xyzz_dbl(p);
+        if (R.is_zero()) return xyzz_dbl_inl(p);
         return XYZZ<F>::inf();
     }
     F PP = sqr(P);
@@ -124,26 +139,40 @@ MI_NOINL XYZZ<F> xyzz_add(const XYZZ<F> &p, const XYZZ<F> &q) {
     r.ZZZ = p.ZZZ * q.ZZZ * PPP;
     return r;
 }
-
-// host/device: XYZZ -> affine (one inversion)
 template <class F>
-MI_NOINL Affine<F> xyzz_to_affine(const XYZZ<F> &p) {
+MI_NOINL XYZZ<F> xyzz_add(const XYZZ<F> &p, const XYZZ<F> &q) {
+    return xyzz_add_inl(p, q);
+}
+
+// XYZZ -> affine (one inversion)
+template <class F>
+MI_HD Affine<F> xyzz_to_affine_inl(const XYZZ<F> &p) {
     if (p.is_inf()) return Affine<F>::inf();
-    F izzz = inverse(p.ZZZ);
+    F izzz = inverse_inl(p.ZZZ);
     F izz_sq = sqr(p.ZZ * izzz);  // (ZZ/ZZZ)^2 = 1/ZZ  (ZZ^3 = ZZZ^2)
     return {p.X * izz_sq, p.Y * izzz};
 }
-
-// scalar multiplication by a canonical little-endian word scalar (host / rare device use)
 template <class F>
-MI_NOINL XYZZ<F> xyzz_mul(const XYZZ<F> &p, const uint32_t *k, int nwords) {
+MI_NOINL Affine<F> xyzz_to_affine(const XYZZ<F> &p) {
+    return xyzz_to_affine_inl(p);
+}
+
+// scalar multiplication by a canonical little-endian word scalar
+template <class F>
+MI_HD XYZZ<F> xyzz_mul_inl(const XYZZ<F> &p, const uint32_t *k, int nwords) {
     XYZZ<F> r = XYZZ<F>::inf();
+#pragma unroll 1
     for (int i = nwords - 1; i >= 0; i--)
+#pragma unroll 1
         for (int b = 31; b >= 0; b--) {
-            r = xyzz_dbl(r);
-            if ((k[i] >> b) & 1) r = xyzz_add(r, p);
+            r = xyzz_dbl_inl(r);
+            if ((k[i] >> b) & 1) r = xyzz_add_inl(r, p);
         }
     return r;
+}
+template <class F>
+MI_NOINL XYZZ<F> xyzz_mul(const XYZZ<F> &p, const uint32_t *k, int nwords) {
+    return xyzz_mul_inl(p, k, nwords);
 }
 
 typedef Affine<fq_t> g1_affine_t;

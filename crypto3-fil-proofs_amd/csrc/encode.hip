@@ -7,6 +7,9 @@
 //     (0x40 = point at infinity).
 //   * scalars: Fr as 32-byte little-endian (core/fr32.hpp:36-52).
 // On device, coordinates are Montgomery 32-bit-limb little-endian; affine infinity is (0, 0).
+#include <stdio.h>
+#include <stdlib.h>
+
 #include "ctx.h"
 
 namespace mi {
@@ -17,26 +20,24 @@ __device__ __forceinline__ uint32_t be32(const uint8_t *p) {
     return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
 }
 
-// 48 big-endian bytes -> raw limbs; returns false when >= p
+// 48 big-endian bytes -> Montgomery Fq; returns false when the integer is >= p
 __device__ __forceinline__ bool fq_from_be48(const uint8_t *p, bool mask_flags, fq_t &out) {
+    fq32_t raw;
     MI_UNROLL for (int i = 0; i < 12; i++) {
         uint32_t w = be32(p + 4 * (11 - i));
         if (i == 11 && mask_flags) w &= 0x1fffffffu;
-        out.v[i] = w;
+        raw.v[i] = w;
     }
-    return !geq_raw(out, fq_t::modulus_raw());
+    out = fq_from_raw(raw);
+    return !geq_raw(raw, fq32_t::modulus_raw());
 }
 
 __device__ bool g1_on_curve(const g1_affine_t &a) {
-    fq_t four = fq_t::zero();
-    four.v[0] = 4;
-    four = to_mont(four);
+    fq_t four = fq_small(4);
     return sqr(a.y) == sqr(a.x) * a.x + four;
 }
 __device__ bool g2_on_curve(const g2_affine_t &a) {
-    fq_t four = fq_t::zero();
-    four.v[0] = 4;
-    four = to_mont(four);
+    fq_t four = fq_small(4);
     fq2_t b = {four, four};
     return sqr(a.y) == sqr(a.x) * a.x + b;
 }
@@ -52,8 +53,6 @@ __global__ void k_g1_decode(const uint8_t *__restrict__ in, g1_affine_t *__restr
     }
     g1_affine_t a;
     bool ok = fq_from_be48(p, true, a.x) & fq_from_be48(p + 48, false, a.y);
-    a.x = to_mont(a.x);
-    a.y = to_mont(a.y);
     if (!ok || !g1_on_curve(a)) atomicAdd(bad, 1);
     out[i] = a;
 }
@@ -70,8 +69,6 @@ __global__ void k_g2_decode(const uint8_t *__restrict__ in, g2_affine_t *__restr
     g2_affine_t a;
     bool ok = fq_from_be48(p, true, a.x.c1) & fq_from_be48(p + 48, false, a.x.c0) &
               fq_from_be48(p + 96, false, a.y.c1) & fq_from_be48(p + 144, false, a.y.c0);
-    a.x = to_mont(a.x);
-    a.y = to_mont(a.y);
     if (!ok || !g2_on_curve(a)) atomicAdd(bad, 1);
     out[i] = a;
 }
@@ -98,6 +95,14 @@ __global__ void k_fr_canon(fr_t *__restrict__ d, uint64_t n) {
 inline unsigned grid1(uint64_t n) { return (unsigned)((n + 255) / 256); }
 
 }  // namespace
+
+void debug_sync(Ctx &c, const char *what) {
+    static const bool on = getenv("MI_DEBUG_SYNC") && getenv("MI_DEBUG_SYNC")[0] == '1';
+    if (!on) return;
+    hipError_t e = hipStreamSynchronize(c.stream);
+    fprintf(stderr, "[mi] %s: %s\n", what, hipGetErrorString(e));
+    if (e != hipSuccess) throw hip_error(e, std::string("kernel ") + what + " failed: " + hipGetErrorString(e));
+}
 
 void g1_decode_uncompressed(Ctx &c, const uint8_t *dev_bytes, g1_affine_t *out, uint64_t n, int *bad_dev) {
     if (!n) return;

@@ -2,11 +2,15 @@
 //
 // Restates crypto3's multiprecision Montgomery backend ([NOT IN TREE]: libs/crypto/multiprecision,
 // used via algebra::curves::bls12<381>, core/crypto/scheme_params.hpp:39-43) for CDNA4:
-//   * limbs are 32-bit so every limb product is one v_mad_u64_u32 (32x32+64 -> 64) -- CDNA has no
-//     64x64->128 multiplier; the memory image is identical to 64-bit little-endian limbs,
-//   * "no-carry" CIOS: both moduli have a top 32-bit limb < 2^31 - 1, so the CIOS inner loops for
-//     the product and the reduction merge and the (N+1)th/(N+2)th words disappear,
-//   * everything is fully unrolled so elements live in VGPRs (Fq = 12, Fr = 8 registers).
+//   * Fq (the MSM hot loop) uses 14 limbs of 29 bits, Montgomery radix R = 2^406, product-scanning
+//     (FIPS) Montgomery multiplication: a column holds <= 28 products < 2^58, so every limb product
+//     is ONE v_mad_u64_u32 accumulating into a 64-bit register pair and carries move once per
+//     column -- 544 instructions per multiplication vs 1453 for 32-bit CIOS, measured 79 vs 39
+//     G Fq-mul/s on MI355X (microbench/fieldmul.hip).  Values are kept lazily in [0, 2p): the
+//     product of two such values is again < 2p because R > 4p, so there is no final subtraction.
+//   * Fr (NTT, scalars) uses 8 limbs of 32 bits with "no-carry" CIOS (top limb < 2^31 - 1); its
+//     memory image is the canonical 32-byte little-endian encoding.
+//   * everything is fully unrolled so elements live in VGPRs (Fq = 14, Fr = 8 registers).
 // The same code compiles for the host (final window combination, proof assembly).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -216,8 +220,199 @@ MI_HD bool geq_raw(const Fp<D> &a, const Fp<D> &b) {
     return true;
 }
 
-typedef Fp<FqDesc> fq_t;
+typedef Fp<FqDesc> fq32_t;  // canonical 12 x 32-bit container (wire format conversions only)
 typedef Fp<FrDesc> fr_t;
+
+// ---------------------------------------------------------------------------------------------
+// Fq: 14 x 29-bit limbs, Montgomery form with R = 2^406, values in [0, 2p)
+// ---------------------------------------------------------------------------------------------
+struct Fq29 {
+    static constexpr int L = 14;
+    static constexpr uint32_t M = (1u << 29) - 1;
+    static constexpr uint32_t INV = 0x1ffcfffdu;  // -p^-1 mod 2^29
+    static constexpr uint32_t P[14] = {0x1fffaaabu, 0x0ff7ffffu, 0x14ffffeeu, 0x17fffd62u, 0x0f6241eau,
+                                       0x09507b58u, 0x0afd9cc3u, 0x109e70a2u, 0x1764774bu, 0x121a5d66u,
+                                       0x12c6e9edu, 0x12ffcd34u, 0x00111ea3u, 0x0000000du};
+    static constexpr uint32_t P2[14] = {0x1fff5556u, 0x1fefffffu, 0x09ffffdcu, 0x0ffffac5u, 0x1ec483d5u,
+                                        0x12a0f6b0u, 0x15fb3986u, 0x013ce144u, 0x0ec8ee97u, 0x0434bacdu,
+                                        0x058dd3dbu, 0x05ff9a69u, 0x00223d47u, 0x0000001au};
+    static constexpr uint32_t ONE[14] = {0x03a9fb84u, 0x0ba00690u, 0x071288f1u, 0x0f59bcc5u, 0x126cb614u,
+                                         0x0585bf36u, 0x1b85ac3du, 0x1cf856fau, 0x1891ecbdu, 0x1a7eec05u,
+                                         0x155a88f0u, 0x0741ac6du, 0x1317c30fu, 0x00000009u};
+    static constexpr uint32_t R2[14] = {0x15bef7aeu, 0x1031cd0eu, 0x02dd93e8u, 0x09226323u, 0x0e6e2cd2u,
+                                        0x11684daau, 0x1170e5dbu, 0x088e25b1u, 0x1b366399u, 0x1c536f47u,
+                                        0x0d1f9cbcu, 0x0278b67fu, 0x1ea66a2bu, 0x0000000cu};
+    // p - 2 as 32-bit words (Fermat inversion exponent)
+    static constexpr uint32_t PM2[12] = {0xffffaaa9u, 0xb9feffffu, 0xb153ffffu, 0x1eabfffeu,
+                                         0xf6b0f624u, 0x6730d2a0u, 0xf38512bfu, 0x64774b84u,
+                                         0x434bacd7u, 0x4b1ba7b6u, 0x397fe69au, 0x1a0111eau};
+};
+
+struct alignas(8) fq_t {
+    static constexpr int L = 14;
+    uint32_t v[14];
+    MI_HD static fq_t zero() {
+        fq_t r;
+        MI_UNROLL for (int i = 0; i < L; i++) r.v[i] = 0;
+        return r;
+    }
+    MI_HD static fq_t one() {
+        fq_t r;
+        MI_UNROLL for (int i = 0; i < L; i++) r.v[i] = Fq29::ONE[i];
+        return r;
+    }
+    // value == 0 mod p (representatives 0 and p)
+    MI_HD bool is_zero() const {
+        uint32_t z = 0, q = 0;
+        MI_UNROLL for (int i = 0; i < L; i++) {
+            z |= v[i];
+            q |= v[i] ^ Fq29::P[i];
+        }
+        return z == 0 || q == 0;
+    }
+    MI_HD bool operator==(const fq_t &o) const;
+    MI_HD bool operator!=(const fq_t &o) const { return !(*this == o); }
+};
+
+// s - 2p if s >= 2p else s;  s normalised, s < 4p
+MI_HD fq_t fq_sub_2p_if_ge(const uint32_t *s) {
+    fq_t d;
+    int32_t bw = 0;
+    MI_UNROLL for (int i = 0; i < 13; i++) {
+        int32_t t = (int32_t)s[i] - (int32_t)Fq29::P2[i] + bw;
+        d.v[i] = (uint32_t)t & Fq29::M;
+        bw = t >> 29;
+    }
+    int32_t top = (int32_t)s[13] - (int32_t)Fq29::P2[13] + bw;
+    d.v[13] = (uint32_t)top;
+    if (top < 0) {
+        MI_UNROLL for (int i = 0; i < 14; i++) d.v[i] = s[i];
+    }
+    return d;
+}
+
+MI_HD fq_t operator+(const fq_t &a, const fq_t &b) {
+    uint32_t s[14];
+    uint32_t c = 0;
+    MI_UNROLL for (int i = 0; i < 13; i++) {
+        uint32_t t = a.v[i] + b.v[i] + c;
+        s[i] = t & Fq29::M;
+        c = t >> 29;
+    }
+    s[13] = a.v[13] + b.v[13] + c;
+    return fq_sub_2p_if_ge(s);
+}
+
+MI_HD fq_t operator-(const fq_t &a, const fq_t &b) {  // a - b + 2p, then reduce below 2p
+    uint32_t s[14];
+    int32_t c = 0;
+    MI_UNROLL for (int i = 0; i < 13; i++) {
+        int32_t t = (int32_t)a.v[i] - (int32_t)b.v[i] + (int32_t)Fq29::P2[i] + c;
+        s[i] = (uint32_t)t & Fq29::M;
+        c = t >> 29;
+    }
+    s[13] = (uint32_t)((int32_t)a.v[13] - (int32_t)b.v[13] + (int32_t)Fq29::P2[13] + c);
+    return fq_sub_2p_if_ge(s);
+}
+
+MI_HD fq_t operator-(const fq_t &a) { return fq_t::zero() - a; }
+MI_HD fq_t dbl(const fq_t &a) { return a + a; }
+
+// canonical representative in [0, p)
+MI_HD fq_t fq_canon(const fq_t &a) {
+    fq_t d;
+    int32_t bw = 0;
+    MI_UNROLL for (int i = 0; i < 13; i++) {
+        int32_t t = (int32_t)a.v[i] - (int32_t)Fq29::P[i] + bw;
+        d.v[i] = (uint32_t)t & Fq29::M;
+        bw = t >> 29;
+    }
+    int32_t top = (int32_t)a.v[13] - (int32_t)Fq29::P[13] + bw;
+    d.v[13] = (uint32_t)top;
+    return top < 0 ? a : d;
+}
+
+MI_HD bool fq_t::operator==(const fq_t &o) const {
+    fq_t a = fq_canon(*this), b = fq_canon(o);
+    uint32_t x = 0;
+    MI_UNROLL for (int i = 0; i < L; i++) x |= a.v[i] ^ b.v[i];
+    return x == 0;
+}
+
+// Product-scanning Montgomery multiplication, a, b < 2p -> a b R^-1 mod p in [0, 2p).
+MI_HD fq_t operator*(const fq_t &a, const fq_t &b) {
+    constexpr int L = 14;
+    uint32_t m[L];
+    fq_t r;
+    uint64_t acc = 0;
+    MI_UNROLL for (int k = 0; k < L; k++) {
+        MI_UNROLL for (int i = 0; i < k; i++) {
+            acc += (uint64_t)a.v[i] * b.v[k - i];
+            acc += (uint64_t)m[i] * Fq29::P[k - i];
+        }
+        acc += (uint64_t)a.v[k] * b.v[0];
+        m[k] = ((uint32_t)acc * Fq29::INV) & Fq29::M;
+        acc += (uint64_t)m[k] * Fq29::P[0];
+        acc >>= 29;
+    }
+    MI_UNROLL for (int k = L; k < 2 * L - 1; k++) {
+        MI_UNROLL for (int i = k - L + 1; i < L; i++) {
+            acc += (uint64_t)a.v[i] * b.v[k - i];
+            acc += (uint64_t)m[i] * Fq29::P[k - i];
+        }
+        r.v[k - L] = (uint32_t)acc & Fq29::M;
+        acc >>= 29;
+    }
+    r.v[L - 1] = (uint32_t)acc;
+    return r;
+}
+MI_HD fq_t sqr(const fq_t &a) { return a * a; }
+
+// canonical 12 x 32-bit integer (< p) -> Montgomery
+MI_HD fq_t fq_from_raw(const fq32_t &raw) {
+    fq_t t;
+    MI_UNROLL for (int i = 0; i < 14; i++) {
+        const int bit = 29 * i, w = bit >> 5, s = bit & 31;
+        uint64_t x = raw.v[w];
+        if (w + 1 < 12) x |= (uint64_t)raw.v[w + 1] << 32;
+        t.v[i] = (uint32_t)(x >> s) & Fq29::M;
+    }
+    fq_t r2;
+    MI_UNROLL for (int i = 0; i < 14; i++) r2.v[i] = Fq29::R2[i];
+    return t * r2;
+}
+// Montgomery -> canonical 12 x 32-bit integer (< p)
+MI_HD fq32_t fq_to_raw(const fq_t &a) {
+    fq_t one = fq_t::zero();
+    one.v[0] = 1;
+    fq_t c = fq_canon(a * one);
+    fq32_t r = fq32_t::zero();
+    MI_UNROLL for (int i = 0; i < 14; i++) {
+        const int bit = 29 * i, w = bit >> 5, s = bit & 31;
+        r.v[w] |= c.v[i] << s;
+        if (s > 3 && w + 1 < 12) r.v[w + 1] |= c.v[i] >> (32 - s);
+    }
+    return r;
+}
+MI_HD fq_t fq_small(uint32_t v) {
+    fq32_t r = fq32_t::zero();
+    r.v[0] = v;
+    return fq_from_raw(r);
+}
+// Fermat inversion a^(p-2).  *_inl versions are for device kernels (no device-side calls: large
+// noinline functions with big by-value structs miscompile / overflow the stack on gfx950).
+MI_HD fq_t inverse_inl(const fq_t &a) {
+    fq_t r = fq_t::one();
+#pragma unroll 1
+    for (int i = 11; i >= 0; i--)
+#pragma unroll 1
+        for (int b = 31; b >= 0; b--) {
+            r = sqr(r);
+            if ((Fq29::PM2[i] >> b) & 1) r = r * a;
+        }
+    return r;
+}
+MI_NOINL fq_t inverse(const fq_t &a) { return inverse_inl(a); }
 
 // ---------------------------------------------------------------------------------------------
 // Fq2 = Fq[u]/(u^2 + 1)  (G2 coordinates)
@@ -234,20 +429,19 @@ MI_HD fq2_t operator+(const fq2_t &a, const fq2_t &b) { return {a.c0 + b.c0, a.c
 MI_HD fq2_t operator-(const fq2_t &a, const fq2_t &b) { return {a.c0 - b.c0, a.c1 - b.c1}; }
 MI_HD fq2_t operator-(const fq2_t &a) { return {-a.c0, -a.c1}; }
 MI_HD fq2_t dbl(const fq2_t &a) { return a + a; }
-MI_NOINL fq2_t operator*(const fq2_t &a, const fq2_t &b) {  // Karatsuba, 3 Fq mults
+MI_HD fq2_t operator*(const fq2_t &a, const fq2_t &b) {  // Karatsuba, 3 Fq mults
     fq_t v0 = a.c0 * b.c0, v1 = a.c1 * b.c1;
     fq_t t = (a.c0 + a.c1) * (b.c0 + b.c1);
     return {v0 - v1, t - v0 - v1};
 }
-MI_NOINL fq2_t sqr(const fq2_t &a) {  // (a0 + a1)(a0 - a1), 2 a0 a1: 2 Fq mults
+MI_HD fq2_t sqr(const fq2_t &a) {  // (a0 + a1)(a0 - a1), 2 a0 a1: 2 Fq mults
     fq_t t = a.c0 * a.c1;
     return {(a.c0 + a.c1) * (a.c0 - a.c1), t + t};
 }
-MI_NOINL fq2_t inverse(const fq2_t &a) {
-    fq_t n = inverse(sqr(a.c0) + sqr(a.c1));
+MI_HD fq2_t inverse_inl(const fq2_t &a) {
+    fq_t n = inverse_inl(sqr(a.c0) + sqr(a.c1));
     return {a.c0 * n, -(a.c1 * n)};
 }
-MI_HD fq2_t to_mont(const fq2_t &a) { return {to_mont(a.c0), to_mont(a.c1)}; }
-MI_HD fq2_t from_mont(const fq2_t &a) { return {from_mont(a.c0), from_mont(a.c1)}; }
+MI_NOINL fq2_t inverse(const fq2_t &a) { return inverse_inl(a); }
 
 }  // namespace mi

@@ -1,4 +1,4 @@
-// msm.hip -- Pippenger multi-scalar multiplication on BLS12-381 G1 / G2 for CDNA4 (gfx950).
+// msm_impl.h -- Pippenger multi-scalar multiplication on BLS12-381 G1 / G2 for CDNA4 (gfx950).
 //
 // Restates crypto3's multiexp ([NOT IN TREE]: libs/crypto/algebra, used by r1cs_gg_ppzksnark's
 // prover for the H, L, A, B_G1 (G1) and B_G2 (G2) queries -- SURVEY.md §8a rows a7/a8).
@@ -14,10 +14,11 @@
 //                     every bucket is one point.  Work per thread is bounded by L whatever the
 //                     scalar distribution (boolean-heavy Filecoin witnesses put most entries in
 //                     bucket 1 of window 0).
-//   5. k_bucket_reduce: running-sum reduction sum_b (b+1) B_b over segments of buckets, each
-//                     segment's offset folded in with a small double-and-add.
-//   6. k_window_sum : per-window sum of segment results (LDS tree).
+//   5. k_bucket_reduce: running-sum reduction sum_b (b+1) B_b over ~2^19 segments of buckets;
+//      k_seg_fold adds each segment's offset (s * seg_len) * run with a short double-and-add.
+//   6. k_sum_groups : per-window tree sum of the segment results.
 //   7. host         : Horner over windows (c doublings each) on the CPU.
+#pragma once
 #include <hipcub/hipcub.hpp>
 
 #include "ctx.h"
@@ -120,7 +121,7 @@ __global__ void __launch_bounds__(256) k_accum_level0(const uint32_t *__restrict
         uint32_t v = vals[p];
         Affine<F> a = bases[v & 0x7fffffffu];
         if (v >> 31) a.y = -a.y;
-        acc = xyzz_add_affine(acc, a);
+        acc = xyzz_add_affine_inl(acc, a);
     }
     out[t] = acc;
 }
@@ -140,88 +141,71 @@ __global__ void __launch_bounds__(256) k_accum_level(const uint32_t *__restrict_
     uint32_t lim = local * L1 + L1 < cnt[b] ? local * L1 + L1 : cnt[b];
     uint32_t end = off[b] + lim;
     XYZZ<F> acc = in[beg];
-    for (uint32_t p = beg + 1; p < end; p++) acc = xyzz_add(acc, in[p]);
+    for (uint32_t p = beg + 1; p < end; p++) acc = xyzz_add_inl(acc, in[p]);
     out[t] = acc;
 }
 
-template <class F>
-MI_HD XYZZ<F> mul_small(const XYZZ<F> &p, uint32_t k) {
-    XYZZ<F> r = XYZZ<F>::inf();
-    for (int b = 31; b >= 0; b--) {
-        r = xyzz_dbl(r);
-        if ((k >> b) & 1) r = xyzz_add(r, p);
-    }
-    return r;
-}
-
+// Running-sum reduction over one segment of seg_len buckets (all group-law code inlined):
+//   seg_run = sum_j B_j,  seg_acc = sum_j (j + 1) B_j   (j = bucket index inside the segment)
 template <class F>
 __global__ void __launch_bounds__(256) k_bucket_reduce(const uint32_t *__restrict__ off,
                                                        const uint32_t *__restrict__ cnt,
-                                                       const XYZZ<F> *__restrict__ P, unsigned nwin,
-                                                       unsigned nbk, unsigned seg_len,
-                                                       XYZZ<F> *__restrict__ segsum) {
+                                                       const XYZZ<F> *__restrict__ P, uint32_t nseg_total,
+                                                       unsigned seg_len, XYZZ<F> *__restrict__ seg_acc,
+                                                       XYZZ<F> *__restrict__ seg_run) {
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t nseg = nbk / seg_len;
-    if (t >= nwin * nseg) return;
-    uint32_t w = t / nseg, s = t % nseg;
-    uint32_t b0 = w * nbk + s * seg_len;
+    if (t >= nseg_total) return;
+    uint32_t b0 = t * seg_len;  // buckets of one window are contiguous and nbk % seg_len == 0
     XYZZ<F> run = XYZZ<F>::inf(), acc = XYZZ<F>::inf();
     for (int j = (int)seg_len - 1; j >= 0; j--) {
         uint32_t b = b0 + j;
-        if (cnt[b]) run = xyzz_add(run, P[off[b]]);
-        acc = xyzz_add(acc, run);
+        if (cnt[b]) run = xyzz_add_inl(run, P[off[b]]);
+        acc = xyzz_add_inl(acc, run);
     }
-    uint32_t k = s * seg_len;
+    seg_acc[t] = acc;
+    seg_run[t] = run;
+}
+
+// out[t] = seg_acc[t] + (s * seg_len) * seg_run[t], s = segment index inside its window
+template <class F>
+__global__ void __launch_bounds__(256) k_seg_fold(const XYZZ<F> *__restrict__ seg_acc,
+                                                  const XYZZ<F> *__restrict__ seg_run, uint32_t nseg_total,
+                                                  uint32_t nseg, unsigned seg_len, XYZZ<F> *__restrict__ out) {
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nseg_total) return;
+    XYZZ<F> acc = seg_acc[t];
+    uint32_t k = (t % nseg) * seg_len;
+    XYZZ<F> run = seg_run[t];
     if (k && !run.is_inf()) {
-        // add k * run with a left-to-right double-and-add starting at k's top bit
+        // k * run, left-to-right double-and-add, group law inlined (no device calls)
         XYZZ<F> m = run;
         int top = 31 - __builtin_clz(k);
         for (int bit = top - 1; bit >= 0; bit--) {
-            m = xyzz_dbl(m);
-            if ((k >> bit) & 1) m = xyzz_add(m, run);
+            m = xyzz_dbl_inl(m);
+            if ((k >> bit) & 1) m = xyzz_add_inl(m, run);
         }
-        acc = xyzz_add(acc, m);
+        acc = xyzz_add_inl(acc, m);
     }
-    segsum[t] = acc;
+    out[t] = acc;
 }
 
-template <class F, int T>
-__global__ void __launch_bounds__(T) k_window_sum(const XYZZ<F> *__restrict__ segsum, unsigned nseg,
-                                                  XYZZ<F> *__restrict__ out) {
-    __shared__ XYZZ<F> sh[T];
-    unsigned w = blockIdx.x;
-    XYZZ<F> acc = XYZZ<F>::inf();
-    for (unsigned s = threadIdx.x; s < nseg; s += T) acc = xyzz_add(acc, segsum[(uint64_t)w * nseg + s]);
-    sh[threadIdx.x] = acc;
-    __syncthreads();
-    for (unsigned half = T / 2; half > 0; half >>= 1) {
-        if (threadIdx.x < half) sh[threadIdx.x] = xyzz_add(sh[threadIdx.x], sh[threadIdx.x + half]);
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) out[w] = sh[0];
+// out[w * (n / G) + g] = sum of in[w * n + g * G ... + G)   (n % G == 0)
+template <class F>
+__global__ void __launch_bounds__(256) k_sum_groups(const XYZZ<F> *__restrict__ in, uint32_t total_out,
+                                                    unsigned G, XYZZ<F> *__restrict__ out) {
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= total_out) return;
+    XYZZ<F> acc = in[(uint64_t)t * G];
+    for (unsigned i = 1; i < G; i++) acc = xyzz_add_inl(acc, in[(uint64_t)t * G + i]);
+    out[t] = acc;
 }
 
 inline unsigned grid_for(uint64_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
 
 }  // namespace
 
-unsigned msm_window_bits(uint64_t n) {
-    // minimise (mixed adds) + 1.4 x (bucket-reduction full adds) over c
-    unsigned best = 4;
-    double best_cost = 1e300;
-    for (unsigned c = 4; c <= 22; c++) {
-        unsigned nwin = (256 + c - 1) / c;
-        double cost = (double)n * nwin + 1.4 * 2.0 * nwin * (double)(1u << (c - 1)) + 64.0 * nwin * c;
-        if (cost < best_cost) {
-            best_cost = cost;
-            best = c;
-        }
-    }
-    return best;
-}
-
 template <class F>
-static void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,
+void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,
                     XYZZ<F> *result) {
     if (n == 0) {
         *result = XYZZ<F>::inf();
@@ -253,6 +237,7 @@ static void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const u
     {
         ScopedTimer tsort(c, &c.stats.sort, n);
         k_digits<<<grid_for(n, 256), 256, 0, st>>>(scalars, idx, (uint32_t)n, cb, nwin, invalid, keys, vals);
+        MI_LAUNCHED(c, "k_digits");
         MI_HIP(hipGetLastError());
         size_t tmp_bytes = 0;
         MI_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys, keys_s, vals, vals_s, np, 0, key_bits,
@@ -262,7 +247,9 @@ static void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const u
         MI_HIP(hipMemsetAsync(offA, 0, sizeof(uint32_t) * nb, st));
         MI_HIP(hipMemsetAsync(cntA, 0, sizeof(uint32_t) * nb, st));
         k_bounds<<<grid_for(np, 256), 256, 0, st>>>(keys_s, np, invalid, offA, cntA);
+        MI_LAUNCHED(c, "k_bounds");
         k_end_to_cnt<<<grid_for(nb, 256), 256, 0, st>>>(offA, cntA, nb);
+        MI_LAUNCHED(c, "k_end_to_cnt");
         MI_HIP(hipGetLastError());
     }
 
@@ -285,6 +272,7 @@ static void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const u
         while (level0 || maxcnt > 1) {
             uint32_t L = level0 ? L0 : L1;
             k_chunk_count<<<grid_for(nb, 256), 256, 0, st>>>(cnt, nb, L, ccnt);
+            MI_LAUNCHED(c, "k_chunk_count");
             size_t tmp_bytes = 0;
             MI_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, ccnt, coff, nb, st));
             void *tmp = c.scratch[4].get(tmp_bytes);
@@ -302,6 +290,7 @@ static void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const u
             uint32_t *chunk_bucket = c.scratch[13].as<uint32_t>(total + 1);
             MI_HIP(hipMemsetAsync(heads, 0, sizeof(uint32_t) * (total + 1), st));
             k_chunk_heads<<<grid_for(nb, 256), 256, 0, st>>>(ccnt, coff, nb, heads);
+            MI_LAUNCHED(c, "k_chunk_heads");
             tmp_bytes = 0;
             MI_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tmp_bytes, heads, chunk_bucket, MaxOp(), total, st));
             tmp = c.scratch[4].get(tmp_bytes);
@@ -311,10 +300,12 @@ static void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const u
                 ScopedTimer tacc(c, sizeof(F) == sizeof(fq_t) ? &c.stats.accum_g1 : &c.stats.accum_g2, n);
                 k_accum_level0<F><<<grid_for(total, 256), 256, 0, st>>>(chunk_bucket, coff, off, cnt, total, vals_s,
                                                                          bases, Pnext);
+                MI_LAUNCHED(c, "k_accum_level0");
                 maxcnt = (maxcnt + L0 - 1) / L0;
             } else {
                 k_accum_level<F><<<grid_for(total, 256), 256, 0, st>>>(chunk_bucket, coff, off, cnt, total, Pcur,
                                                                         Pnext);
+                MI_LAUNCHED(c, "k_accum_level");
                 maxcnt = (maxcnt + L1 - 1) / L1;
             }
             MI_HIP(hipGetLastError());
@@ -326,16 +317,32 @@ static void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const u
         }
     }
 
-    // bucket reduction
+    // bucket reduction: ~2^19 threads of seg_len buckets each, then fold offsets, then tree-sum
     unsigned seg_len = 1;
-    while (seg_len < nbk && (uint64_t)nwin * (nbk / (seg_len * 2)) >= 16384) seg_len *= 2;
-    uint32_t nseg = nbk / seg_len;
-    XYZZ<F> *segsum = c.scratch[12].as<XYZZ<F>>((uint64_t)nwin * nseg);
-    k_bucket_reduce<F><<<grid_for((uint64_t)nwin * nseg, 256), 256, 0, st>>>(off, cnt, Pcur, nwin, nbk, seg_len,
-                                                                           segsum);
-    XYZZ<F> *wsum = c.scratch[14].as<XYZZ<F>>(nwin);
-    k_window_sum<F, 64><<<nwin, 64, 0, st>>>(segsum, nseg, wsum);
+    while (seg_len < nbk && (uint64_t)nb / (seg_len * 2) >= (1u << 19)) seg_len *= 2;
+    const uint32_t nseg = nbk / seg_len, nseg_total = nwin * nseg;
+    XYZZ<F> *seg_acc = c.scratch[12].as<XYZZ<F>>(2 * (uint64_t)nseg_total);
+    XYZZ<F> *seg_run = seg_acc + nseg_total;
+    k_bucket_reduce<F><<<grid_for(nseg_total, 256), 256, 0, st>>>(off, cnt, Pcur, nseg_total, seg_len, seg_acc,
+                                                                 seg_run);
+    MI_LAUNCHED(c, "k_bucket_reduce");
+    XYZZ<F> *folded = c.scratch[14].as<XYZZ<F>>(nseg_total);
+    k_seg_fold<F><<<grid_for(nseg_total, 256), 256, 0, st>>>(seg_acc, seg_run, nseg_total, nseg, seg_len, folded);
+    MI_LAUNCHED(c, "k_seg_fold");
     MI_HIP(hipGetLastError());
+    // per-window tree sum of nseg (a power of two) entries, groups of <= 32
+    XYZZ<F> *cur = folded, *nxt = seg_acc;
+    uint32_t per = nseg;
+    while (per > 1) {
+        unsigned G = per >= 32 ? 32 : per;
+        uint32_t outs = nwin * (per / G);
+        k_sum_groups<F><<<grid_for(outs, 256), 256, 0, st>>>(cur, outs, G, nxt);
+        MI_LAUNCHED(c, "k_sum_groups");
+        MI_HIP(hipGetLastError());
+        per /= G;
+        std::swap(cur, nxt);
+    }
+    XYZZ<F> *wsum = cur;
     std::vector<XYZZ<F>> W(nwin);
     MI_HIP(hipMemcpyAsync(W.data(), wsum, sizeof(XYZZ<F>) * nwin, hipMemcpyDeviceToHost, st));
     MI_HIP(hipStreamSynchronize(st));
@@ -348,13 +355,5 @@ static void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const u
     c.timer.resolve();
 }
 
-void msm_g1(Ctx &c, const g1_affine_t *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,
-            g1_xyzz_t *result_host) {
-    msm_run<fq_t>(c, bases, scalars, idx, n, result_host);
-}
-void msm_g2(Ctx &c, const g2_affine_t *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,
-            g2_xyzz_t *result_host) {
-    msm_run<fq2_t>(c, bases, scalars, idx, n, result_host);
-}
 
 }  // namespace mi

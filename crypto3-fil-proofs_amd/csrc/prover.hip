@@ -118,6 +118,23 @@ __global__ void k_col_sums(const uint32_t *__restrict__ start, const uint32_t *_
     }
     out[v] = acc;
 }
+// prod[p] = coeff[perm[p]] * lag[rows[perm[p]]]   (entries in column-sorted order)
+__global__ void k_entry_products(const uint32_t *__restrict__ perm, const uint32_t *__restrict__ rows,
+                                 const fr_t *__restrict__ coeff, const fr_t *__restrict__ lag, uint64_t nnz,
+                                 fr_t *__restrict__ prod) {
+    uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= nnz) return;
+    uint32_t e = perm[p];
+    prod[p] = coeff[e] * lag[rows[e]];
+}
+__global__ void k_scatter_runs(const uint32_t *__restrict__ keys, const fr_t *__restrict__ vals,
+                               const uint32_t *__restrict__ nruns, fr_t *__restrict__ out) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < *nruns) out[keys[i]] = vals[i];
+}
+struct FrAdd {
+    MI_HD fr_t operator()(const fr_t &a, const fr_t &b) const { return a + b; }
+};
 __global__ void k_add_input_rows(fr_t *__restrict__ at, const fr_t *__restrict__ lag, uint64_t n, uint64_t n_in) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n_in) at[i] = at[i] + lag[n + i];
@@ -153,8 +170,8 @@ __global__ void k_fb_table(Affine<F> G, Affine<F> *__restrict__ table) {
     unsigned bit = 8 * j;
     k[bit / 32] |= m << (bit % 32);
     if (bit % 32 > 24 && bit / 32 + 1 < 9) k[bit / 32 + 1] |= m >> (32 - bit % 32);
-    XYZZ<F> p = xyzz_mul(xyzz_from_affine(G), k, 8);
-    table[t] = xyzz_to_affine(p);
+    XYZZ<F> p = xyzz_mul_inl(xyzz_from_affine(G), k, 8);
+    table[t] = xyzz_to_affine_inl(p);
 }
 
 template <class F>
@@ -167,7 +184,7 @@ __global__ void __launch_bounds__(256) k_fixed_base(const fr_t *__restrict__ k, 
 #pragma unroll 1
     for (unsigned j = 0; j < 32; j++) {
         uint32_t m = byte_of<F>(s, j);
-        if (m) acc = xyzz_add_affine(acc, table[j * 255 + m - 1]);
+        if (m) acc = xyzz_add_affine_inl(acc, table[j * 255 + m - 1]);
     }
     out[i] = acc;
 }
@@ -186,7 +203,7 @@ __global__ void __launch_bounds__(256) k_batch_affine(const XYZZ<F> *__restrict_
         XYZZ<F> p = in[i];
         if (!p.is_inf()) prod = prod * p.ZZZ;
     }
-    F inv = inverse(prod);
+    F inv = inverse_inl(prod);
     for (uint64_t i = end; i-- > beg;) {
         XYZZ<F> p = in[i];
         if (p.is_inf()) {
@@ -218,7 +235,7 @@ __global__ void k_dot(const fr_t *__restrict__ z, const fr_t *__restrict__ e, ui
 
 // ------------------------------------------------------------------------------ host helpers
 void fq_to_be48(const fq_t &mont, uint8_t *out) {
-    fq_t raw = from_mont(mont);
+    fq32_t raw = fq_to_raw(mont);
     for (int i = 0; i < 12; i++) {
         uint32_t w = raw.v[i];
         uint8_t *p = out + 4 * (11 - i);
@@ -229,19 +246,19 @@ void fq_to_be48(const fq_t &mont, uint8_t *out) {
     }
 }
 bool fq_from_be48_host(const uint8_t *p, bool mask, fq_t &out) {
-    fq_t raw;
+    fq32_t raw;
     for (int i = 0; i < 12; i++) {
         const uint8_t *q = p + 4 * (11 - i);
         uint32_t w = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
         if (i == 11 && mask) w &= 0x1fffffffu;
         raw.v[i] = w;
     }
-    if (geq_raw(raw, fq_t::modulus_raw())) return false;
-    out = to_mont(raw);
+    if (geq_raw(raw, fq32_t::modulus_raw())) return false;
+    out = fq_from_raw(raw);
     return true;
 }
 bool fq_lex_largest(const fq_t &y) {
-    fq_t a = from_mont(y), b = from_mont(-y);
+    fq32_t a = fq_to_raw(y), b = fq_to_raw(-y);
     for (int i = 11; i >= 0; i--)
         if (a.v[i] != b.v[i]) return a.v[i] > b.v[i];
     return false;
@@ -591,8 +608,6 @@ Srs *srs_generate(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5]) {
             uint32_t *perm_in = c.scratch[1].as<uint32_t>(nnz);
             uint32_t *cols_s = c.scratch[2].as<uint32_t>(nnz);
             uint32_t *perm = c.scratch[3].as<uint32_t>(nnz);
-            uint32_t *cstart = c.scratch[5].as<uint32_t>(nv);
-            uint32_t *cend = c.scratch[6].as<uint32_t>(nv);
             k_entry_rows<<<grid1(n), 256, 0, st>>>(circ.row_ptr[m], n, rows);
             k_iota<<<grid1(nnz), 256, 0, st>>>(perm_in, nnz);
             unsigned bits = 1;
@@ -602,10 +617,18 @@ Srs *srs_generate(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5]) {
                                                       st));
             void *tmp = c.scratch[4].get(tb);
             MI_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tb, circ.col[m], cols_s, perm_in, perm, nnz, 0, bits, st));
-            MI_HIP(hipMemsetAsync(cstart, 0, 4 * nv, st));
-            MI_HIP(hipMemsetAsync(cend, 0, 4 * nv, st));
-            k_col_bounds<<<grid1(nnz), 256, 0, st>>>(cols_s, nnz, cstart, cend);
-            k_col_sums<<<grid1(nv), 256, 0, st>>>(cstart, cend, perm, rows, circ.coeff[m], lag, nv, outs[m]);
+            // column sums by reduce-by-key over the column-sorted products: load-balanced whatever
+            // the column lengths (ONE appears in ~half the rows of B)
+            fr_t *prod = c.scratch[13].as<fr_t>(nnz);
+            k_entry_products<<<grid1(nnz), 256, 0, st>>>(perm, rows, circ.coeff[m], lag, nnz, prod);
+            uint32_t *ukeys = c.scratch[5].as<uint32_t>(nnz);
+            fr_t *uvals = c.scratch[14].as<fr_t>(nnz);
+            uint32_t *nruns = c.scratch[6].as<uint32_t>(4);
+            tb = 0;
+            MI_HIP(hipcub::DeviceReduce::ReduceByKey(nullptr, tb, cols_s, ukeys, prod, uvals, nruns, FrAdd(), nnz, st));
+            tmp = c.scratch[4].get(tb);
+            MI_HIP(hipcub::DeviceReduce::ReduceByKey(tmp, tb, cols_s, ukeys, prod, uvals, nruns, FrAdd(), nnz, st));
+            k_scatter_runs<<<grid1(nnz), 256, 0, st>>>(ukeys, uvals, nruns, outs[m]);
             MI_HIP(hipGetLastError());
         }
         k_add_input_rows<<<grid1(circ.n_in), 256, 0, st>>>(S->at, lag, n, circ.n_in);

@@ -1,0 +1,284 @@
+// fieldmul.hip -- microbenchmark: instruction throughput and Montgomery-multiplication variants
+// for the 381-bit BLS12-381 base field on gfx950.  Standalone executable (not part of the library).
+//
+//   raw   : v_mad_u64_u32 and v_add_co/v_addc_co throughput (inline asm, independent chains)
+//   v0    : mi::operator* -- 32-bit limbs, no-carry CIOS as the compiler emits it (library today)
+//   v1    : 32-bit limbs, product scanning (FIPS), v_mad_u64_u32 accumulating into a 64-bit column
+//           register with its hardware carry-out counted by v_addc (inline asm)
+//   v2    : 29-bit limbs (14), product scanning; column sums of <= 28 products < 2^58 fit in 64 bits,
+//           so each limb product is ONE v_mad_u64_u32 and carries are propagated once per column
+// Correctness: v1, v2 results (converted back to canonical) are compared with v0 on random inputs.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "../csrc/field.h"
+
+using namespace mi;
+
+#define CHECK(x)                                                                       \
+    do {                                                                               \
+        hipError_t e = (x);                                                            \
+        if (e != hipSuccess) {                                                         \
+            fprintf(stderr, "%s: %s line %d\n", #x, hipGetErrorString(e), __LINE__); \
+            exit(1);                                                                   \
+        }                                                                              \
+    } while (0)
+
+// ------------------------------------------------------------------------------ raw throughput
+__global__ void k_raw_mad(uint32_t *out, int iters) {
+    uint32_t a = threadIdx.x + 1, b = blockIdx.x + 3;
+    uint64_t acc[8];
+    for (int i = 0; i < 8; i++) acc[i] = i * 77 + threadIdx.x;
+    for (int it = 0; it < iters; it++) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc[i]) : "v"(a), "v"(b) : "vcc");
+    }
+    uint64_t s = 0;
+    for (int i = 0; i < 8; i++) s ^= acc[i];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)s ^ (uint32_t)(s >> 32);
+}
+__global__ void k_raw_add(uint32_t *out, int iters) {
+    uint32_t a = threadIdx.x + 1;
+    uint32_t x[8];
+    for (int i = 0; i < 8; i++) x[i] = i * 77 + threadIdx.x;
+    for (int it = 0; it < iters; it++) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) asm volatile("v_add_u32 %0, %0, %1" : "+v"(x[i]) : "v"(a));
+    }
+    uint32_t s = 0;
+    for (int i = 0; i < 8; i++) s ^= x[i];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+__global__ void k_raw_mullo(uint32_t *out, int iters) {
+    uint32_t a = threadIdx.x + 1;
+    uint32_t x[8];
+    for (int i = 0; i < 8; i++) x[i] = i * 77 + threadIdx.x;
+    for (int it = 0; it < iters; it++) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(x[i]) : "v"(a));
+    }
+    uint32_t s = 0;
+    for (int i = 0; i < 8; i++) s ^= x[i];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+// ------------------------------------------------------------------------------ v1: FIPS 32-bit
+struct Acc96 {
+    uint64_t lo;  // c1:c0
+    uint32_t c2;
+};
+__device__ __forceinline__ void mac(Acc96 &a, uint32_t x, uint32_t y) {
+    asm volatile(
+        "v_mad_u64_u32 %0, vcc, %2, %3, %0\n\t"
+        "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+        : "+v"(a.lo), "+v"(a.c2)
+        : "v"(x), "v"(y)
+        : "vcc");
+}
+__device__ __forceinline__ fq_t mul_v1(const fq_t &a, const fq_t &b) {
+    constexpr int N = 12;
+    uint32_t m[N], t[N];
+    Acc96 acc = {0, 0};
+    MI_UNROLL for (int k = 0; k < N; k++) {
+        MI_UNROLL for (int i = 0; i < k; i++) {
+            mac(acc, a.v[i], b.v[k - i]);
+            mac(acc, m[i], FqDesc::MOD[k - i]);
+        }
+        mac(acc, a.v[k], b.v[0]);
+        m[k] = (uint32_t)acc.lo * FqDesc::INV;
+        mac(acc, m[k], FqDesc::MOD[0]);
+        acc.lo = (acc.lo >> 32) | ((uint64_t)acc.c2 << 32);
+        acc.c2 = 0;
+    }
+    MI_UNROLL for (int k = N; k < 2 * N - 1; k++) {
+        MI_UNROLL for (int i = k - N + 1; i < N; i++) {
+            mac(acc, a.v[i], b.v[k - i]);
+            mac(acc, m[i], FqDesc::MOD[k - i]);
+        }
+        t[k - N] = (uint32_t)acc.lo;
+        acc.lo = (acc.lo >> 32) | ((uint64_t)acc.c2 << 32);
+        acc.c2 = 0;
+    }
+    t[N - 1] = (uint32_t)acc.lo;
+    fq_t r;
+    MI_UNROLL for (int i = 0; i < N; i++) r.v[i] = t[i];
+    return reduce_once(r);
+}
+
+// ------------------------------------------------------------------------------ v2: 29-bit limbs
+constexpr int L29 = 14;
+constexpr uint32_t M29 = (1u << 29) - 1;
+constexpr uint32_t P29[L29] = {0x1fffaaabu, 0x0ff7ffffu, 0x14ffffeeu, 0x17fffd62u, 0x0f6241eau, 0x09507b58u, 0x0afd9cc3u,
+                               0x109e70a2u, 0x1764774bu, 0x121a5d66u, 0x12c6e9edu, 0x12ffcd34u, 0x00111ea3u, 0x0000000du};
+constexpr uint32_t R2_29[L29] = {0x15bef7aeu, 0x1031cd0eu, 0x02dd93e8u, 0x09226323u, 0x0e6e2cd2u,
+                                 0x11684daau, 0x1170e5dbu, 0x088e25b1u, 0x1b366399u, 0x1c536f47u,
+                                 0x0d1f9cbcu, 0x0278b67fu, 0x1ea66a2bu, 0x0000000cu};
+constexpr uint32_t INV29 = 0x1ffcfffdu;
+struct fq29 {
+    uint32_t v[L29];
+};
+// result < 2p for inputs < 2p (R = 2^406 >> 4p): no final subtraction
+__device__ __forceinline__ fq29 mul_v2(const fq29 &a, const fq29 &b) {
+    uint32_t m[L29];
+    fq29 r;
+    uint64_t acc = 0;
+    MI_UNROLL for (int k = 0; k < L29; k++) {
+        MI_UNROLL for (int i = 0; i < k; i++) {
+            acc += (uint64_t)a.v[i] * b.v[k - i];
+            acc += (uint64_t)m[i] * P29[k - i];
+        }
+        acc += (uint64_t)a.v[k] * b.v[0];
+        m[k] = ((uint32_t)acc * INV29) & M29;
+        acc += (uint64_t)m[k] * P29[0];
+        acc >>= 29;
+    }
+    MI_UNROLL for (int k = L29; k < 2 * L29 - 1; k++) {
+        MI_UNROLL for (int i = k - L29 + 1; i < L29; i++) {
+            acc += (uint64_t)a.v[i] * b.v[k - i];
+            acc += (uint64_t)m[i] * P29[k - i];
+        }
+        r.v[k - L29] = (uint32_t)acc & M29;
+        acc >>= 29;
+    }
+    r.v[L29 - 1] = (uint32_t)acc;
+    return r;
+}
+__device__ fq29 to29(const fq_t &raw) {  // 12x32 -> 14x29 (raw integer)
+    fq29 r;
+    MI_UNROLL for (int i = 0; i < L29; i++) {
+        int bit = 29 * i, w = bit >> 5, s = bit & 31;
+        uint64_t x = raw.v[w];
+        if (w + 1 < 12) x |= (uint64_t)raw.v[w + 1] << 32;
+        r.v[i] = (uint32_t)(x >> s) & M29;
+    }
+    return r;
+}
+__device__ fq_t from29(const fq29 &a) {  // 14x29 -> 12x32 (assumes normalized, < 2^384)
+    fq_t r = fq_t::zero();
+    MI_UNROLL for (int i = 0; i < L29; i++) {
+        int bit = 29 * i, w = bit >> 5, s = bit & 31;
+        r.v[w] |= a.v[i] << s;
+        if (s > 3 && w + 1 < 12) r.v[w + 1] |= a.v[i] >> (32 - s);
+    }
+    return r;
+}
+
+// ------------------------------------------------------------------------------ throughput kernels
+__global__ void __launch_bounds__(256) k_v0(fq_t *d, int iters) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    fq_t x = d[i], y = d[i ^ 1];
+    for (int it = 0; it < iters; it++) x = x * y;
+    d[i] = x;
+}
+__global__ void __launch_bounds__(256) k_v1(fq_t *d, int iters) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    fq_t x = d[i], y = d[i ^ 1];
+    for (int it = 0; it < iters; it++) x = mul_v1(x, y);
+    d[i] = x;
+}
+__global__ void __launch_bounds__(256) k_v2(fq29 *d, int iters) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    fq29 x = d[i], y = d[i ^ 1];
+    for (int it = 0; it < iters; it++) x = mul_v2(x, y);
+    d[i] = x;
+}
+
+// correctness: x*y for random canonical x, y through each variant, compared canonically
+__global__ void k_check(const fq_t *xs, const fq_t *ys, int n, int *bad) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fq_t x = xs[i], y = ys[i];
+    fq_t ref = from_mont(to_mont(x) * to_mont(y));
+    fq_t r2;
+    MI_UNROLL for (int k = 0; k < 12; k++) r2.v[k] = FqDesc::R2[k];
+    fq_t one = fq_t::zero();
+    one.v[0] = 1;
+    fq_t v1 = mul_v1(mul_v1(mul_v1(x, r2), mul_v1(y, r2)), one);
+    fq29 R2v, one29 = {};
+    MI_UNROLL for (int k = 0; k < L29; k++) R2v.v[k] = R2_29[k];
+    one29.v[0] = 1;
+    fq29 a = mul_v2(to29(x), R2v), b = mul_v2(to29(y), R2v);
+    fq29 c = mul_v2(mul_v2(a, b), one29);
+    fq_t v2 = reduce_once(from29(c));
+    if (!(v1 == ref)) atomicAdd(bad, 1);
+    if (!(v2 == ref)) atomicAdd(bad + 1, 1);
+}
+
+template <class K, class... A>
+float timeit(K k, dim3 g, dim3 b, A... args) {
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    hipLaunchKernelGGL(k, g, b, 0, 0, args...);  // warm
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipEventRecord(e0));
+    hipLaunchKernelGGL(k, g, b, 0, 0, args...);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    return ms;
+}
+
+int main() {
+    const int threads = 256, blocks = 256 * 16;  // 16 blocks per CU
+    const size_t nt = (size_t)threads * blocks;
+    uint32_t *o;
+    CHECK(hipMalloc(&o, nt * 4));
+    int it = 2000;
+    float ms = timeit(k_raw_mad, dim3(blocks), dim3(threads), o, it);
+    double ops = (double)nt * it * 8;
+    printf("raw v_mad_u64_u32 : %.1f G lane-ops/s  (%.2f cycles/wave-instr/SIMD @2.4GHz)\n", ops / ms / 1e6,
+           (1024.0 * 2.4e9 / (ops / ms * 1e3)) * 64);
+    ms = timeit(k_raw_add, dim3(blocks), dim3(threads), o, it);
+    printf("raw v_add_u32     : %.1f G lane-ops/s  (%.2f cycles/wave-instr/SIMD)\n", ops / ms / 1e6,
+           (1024.0 * 2.4e9 / (ops / ms * 1e3)) * 64);
+    ms = timeit(k_raw_mullo, dim3(blocks), dim3(threads), o, it);
+    printf("raw v_mul_lo_u32  : %.1f G lane-ops/s  (%.2f cycles/wave-instr/SIMD)\n", ops / ms / 1e6,
+           (1024.0 * 2.4e9 / (ops / ms * 1e3)) * 64);
+
+    // correctness
+    const int nc = 1 << 16;
+    fq_t *hx = (fq_t *)malloc(sizeof(fq_t) * nc * 2);
+    srand(1);
+    for (int i = 0; i < 2 * nc; i++) {
+        for (int k = 0; k < 12; k++) hx[i].v[k] = ((uint32_t)rand() << 16) ^ (uint32_t)rand();
+        hx[i].v[11] &= 0x0fffffffu;  // < p
+    }
+    // edge values: 0, 1, p-1
+    for (int k = 0; k < 12; k++) {
+        hx[0].v[k] = 0;
+        hx[1].v[k] = FqDesc::MOD[k];
+        hx[nc].v[k] = FqDesc::MOD[k];
+    }
+    hx[1].v[0] -= 1;
+    hx[nc].v[0] -= 1;
+    fq_t *dx;
+    int *bad;
+    CHECK(hipMalloc(&dx, sizeof(fq_t) * nc * 2));
+    CHECK(hipMalloc(&bad, 8));
+    CHECK(hipMemset(bad, 0, 8));
+    CHECK(hipMemcpy(dx, hx, sizeof(fq_t) * nc * 2, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_check, dim3(nc / 256), dim3(256), 0, 0, dx, dx + nc, nc, bad);
+    int hb[2];
+    CHECK(hipMemcpy(hb, bad, 8, hipMemcpyDeviceToHost));
+    printf("correctness vs v0 over %d random products: v1 mismatches %d, v2 mismatches %d\n", nc, hb[0], hb[1]);
+
+    // throughput
+    it = 200;
+    fq_t *d0;
+    CHECK(hipMalloc(&d0, sizeof(fq_t) * nt));
+    CHECK(hipMemset(d0, 1, sizeof(fq_t) * nt));
+    double muls = (double)nt * it;
+    ms = timeit(k_v0, dim3(blocks), dim3(threads), d0, it);
+    printf("v0 CIOS (compiler)     : %.2f G Fq-mul/s\n", muls / ms / 1e6);
+    ms = timeit(k_v1, dim3(blocks), dim3(threads), d0, it);
+    printf("v1 FIPS 32-bit + vcc   : %.2f G Fq-mul/s\n", muls / ms / 1e6);
+    fq29 *d2;
+    CHECK(hipMalloc(&d2, sizeof(fq29) * nt));
+    CHECK(hipMemset(d2, 1, sizeof(fq29) * nt));
+    ms = timeit(k_v2, dim3(blocks), dim3(threads), d2, it);
+    printf("v2 FIPS 29-bit limbs   : %.2f G Fq-mul/s\n", muls / ms / 1e6);
+    return 0;
+}
