@@ -24,6 +24,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "crypto3-fil-proofs_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# VALU bound of the accumulation kernel: v_mad_u64_u32 issue rate measured on MI355X by
+# crypto3-fil-proofs_amd/microbench/fieldmul.hip (29.99e12 lane-MADs/s), one 29-bit-limb Fq
+# multiplication = 392 MADs -> 76.5e9 Fq-mul/s; the same microbench sustains 79.4e9 on a
+# multiply-only loop, so MAD issue is the binding limit.
+MAD_RATE = 29.99e12
+FQ_MUL_MADS = 392
+FQ_MUL_PER_MIXED_ADD = {"G1": 10, "G2": 28}  # madd-2008-s: 8M + 2S over Fq / Fq2 (Karatsuba 3M, 2M per sqr)
 TOXIC_SEED = 0x5EED
 
 
@@ -190,13 +197,35 @@ def main():
 
     # roofline of the dominant kernel (largest share of device time in the timed region)
     kernels = {
-        "k_accum_level0<G1>": (stats["accum_g1"], 128.0),
-        "k_accum_level0<G2>": (stats["accum_g2"], 224.0),
+        "k_accum_level0<G1>": (stats["accum_g1"], 128.0, "G1"),
+        "k_accum_level0<G2>": (stats["accum_g2"], 224.0, "G2"),
     }
-    dom_name, (dom, bytes_per_unit) = max(kernels.items(), key=lambda kv: kv[1][0]["ms"])
+    dom_name, (dom, bytes_per_unit, grp) = max(kernels.items(), key=lambda kv: kv[1][0]["ms"])
     avg_ms = dom["ms"] / max(dom["launches"], 1)
     units_per_launch = dom["units"] / max(dom["launches"], 1)
     achieved = bytes_per_unit * units_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else None
+    # HBM traffic per launch from the committed rocprofv3 PMC summary of the same kernel/workload
+    traffic, traffic_src = None, None
+    prof_dir = os.path.join(ROOT, "profiles")
+    if os.path.isdir(prof_dir):
+        for fn in sorted(os.listdir(prof_dir), reverse=True):
+            if fn.endswith("_summary.json"):
+                try:
+                    ps = json.load(open(os.path.join(prof_dir, fn)))
+                    dk = ps.get("dominant_kernel", {})
+                    if grp == "G1" and "hbm_bytes_per_point" in dk and ps.get("workload") == \
+                            f"synthetic 2^{args.log_rows}-constraint R1CS full Groth16 prove (BASELINE config 3)":
+                        traffic = dk["hbm_bytes_per_point"] * units_per_launch
+                        traffic_src = fn
+                        break
+                except Exception:
+                    pass
+    # secondary (binding) roofline: Fq multiplications per second vs the MAD-issue bound
+    c_bits = fg.msm_window_bits(int(units_per_launch))
+    nwin = (256 + c_bits - 1) // c_bits
+    fq_muls = units_per_launch * nwin * FQ_MUL_PER_MIXED_ADD[grp]
+    valu_ach = fq_muls / (avg_ms * 1e-3) if avg_ms > 0 else None
+    valu_peak = MAD_RATE / FQ_MUL_MADS
     total_steps = args.steps * world
     value = n * total_steps / dt
     out = {
@@ -226,17 +255,29 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS if achieved else None,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_source": f"profiles/{traffic_src} (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, per point x "
+                              f"points per launch)" if traffic_src else None,
             "avg_launch_ms": avg_ms,
             "units_per_launch": units_per_launch,
             "algorithmic_bytes_per_unit": bytes_per_unit,
             "note": "VALU-integer-bound kernel (BLS12-381 Montgomery multiplications); HBM fraction is reported "
-                    "per BASELINE.json north_star, see DESIGN.md for the VALU roofline",
+                    "per BASELINE.json north_star; the binding roofline is 'valu_roofline'",
+        },
+        "valu_roofline": {
+            "bound": "valu (v_mad_u64_u32 issue)",
+            "kernel": dom_name,
+            "achieved": valu_ach,
+            "peak": valu_peak,
+            "unit": "Fq-mul/s",
+            "frac": valu_ach / valu_peak if valu_ach else None,
+            "model": f"{FQ_MUL_PER_MIXED_ADD[grp]} Fq-mul per mixed add x {nwin} windows (c={c_bits}) per point",
         },
         "cpu_baseline": cpu,
         "timers_ms": {k: round(v["ms"], 3) for k, v in stats.items()},
         "setup_s": {"synth": t_synth, "circuit_load": t_load, "srs_generate": t_srs},
         "multiproof_bytes": len(gathered),
+        "msm_reps": args.msm_reps,
     }
     if cpu and cpu.get("value"):
         out["gpu_over_cpu"] = value / cpu["value"]

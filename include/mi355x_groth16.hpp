@@ -1,0 +1,137 @@
+// mi355x_groth16.hpp -- header-only C++ host layer over the C ABI (mi355x_groth16.h).
+//
+// Mirrors the reference's prover-side C++ interface so a maintainer can swap the crypto3 CPU
+// prover for the MI355X one behind the same call shapes:
+//   * proving_key  ~ r1cs_gg_ppzksnark_mapped_scheme_params / scheme_params{vk,h,l,a,b_g1,b_g2}
+//                    (libs/storage/include/nil/filecoin/storage/proofs/core/crypto/scheme_params.hpp:38-67)
+//   * prove(...)   ~ crypto3 r1cs_gg_ppzksnark prove(pk, primary_input, auxiliary_input)
+//   * circuit_proofs(...) ~ compound_proof::circuit_proofs partition loop (core/proof/compound_proof.hpp:127-137)
+//   * multi_proof  ~ multi_proof{circuit_proofs, verifying_key} (core/proof/multi_proof.hpp:38-58),
+//                    written as P x 192 bytes (api/seal.hpp:306-308)
+//   * partition_count ~ core/partitions.hpp:36-38
+// Errors are thrown as mi355x::error, like the reference's BOOST_ASSERT_MSG / throw style
+// (compound_proof.hpp:94).
+#pragma once
+#include <array>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "mi355x_groth16.h"
+
+namespace mi355x {
+
+struct error : std::runtime_error {
+    int code;
+    error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+inline void check(int rc) {
+    if (rc != MI_OK) throw error(rc, std::string("libfilgpu: ") + mi_last_error());
+}
+
+using fr32 = std::array<uint8_t, 32>;  // Fr, 32 bytes little-endian (core/fr32.hpp:36-52)
+using proof_bytes = std::array<uint8_t, MI_PROOF_BYTES>;
+
+inline std::int64_t partition_count(std::int64_t partitions) {  // core/partitions.hpp:36-38
+    return partitions == -1 ? 1 : (partitions == 0 ? -1 : partitions);
+}
+
+class context {
+public:
+    explicit context(int device = 0) { check(mi_ctx_create(device, &h_)); }
+    ~context() { mi_ctx_destroy(h_); }
+    context(const context &) = delete;
+    context &operator=(const context &) = delete;
+    mi_ctx *get() const { return h_; }
+    void synchronize() { check(mi_ctx_synchronize(h_)); }
+
+private:
+    mi_ctx *h_ = nullptr;
+};
+
+class circuit {
+public:
+    circuit(context &ctx, const mi_r1cs &cs) { check(mi_circuit_load(ctx.get(), &cs, &h_)); }
+    ~circuit() { mi_circuit_free(h_); }
+    circuit(const circuit &) = delete;
+    circuit &operator=(const circuit &) = delete;
+    mi_circuit *get() const { return h_; }
+    std::uint64_t num_variables() const {
+        std::uint64_t info[9];
+        check(mi_circuit_info(h_, info));
+        return info[1] + info[2];
+    }
+
+private:
+    mi_circuit *h_ = nullptr;
+};
+
+class proving_key {
+public:
+    // load a bellman-layout key (uncompressed points); checked -> on-curve validation
+    proving_key(context &ctx, const circuit *c, const mi_srs_host &host, bool checked) {
+        check(mi_srs_load(ctx.get(), c ? c->get() : nullptr, &host, checked ? 1 : 0, &h_));
+    }
+    // groth16::generate_random_parameters with known toxic waste (tests / benches)
+    static proving_key generate(context &ctx, const circuit &c, const std::array<fr32, 5> &toxic) {
+        std::array<uint8_t, 160> t;
+        for (int i = 0; i < 5; i++)
+            for (int j = 0; j < 32; j++) t[32 * i + j] = toxic[i][j];
+        mi_srs *h = nullptr;
+        check(mi_srs_generate(ctx.get(), c.get(), t.data(), &h));
+        return proving_key(h);
+    }
+    proving_key(proving_key &&o) noexcept : h_(std::exchange(o.h_, nullptr)) {}
+    ~proving_key() { mi_srs_free(h_); }
+    mi_srs *get() const { return h_; }
+    std::vector<uint8_t> verifying_key() const {
+        std::vector<uint8_t> vk(MI_VK_BYTES);
+        check(mi_srs_export_vk(h_, vk.data(), nullptr));
+        return vk;
+    }
+
+private:
+    explicit proving_key(mi_srs *h) : h_(h) {}
+    mi_srs *h_ = nullptr;
+};
+
+// One proof: primary (ONE first) ++ auxiliary assignment, injected blinding r, s.
+inline proof_bytes prove(context &ctx, const proving_key &pk, const circuit &c, const std::vector<fr32> &z,
+                         const fr32 &r, const fr32 &s, bool priority = false) {
+    if (z.size() != c.num_variables()) throw error(MI_ERR_ARG, "assignment length != number of variables");
+    proof_bytes out;
+    check(mi_groth16_prove(ctx.get(), pk.get(), c.get(), z.front().data(), r.data(), s.data(), priority ? 1 : 0,
+                           out.data(), nullptr));
+    return out;
+}
+
+struct multi_proof {
+    std::vector<proof_bytes> circuit_proofs;
+    std::vector<uint8_t> verifying_key;
+    std::vector<uint8_t> write() const {  // api/seal.hpp:306-308
+        std::vector<uint8_t> buf;
+        buf.reserve(circuit_proofs.size() * MI_PROOF_BYTES);
+        for (auto &p : circuit_proofs) buf.insert(buf.end(), p.begin(), p.end());
+        return buf;
+    }
+};
+
+// compound_proof::circuit_proofs: one Groth16 proof per partition, in partition order.
+inline multi_proof circuit_proofs(context &ctx, const proving_key &pk, const circuit &c,
+                                  const std::vector<std::vector<fr32>> &partition_assignments,
+                                  const std::vector<std::pair<fr32, fr32>> &blindings, bool priority = false) {
+    if (partition_assignments.empty())
+        throw error(MI_ERR_ARG, "Cannot create a circuit proof over missing vanilla proofs");
+    if (blindings.size() != partition_assignments.size()) throw error(MI_ERR_ARG, "one (r, s) per partition");
+    multi_proof mp;
+    for (size_t k = 0; k < partition_assignments.size(); k++)
+        mp.circuit_proofs.push_back(
+            prove(ctx, pk, c, partition_assignments[k], blindings[k].first, blindings[k].second, priority));
+    mp.verifying_key = pk.verifying_key();
+    return mp;
+}
+
+}  // namespace mi355x

@@ -1,5 +1,7 @@
 // oracle.cpp -- CPU restatement of the BLS12-381 Groth16 hot path.
 // TEST INFRASTRUCTURE ONLY: used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline.
+// Parity unpinned against the reference itself (unbuildable, no golden vectors); pinned by published
+// constants, the independent Python restatement and pairing checks -- see oracle.h / DESIGN.md §3.
 // The product (libfilgpu.so) never links or calls this file.  See oracle.h for the reference map.
 //
 // Style is intentionally different from the device code: 64-bit limbs with unsigned __int128

@@ -1,6 +1,11 @@
 /*
  * oracle.h -- CPU restatement of the Groth16/BLS12-381 hot path (TEST INFRASTRUCTURE ONLY).
  *
+ * PARITY UNPINNED (task rules): the reference's own prover cannot be built or imported here and its
+ * tests hold no golden proof vector.  The oracle is pinned instead by published
+ * BLS12-381 constants, an independent pure-Python restatement (tests/golden/pyref.py ->
+ * golden.json) and the Groth16 pairing equation.
+ *
  * This is the parity oracle for the MI355X proving core.  Only tests/, __graft_entry__.smoke()
  * and bench.py's cpu_baseline leg may load it; the product library (libfilgpu.so) never links it.
  *

@@ -125,3 +125,19 @@ def test_no_gpu_raises_loudly():
         pytest.skip("GPU present")
     with pytest.raises(fg.FilGpuError):
         fg.Context(0)
+
+
+def test_cpp_host_layer_builds_and_fails_loudly_without_gpu():
+    """include/mi355x_groth16.hpp compiles against the C ABI; without a device the example exits
+    with MI_ERR_NO_DEVICE (3) instead of computing anything on the CPU."""
+    import subprocess
+
+    pkg = os.path.join(ROOT, "crypto3-fil-proofs_amd")
+    subprocess.check_call(["make", "-s", "-C", pkg, "build/prove_synthetic"])
+    exe = os.path.join(pkg, "build", "prove_synthetic")
+    n = ctypes.c_int(-1)
+    fg.lib().mi_device_count(ctypes.byref(n))
+    if n.value > 0:
+        pytest.skip("GPU present (covered by tests/test_gpu_cpp.py)")
+    r = subprocess.run([exe, "8", "2"], capture_output=True, text=True)
+    assert r.returncode == 3 and "no HIP device" in r.stderr
