@@ -284,19 +284,26 @@ int mi_srs_export_query(mi_ctx *ctx, const mi_srs *srs, int which, uint8_t *out,
         }
         need(cap >= n, "output buffer too small");
         if (!n) return;
-        if (g2) {
-            std::vector<mi::g2_affine_t> h(n);
-            MI_HIP(hipMemcpy(h.data(), src, sizeof(mi::g2_affine_t) * n, hipMemcpyDeviceToHost));
-            for (uint64_t i = 0; i < n; i++) mi::g2_encode(h[i], out + 192 * i);
+        const uint64_t chunk = 1ull << 22;
+        const size_t esz = g2 ? 192 : 96;
+        uint8_t *stage = ctx->c.scratch[0].as<uint8_t>(esz * (n < chunk ? n : chunk));
+        if (which == 0 && s.log_d) {
+            // h is stored bit-reversed: encode the whole query in one pass (source index un-permuted)
+            uint8_t *all = ctx->c.scratch[1].as<uint8_t>(esz * n);
+            mi::g1_encode_uncompressed(ctx->c, (const mi::g1_affine_t *)src, all, n, s.log_d);
+            MI_HIP(hipMemcpyAsync(out, all, esz * n, hipMemcpyDeviceToHost, ctx->c.stream));
         } else {
-            std::vector<mi::g1_affine_t> h(n);
-            MI_HIP(hipMemcpy(h.data(), src, sizeof(mi::g1_affine_t) * n, hipMemcpyDeviceToHost));
-            for (uint64_t i = 0; i < n; i++) {
-                uint64_t dst = i;
-                if (which == 0 && s.log_d) dst = __builtin_bitreverse64(i) >> (64 - s.log_d);  // un-permute
-                mi::g1_encode(h[i], out + 96 * dst);
+            for (uint64_t o = 0; o < n; o += chunk) {
+                uint64_t m = n - o < chunk ? n - o : chunk;
+                if (g2)
+                    mi::g2_encode_uncompressed(ctx->c, (const mi::g2_affine_t *)src + o, stage, m);
+                else
+                    mi::g1_encode_uncompressed(ctx->c, (const mi::g1_affine_t *)src + o, stage, m, 0);
+                MI_HIP(hipMemcpyAsync(out + esz * o, stage, esz * m, hipMemcpyDeviceToHost, ctx->c.stream));
+                MI_HIP(hipStreamSynchronize(ctx->c.stream));
             }
         }
+        MI_HIP(hipStreamSynchronize(ctx->c.stream));
     });
 }
 

@@ -198,6 +198,9 @@ unsigned msm_window_bits(uint64_t n);
 // zcash uncompressed big-endian -> device Montgomery affine; returns count of invalid points
 void g1_decode_uncompressed(Ctx &c, const uint8_t *dev_bytes, g1_affine_t *out, uint64_t n, int *bad_dev);
 void g2_decode_uncompressed(Ctx &c, const uint8_t *dev_bytes, g2_affine_t *out, uint64_t n, int *bad_dev);
+// device affine -> zcash uncompressed bytes (device buffer); perm_log != 0 un-bit-reverses the source
+void g1_encode_uncompressed(Ctx &c, const g1_affine_t *in, uint8_t *dev_out, uint64_t n, unsigned perm_log);
+void g2_encode_uncompressed(Ctx &c, const g2_affine_t *in, uint8_t *dev_out, uint64_t n);
 // canonical LE Fr bytes (already on device, 32B each) -> canonical, reduced mod r (in place)
 void fr_canonicalize(Ctx &c, fr_t *d, uint64_t n);
 

@@ -73,6 +73,49 @@ __global__ void k_g2_decode(const uint8_t *__restrict__ in, g2_affine_t *__restr
     out[i] = a;
 }
 
+__device__ __forceinline__ void fq_to_be48_dev(const fq_t &a, uint8_t *out) {
+    fq32_t raw = fq_to_raw(a);
+    MI_UNROLL for (int i = 0; i < 12; i++) {
+        uint32_t w = raw.v[i];
+        uint8_t *p = out + 4 * (11 - i);
+        p[0] = (uint8_t)(w >> 24);
+        p[1] = (uint8_t)(w >> 16);
+        p[2] = (uint8_t)(w >> 8);
+        p[3] = (uint8_t)w;
+    }
+}
+// device affine -> zcash uncompressed; src index = perm_log ? bitrev(i) : i (h is stored bit-reversed)
+__global__ void k_g1_encode(const g1_affine_t *__restrict__ in, uint8_t *__restrict__ out, uint64_t n,
+                            unsigned perm_log) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t src = perm_log ? (__builtin_bitreverse64(i) >> (64 - perm_log)) : i;
+    uint8_t *p = out + 96 * i;
+    const g1_affine_t a = in[src];
+    if (a.is_inf()) {
+        for (int k = 0; k < 96; k++) p[k] = 0;
+        p[0] = 0x40;
+        return;
+    }
+    fq_to_be48_dev(a.x, p);
+    fq_to_be48_dev(a.y, p + 48);
+}
+__global__ void k_g2_encode(const g2_affine_t *__restrict__ in, uint8_t *__restrict__ out, uint64_t n) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint8_t *p = out + 192 * i;
+    const g2_affine_t a = in[i];
+    if (a.is_inf()) {
+        for (int k = 0; k < 192; k++) p[k] = 0;
+        p[0] = 0x40;
+        return;
+    }
+    fq_to_be48_dev(a.x.c1, p);
+    fq_to_be48_dev(a.x.c0, p + 48);
+    fq_to_be48_dev(a.y.c1, p + 96);
+    fq_to_be48_dev(a.y.c0, p + 144);
+}
+
 // x mod r for x < 2^256 (at most two subtractions: 2^256 < 3r)
 __global__ void k_fr_canon(fr_t *__restrict__ d, uint64_t n) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -112,6 +155,16 @@ void g1_decode_uncompressed(Ctx &c, const uint8_t *dev_bytes, g1_affine_t *out, 
 void g2_decode_uncompressed(Ctx &c, const uint8_t *dev_bytes, g2_affine_t *out, uint64_t n, int *bad_dev) {
     if (!n) return;
     k_g2_decode<<<grid1(n), 256, 0, c.stream>>>(dev_bytes, out, n, bad_dev);
+    MI_HIP(hipGetLastError());
+}
+void g1_encode_uncompressed(Ctx &c, const g1_affine_t *in, uint8_t *dev_out, uint64_t n, unsigned perm_log) {
+    if (!n) return;
+    k_g1_encode<<<grid1(n), 256, 0, c.stream>>>(in, dev_out, n, perm_log);
+    MI_HIP(hipGetLastError());
+}
+void g2_encode_uncompressed(Ctx &c, const g2_affine_t *in, uint8_t *dev_out, uint64_t n) {
+    if (!n) return;
+    k_g2_encode<<<grid1(n), 256, 0, c.stream>>>(in, dev_out, n);
     MI_HIP(hipGetLastError());
 }
 void fr_canonicalize(Ctx &c, fr_t *d, uint64_t n) {
