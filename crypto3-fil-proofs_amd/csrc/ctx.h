@@ -177,6 +177,10 @@ void ntt_dif(Ctx &c, fr_t *d, unsigned log_n, bool inverse);
 // DIT: bit-reversed in -> natural out
 void ntt_dit(Ctx &c, fr_t *d, unsigned log_n, bool inverse);
 void bitrev_permute(Ctx &c, fr_t *d, unsigned log_n);
+// DIF NTT whose last pass also multiplies position pos by g^(+-bitrev(pos)) * scale (and optionally
+// converts to canonical): iNTT + coset shift (+ 1/d) in the same HBM passes
+void ntt_dif_coset_epilogue(Ctx &c, fr_t *d, unsigned log_n, bool inverse, bool inverse_gen, const fr_t &scale,
+                            bool to_canonical);
 // d[pos] *= g^(±bitrev(pos)) * scale (scale may be null)
 void coset_scale_bitrev(Ctx &c, fr_t *d, unsigned log_n, bool inverse_gen, const fr_t *scale_host,
                         bool to_canonical);

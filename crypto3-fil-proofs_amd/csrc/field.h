@@ -42,10 +42,15 @@ struct FrDesc {
     static constexpr uint32_t INV = 0xffffffffu;  // r = 1 mod 2^32
     static constexpr uint32_t MOD[8] = {0x00000001u, 0xffffffffu, 0xfffe5bfeu, 0x53bda402u,
                                         0x09a1d805u, 0x3339d808u, 0x299d7d48u, 0x73eda753u};
-    static constexpr uint32_t R1[8] = {0xfffffffeu, 0x00000001u, 0x00034802u, 0x5884b7fau,
-                                       0xecbc4ff5u, 0x998c4fefu, 0xacc5056fu, 0x1824b159u};
-    static constexpr uint32_t R2[8] = {0xf3f29c6du, 0xc999e990u, 0x87925c23u, 0x2b6cedcbu,
-                                       0x7254398fu, 0x05d31496u, 0x9f59ff11u, 0x0748d9d9u};
+    // Montgomery radix R = 2^261 (products are computed over 9 x 29-bit limbs, see operator*)
+    static constexpr uint32_t R1[8] = {0xffffffbau, 0x00000045u, 0x0072d846u, 0x1a25272eu,
+                                       0x5dbeee8bu, 0xfe2eedcdu, 0x9eefbe41u, 0x4d043f42u};
+    static constexpr uint32_t R2[8] = {0xca71b3c0u, 0x67a6440fu, 0x49d98f66u, 0xc44e2d5eu,
+                                       0xe8703b58u, 0x7ddc57c6u, 0x009cf20au, 0x27fd91b3u};
+    static constexpr int L29 = 9;
+    static constexpr uint32_t MOD29[9] = {0x00000001u, 0x1ffffff8u, 0x1f96ffbfu, 0x1b4805ffu, 0x1d80553bu,
+                                          0x0c0404d0u, 0x1520cce7u, 0x0a6533afu, 0x0073eda7u};
+    static constexpr uint32_t INV29 = 0x1fffffffu;  // -r^-1 mod 2^29
 };
 
 template <class D>
@@ -161,6 +166,54 @@ MI_HD Fp<D> operator*(const Fp<D> &a, const Fp<D> &b) {
     }
     Fp<D> r;
     MI_UNROLL for (int j = 0; j < N; j++) r.v[j] = t[j];
+    return reduce_once(r);
+}
+
+// Fr: storage stays 8 x 32-bit (canonical Montgomery value < r, the wire/memory image), but the
+// product is computed by product scanning over 9 x 29-bit limbs (R = 2^261): 162 v_mad_u64_u32 and
+// no carry chains instead of the 32-bit CIOS above; result < 2r, one conditional subtraction.
+template <>
+MI_HD Fp<FrDesc> operator*<FrDesc>(const Fp<FrDesc> &a, const Fp<FrDesc> &b) {
+    constexpr int L = 9;
+    constexpr uint32_t M = (1u << 29) - 1;
+    uint32_t x[L], y[L], m[L], t[L];
+    MI_UNROLL for (int i = 0; i < L; i++) {
+        const int bit = 29 * i, w = bit >> 5, s = bit & 31;
+        uint64_t xa = a.v[w], xb = b.v[w];
+        if (w + 1 < 8) {
+            xa |= (uint64_t)a.v[w + 1] << 32;
+            xb |= (uint64_t)b.v[w + 1] << 32;
+        }
+        x[i] = (uint32_t)(xa >> s) & M;
+        y[i] = (uint32_t)(xb >> s) & M;
+    }
+    uint64_t acc = 0;
+    MI_UNROLL for (int k = 0; k < L; k++) {
+        MI_UNROLL for (int i = 0; i < k; i++) {
+            acc += (uint64_t)x[i] * y[k - i];
+            acc += (uint64_t)m[i] * FrDesc::MOD29[k - i];
+        }
+        acc += (uint64_t)x[k] * y[0];
+        m[k] = ((uint32_t)acc * FrDesc::INV29) & M;
+        acc += (uint64_t)m[k] * FrDesc::MOD29[0];
+        acc >>= 29;
+    }
+    MI_UNROLL for (int k = L; k < 2 * L - 1; k++) {
+        MI_UNROLL for (int i = k - L + 1; i < L; i++) {
+            acc += (uint64_t)x[i] * y[k - i];
+            acc += (uint64_t)m[i] * FrDesc::MOD29[k - i];
+        }
+        t[k - L] = (uint32_t)acc & M;
+        acc >>= 29;
+    }
+    t[L - 1] = (uint32_t)acc;
+    Fp<FrDesc> r;
+    MI_UNROLL for (int j = 0; j < 8; j++) r.v[j] = 0;
+    MI_UNROLL for (int i = 0; i < L; i++) {
+        const int bit = 29 * i, w = bit >> 5, s = bit & 31;
+        r.v[w] |= t[i] << s;
+        if (s > 3 && w + 1 < 8) r.v[w + 1] |= t[i] >> (32 - s);
+    }
     return reduce_once(r);
 }
 

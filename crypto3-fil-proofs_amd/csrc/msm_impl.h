@@ -6,7 +6,7 @@
 // Pipeline (one MSM):
 //   1. k_digits     : every scalar -> ceil(256/c) signed c-bit digits; one (bucket key, point
 //                     index | sign) pair per non-zero digit, laid out [window][point] (coalesced).
-//   2. radix sort   : rocPRIM onesweep over only the key bits in use (hipcub::DeviceRadixSort).
+//   2. radix sort   : rocPRIM onesweep per window over the c window-local key bits.
 //   3. k_bounds     : bucket start / end from the sorted keys.
 //   4. accumulation : buckets are cut into chunks of <= L sorted entries, one thread per chunk
 //                     (mixed XYZZ += affine adds, point gathered by index); chunk partials of
@@ -14,7 +14,7 @@
 //                     every bucket is one point.  Work per thread is bounded by L whatever the
 //                     scalar distribution (boolean-heavy Filecoin witnesses put most entries in
 //                     bucket 1 of window 0).
-//   5. k_bucket_reduce: running-sum reduction sum_b (b+1) B_b over ~2^19 segments of buckets;
+//   5. k_bucket_reduce: running-sum reduction sum_b (b+1) B_b over ~2^18 (G1) / 2^16 (G2) segments;
 //      k_seg_fold adds each segment's offset (s * seg_len) * run with a short double-and-add.
 //   6. k_sum_groups : per-window tree sum of the segment results.
 //   7. host         : Horner over windows (c doublings each) on the CPU.
@@ -62,19 +62,22 @@ __global__ void k_digits(const fr_t *__restrict__ scalars, const uint32_t *__res
             carry = 0;
         }
         uint64_t o = (uint64_t)w * n + i;
-        keys[o] = d ? w * nbk + d - 1 : invalid;
+        keys[o] = d ? d - 1 : invalid;  // bucket within the window; windows are sorted separately
         vals[o] = i | (neg << 31);
     }
 }
 
-__global__ void k_bounds(const uint32_t *__restrict__ keys, uint32_t np, uint32_t invalid,
+// keys are window-local (sorted per window): global bucket = window * nbk + key
+__global__ void k_bounds(const uint32_t *__restrict__ keys, uint32_t np, uint32_t n, uint32_t nbk,
                          uint32_t *__restrict__ start, uint32_t *__restrict__ cnt) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= np) return;
     uint32_t k = keys[i];
-    if (k == invalid) return;
-    if (i == 0 || keys[i - 1] != k) start[k] = i;
-    if (i == np - 1 || keys[i + 1] != k) cnt[k] = i + 1;  // end; converted to a count below
+    if (k == nbk) return;  // zero digit
+    uint32_t w = i / n, lo = w * n, hi = lo + n;
+    uint32_t g = w * nbk + k;
+    if (i == lo || keys[i - 1] != k) start[g] = i;
+    if (i + 1 == hi || keys[i + 1] != k) cnt[g] = i + 1;  // end; converted to a count below
 }
 
 __global__ void k_end_to_cnt(const uint32_t *__restrict__ start, uint32_t *__restrict__ cnt, uint32_t nb) {
@@ -220,9 +223,9 @@ void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const uint32_t
     const uint64_t np64 = (uint64_t)nwin * n;
     if (np64 >= 0xffffffffull || nb64 >= 0x7fffffffull || n >= 0x80000000ull)
         throw std::runtime_error("msm: instance too large for 32-bit sort indices");
-    const uint32_t nb = (uint32_t)nb64, np = (uint32_t)np64, invalid = nb;
+    const uint32_t nb = (uint32_t)nb64, np = (uint32_t)np64, invalid = nbk;  // window-local keys
     unsigned key_bits = 1;
-    while ((1ull << key_bits) <= invalid) key_bits++;
+    while ((1ull << key_bits) <= invalid) key_bits++;  // cb bits: one fewer onesweep pass than global keys
 
     uint32_t *keys = c.scratch[0].as<uint32_t>(np);
     uint32_t *vals = c.scratch[1].as<uint32_t>(np);
@@ -240,13 +243,17 @@ void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const uint32_t
         MI_LAUNCHED(c, "k_digits");
         MI_HIP(hipGetLastError());
         size_t tmp_bytes = 0;
-        MI_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys, keys_s, vals, vals_s, np, 0, key_bits,
-                                                  st));
+        MI_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys, keys_s, vals, vals_s, (uint32_t)n, 0,
+                                                  key_bits, st));
         void *tmp = c.scratch[4].get(tmp_bytes);
-        MI_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys, keys_s, vals, vals_s, np, 0, key_bits, st));
+        for (unsigned w = 0; w < nwin; w++) {
+            uint64_t o = (uint64_t)w * n;
+            MI_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys + o, keys_s + o, vals + o, vals_s + o,
+                                                      (uint32_t)n, 0, key_bits, st));
+        }
         MI_HIP(hipMemsetAsync(offA, 0, sizeof(uint32_t) * nb, st));
         MI_HIP(hipMemsetAsync(cntA, 0, sizeof(uint32_t) * nb, st));
-        k_bounds<<<grid_for(np, 256), 256, 0, st>>>(keys_s, np, invalid, offA, cntA);
+        k_bounds<<<grid_for(np, 256), 256, 0, st>>>(keys_s, np, (uint32_t)n, nbk, offA, cntA);
         MI_LAUNCHED(c, "k_bounds");
         k_end_to_cnt<<<grid_for(nb, 256), 256, 0, st>>>(offA, cntA, nb);
         MI_LAUNCHED(c, "k_end_to_cnt");
@@ -317,9 +324,11 @@ void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const uint32_t
         }
     }
 
-    // bucket reduction: ~2^19 threads of seg_len buckets each, then fold offsets, then tree-sum
+    // bucket reduction: ~2^18 (G1) / 2^16 (G2: one wave per SIMD) threads of seg_len buckets each,
+    // then fold offsets (a double-and-add per segment, so fewer segments = less fold work), then tree-sum
+    const uint64_t seg_target = sizeof(F) == sizeof(fq_t) ? (1u << 18) : (1u << 16);
     unsigned seg_len = 1;
-    while (seg_len < nbk && (uint64_t)nb / (seg_len * 2) >= (1u << 19)) seg_len *= 2;
+    while (seg_len < nbk && (uint64_t)nb / (seg_len * 2) >= seg_target) seg_len *= 2;
     const uint32_t nseg = nbk / seg_len, nseg_total = nwin * nseg;
     XYZZ<F> *seg_acc = c.scratch[12].as<XYZZ<F>>(2 * (uint64_t)nseg_total);
     XYZZ<F> *seg_run = seg_acc + nseg_total;

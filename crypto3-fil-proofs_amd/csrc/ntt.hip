@@ -36,14 +36,21 @@ __device__ __forceinline__ uint32_t brev(uint32_t x, unsigned bits) {
     return bits ? (__builtin_bitreverse32(x) >> (32 - bits)) : 0;
 }
 
-// One pass.  DIF: load -> b DIF stages -> optional inter-pass twiddle -> store.
+// One pass.  DIF: load -> b DIF stages -> optional inter-pass twiddle -> [epilogue] -> store.
 //            DIT: load -> optional inter-pass twiddle -> b DIT stages (reverse) -> store.
+// In-tile twiddles omega_{2^b}^j (j < 2^(b-1)) are staged into LDS once per workgroup.
+// Epilogue (last DIF pass only): epi = 1 multiplies the element at global position pos by
+// G^bitrev_L(pos) * scale (coset shift of the bit-reversed coefficients, fused 1/d); epi = 2 also
+// converts to canonical form (icoset: H for the MSM).
 template <bool DIF>
-__global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(fr_t *__restrict__ d, unsigned M, unsigned b,
+__global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(fr_t *__restrict__ d, unsigned L, unsigned M, unsigned b,
                                                           unsigned Tlog, unsigned Glog, int twiddle,
                                                           const fr_t *__restrict__ lo,
-                                                          const fr_t *__restrict__ hi) {
+                                                          const fr_t *__restrict__ hi, int epi,
+                                                          const fr_t *__restrict__ glo,
+                                                          const fr_t *__restrict__ ghi, fr_t scale) {
     __shared__ fr_t sh[TILE];
+    __shared__ fr_t tw[TILE / 2];
     const unsigned T = 1u << Tlog;
     const unsigned Slog = M - b;
     const uint64_t S = 1ull << Slog;
@@ -59,6 +66,7 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(fr_t *__restrict__ d, 
         i20 = (blockIdx.x % blocks_per_sub) << Tlog;
     }
     const unsigned bmask = (1u << b) - 1;
+    for (unsigned j = threadIdx.x; j < (1u << (b - 1)); j += NTT_THREADS) tw[j] = hi[j << (16 - b)];
     // load
     for (unsigned e = threadIdx.x; e < tile; e += NTT_THREADS) {
         unsigned t = e & (T - 1), i1 = (e >> Tlog) & bmask, g = e >> (Tlog + b);
@@ -91,9 +99,9 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(fr_t *__restrict__ d, 
             if (DIF) {
                 fr_t dd = u - v;
                 sh[e0] = u + v;
-                sh[e1] = j ? dd * hi[j << (16 - b)] : dd;
+                sh[e1] = j ? dd * tw[j] : dd;
             } else {
-                fr_t w = j ? v * hi[j << (16 - b)] : v;
+                fr_t w = j ? v * tw[j] : v;
                 sh[e0] = u + w;
                 sh[e1] = u - w;
             }
@@ -109,6 +117,12 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(fr_t *__restrict__ d, 
             uint32_t k1 = brev(i1, b);
             uint32_t ex = (uint32_t)(((uint64_t)(i20 + t) * k1) << (32 - M));
             if (ex) x = x * tw_full(lo, hi, ex);
+        }
+        if (DIF && epi) {
+            uint32_t ex = brev((uint32_t)gi, L);
+            if (ex) x = x * tw_full(glo, ghi, ex);
+            x = x * scale;
+            if (epi == 2) x = from_mont(x);
         }
         d[gi] = x;
     }
@@ -247,25 +261,43 @@ void ntt_free_tables(Ctx &c) {
     c.tw = NttTables();
 }
 
-static void ntt_run(Ctx &c, fr_t *d, unsigned L, bool inverse, bool dif) {
+static void ntt_run(Ctx &c, fr_t *d, unsigned L, bool inverse, bool dif, int epi = 0, bool inv_gen = false,
+                    const fr_t &scale = fr_t::one()) {
     if (L > 32) throw std::runtime_error("ntt: domain larger than 2^32");
-    if (L == 0) return;
+    if (L == 0) {
+        if (epi) {  // single element: coset factor g^0 = 1
+            fr_t one = scale;
+            scale_all(c, d, 1, one);
+            if (epi == 2) fr_from_mont_inplace(c, d, 1);
+        }
+        return;
+    }
     ScopedTimer tm(c, &c.stats.ntt, 1ull << L);
     const fr_t *lo = inverse ? c.tw.iv_lo : c.tw.fw_lo;
     const fr_t *hi = inverse ? c.tw.iv_hi : c.tw.fw_hi;
+    const fr_t *glo = inv_gen ? c.tw.gi_lo : c.tw.g_lo;
+    const fr_t *ghi = inv_gen ? c.tw.gi_hi : c.tw.g_hi;
     auto plan = plan_passes(L);
     if (dif) {
-        for (auto &p : plan)
-            k_ntt_pass<true><<<(unsigned)p.blocks, NTT_THREADS, 0, c.stream>>>(d, p.M, p.b, p.Tlog, p.Glog,
-                                                                             p.twiddle, lo, hi);
+        for (size_t i = 0; i < plan.size(); i++) {
+            auto &p = plan[i];
+            int e = (i + 1 == plan.size()) ? epi : 0;
+            k_ntt_pass<true><<<(unsigned)p.blocks, NTT_THREADS, 0, c.stream>>>(d, L, p.M, p.b, p.Tlog, p.Glog,
+                                                                             p.twiddle, lo, hi, e, glo, ghi, scale);
+        }
     } else {
         for (int i = (int)plan.size() - 1; i >= 0; i--) {
             auto &p = plan[i];
-            k_ntt_pass<false><<<(unsigned)p.blocks, NTT_THREADS, 0, c.stream>>>(d, p.M, p.b, p.Tlog, p.Glog,
-                                                                              p.twiddle, lo, hi);
+            k_ntt_pass<false><<<(unsigned)p.blocks, NTT_THREADS, 0, c.stream>>>(d, L, p.M, p.b, p.Tlog, p.Glog,
+                                                                              p.twiddle, lo, hi, 0, glo, ghi, scale);
         }
     }
     MI_HIP(hipGetLastError());
+}
+
+void ntt_dif_coset_epilogue(Ctx &c, fr_t *d, unsigned log_n, bool inverse, bool inverse_gen, const fr_t &scale,
+                            bool to_canonical) {
+    ntt_run(c, d, log_n, inverse, true, to_canonical ? 2 : 1, inverse_gen, scale);
 }
 
 void ntt_dif(Ctx &c, fr_t *d, unsigned log_n, bool inverse) { ntt_run(c, d, log_n, inverse, true); }

@@ -707,15 +707,13 @@ ProofPoints groth16_prove(Ctx &c, const Srs &srs, const Circuit &circ, const fr_
     fr_t dinv = inverse(to_mont(dd));
     fr_t *vecs[3] = {a, b, cc};
     for (fr_t *x : vecs) {
-        ntt_dif(c, x, L, true);                         // ifft (bit-reversed coefficients)
-        coset_scale_bitrev(c, x, L, false, &dinv, false);  // * g^i / d
-        ntt_dit(c, x, L, false);                        // fft on the coset (natural order)
+        ntt_dif_coset_epilogue(c, x, L, true, false, dinv, false);  // ifft, then * g^i / d (bit-reversed)
+        ntt_dit(c, x, L, false);                                    // fft on the coset (natural order)
     }
     fr_t g = fr_small_mont(7);
     fr_t zinv = inverse(pow_u64(g, d) - fr_t::one());
     k_qap_divide<<<grid1(d), 256, 0, st>>>(a, b, cc, d, zinv);
-    ntt_dif(c, a, L, true);
-    coset_scale_bitrev(c, a, L, true, &dinv, true);  // icoset, canonical H (bit-reversed order)
+    ntt_dif_coset_epilogue(c, a, L, true, true, dinv, true);  // icoset, canonical H (bit-reversed order)
     g1_xyzz_t H, Lq, As, B1;
     g2_xyzz_t B2;
     msm_g1(c, srs.h_perm, a, nullptr, d - 1, &H);
