@@ -8,7 +8,8 @@
 //                     index | sign) pair per non-zero digit, laid out [window][point] (coalesced).
 //   2. radix sort   : rocPRIM onesweep per window over the c window-local key bits.
 //   3. k_bounds     : bucket start / end from the sorted keys.
-//   4. accumulation : buckets are cut into chunks of <= L sorted entries, one thread per chunk
+//   4. accumulation : buckets are cut into chunks of <= L sorted entries, one thread per chunk,
+//                     chunks length-sorted (6-7 bit radix sort) so a wave runs equal-length chunks
 //                     (mixed XYZZ += affine adds, point gathered by index); chunk partials of
 //                     the same bucket are summed by the same kernel shape level by level until
 //                     every bucket is one point.  Work per thread is bounded by L whatever the
@@ -27,7 +28,7 @@ namespace mi {
 
 namespace {
 
-constexpr uint32_t L0 = 32;  // sorted entries per chunk at level 0 (mixed adds)
+constexpr uint32_t L0_DEFAULT = 64;  // sorted entries per chunk at level 0 (mixed adds); MI_MSM_L0 overrides
 constexpr uint32_t L1 = 16;  // partials per chunk at levels >= 1 (full adds)
 
 MI_HD uint32_t word_of(const fr_t &s, unsigned k) {
@@ -104,16 +105,33 @@ struct MaxOp {
     __device__ __host__ uint32_t operator()(uint32_t a, uint32_t b) const { return a > b ? a : b; }
 };
 
+// Level-0 chunk lengths, keyed so a radix sort puts equal lengths next to each other: a wave then
+// runs chunks of (nearly) one length instead of "full chunks + remainders" (~69% lane use for
+// Poisson(32) buckets).  key = L0 - len (full chunks first).
+__global__ void k_chunk_len_keys(const uint32_t *__restrict__ chunk_bucket, const uint32_t *__restrict__ coff,
+                                 const uint32_t *__restrict__ cnt, uint32_t total, uint32_t L0,
+                                 uint32_t *__restrict__ keys, uint32_t *__restrict__ ids) {
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= total) return;
+    uint32_t b = chunk_bucket[t];
+    uint32_t local = t - coff[b];
+    uint32_t rest = cnt[b] - local * L0;
+    keys[t] = L0 - (rest < L0 ? rest : L0);
+    ids[t] = t;
+}
+
 template <class F>
-__global__ void __launch_bounds__(256) k_accum_level0(const uint32_t *__restrict__ chunk_bucket,
+__global__ void __launch_bounds__(256) k_accum_level0(const uint32_t *__restrict__ order,
+                                                      const uint32_t *__restrict__ chunk_bucket,
                                                       const uint32_t *__restrict__ coff,
                                                       const uint32_t *__restrict__ off,
-                                                      const uint32_t *__restrict__ cnt, uint32_t total,
+                                                      const uint32_t *__restrict__ cnt, uint32_t total, uint32_t L0,
                                                       const uint32_t *__restrict__ vals,
                                                       const Affine<F> *__restrict__ bases,
                                                       XYZZ<F> *__restrict__ out) {
-    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= total) return;
+    uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= total) return;
+    uint32_t t = order[u];  // chunk id, length-sorted
     uint32_t b = chunk_bucket[t];
     uint32_t local = t - coff[b];
     uint32_t beg = off[b] + local * L0;
@@ -271,6 +289,13 @@ void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const uint32_t
         MI_HIP(hipStreamSynchronize(st));
     }
 
+    static const uint32_t L0 = [] {
+        const char *e = getenv("MI_MSM_L0");
+        uint32_t v = e ? (uint32_t)atoi(e) : L0_DEFAULT;
+        return v >= 2 && v <= 1024 ? v : L0_DEFAULT;
+    }();
+    unsigned len_bits = 1;
+    while ((1u << len_bits) <= L0) len_bits++;
     XYZZ<F> *Pcur = nullptr;
     int pbuf = 10;
     bool level0 = true;
@@ -304,9 +329,21 @@ void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const uint32_t
             MI_HIP(hipcub::DeviceScan::InclusiveScan(tmp, tmp_bytes, heads, chunk_bucket, MaxOp(), total, st));
             XYZZ<F> *Pnext = c.scratch[pbuf].as<XYZZ<F>>(total);
             if (level0) {
+                // length-sorted chunk order (keys/vals scratch of the main sort are free by now)
+                uint32_t *lkeys = c.scratch[0].as<uint32_t>(total), *lids = c.scratch[1].as<uint32_t>(total);
+                uint32_t *lkeys_s = c.scratch[2].as<uint32_t>(total), *order = c.scratch[16].as<uint32_t>(total);
+                k_chunk_len_keys<<<grid_for(total, 256), 256, 0, st>>>(chunk_bucket, coff, cnt, total, L0, lkeys,
+                                                                      lids);
+                MI_LAUNCHED(c, "k_chunk_len_keys");
+                size_t tb = 0;
+                MI_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, lkeys, lkeys_s, lids, order, total, 0,
+                                                          len_bits, st));
+                void *tmp2 = c.scratch[4].get(tb);
+                MI_HIP(hipcub::DeviceRadixSort::SortPairs(tmp2, tb, lkeys, lkeys_s, lids, order, total, 0, len_bits,
+                                                          st));
                 ScopedTimer tacc(c, sizeof(F) == sizeof(fq_t) ? &c.stats.accum_g1 : &c.stats.accum_g2, n);
-                k_accum_level0<F><<<grid_for(total, 256), 256, 0, st>>>(chunk_bucket, coff, off, cnt, total, vals_s,
-                                                                         bases, Pnext);
+                k_accum_level0<F><<<grid_for(total, 256), 256, 0, st>>>(order, chunk_bucket, coff, off, cnt, total,
+                                                                         L0, vals_s, bases, Pnext);
                 MI_LAUNCHED(c, "k_accum_level0");
                 maxcnt = (maxcnt + L0 - 1) / L0;
             } else {
