@@ -24,11 +24,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "crypto3-fil-proofs_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# VALU bound of the accumulation kernel: v_mad_u64_u32 issue rate measured on MI355X by
-# crypto3-fil-proofs_amd/microbench/fieldmul.hip (29.99e12 lane-MADs/s), one 29-bit-limb Fq
-# multiplication = 392 MADs -> 76.5e9 Fq-mul/s; the same microbench sustains 79.4e9 on a
-# multiply-only loop, so MAD issue is the binding limit.
-MAD_RATE = 29.99e12
+# VALU bound of the accumulation kernel: v_mad_u64_u32 issue.  One wave64 MAD occupies its SIMD
+# for 4 cycles: 1024 SIMDs x 64 lanes / 4 x 2.4 GHz = 39.3e12 lane-MADs/s.  (The dependent-chain
+# microbench crypto3-fil-proofs_amd/microbench/madrate.hip sustains only 30.9e12 = 5.1 cycles,
+# because each chain waits on its own previous MAD; the accumulation kernel's ISA -- 3920 MADs
+# + ~1700 other VALU per mixed add, 14x29-bit limbs -- and its measured time imply the 4-cycle
+# rate.)  One Fq multiplication = 392 MADs -> 100.3e9 Fq-mul/s of pure MAD issue; the remaining
+# gap to it is the non-MAD instructions (carries, subtractions, selects).
+MAD_RATE = 1024 * 64 / 4 * 2.4e9
 FQ_MUL_MADS = 392
 FQ_MUL_PER_MIXED_ADD = {"G1": 10, "G2": 28}  # madd-2008-s: 8M + 2S over Fq / Fq2 (Karatsuba 3M, 2M per sqr)
 TOXIC_SEED = 0x5EED

@@ -10,14 +10,15 @@
 //   3. k_bounds     : bucket start / end from the sorted keys.
 //   4. accumulation : buckets are cut into chunks of <= L sorted entries, one thread per chunk,
 //                     chunks length-sorted (6-7 bit radix sort) so a wave runs equal-length chunks
-//                     (mixed XYZZ += affine adds, point gathered by index); chunk partials of
-//                     the same bucket are summed by the same kernel shape level by level until
-//                     every bucket is one point.  Work per thread is bounded by L whatever the
-//                     scalar distribution (boolean-heavy Filecoin witnesses put most entries in
-//                     bucket 1 of window 0).
-//   5. k_bucket_reduce: running-sum reduction sum_b (b+1) B_b over ~2^18 (G1) / 2^16 (G2) segments;
-//      k_seg_fold adds each segment's offset (s * seg_len) * run with a short double-and-add.
-//   6. k_sum_groups : per-window tree sum of the segment results.
+//                     (mixed XYZZ += affine adds, point gathered by index); the chunk partials
+//                     of buckets with several chunks are summed in place by a strided tree
+//                     (only those buckets take part).  Work per thread is bounded by L whatever
+//                     the scalar distribution (boolean-heavy Filecoin witnesses put most entries
+//                     in bucket 1 of window 0).
+//   5. k_bucket_reduce: running-sum reduction sum_b (b+1) B_b over ~2^20 (G1) / 2^18 (G2) segments,
+//      then a second running-sum level over the segment sums (k_bucket_reduce_dense), whose <= 8192
+//      segments per window are offset by a short double-and-add (k_seg_fold).
+//   6. k_sum_groups : stacked per-window tree sums; host combines W = sum acc + S (V - R).
 //   7. host         : Horner over windows (c doublings each) on the CPU.
 #pragma once
 #include <hipcub/hipcub.hpp>
@@ -29,7 +30,7 @@ namespace mi {
 namespace {
 
 constexpr uint32_t L0_DEFAULT = 64;  // sorted entries per chunk at level 0 (mixed adds); MI_MSM_L0 overrides
-constexpr uint32_t L1 = 16;  // partials per chunk at levels >= 1 (full adds)
+constexpr uint32_t L1 = 16;  // chunk partials summed per thread per tree level (full adds)
 
 MI_HD uint32_t word_of(const fr_t &s, unsigned k) {
     uint32_t r = 0;
@@ -147,27 +148,57 @@ __global__ void __launch_bounds__(256) k_accum_level0(const uint32_t *__restrict
     out[t] = acc;
 }
 
+// Buckets that span several level-0 chunks: their chunk partials P0[coff[b] + j] (j < ccnt[b]) are
+// summed in place by a strided tree, L1 partials per thread per level.  Only those buckets take
+// part (compacted list), so single-chunk buckets are never copied.
+__global__ void k_flag_multi(const uint32_t *__restrict__ ccnt, uint32_t nb, uint8_t *__restrict__ flag) {
+    uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    flag[b] = ccnt[b] > 1;
+}
+
+__global__ void k_tree_count(const uint32_t *__restrict__ mlist, const uint32_t *__restrict__ ccnt, uint32_t m,
+                             uint32_t stride, uint32_t *__restrict__ qcnt) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    uint32_t n = ccnt[mlist[i]];
+    uint32_t parts = (n + stride - 1) / stride;
+    qcnt[i] = (parts + L1 - 1) / L1;
+}
+
+__global__ void k_tree_heads(const uint32_t *__restrict__ qcnt, const uint32_t *__restrict__ qoff, uint32_t m,
+                             uint32_t *__restrict__ heads) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    if (qcnt[i]) heads[qoff[i]] = i;
+}
+
 template <class F>
-__global__ void __launch_bounds__(256) k_accum_level(const uint32_t *__restrict__ chunk_bucket,
-                                                     const uint32_t *__restrict__ coff,
-                                                     const uint32_t *__restrict__ off,
-                                                     const uint32_t *__restrict__ cnt, uint32_t total,
-                                                     const XYZZ<F> *__restrict__ in,
-                                                     XYZZ<F> *__restrict__ out) {
-    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= total) return;
-    uint32_t b = chunk_bucket[t];
-    uint32_t local = t - coff[b];
-    uint32_t beg = off[b] + local * L1;
-    uint32_t lim = local * L1 + L1 < cnt[b] ? local * L1 + L1 : cnt[b];
-    uint32_t end = off[b] + lim;
-    XYZZ<F> acc = in[beg];
-    for (uint32_t p = beg + 1; p < end; p++) acc = xyzz_add_inl(acc, in[p]);
-    out[t] = acc;
+__global__ void __launch_bounds__(256) k_tree_level(const uint32_t *__restrict__ map,
+                                                    const uint32_t *__restrict__ qoff,
+                                                    const uint32_t *__restrict__ mlist,
+                                                    const uint32_t *__restrict__ coff,
+                                                    const uint32_t *__restrict__ ccnt, uint32_t total,
+                                                    uint32_t stride, XYZZ<F> *__restrict__ P) {
+    uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= total) return;
+    uint32_t i = map[u];
+    uint32_t b = mlist[i];
+    uint32_t q = u - qoff[i];
+    uint32_t n = ccnt[b];
+    XYZZ<F> *base = P + coff[b];
+    uint64_t first = (uint64_t)q * L1 * stride;
+    XYZZ<F> acc = base[first];
+    for (uint32_t j = 1; j < L1; j++) {
+        uint64_t idx = first + (uint64_t)j * stride;
+        if (idx < n) acc = xyzz_add_inl(acc, base[idx]);
+    }
+    base[first] = acc;
 }
 
 // Running-sum reduction over one segment of seg_len buckets (all group-law code inlined):
 //   seg_run = sum_j B_j,  seg_acc = sum_j (j + 1) B_j   (j = bucket index inside the segment)
+// Bucket b's sum is P[off[b]] when cnt[b] != 0 (level-0 chunk slot of its first chunk).
 template <class F>
 __global__ void __launch_bounds__(256) k_bucket_reduce(const uint32_t *__restrict__ off,
                                                        const uint32_t *__restrict__ cnt,
@@ -185,6 +216,29 @@ __global__ void __launch_bounds__(256) k_bucket_reduce(const uint32_t *__restric
     }
     seg_acc[t] = acc;
     seg_run[t] = run;
+}
+
+// The same over a dense array of points (second level: the first level's segment sums), also
+// summing the first level's accumulators over the segment (sum_acc).
+template <class F>
+__global__ void __launch_bounds__(256) k_bucket_reduce_dense(const XYZZ<F> *__restrict__ P,
+                                                             const XYZZ<F> *__restrict__ A, uint32_t nseg_total,
+                                                             unsigned seg_len, XYZZ<F> *__restrict__ seg_acc,
+                                                             XYZZ<F> *__restrict__ seg_run,
+                                                             XYZZ<F> *__restrict__ sum_acc) {
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nseg_total) return;
+    const XYZZ<F> *p = P + (uint64_t)t * seg_len;
+    const XYZZ<F> *a = A + (uint64_t)t * seg_len;
+    XYZZ<F> run = XYZZ<F>::inf(), acc = XYZZ<F>::inf(), sa = XYZZ<F>::inf();
+    for (int j = (int)seg_len - 1; j >= 0; j--) {
+        run = xyzz_add_inl(run, p[j]);
+        acc = xyzz_add_inl(acc, run);
+        sa = xyzz_add_inl(sa, a[j]);
+    }
+    seg_acc[t] = acc;
+    seg_run[t] = run;
+    sum_acc[t] = sa;
 }
 
 // out[t] = seg_acc[t] + (s * seg_len) * seg_run[t], s = segment index inside its window
@@ -296,102 +350,140 @@ void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const uint32_t
     }();
     unsigned len_bits = 1;
     while ((1u << len_bits) <= L0) len_bits++;
-    XYZZ<F> *Pcur = nullptr;
-    int pbuf = 10;
-    bool level0 = true;
-    uint32_t *off = offA, *cnt = cntA, *coff = offB, *ccnt = cntB;
-    {
-        while (level0 || maxcnt > 1) {
-            uint32_t L = level0 ? L0 : L1;
-            k_chunk_count<<<grid_for(nb, 256), 256, 0, st>>>(cnt, nb, L, ccnt);
-            MI_LAUNCHED(c, "k_chunk_count");
-            size_t tmp_bytes = 0;
-            MI_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, ccnt, coff, nb, st));
-            void *tmp = c.scratch[4].get(tmp_bytes);
-            MI_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, ccnt, coff, nb, st));
+    uint32_t *coff = offB, *ccnt = cntB;
+    XYZZ<F> *P0 = nullptr;
+    {  // level 0: buckets cut into chunks of <= L0 sorted entries; one mixed-add chain per chunk
+        k_chunk_count<<<grid_for(nb, 256), 256, 0, st>>>(cntA, nb, L0, ccnt);
+        MI_LAUNCHED(c, "k_chunk_count");
+        size_t tmp_bytes = 0;
+        MI_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, ccnt, coff, nb, st));
+        void *tmp = c.scratch[4].get(tmp_bytes);
+        MI_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, ccnt, coff, nb, st));
+        uint32_t tail[2];
+        MI_HIP(hipMemcpyAsync(&tail[0], coff + nb - 1, 4, hipMemcpyDeviceToHost, st));
+        MI_HIP(hipMemcpyAsync(&tail[1], ccnt + nb - 1, 4, hipMemcpyDeviceToHost, st));
+        MI_HIP(hipStreamSynchronize(st));
+        uint32_t total = tail[0] + tail[1];
+        if (total == 0) {  // every scalar is zero
+            *result = XYZZ<F>::inf();
+            return;
+        }
+        uint32_t *heads = c.scratch[15].as<uint32_t>(total + 1);
+        uint32_t *chunk_bucket = c.scratch[13].as<uint32_t>(total + 1);
+        MI_HIP(hipMemsetAsync(heads, 0, sizeof(uint32_t) * (total + 1), st));
+        k_chunk_heads<<<grid_for(nb, 256), 256, 0, st>>>(ccnt, coff, nb, heads);
+        MI_LAUNCHED(c, "k_chunk_heads");
+        tmp_bytes = 0;
+        MI_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tmp_bytes, heads, chunk_bucket, MaxOp(), total, st));
+        tmp = c.scratch[4].get(tmp_bytes);
+        MI_HIP(hipcub::DeviceScan::InclusiveScan(tmp, tmp_bytes, heads, chunk_bucket, MaxOp(), total, st));
+        P0 = c.scratch[10].as<XYZZ<F>>(total);
+        // length-sorted chunk order (keys/vals scratch of the main sort are free by now)
+        uint32_t *lkeys = c.scratch[0].as<uint32_t>(total), *lids = c.scratch[1].as<uint32_t>(total);
+        uint32_t *lkeys_s = c.scratch[2].as<uint32_t>(total), *order = c.scratch[16].as<uint32_t>(total);
+        k_chunk_len_keys<<<grid_for(total, 256), 256, 0, st>>>(chunk_bucket, coff, cntA, total, L0, lkeys, lids);
+        MI_LAUNCHED(c, "k_chunk_len_keys");
+        size_t tb = 0;
+        MI_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, lkeys, lkeys_s, lids, order, total, 0, len_bits, st));
+        void *tmp2 = c.scratch[4].get(tb);
+        MI_HIP(hipcub::DeviceRadixSort::SortPairs(tmp2, tb, lkeys, lkeys_s, lids, order, total, 0, len_bits, st));
+        ScopedTimer tacc(c, sizeof(F) == sizeof(fq_t) ? &c.stats.accum_g1 : &c.stats.accum_g2, n);
+        k_accum_level0<F><<<grid_for(total, 256), 256, 0, st>>>(order, chunk_bucket, coff, offA, cntA, total, L0,
+                                                                 vals_s, bases, P0);
+        MI_LAUNCHED(c, "k_accum_level0");
+        MI_HIP(hipGetLastError());
+    }
+
+    const uint32_t maxchunks = (maxcnt + L0 - 1) / L0;
+    if (maxchunks > 1) {  // in-place strided tree over the chunk partials of multi-chunk buckets only
+        uint8_t *flag = c.scratch[1].as<uint8_t>(nb);
+        uint32_t *mlist = c.scratch[0].as<uint32_t>(nb);
+        uint32_t *dm = c.scratch[9].as<uint32_t>(4);
+        k_flag_multi<<<grid_for(nb, 256), 256, 0, st>>>(ccnt, nb, flag);
+        MI_LAUNCHED(c, "k_flag_multi");
+        size_t tb = 0;
+        hipcub::CountingInputIterator<uint32_t> ids(0);
+        MI_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, ids, flag, mlist, dm, nb, st));
+        void *tmp = c.scratch[4].get(tb);
+        MI_HIP(hipcub::DeviceSelect::Flagged(tmp, tb, ids, flag, mlist, dm, nb, st));
+        uint32_t m = 0;
+        MI_HIP(hipMemcpyAsync(&m, dm, 4, hipMemcpyDeviceToHost, st));
+        MI_HIP(hipStreamSynchronize(st));
+        uint32_t *qcnt = c.scratch[2].as<uint32_t>(m), *qoff = c.scratch[11].as<uint32_t>(m);
+        for (uint64_t stride = 1; stride < maxchunks; stride *= L1) {
+            k_tree_count<<<grid_for(m, 256), 256, 0, st>>>(mlist, ccnt, m, (uint32_t)stride, qcnt);
+            MI_LAUNCHED(c, "k_tree_count");
+            tb = 0;
+            MI_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, qcnt, qoff, m, st));
+            tmp = c.scratch[4].get(tb);
+            MI_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, qcnt, qoff, m, st));
             uint32_t tail[2];
-            MI_HIP(hipMemcpyAsync(&tail[0], coff + nb - 1, 4, hipMemcpyDeviceToHost, st));
-            MI_HIP(hipMemcpyAsync(&tail[1], ccnt + nb - 1, 4, hipMemcpyDeviceToHost, st));
+            MI_HIP(hipMemcpyAsync(&tail[0], qoff + m - 1, 4, hipMemcpyDeviceToHost, st));
+            MI_HIP(hipMemcpyAsync(&tail[1], qcnt + m - 1, 4, hipMemcpyDeviceToHost, st));
             MI_HIP(hipStreamSynchronize(st));
             uint32_t total = tail[0] + tail[1];
-            if (total == 0) {  // every scalar is zero
-                *result = XYZZ<F>::inf();
-                return;
-            }
-            uint32_t *heads = c.scratch[15].as<uint32_t>(total + 1);
-            uint32_t *chunk_bucket = c.scratch[13].as<uint32_t>(total + 1);
+            uint32_t *heads = c.scratch[15].as<uint32_t>(total + 1), *map = c.scratch[13].as<uint32_t>(total + 1);
             MI_HIP(hipMemsetAsync(heads, 0, sizeof(uint32_t) * (total + 1), st));
-            k_chunk_heads<<<grid_for(nb, 256), 256, 0, st>>>(ccnt, coff, nb, heads);
-            MI_LAUNCHED(c, "k_chunk_heads");
-            tmp_bytes = 0;
-            MI_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tmp_bytes, heads, chunk_bucket, MaxOp(), total, st));
-            tmp = c.scratch[4].get(tmp_bytes);
-            MI_HIP(hipcub::DeviceScan::InclusiveScan(tmp, tmp_bytes, heads, chunk_bucket, MaxOp(), total, st));
-            XYZZ<F> *Pnext = c.scratch[pbuf].as<XYZZ<F>>(total);
-            if (level0) {
-                // length-sorted chunk order (keys/vals scratch of the main sort are free by now)
-                uint32_t *lkeys = c.scratch[0].as<uint32_t>(total), *lids = c.scratch[1].as<uint32_t>(total);
-                uint32_t *lkeys_s = c.scratch[2].as<uint32_t>(total), *order = c.scratch[16].as<uint32_t>(total);
-                k_chunk_len_keys<<<grid_for(total, 256), 256, 0, st>>>(chunk_bucket, coff, cnt, total, L0, lkeys,
-                                                                      lids);
-                MI_LAUNCHED(c, "k_chunk_len_keys");
-                size_t tb = 0;
-                MI_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, lkeys, lkeys_s, lids, order, total, 0,
-                                                          len_bits, st));
-                void *tmp2 = c.scratch[4].get(tb);
-                MI_HIP(hipcub::DeviceRadixSort::SortPairs(tmp2, tb, lkeys, lkeys_s, lids, order, total, 0, len_bits,
-                                                          st));
-                ScopedTimer tacc(c, sizeof(F) == sizeof(fq_t) ? &c.stats.accum_g1 : &c.stats.accum_g2, n);
-                k_accum_level0<F><<<grid_for(total, 256), 256, 0, st>>>(order, chunk_bucket, coff, off, cnt, total,
-                                                                         L0, vals_s, bases, Pnext);
-                MI_LAUNCHED(c, "k_accum_level0");
-                maxcnt = (maxcnt + L0 - 1) / L0;
-            } else {
-                k_accum_level<F><<<grid_for(total, 256), 256, 0, st>>>(chunk_bucket, coff, off, cnt, total, Pcur,
-                                                                        Pnext);
-                MI_LAUNCHED(c, "k_accum_level");
-                maxcnt = (maxcnt + L1 - 1) / L1;
-            }
+            k_tree_heads<<<grid_for(m, 256), 256, 0, st>>>(qcnt, qoff, m, heads);
+            MI_LAUNCHED(c, "k_tree_heads");
+            tb = 0;
+            MI_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, heads, map, MaxOp(), total, st));
+            tmp = c.scratch[4].get(tb);
+            MI_HIP(hipcub::DeviceScan::InclusiveScan(tmp, tb, heads, map, MaxOp(), total, st));
+            k_tree_level<F><<<grid_for(total, 256), 256, 0, st>>>(map, qoff, mlist, coff, ccnt, total,
+                                                                   (uint32_t)stride, P0);
+            MI_LAUNCHED(c, "k_tree_level");
             MI_HIP(hipGetLastError());
-            Pcur = Pnext;
-            pbuf = pbuf == 10 ? 11 : 10;
-            std::swap(off, coff);
-            std::swap(cnt, ccnt);
-            level0 = false;
         }
     }
 
-    // bucket reduction: ~2^18 (G1) / 2^16 (G2: one wave per SIMD) threads of seg_len buckets each,
-    // then fold offsets (a double-and-add per segment, so fewer segments = less fold work), then tree-sum
-    const uint64_t seg_target = sizeof(F) == sizeof(fq_t) ? (1u << 18) : (1u << 16);
-    unsigned seg_len = 1;
-    while (seg_len < nbk && (uint64_t)nb / (seg_len * 2) >= seg_target) seg_len *= 2;
-    const uint32_t nseg = nbk / seg_len, nseg_total = nwin * nseg;
-    XYZZ<F> *seg_acc = c.scratch[12].as<XYZZ<F>>(2 * (uint64_t)nseg_total);
-    XYZZ<F> *seg_run = seg_acc + nseg_total;
-    k_bucket_reduce<F><<<grid_for(nseg_total, 256), 256, 0, st>>>(off, cnt, Pcur, nseg_total, seg_len, seg_acc,
-                                                                 seg_run);
+    // Bucket reduction, two running-sum levels (no per-segment scalar multiplication on the big level):
+    //   W = sum_b (b+1) B_b,  b = s*S + j:  W = sum_s accA_s + S * (V - R),
+    //   accA_s = sum_j (j+1) B_{sS+j},  runA_s = sum_j B_{sS+j},  R = sum_s runA_s,  V = sum_s (s+1) runA_s,
+    // V by a second running-sum level over runA (segments of SB) whose few segment offsets are folded
+    // by double-and-add (k_seg_fold).
+    const uint64_t segA_target = sizeof(F) == sizeof(fq_t) ? (1u << 20) : (1u << 18);
+    unsigned SA = 1;
+    while (SA < nbk && (uint64_t)nb / (SA * 2) >= segA_target) SA *= 2;
+    const uint32_t nsegA = nbk / SA, totA = nwin * nsegA;
+    const uint32_t nsegB = nsegA < 8192 ? nsegA : 8192, SB = nsegA / nsegB, totB = nwin * nsegB;
+    XYZZ<F> *accA = c.scratch[12].as<XYZZ<F>>(2 * (uint64_t)totA), *runA = accA + totA;
+    // [sumAccB | runB | foldB] contiguous (one stacked tree sum over 3 * nwin rows), then accB
+    XYZZ<F> *sumB = c.scratch[14].as<XYZZ<F>>(4 * (uint64_t)totB), *runB = sumB + totB, *foldB = runB + totB,
+            *accB = foldB + totB;
+    k_bucket_reduce<F><<<grid_for(totA, 256), 256, 0, st>>>(coff, cntA, P0, totA, SA, accA, runA);
     MI_LAUNCHED(c, "k_bucket_reduce");
-    XYZZ<F> *folded = c.scratch[14].as<XYZZ<F>>(nseg_total);
-    k_seg_fold<F><<<grid_for(nseg_total, 256), 256, 0, st>>>(seg_acc, seg_run, nseg_total, nseg, seg_len, folded);
+    k_bucket_reduce_dense<F><<<grid_for(totB, 256), 256, 0, st>>>(runA, accA, totB, SB, accB, runB, sumB);
+    MI_LAUNCHED(c, "k_bucket_reduce_dense");
+    k_seg_fold<F><<<grid_for(totB, 256), 256, 0, st>>>(accB, runB, totB, nsegB, SB, foldB);
     MI_LAUNCHED(c, "k_seg_fold");
     MI_HIP(hipGetLastError());
-    // per-window tree sum of nseg (a power of two) entries, groups of <= 32
-    XYZZ<F> *cur = folded, *nxt = seg_acc;
-    uint32_t per = nseg;
-    while (per > 1) {
-        unsigned G = per >= 32 ? 32 : per;
-        uint32_t outs = nwin * (per / G);
-        k_sum_groups<F><<<grid_for(outs, 256), 256, 0, st>>>(cur, outs, G, nxt);
+    // stacked per-row tree sum of nsegB (a power of two) entries, groups of <= 8 (shallow chains)
+    const uint32_t rows = 3 * nwin;
+    XYZZ<F> *tsum = c.scratch[11].as<XYZZ<F>>(2 * ((uint64_t)rows * nsegB / 2 + rows));
+    XYZZ<F> *bufs[2] = {tsum, tsum + (uint64_t)rows * nsegB / 2 + rows};
+    const XYZZ<F> *cur = sumB;
+    int k = 0;
+    for (uint32_t per = nsegB; per > 1;) {
+        unsigned G = per >= 8 ? 8 : per;
+        uint32_t outs = rows * (per / G);
+        k_sum_groups<F><<<grid_for(outs, 256), 256, 0, st>>>(cur, outs, G, bufs[k]);
         MI_LAUNCHED(c, "k_sum_groups");
         MI_HIP(hipGetLastError());
         per /= G;
-        std::swap(cur, nxt);
+        cur = bufs[k];
+        k ^= 1;
     }
-    XYZZ<F> *wsum = cur;
-    std::vector<XYZZ<F>> W(nwin);
-    MI_HIP(hipMemcpyAsync(W.data(), wsum, sizeof(XYZZ<F>) * nwin, hipMemcpyDeviceToHost, st));
+    std::vector<XYZZ<F>> sums(rows);
+    MI_HIP(hipMemcpyAsync(sums.data(), cur, sizeof(XYZZ<F>) * rows, hipMemcpyDeviceToHost, st));
     MI_HIP(hipStreamSynchronize(st));
+    std::vector<XYZZ<F>> W(nwin);
+    for (unsigned w = 0; w < nwin; w++) {  // W = SumA + SA * (V - R)
+        const XYZZ<F> &SumA = sums[w], &R = sums[nwin + w], &V = sums[2 * nwin + w];
+        XYZZ<F> t = xyzz_add(V, xyzz_neg(R));
+        for (unsigned sa = SA; sa > 1; sa >>= 1) t = xyzz_dbl(t);
+        W[w] = xyzz_add(SumA, t);
+    }
     XYZZ<F> acc = W[nwin - 1];
     for (int w = (int)nwin - 2; w >= 0; w--) {
         for (unsigned i = 0; i < cb; i++) acc = xyzz_dbl(acc);

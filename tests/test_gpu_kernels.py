@@ -146,3 +146,38 @@ def test_msm_g1_linearity_2_20(ctx, oracle):
         ss = [int(a) | int(b) << 64 | int(c) << 128 | int(d) << 192 for a, b, c, d in s[i:i + 4096]]
         acc = (acc + sum(x * y for x, y in zip(kk, ss))) % R
     assert got == oracle.g1_mul(oracle.g1_generator(), acc)
+
+
+def test_msm_g1_boolean_heavy_2_20(ctx, oracle):
+    """Boolean-heavy scalars (Filecoin witnesses): ~2^19 entries land in bucket 1 of window 0, so
+    the in-place chunk tree runs four levels.  Checked by linearity on bases k_i G."""
+    n = 1 << 20
+    rng = np.random.default_rng(7)
+    kw = rng.integers(0, 2**64, size=(n, 4), dtype=np.uint64)
+    kw[:, 3] &= np.uint64(0x3FFFFFFFFFFFFFFF)
+    kb = kw.tobytes()
+    bases = oracle.g1_fixed_base(kb)
+    sel = rng.integers(0, 16, size=n)
+    sw = np.zeros((n, 4), dtype=np.uint64)
+    sw[sel < 9, 0] = 1  # ~56% ones, ~6% random, rest zero
+    rnd = sel == 15
+    sw[rnd] = rng.integers(0, 2**64, size=(int(rnd.sum()), 4), dtype=np.uint64)
+    sw[rnd, 3] &= np.uint64(0x0FFFFFFFFFFFFFFF)
+    sb = sw.tobytes()
+    got = ctx.msm_g1(bases, sb)
+    acc = 0
+    for i in range(0, n, 4096):
+        kk = [int(a) | int(b) << 64 | int(c) << 128 | int(d) << 192 for a, b, c, d in kw[i:i + 4096]]
+        ss = [int(a) | int(b) << 64 | int(c) << 128 | int(d) << 192 for a, b, c, d in sw[i:i + 4096]]
+        acc = (acc + sum(x * y for x, y in zip(kk, ss))) % R
+    assert got == oracle.g1_mul(oracle.g1_generator(), acc)
+
+
+def test_msm_g2_boolean_heavy(ctx, oracle):
+    """G2 with one huge bucket (three tree levels) next to random scalars, against the oracle."""
+    n = 1 << 16
+    bases = _bases_g2(oracle, n, 555)
+    rng = random.Random(556)
+    sc = [1 if rng.random() < 0.8 else rng.randrange(R) for _ in range(n)]
+    sb = b"".join(s.to_bytes(32, "little") for s in sc)
+    assert ctx.msm_g2(bases, sb) == oracle.msm_g2(bases, sb)
