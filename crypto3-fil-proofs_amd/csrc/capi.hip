@@ -144,6 +144,7 @@ void mi_ctx_destroy(mi_ctx *ctx) {
     hipSetDevice(ctx->c.device);
     hipDeviceSynchronize();
     mi::ntt_free_tables(ctx->c);
+    mi::ctx_aux_free(ctx->c);
     for (auto &b : ctx->c.scratch) b.release();
     if (ctx->normal) hipStreamDestroy(ctx->normal);
     if (ctx->high) hipStreamDestroy(ctx->high);

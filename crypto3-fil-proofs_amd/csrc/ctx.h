@@ -79,6 +79,15 @@ struct Stats {
     KStat sort;                // digit extraction + radix sort + bucket bounds
     KStat ntt;                 // NTT passes (all launches of one transform)
     KStat prove;               // whole Groth16 prove (device part through host assembly)
+    void merge(const Stats &o) {
+        KStat *d[] = {&accum_g1, &accum_g2, &msm_g1, &msm_g2, &sort, &ntt, &prove};
+        const KStat *x[] = {&o.accum_g1, &o.accum_g2, &o.msm_g1, &o.msm_g2, &o.sort, &o.ntt, &o.prove};
+        for (int i = 0; i < 7; i++) {
+            d[i]->ms += x[i]->ms;
+            d[i]->launches += x[i]->launches;
+            d[i]->units += x[i]->units;
+        }
+    }
 };
 
 struct Ctx;
@@ -135,7 +144,17 @@ struct Ctx {
     DevBuf scratch[24];  // 0-15: MSM / NTT / upload temporaries, 20-21: prover vectors / staging
     Stats stats;
     EventTimer timer;
+    // Auxiliary lane: a second stream with its own scratch arena and timers, driven from a second
+    // host thread inside one prove so MSMs that do not depend on the NTT chain overlap it (the
+    // accumulation is VALU-bound, the NTT / sort phases are LDS- / HBM-bound).  Created on first
+    // use; ctx_aux_free releases it.
+    Ctx *aux = nullptr;
+    hipStream_t aux_streams[2] = {nullptr, nullptr};  // (in the aux ctx) normal, high priority
 };
+
+// the owner's auxiliary lane, its stream matched to the owner's current stream priority
+Ctx &ctx_aux(Ctx &c);
+void ctx_aux_free(Ctx &c);
 
 // Records a start event now and an end event at scope exit, on the ctx stream; no synchronisation.
 struct ScopedTimer {

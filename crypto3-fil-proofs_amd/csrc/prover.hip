@@ -16,6 +16,9 @@
 
 #include <string.h>
 
+#include <exception>
+#include <thread>
+
 #include "prover.h"
 
 namespace mi {
@@ -694,33 +697,64 @@ ProofPoints groth16_prove(Ctx &c, const Srs &srs, const Circuit &circ, const fr_
     ProofPoints out;
     {
     ScopedTimer whole(c, &c.stats.prove, circ.n);
-    fr_t *zm = c.scratch[20].as<fr_t>(nv + 3 * d);
-    fr_t *a = zm + nv, *b = a + d, *cc = b + d;
-    k_copy_to_mont<<<grid1(nv), 256, 0, st>>>(z_dev, zm, nv);
-    k_eval_rows<<<grid1(d), 256, 0, st>>>(circ.row_ptr[0], circ.col[0], circ.coeff[0], circ.row_ptr[1], circ.col[1],
-                                          circ.coeff[1], circ.row_ptr[2], circ.col[2], circ.coeff[2], zm, circ.n,
-                                          circ.n_in, d, a, b, cc);
-    MI_HIP(hipGetLastError());
-    fr_t dd = fr_t::zero();
-    dd.v[0] = (uint32_t)d;
-    dd.v[1] = (uint32_t)(d >> 32);
-    fr_t dinv = inverse(to_mont(dd));
-    fr_t *vecs[3] = {a, b, cc};
-    for (fr_t *x : vecs) {
-        ntt_dif_coset_epilogue(c, x, L, true, false, dinv, false);  // ifft, then * g^i / d (bit-reversed)
-        ntt_dit(c, x, L, false);                                    // fft on the coset (natural order)
-    }
-    fr_t g = fr_small_mont(7);
-    fr_t zinv = inverse(pow_u64(g, d) - fr_t::one());
-    k_qap_divide<<<grid1(d), 256, 0, st>>>(a, b, cc, d, zinv);
-    ntt_dif_coset_epilogue(c, a, L, true, true, dinv, true);  // icoset, canonical H (bit-reversed order)
     g1_xyzz_t H, Lq, As, B1;
     g2_xyzz_t B2;
-    msm_g1(c, srs.h_perm, a, nullptr, d - 1, &H);
-    msm_g1(c, srs.l, z_dev + circ.n_in, nullptr, circ.n_aux, &Lq);
-    msm_g1(c, srs.a, z_dev, circ.idx_a, circ.n_a, &As);
-    msm_g1(c, srs.b_g1, z_dev, circ.idx_b, circ.n_b, &B1);
-    msm_g2(c, srs.b_g2, z_dev, circ.idx_b, circ.n_b, &B2);
+    {
+        // L, B_G1 and B_G2 do not depend on the QAP: they run on the auxiliary lane (second stream,
+        // second host thread) while this stream runs the witness map, the NTT chain, H and A.
+        Ctx &x = ctx_aux(c);
+        hipEvent_t ready = x.timer.get(), done = x.timer.get();
+        MI_HIP(hipEventRecord(ready, st));  // z_dev and everything queued before this prove
+        MI_HIP(hipStreamWaitEvent(x.stream, ready, 0));
+        std::exception_ptr err;
+        std::thread lane([&] {
+            try {
+                MI_HIP(hipSetDevice(c.device));
+                msm_g1(x, srs.l, z_dev + circ.n_in, nullptr, circ.n_aux, &Lq);
+                msm_g1(x, srs.b_g1, z_dev, circ.idx_b, circ.n_b, &B1);
+                msm_g2(x, srs.b_g2, z_dev, circ.idx_b, circ.n_b, &B2);
+                MI_HIP(hipEventRecord(done, x.stream));
+            } catch (...) {
+                err = std::current_exception();
+            }
+        });
+        std::exception_ptr err_main;
+        try {
+            fr_t *zm = c.scratch[20].as<fr_t>(nv + 3 * d);
+            fr_t *a = zm + nv, *b = a + d, *cc = b + d;
+            k_copy_to_mont<<<grid1(nv), 256, 0, st>>>(z_dev, zm, nv);
+            k_eval_rows<<<grid1(d), 256, 0, st>>>(circ.row_ptr[0], circ.col[0], circ.coeff[0], circ.row_ptr[1],
+                                                  circ.col[1], circ.coeff[1], circ.row_ptr[2], circ.col[2],
+                                                  circ.coeff[2], zm, circ.n, circ.n_in, d, a, b, cc);
+            MI_HIP(hipGetLastError());
+            fr_t dd = fr_t::zero();
+            dd.v[0] = (uint32_t)d;
+            dd.v[1] = (uint32_t)(d >> 32);
+            fr_t dinv = inverse(to_mont(dd));
+            fr_t *vecs[3] = {a, b, cc};
+            for (fr_t *v : vecs) {
+                ntt_dif_coset_epilogue(c, v, L, true, false, dinv, false);  // ifft, then * g^i / d (bit-reversed)
+                ntt_dit(c, v, L, false);                                    // fft on the coset (natural order)
+            }
+            fr_t g = fr_small_mont(7);
+            fr_t zinv = inverse(pow_u64(g, d) - fr_t::one());
+            k_qap_divide<<<grid1(d), 256, 0, st>>>(a, b, cc, d, zinv);
+            ntt_dif_coset_epilogue(c, a, L, true, true, dinv, true);  // icoset, canonical H (bit-reversed order)
+            msm_g1(c, srs.h_perm, a, nullptr, d - 1, &H);
+            msm_g1(c, srs.a, z_dev, circ.idx_a, circ.n_a, &As);
+        } catch (...) {
+            err_main = std::current_exception();
+        }
+        lane.join();
+        if (err_main) std::rethrow_exception(err_main);
+        if (err) std::rethrow_exception(err);
+        MI_HIP(hipStreamWaitEvent(st, done, 0));  // the prove timer ends after both lanes
+        x.timer.pool.push_back(ready);
+        x.timer.pool.push_back(done);
+        x.timer.resolve();
+        c.stats.merge(x.stats);
+        x.stats = Stats();
+    }
     // assembly on the host
     fr_t rs = from_mont(to_mont(r) * to_mont(s));
     g1_xyzz_t A = xyzz_add(xyzz_add_affine(As, srs.alpha_g1), xyzz_mul(xyzz_from_affine(srs.delta_g1), r.v, 8));
@@ -739,6 +773,38 @@ ProofPoints groth16_prove(Ctx &c, const Srs &srs, const Circuit &circ, const fr_
     MI_HIP(hipStreamSynchronize(st));
     c.timer.resolve();
     return out;
+}
+
+Ctx &ctx_aux(Ctx &c) {
+    if (!c.aux) {
+        Ctx *x = new Ctx();
+        x->device = c.device;
+        try {
+            int lo = 0, hi = 0;
+            MI_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            MI_HIP(hipStreamCreateWithFlags(&x->aux_streams[0], hipStreamNonBlocking));
+            MI_HIP(hipStreamCreateWithPriority(&x->aux_streams[1], hipStreamNonBlocking, hi));
+        } catch (...) {
+            if (x->aux_streams[0]) hipStreamDestroy(x->aux_streams[0]);
+            delete x;
+            throw;
+        }
+        c.aux = x;
+    }
+    int prio = 0, lo = 0, hi = 0;
+    MI_HIP(hipStreamGetPriority(c.stream, &prio));
+    MI_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    c.aux->stream = (prio == hi && hi != lo) ? c.aux->aux_streams[1] : c.aux->aux_streams[0];
+    return *c.aux;
+}
+
+void ctx_aux_free(Ctx &c) {
+    if (!c.aux) return;
+    for (auto &b : c.aux->scratch) b.release();
+    for (auto s : c.aux->aux_streams)
+        if (s) hipStreamDestroy(s);
+    delete c.aux;
+    c.aux = nullptr;
 }
 
 static fr_t device_dot(Ctx &c, const fr_t *z, const fr_t *e, uint64_t off, uint64_t n) {
