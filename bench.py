@@ -37,6 +37,11 @@ FQ_MUL_PER_MIXED_ADD = {"G1": 10, "G2": 28}  # madd-2008-s: 8M + 2S over Fq / Fq
 TOXIC_SEED = 0x5EED
 
 
+def workload_name(log_rows):
+    cfg = {26: " (BASELINE config 3)", 27: " (BASELINE config 4 shape: 32 GiB PoRep-sized, d = 2^27)"}
+    return f"synthetic 2^{log_rows}-constraint R1CS full Groth16 prove" + cfg.get(log_rows, "")
+
+
 def splitmix_frs(seed, n):
     out = []
     s = seed & 0xFFFFFFFFFFFFFFFF
@@ -217,7 +222,7 @@ def main():
                     ps = json.load(open(os.path.join(prof_dir, fn)))
                     dk = ps.get("dominant_kernel", {})
                     if grp == "G1" and "hbm_bytes_per_point" in dk and ps.get("workload") == \
-                            f"synthetic 2^{args.log_rows}-constraint R1CS full Groth16 prove (BASELINE config 3)":
+                            workload_name(args.log_rows):
                         traffic = dk["hbm_bytes_per_point"] * units_per_launch
                         traffic_src = fn
                         break
@@ -245,7 +250,7 @@ def main():
         "dtype": "u32 limbs (Fq 381-bit / Fr 255-bit Montgomery)",
         "data": "synthetic R1CS + satisfying witness (csrc/synth.hip), proving key generated on device from "
                 "fixed toxic waste",
-        "config": {"workload": f"synthetic 2^{args.log_rows}-constraint R1CS full Groth16 prove (BASELINE config 3)",
+        "config": {"workload": workload_name(args.log_rows),
                    "constraints": n, "domain": circ.d, "num_inputs": sc.n_in, "num_aux": sc.n_aux,
                    "a_query": circ.n_a, "b_query": circ.n_b, "proofs_per_step": world,
                    "parallelism": f"partition-sharded x{world}"},

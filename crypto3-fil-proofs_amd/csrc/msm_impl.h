@@ -22,6 +22,7 @@
 //   7. host         : Horner over windows (c doublings each) on the CPU.
 #pragma once
 #include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include "ctx.h"
 
@@ -277,6 +278,18 @@ __global__ void __launch_bounds__(256) k_sum_groups(const XYZZ<F> *__restrict__ 
 
 inline unsigned grid_for(uint64_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
 
+// (bucket key, point index) pair sort of one window: rocPRIM onesweep with 11-bit places, so the
+// 22-bit keys of a 2^26 MSM take 2 places instead of 3 at the gfx950 default of 8 (-8% sort time).
+using onesweep11_cfg = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>, 11,
+                                        rocprim::block_radix_rank_algorithm::match>>;
+
+inline void sort_pairs_u32(void *tmp, size_t &bytes, const uint32_t *k_in, uint32_t *k_out, const uint32_t *v_in,
+                           uint32_t *v_out, uint32_t n, unsigned bits, hipStream_t st) {
+    MI_HIP(rocprim::radix_sort_pairs<onesweep11_cfg>(tmp, bytes, k_in, k_out, v_in, v_out, n, 0, bits, st));
+}
+
 }  // namespace
 
 template <class F>
@@ -315,13 +328,11 @@ void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const uint32_t
         MI_LAUNCHED(c, "k_digits");
         MI_HIP(hipGetLastError());
         size_t tmp_bytes = 0;
-        MI_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys, keys_s, vals, vals_s, (uint32_t)n, 0,
-                                                  key_bits, st));
+        sort_pairs_u32(nullptr, tmp_bytes, keys, keys_s, vals, vals_s, (uint32_t)n, key_bits, st);
         void *tmp = c.scratch[4].get(tmp_bytes);
         for (unsigned w = 0; w < nwin; w++) {
             uint64_t o = (uint64_t)w * n;
-            MI_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys + o, keys_s + o, vals + o, vals_s + o,
-                                                      (uint32_t)n, 0, key_bits, st));
+            sort_pairs_u32(tmp, tmp_bytes, keys + o, keys_s + o, vals + o, vals_s + o, (uint32_t)n, key_bits, st);
         }
         MI_HIP(hipMemsetAsync(offA, 0, sizeof(uint32_t) * nb, st));
         MI_HIP(hipMemsetAsync(cntA, 0, sizeof(uint32_t) * nb, st));

@@ -38,7 +38,8 @@ __device__ __forceinline__ uint32_t brev(uint32_t x, unsigned bits) {
 
 // One pass.  DIF: load -> b DIF stages -> optional inter-pass twiddle -> [epilogue] -> store.
 //            DIT: load -> optional inter-pass twiddle -> b DIT stages (reverse) -> store.
-// In-tile twiddles omega_{2^b}^j (j < 2^(b-1)) are staged into LDS once per workgroup.
+// In-tile twiddles omega_{2^b}^j come from the 512-entry omega_1024 table (16 KiB, L1-resident), so
+// the tile is the only LDS use (32 KiB: 5 workgroups per CU).
 // Epilogue (last DIF pass only): epi = 1 multiplies the element at global position pos by
 // G^bitrev_L(pos) * scale (coset shift of the bit-reversed coefficients, fused 1/d); epi = 2 also
 // converts to canonical form (icoset: H for the MSM).
@@ -46,11 +47,11 @@ template <bool DIF>
 __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(fr_t *__restrict__ d, unsigned L, unsigned M, unsigned b,
                                                           unsigned Tlog, unsigned Glog, int twiddle,
                                                           const fr_t *__restrict__ lo,
-                                                          const fr_t *__restrict__ hi, int epi,
+                                                          const fr_t *__restrict__ hi,
+                                                          const fr_t *__restrict__ tw10, int epi,
                                                           const fr_t *__restrict__ glo,
                                                           const fr_t *__restrict__ ghi, fr_t scale) {
     __shared__ fr_t sh[TILE];
-    __shared__ fr_t tw[TILE / 2];
     const unsigned T = 1u << Tlog;
     const unsigned Slog = M - b;
     const uint64_t S = 1ull << Slog;
@@ -66,7 +67,6 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(fr_t *__restrict__ d, 
         i20 = (blockIdx.x % blocks_per_sub) << Tlog;
     }
     const unsigned bmask = (1u << b) - 1;
-    for (unsigned j = threadIdx.x; j < (1u << (b - 1)); j += NTT_THREADS) tw[j] = hi[j << (16 - b)];
     // load
     for (unsigned e = threadIdx.x; e < tile; e += NTT_THREADS) {
         unsigned t = e & (T - 1), i1 = (e >> Tlog) & bmask, g = e >> (Tlog + b);
@@ -99,9 +99,9 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(fr_t *__restrict__ d, 
             if (DIF) {
                 fr_t dd = u - v;
                 sh[e0] = u + v;
-                sh[e1] = j ? dd * tw[j] : dd;
+                sh[e1] = j ? dd * tw10[j << (TILE_LOG - b)] : dd;
             } else {
-                fr_t w = j ? v * tw[j] : v;
+                fr_t w = j ? v * tw10[j << (TILE_LOG - b)] : v;
                 sh[e0] = u + w;
                 sh[e1] = u - w;
             }
@@ -251,11 +251,19 @@ void ntt_init_tables(Ctx &c) {
         MI_HIP(hipMalloc(dst[k][1], sizeof(fr_t) * 65536));
         MI_HIP(hipMemcpy(*dst[k][0], lo.data(), sizeof(fr_t) * 65536, hipMemcpyHostToDevice));
         MI_HIP(hipMemcpy(*dst[k][1], hi.data(), sizeof(fr_t) * 65536, hipMemcpyHostToDevice));
+        if (k < 2) {  // omega_1024^j = HI[j * 64] (HI[h] = omega_{2^16}^h), j < 512
+            std::vector<fr_t> t10(TILE / 2);
+            for (unsigned j = 0; j < TILE / 2; j++) t10[j] = hi[j << (16 - TILE_LOG)];
+            fr_t **p10 = k == 0 ? &c.tw.fw_1024 : &c.tw.iv_1024;
+            MI_HIP(hipMalloc(p10, sizeof(fr_t) * (TILE / 2)));
+            MI_HIP(hipMemcpy(*p10, t10.data(), sizeof(fr_t) * (TILE / 2), hipMemcpyHostToDevice));
+        }
     }
 }
 
 void ntt_free_tables(Ctx &c) {
-    fr_t *ps[8] = {c.tw.fw_lo, c.tw.fw_hi, c.tw.iv_lo, c.tw.iv_hi, c.tw.g_lo, c.tw.g_hi, c.tw.gi_lo, c.tw.gi_hi};
+    fr_t *ps[10] = {c.tw.fw_lo, c.tw.fw_hi, c.tw.iv_lo, c.tw.iv_hi, c.tw.g_lo,   c.tw.g_hi,
+                    c.tw.gi_lo, c.tw.gi_hi, c.tw.fw_1024, c.tw.iv_1024};
     for (auto p : ps)
         if (p) hipFree(p);
     c.tw = NttTables();
@@ -277,19 +285,22 @@ static void ntt_run(Ctx &c, fr_t *d, unsigned L, bool inverse, bool dif, int epi
     const fr_t *hi = inverse ? c.tw.iv_hi : c.tw.fw_hi;
     const fr_t *glo = inv_gen ? c.tw.gi_lo : c.tw.g_lo;
     const fr_t *ghi = inv_gen ? c.tw.gi_hi : c.tw.g_hi;
+    const fr_t *tw10 = inverse ? c.tw.iv_1024 : c.tw.fw_1024;
     auto plan = plan_passes(L);
     if (dif) {
         for (size_t i = 0; i < plan.size(); i++) {
             auto &p = plan[i];
             int e = (i + 1 == plan.size()) ? epi : 0;
             k_ntt_pass<true><<<(unsigned)p.blocks, NTT_THREADS, 0, c.stream>>>(d, L, p.M, p.b, p.Tlog, p.Glog,
-                                                                             p.twiddle, lo, hi, e, glo, ghi, scale);
+                                                                                 p.twiddle, lo, hi, tw10, e, glo,
+                                                                                 ghi, scale);
         }
     } else {
         for (int i = (int)plan.size() - 1; i >= 0; i--) {
             auto &p = plan[i];
             k_ntt_pass<false><<<(unsigned)p.blocks, NTT_THREADS, 0, c.stream>>>(d, L, p.M, p.b, p.Tlog, p.Glog,
-                                                                              p.twiddle, lo, hi, 0, glo, ghi, scale);
+                                                                                  p.twiddle, lo, hi, tw10, 0, glo,
+                                                                                  ghi, scale);
         }
     }
     MI_HIP(hipGetLastError());

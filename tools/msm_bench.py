@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Standalone G1 MSM timing over the resident h-query points of a generated 2^L proving key
+(random dense scalars, device-resident), with the library's phase timers (sort / accumulation /
+whole MSM).  Used to tune MSM phases in isolation from the two-lane prove.
+
+    python tools/msm_bench.py --log-rows 26 --reps 3
+"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "crypto3-fil-proofs_amd"))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--log-rows", type=int, default=26)
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+    import fil_groth16 as fg
+    from fil_groth16 import synth
+    from bench import TOXIC_SEED, splitmix_frs
+
+    ctx = fg.Context(0)
+    sc = synth.SynthCircuit(a.log_rows, 4, 1)
+    circ = sc.load(ctx)
+    pk = fg.generate_random_parameters(ctx, circ, splitmix_frs(TOXIC_SEED, 5))
+    n = pk.n_h
+    pts = pk.points(0)
+    rng = np.random.default_rng(7)
+    sw = rng.integers(0, 2**64, size=(n, 4), dtype=np.uint64)
+    sw[:, 3] &= np.uint64(0x3FFFFFFFFFFFFFFF)
+    s_dev = torch.from_numpy(sw.view(np.uint8).reshape(-1)).to("cuda")
+    pts.msm_dev(s_dev.data_ptr(), n)
+    ctx.synchronize()
+    ctx.reset_stats()
+    t = time.perf_counter()
+    for _ in range(a.reps):
+        pts.msm_dev(s_dev.data_ptr(), n)
+    ctx.synchronize()
+    dt = (time.perf_counter() - t) / a.reps * 1e3
+    st = ctx.stats()
+    per = {k: round(st[k]["ms"] / a.reps, 2) for k in ("sort", "accum_g1", "msm_g1")}
+    print(f"G1 MSM n={n}: {dt:.1f} ms wall ({n / dt / 1e3:.1f} Mpts/s); per MSM {per}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
