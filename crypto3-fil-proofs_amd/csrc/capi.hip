@@ -2,7 +2,11 @@
 // wire formats, owns object lifetimes, serialises each context and turns C++ exceptions into
 // status codes + mi_last_error().  No CPU fallback exists: every compute entry point runs the
 // HIP kernels of this library or fails.
+#include <fcntl.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <string>
 
@@ -43,6 +47,9 @@ int guard(Fn &&f) {
     } catch (const std::invalid_argument &e) {
         g_err = e.what();
         return MI_ERR_ARG;
+    } catch (const std::domain_error &e) {
+        g_err = e.what();
+        return MI_ERR_INVALID_POINT;
     } catch (const std::length_error &e) {
         g_err = e.what();
         return MI_ERR_SIZE;
@@ -57,6 +64,73 @@ int guard(Fn &&f) {
 
 void need(bool cond, const char *msg) {
     if (!cond) throw std::invalid_argument(msg);
+}
+
+// ---- bellman / filecoin Groth16 parameter files (v28-*.params, *.vk) ----------------------
+// Parameters::write: vk (MI_VK_BYTES) | u32 BE n_ic | ic (96 B each) | then for h, l, a, b_g1
+// (96 B points) and b_g2 (192 B points): u32 BE count | points.  The reference mmaps the file and
+// keeps offsets (core/crypto/mapped_scheme_params.hpp:43-84, read_cached_params at
+// core/parameter_cache.hpp:125-129).
+struct ParamsLayout {
+    uint64_t n[6] = {0, 0, 0, 0, 0, 0};    // ic, h, l, a, b_g1, b_g2
+    uint64_t off[6] = {0, 0, 0, 0, 0, 0};  // byte offset of the first point of each vector
+};
+
+uint32_t be32(const uint8_t *p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
+
+ParamsLayout parse_params(const uint8_t *p, uint64_t len) {
+    static const uint64_t esz[6] = {96, 96, 96, 96, 96, 192};
+    static const char *names[6] = {"ic", "h", "l", "a", "b_g1", "b_g2"};
+    ParamsLayout L;
+    uint64_t o = MI_VK_BYTES;
+    if (len < o) throw std::invalid_argument("params file truncated in the verifying key");
+    for (int i = 0; i < 6; i++) {
+        if (len - o < 4) throw std::invalid_argument(std::string("params file truncated before the ") + names[i] +
+                                                     " length");
+        L.n[i] = be32(p + o);
+        o += 4;
+        L.off[i] = o;
+        if ((len - o) / esz[i] < L.n[i])
+            throw std::invalid_argument(std::string("params file truncated in the ") + names[i] + " points");
+        o += esz[i] * L.n[i];
+    }
+    if (o != len) throw std::invalid_argument("params file has trailing bytes after b_g2");
+    return L;
+}
+
+struct MappedFile {
+    int fd = -1;
+    void *p = nullptr;
+    uint64_t len = 0;
+    explicit MappedFile(const char *path) {
+        fd = open(path, O_RDONLY);
+        if (fd < 0) throw std::invalid_argument(std::string("cannot open ") + path);
+        struct stat st;
+        if (fstat(fd, &st) != 0) throw std::runtime_error(std::string("cannot stat ") + path);
+        len = (uint64_t)st.st_size;
+        if (len) {
+            p = mmap(nullptr, len, PROT_READ, MAP_PRIVATE, fd, 0);
+            if (p == MAP_FAILED) {
+                p = nullptr;
+                throw std::runtime_error(std::string("cannot mmap ") + path);
+            }
+            madvise(p, len, MADV_SEQUENTIAL);
+        }
+    }
+    ~MappedFile() {
+        if (p) munmap(p, len);
+        if (fd >= 0) close(fd);
+    }
+    const uint8_t *data() const { return (const uint8_t *)p; }
+};
+
+void write_all(FILE *f, const void *p, size_t n) {
+    if (n && fwrite(p, 1, n, f) != n) throw std::runtime_error("short write");
+}
+void write_be32(FILE *f, uint64_t v) {
+    if (v > 0xffffffffull) throw std::length_error("vector too long for a u32 length");
+    uint8_t b[4] = {(uint8_t)(v >> 24), (uint8_t)(v >> 16), (uint8_t)(v >> 8), (uint8_t)v};
+    write_all(f, b, 4);
 }
 
 struct CtxLock {
@@ -560,5 +634,129 @@ int mi_ctx_reset_stats(mi_ctx *ctx) {
     });
 }
 unsigned mi_msm_window_bits(uint64_t n) { return mi::msm_window_bits(n); }
+
+// ---- verification (host) ---------------------------------------------------------------------
+int mi_groth16_verify(const uint8_t *vk, const uint8_t *ic, uint64_t n_ic, const uint8_t *inputs,
+                      const uint8_t proof[MI_PROOF_BYTES], int *valid) {
+    return guard([&] {
+        need(vk && ic && proof && valid && (n_ic <= 1 || inputs), "null argument");
+        *valid = 0;
+        *valid = mi::groth16_verify(vk, ic, n_ic, inputs, proof) ? 1 : 0;
+    });
+}
+
+int mi_groth16_verify_batch(const uint8_t *vk, const uint8_t *ic, uint64_t n_ic, uint64_t count,
+                            const uint8_t *inputs, const uint8_t *proofs, const uint8_t *seed32, int *valid) {
+    return guard([&] {
+        need(vk && ic && valid && (count == 0 || proofs) && (count == 0 || n_ic <= 1 || inputs), "null argument");
+        *valid = 0;
+        *valid = mi::groth16_verify_batch(vk, ic, n_ic, count, inputs, proofs, seed32) ? 1 : 0;
+    });
+}
+
+int mi_pairing(const uint8_t g1_96[96], const uint8_t g2_192[192], uint8_t out[576]) {
+    return guard([&] {
+        need(g1_96 && g2_192 && out, "null argument");
+        mi::g1_affine_t p;
+        mi::g2_affine_t q;
+        if (!mi::g1_decode_host(g1_96, p) || !mi::g2_decode_host(g2_192, q))
+            throw std::domain_error("invalid point encoding");
+        mi::fq_t f[12];
+        mi::pairing_host(p, q, f);
+        for (int i = 0; i < 12; i++) {
+            mi::fq32_t raw = mi::fq_to_raw(f[i]);
+            for (int w = 0; w < 12; w++)
+                for (int b = 0; b < 4; b++) out[48 * i + 4 * (11 - w) + b] = (uint8_t)(raw.v[w] >> (24 - 8 * b));
+        }
+    });
+}
+
+// ---- parameter files -------------------------------------------------------------------------
+int mi_params_inspect(const char *path, uint64_t out[6]) {
+    return guard([&] {
+        need(path && out, "null argument");
+        MappedFile f(path);
+        ParamsLayout L = parse_params(f.data(), f.len);
+        for (int i = 0; i < 6; i++) out[i] = L.n[i];
+    });
+}
+
+int mi_params_load(mi_ctx *ctx, const mi_circuit *circ, const char *path, int checked, mi_srs **out) {
+    int rc = MI_OK;
+    int prc = guard([&] {
+        need(ctx && path && out, "null argument");
+        *out = nullptr;
+        MappedFile f(path);
+        ParamsLayout L = parse_params(f.data(), f.len);
+        const uint8_t *b = f.data();
+        mi_srs_host h{};
+        h.vk = b;
+        h.ic = b + L.off[0];
+        h.n_ic = L.n[0];
+        h.h = b + L.off[1];
+        h.n_h = L.n[1];
+        h.l = b + L.off[2];
+        h.n_l = L.n[2];
+        h.a = b + L.off[3];
+        h.n_a = L.n[3];
+        h.b_g1 = b + L.off[4];
+        h.n_b_g1 = L.n[4];
+        h.b_g2 = b + L.off[5];
+        h.n_b_g2 = L.n[5];
+        rc = mi_srs_load(ctx, circ, &h, checked, out);  // sets the error text itself on failure
+    });
+    return prc != MI_OK ? prc : rc;
+}
+
+int mi_params_write(mi_ctx *ctx, const mi_srs *srs, const char *path) {
+    return guard([&] {
+        need(ctx && srs && path, "null argument");
+        uint64_t info[6];
+        if (mi_srs_info(srs, info) != MI_OK) throw std::runtime_error(g_err);
+        // info: d, |h|, |l|, |a|, |b|, |ic|
+        std::vector<uint8_t> vk(MI_VK_BYTES), ic(96 * info[5]);
+        if (mi_srs_export_vk(srs, vk.data(), ic.data()) != MI_OK) throw std::runtime_error(g_err);
+        FILE *f = fopen(path, "wb");
+        if (!f) throw std::invalid_argument(std::string("cannot create ") + path);
+        try {
+            write_all(f, vk.data(), vk.size());
+            write_be32(f, info[5]);
+            write_all(f, ic.data(), ic.size());
+            const uint64_t counts[5] = {info[1], info[2], info[3], info[4], info[4]};
+            for (int which = 0; which < 5; which++) {
+                std::vector<uint8_t> buf((which == 4 ? 192 : 96) * counts[which]);
+                if (mi_srs_export_query(ctx, srs, which, buf.data(), counts[which]) != MI_OK)
+                    throw std::runtime_error(g_err);
+                write_be32(f, counts[which]);
+                write_all(f, buf.data(), buf.size());
+            }
+        } catch (...) {
+            fclose(f);
+            throw;
+        }
+        if (fclose(f) != 0) throw std::runtime_error("close failed");
+    });
+}
+
+int mi_vk_write(const mi_srs *srs, const char *path) {
+    return guard([&] {
+        need(srs && path, "null argument");
+        uint64_t info[6];
+        if (mi_srs_info(srs, info) != MI_OK) throw std::runtime_error(g_err);
+        std::vector<uint8_t> vk(MI_VK_BYTES), ic(96 * info[5]);
+        if (mi_srs_export_vk(srs, vk.data(), ic.data()) != MI_OK) throw std::runtime_error(g_err);
+        FILE *f = fopen(path, "wb");
+        if (!f) throw std::invalid_argument(std::string("cannot create ") + path);
+        try {
+            write_all(f, vk.data(), vk.size());
+            write_be32(f, info[5]);
+            write_all(f, ic.data(), ic.size());
+        } catch (...) {
+            fclose(f);
+            throw;
+        }
+        if (fclose(f) != 0) throw std::runtime_error("close failed");
+    });
+}
 
 }  // extern "C"

@@ -80,6 +80,15 @@ void g2_encode(const g2_affine_t &a, uint8_t out[192]);
 bool g1_decode_host(const uint8_t in[96], g1_affine_t &out);
 bool g2_decode_host(const uint8_t in[192], g2_affine_t &out);
 fr_t fr_from_le(const uint8_t in[32]);  // canonical raw (not Montgomery)
+
+// Groth16 verification on the host (verify.hip).  vk: MI_VK_BYTES uncompressed, ic: n_ic x 96 B,
+// inputs: (n_ic - 1) x 32 B LE canonical (without the implicit ONE), proof: 192 B compressed.
+// Throws std::domain_error for undecodable / off-curve / non-subgroup points.
+bool groth16_verify(const uint8_t *vk, const uint8_t *ic, uint64_t n_ic, const uint8_t *inputs,
+                    const uint8_t proof[192]);
+bool groth16_verify_batch(const uint8_t *vk, const uint8_t *ic, uint64_t n_ic, uint64_t count, const uint8_t *inputs,
+                          const uint8_t *proofs, const uint8_t *seed32);
+void pairing_host(const g1_affine_t &p, const g2_affine_t &q, fq_t out[12]);
 void fr_to_le(const fr_t &raw, uint8_t out[32]);
 
 }  // namespace mi

@@ -1,6 +1,7 @@
 // prove_synthetic.cpp -- C++ host example over include/mi355x_groth16.hpp: builds a synthetic
 // R1CS (mi_synth), generates a proving key on the GPU from fixed toxic waste, and runs the
-// compound_proof::circuit_proofs partition loop.  Prints one hex proof per partition.
+// compound_proof::circuit_proofs partition loop, self-verifies the MultiProof (api/seal.hpp:310-313)
+// and prints one hex proof per partition.
 //
 //   g++ -std=c++17 -I../../include prove_synthetic.cpp -L../build -lfilgpu -o prove_synthetic
 //   ./prove_synthetic <log_rows> <partitions>
@@ -38,6 +39,13 @@ int main(int argc, char **argv) {
             blind[k].second[0] = (uint8_t)(200 + k);
         }
         mi355x::multi_proof mp = mi355x::circuit_proofs(ctx, pk, circ, assignments, blind);
+        // seal_commit_phase2 never returns a proof that does not verify (api/seal.hpp:310-313)
+        std::vector<std::vector<mi355x::fr32>> inputs(parts);
+        for (int k = 0; k < parts; k++) inputs[k].assign(z.begin() + 1, z.begin() + cs.num_inputs);
+        if (!mp.verify(inputs)) {
+            fprintf(stderr, "post-seal verification sanity check failed\n");
+            return 2;
+        }
         for (auto &p : mp.circuit_proofs) {
             for (uint8_t b : p) printf("%02x", b);
             printf("\n");

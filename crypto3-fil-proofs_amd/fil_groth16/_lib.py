@@ -20,6 +20,8 @@ EXPORTS = [
     "mi_msm_g1_dev", "mi_msm_g2_dev", "mi_ntt_fr_dev",
     "mi_ctx_get_stats", "mi_ctx_reset_stats", "mi_msm_window_bits",
     "mi_synth_generate", "mi_synth_r1cs", "mi_synth_witness", "mi_synth_free",
+    "mi_params_inspect", "mi_params_load", "mi_params_write", "mi_vk_write",
+    "mi_groth16_verify", "mi_groth16_verify_batch", "mi_pairing",
 ]
 
 _lib = None
@@ -94,6 +96,13 @@ def lib():
         "mi_synth_r1cs": ([vp, vp], c_int),
         "mi_synth_witness": ([vp, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(u64)], c_int),
         "mi_synth_free": ([vp], None),
+        "mi_params_inspect": ([u8p, vp], c_int),
+        "mi_params_load": ([vp, vp, u8p, c_int, pp], c_int),
+        "mi_params_write": ([vp, vp, u8p], c_int),
+        "mi_vk_write": ([vp, u8p], c_int),
+        "mi_groth16_verify": ([u8p, u8p, u64, u8p, u8p, ctypes.POINTER(c_int)], c_int),
+        "mi_groth16_verify_batch": ([u8p, u8p, u64, u64, u8p, u8p, u8p, ctypes.POINTER(c_int)], c_int),
+        "mi_pairing": ([u8p, u8p, vp], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

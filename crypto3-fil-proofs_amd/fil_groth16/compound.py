@@ -5,10 +5,13 @@
                                   one Groth16 proof per partition / vanilla proof
   MultiProof                      multi_proof{circuit_proofs, verifying_key} (core/proof/multi_proof.hpp:38-58)
                                   serialised as P x 192 bytes (api/seal.hpp:306-308, constants.hpp:93)
+  MultiProof.verify               verify_seal's Groth16 batch check of all partitions (api/seal.hpp:339-485)
+  seal_commit_phase2_proofs       the C2 tail (api/seal.hpp:296-313): circuit_proofs -> MultiProof ->
+                                  self-verification ("post-seal verification sanity check failed")
   get_partitions_for_window_post  libs/filecoin/src/api/post.cpp:37-46
   shard_partitions                one process per GPU: partition k goes to rank k % world
 """
-from .core import PROOF_BYTES, prove
+from .core import PROOF_BYTES, prove, verify_batch
 
 
 def partition_count(partitions: int) -> int:
@@ -42,6 +45,16 @@ class MultiProof:
             assert len(p) == PROOF_BYTES
         return b"".join(self.circuit_proofs)
 
+    def verify(self, public_inputs, seed=None) -> bool:
+        """Batch-verify every partition proof against ``verifying_key`` = (vk, ic) with the per-partition
+        public inputs (without ONE).  One multi-pairing, random weights from ``seed``."""
+        if self.verifying_key is None:
+            raise ValueError("multi-proof has no verifying key")
+        vk, ic = self.verifying_key
+        if len(public_inputs) != len(self.circuit_proofs):
+            raise ValueError("one public-input vector per partition is required")
+        return verify_batch(vk, ic, list(public_inputs), self.circuit_proofs, seed)
+
     @classmethod
     def from_bytes(cls, buf: bytes, verifying_key=None):
         if len(buf) % PROOF_BYTES:
@@ -56,6 +69,18 @@ def circuit_proofs(ctx, pk, circuit, witnesses, blindings, priority=False):
     if len(witnesses) != len(blindings):
         raise ValueError("one (r, s) pair per partition is required")
     return [prove(ctx, pk, circuit, z, r, s, priority=priority) for z, (r, s) in zip(witnesses, blindings)]
+
+
+def seal_commit_phase2_proofs(ctx, pk, circuit, witnesses, blindings, num_inputs, priority=False) -> bytes:
+    """api/seal.hpp:296-313: prove every partition, pack the MultiProof buffer and refuse to return
+    one that does not verify.  ``witnesses`` are full assignments (ONE first); the public inputs of
+    partition k are its witness entries 1 .. num_inputs - 1."""
+    proofs = circuit_proofs(ctx, pk, circuit, witnesses, blindings, priority=priority)
+    mp = MultiProof(proofs, pk.verifying_key())
+    inputs = [bytes(z[32:32 * num_inputs]) for z in witnesses]
+    if not mp.verify(inputs):
+        raise RuntimeError("post-seal verification sanity check failed")
+    return mp.to_bytes()
 
 
 def shard_partitions(num_partitions: int, rank: int, world: int):

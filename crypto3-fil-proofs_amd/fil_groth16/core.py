@@ -13,6 +13,7 @@ Reference names kept (paths relative to the reference root):
 Errors raise ``FilGpuError`` (the reference asserts / throws: compound_proof.hpp:94).
 """
 import ctypes
+import os
 
 import numpy as np
 
@@ -219,6 +220,23 @@ class ProvingKey:
                                 ctypes.byref(hd)))
         return cls(ctx, hd)
 
+    @classmethod
+    def load_params(cls, ctx: Context, circuit, path: str, checked=True):
+        """Upload a bellman / filecoin ``v28-*.params`` file (mmapped, streamed to the device) --
+        read_cached_params / get_groth_params (core/parameter_cache.hpp:125-129,185-200)."""
+        hd = ctypes.c_void_p()
+        check(lib().mi_params_load(ctx.h, circuit.h if circuit is not None else None, os.fsencode(path),
+                                   int(checked), ctypes.byref(hd)))
+        return cls(ctx, hd)
+
+    def write_params(self, path: str):
+        """bellman Parameters::write (write_cached_params, core/parameter_cache.hpp:146-152)."""
+        check(lib().mi_params_write(self.ctx.h, self.h, os.fsencode(path)))
+
+    def write_vk(self, path: str):
+        """bellman VerifyingKey::write (write_cached_verifying_key, core/parameter_cache.hpp:136-144)."""
+        check(lib().mi_vk_write(self.h, os.fsencode(path)))
+
     def verifying_key(self):
         vk = ctypes.create_string_buffer(VK_BYTES)
         ic = ctypes.create_string_buffer(96 * self.n_ic)
@@ -244,6 +262,42 @@ class ProvingKey:
             lib().mi_srs_free(self.h)
         except Exception:
             pass
+
+
+def verify(vk: bytes, ic: bytes, inputs: bytes, proof: bytes) -> bool:
+    """bellman verify_proof on the host (the C2 self-check, api/seal.hpp:310-313).  ``inputs`` are the
+    public inputs without the implicit ONE, 32 B LE each (len(ic) / 96 - 1 of them)."""
+    n_ic = len(ic) // 96
+    assert len(vk) == VK_BYTES and len(inputs) == 32 * (n_ic - 1) and len(proof) == PROOF_BYTES
+    ok = ctypes.c_int(0)
+    check(lib().mi_groth16_verify(vk, ic, n_ic, inputs or None, proof, ctypes.byref(ok)))
+    return bool(ok.value)
+
+
+def verify_batch(vk: bytes, ic: bytes, inputs, proofs, seed: bytes = None) -> bool:
+    """bellman verify_proofs_batch (verify_batch_seal, api/seal.hpp:339-485): one multi-pairing with
+    random 128-bit weights drawn from ``seed`` (32 B; None = OS randomness)."""
+    n_ic = len(ic) // 96
+    assert len(inputs) == len(proofs) and all(len(x) == 32 * (n_ic - 1) for x in inputs)
+    assert seed is None or len(seed) == 32
+    ok = ctypes.c_int(0)
+    check(lib().mi_groth16_verify_batch(vk, ic, n_ic, len(proofs), b"".join(inputs) or None,
+                                        b"".join(proofs) or None, seed, ctypes.byref(ok)))
+    return bool(ok.value)
+
+
+def pairing(g1_96: bytes, g2_192: bytes) -> bytes:
+    """Reduced optimal-ate pairing e(P, Q): 12 x 48 B big-endian Fq coefficients (w^0..w^5 basis)."""
+    out = ctypes.create_string_buffer(576)
+    check(lib().mi_pairing(bytes(g1_96), bytes(g2_192), out))
+    return out.raw
+
+
+def params_inspect(path: str) -> dict:
+    """Vector lengths of a params file (no device needed): ic, h, l, a, b_g1, b_g2."""
+    out = (ctypes.c_uint64 * 6)()
+    check(lib().mi_params_inspect(os.fsencode(path), out))
+    return dict(zip(("ic", "h", "l", "a", "b_g1", "b_g2"), list(out)))
 
 
 def generate_random_parameters(ctx: Context, circuit: Circuit, toxic) -> ProvingKey:

@@ -119,6 +119,38 @@ int mi_srs_export_query(mi_ctx *ctx, const mi_srs *srs, int which, uint8_t *out,
 int mi_srs_info(const mi_srs *srs, uint64_t out[6]);
 void mi_srs_free(mi_srs *srs);
 
+/* ---- verification (host CPU; no device needed) ----
+ *   mi_groth16_verify       <- crypto3 r1cs_gg_ppzksnark verify / bellman verify_proof, used by the
+ *                              self-check of every C2 proof (api/seal.hpp:310-313) and verify_seal
+ *   mi_groth16_verify_batch <- bellman verify_proofs_batch behind verify_batch_seal (api/seal.hpp:339-485);
+ *                              seed32 = randomness of the linear combination (NULL: std::random_device)
+ * vk: MI_VK_BYTES, ic: n_ic x 96 B (uncompressed); inputs: (n_ic - 1) x 32 B LE canonical public
+ * inputs WITHOUT the implicit ONE (generate_public_inputs order), per proof; proofs: 192 B each.
+ * *valid = 1 / 0.  Undecodable, off-curve or non-subgroup proof points: MI_ERR_INVALID_POINT;
+ * non-canonical inputs: MI_ERR_ARG.
+ *   mi_pairing              <- the reduced optimal-ate pairing e(P, Q) (tests: bilinearity); out =
+ *                              12 x 48 B big-endian Fq coefficients on the basis w^0..w^5 (Fq2 = c0, c1). */
+int mi_groth16_verify(const uint8_t *vk, const uint8_t *ic, uint64_t n_ic, const uint8_t *inputs,
+                      const uint8_t proof[MI_PROOF_BYTES], int *valid);
+int mi_groth16_verify_batch(const uint8_t *vk, const uint8_t *ic, uint64_t n_ic, uint64_t count,
+                            const uint8_t *inputs, const uint8_t *proofs, const uint8_t *seed32, int *valid);
+int mi_pairing(const uint8_t g1_96[96], const uint8_t g2_192[192], uint8_t out[576]);
+
+/* ---- parameter files (bellman Parameters::write layout = filecoin v28-*.params) ----
+ *   mi_params_inspect <- the header walk of mapped_scheme_params::build_mapped_parameters
+ *                        (core/crypto/mapped_scheme_params.hpp:43-84); no device needed:
+ *                        out = n_ic, n_h, n_l, n_a, n_b_g1, n_b_g2
+ *   mi_params_load    <- read_cached_params / get_groth_params (core/parameter_cache.hpp:125-129,185-200):
+ *                        mmap + upload once, resident on the device; checked -> point validation
+ *   mi_params_write   <- write_cached_params (core/parameter_cache.hpp:146-152; bellman Parameters::write)
+ *   mi_vk_write       <- write_cached_verifying_key (core/parameter_cache.hpp:136-144; bellman VerifyingKey::write: vk | u32 BE n_ic | ic)
+ * Malformed files (truncated, trailing bytes) fail with MI_ERR_ARG. */
+int mi_params_inspect(const char *path, uint64_t out[6]);
+int mi_params_load(mi_ctx *ctx, const mi_circuit *circuit_or_null, const char *path, int checked,
+                   mi_srs **out);
+int mi_params_write(mi_ctx *ctx, const mi_srs *srs, const char *path);
+int mi_vk_write(const mi_srs *srs, const char *path);
+
 /* ---- Groth16 ---- */
 /* z: (num_inputs + num_aux) x 32 B, z[0] = ONE.  r, s: injected blinding (tests / parity);
  * priority != 0 runs on the context's high-priority stream (post_config.priority,

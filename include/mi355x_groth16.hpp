@@ -75,6 +75,15 @@ public:
     proving_key(context &ctx, const circuit *c, const mi_srs_host &host, bool checked) {
         check(mi_srs_load(ctx.get(), c ? c->get() : nullptr, &host, checked ? 1 : 0, &h_));
     }
+    // a bellman / filecoin v28-*.params file: mmapped and streamed to the device once
+    // (read_cached_params / get_groth_params, core/parameter_cache.hpp:125-129,185-200)
+    static proving_key from_params_file(context &ctx, const circuit *c, const std::string &path, bool checked) {
+        mi_srs *h = nullptr;
+        check(mi_params_load(ctx.get(), c ? c->get() : nullptr, path.c_str(), checked ? 1 : 0, &h));
+        return proving_key(h);
+    }
+    void write_params(context &ctx, const std::string &path) const { check(mi_params_write(ctx.get(), h_, path.c_str())); }
+    void write_vk(const std::string &path) const { check(mi_vk_write(h_, path.c_str())); }
     // groth16::generate_random_parameters with known toxic waste (tests / benches)
     static proving_key generate(context &ctx, const circuit &c, const std::array<fr32, 5> &toxic) {
         std::array<uint8_t, 160> t;
@@ -92,6 +101,13 @@ public:
         check(mi_srs_export_vk(h_, vk.data(), nullptr));
         return vk;
     }
+    std::vector<uint8_t> ic() const {
+        uint64_t info[6];
+        check(mi_srs_info(h_, info));
+        std::vector<uint8_t> out(96 * info[5]);
+        check(mi_srs_export_vk(h_, nullptr, out.data()));
+        return out;
+    }
 
 private:
     explicit proving_key(mi_srs *h) : h_(h) {}
@@ -108,9 +124,35 @@ inline proof_bytes prove(context &ctx, const proving_key &pk, const circuit &c, 
     return out;
 }
 
+// bellman verify_proof on the host; inputs = public inputs without ONE (generate_public_inputs order)
+inline bool verify(const std::vector<uint8_t> &vk, const std::vector<uint8_t> &ic, const std::vector<fr32> &inputs,
+                   const proof_bytes &proof) {
+    if (ic.size() / 96 != inputs.size() + 1) throw error(MI_ERR_ARG, "inputs.size() must be |ic| - 1");
+    int ok = 0;
+    check(mi_groth16_verify(vk.data(), ic.data(), ic.size() / 96, inputs.empty() ? nullptr : inputs.front().data(),
+                            proof.data(), &ok));
+    return ok != 0;
+}
+
 struct multi_proof {
     std::vector<proof_bytes> circuit_proofs;
     std::vector<uint8_t> verifying_key;
+    std::vector<uint8_t> ic;
+    // verify_seal's batch check over all partitions (api/seal.hpp:339-485); seed: 32 B or nullptr
+    bool verify(const std::vector<std::vector<fr32>> &public_inputs, const uint8_t *seed32 = nullptr) const {
+        if (public_inputs.size() != circuit_proofs.size()) throw error(MI_ERR_ARG, "one input vector per partition");
+        std::vector<uint8_t> in, pr;
+        for (auto &v : public_inputs) {
+            if (v.size() + 1 != ic.size() / 96) throw error(MI_ERR_ARG, "inputs.size() must be |ic| - 1");
+            for (auto &x : v) in.insert(in.end(), x.begin(), x.end());
+        }
+        for (auto &p : circuit_proofs) pr.insert(pr.end(), p.begin(), p.end());
+        int ok = 0;
+        check(mi_groth16_verify_batch(verifying_key.data(), ic.data(), ic.size() / 96, circuit_proofs.size(),
+                                      in.empty() ? nullptr : in.data(), pr.empty() ? nullptr : pr.data(), seed32,
+                                      &ok));
+        return ok != 0;
+    }
     std::vector<uint8_t> write() const {  // api/seal.hpp:306-308
         std::vector<uint8_t> buf;
         buf.reserve(circuit_proofs.size() * MI_PROOF_BYTES);
@@ -131,6 +173,7 @@ inline multi_proof circuit_proofs(context &ctx, const proving_key &pk, const cir
         mp.circuit_proofs.push_back(
             prove(ctx, pk, c, partition_assignments[k], blindings[k].first, blindings[k].second, priority));
     mp.verifying_key = pk.verifying_key();
+    mp.ic = pk.ic();
     return mp;
 }
 

@@ -141,3 +141,51 @@ def test_groth16_trapdoor_2_20(ctx, oracle):
     assert raw[288:] == oracle.g1_mul(g1, c)
     vk, ic = pk.verifying_key()
     assert oracle.groth16_verify(vk, ic, sc.z_bytes()[:32 * sc.n_in], raw)
+
+
+@pytest.mark.parametrize("name", ["random_11_24", "toy_chain_1022"])
+def test_groth16_params_file_roundtrip(ctx, oracle, golden, name, tmp_path):
+    """v28-style params files: a file written in bellman's layout from the oracle key loads through
+    mi_params_load and proves the golden bytes; the GPU-generated key written by mi_params_write is
+    byte-identical to it, and so is the verifying-key file."""
+    import params_io
+
+    g = golden["groth16"][name]
+    n_in, n_aux, rows, z = _circuit_from_name(name)
+    oc, gc = _load(ctx, oracle, n_in, n_aux, rows, z)
+    ex = oracle.OracleParams(oc, circuits.toxic()).export()
+    ref = params_io.params_bytes(ex)
+    p_ref = tmp_path / "oracle.params"
+    p_ref.write_bytes(ref)
+    pk = fg.ProvingKey.load_params(ctx, gc, str(p_ref), checked=True)
+    r, s = circuits.blinding()
+    assert fg.prove(ctx, pk, gc, circuits.z_bytes(z), r, s).hex() == g["proof"]
+    gen = fg.generate_random_parameters(ctx, gc, circuits.toxic())
+    p_gen, p_vk = tmp_path / "gpu.params", tmp_path / "gpu.vk"
+    gen.write_params(str(p_gen))
+    gen.write_vk(str(p_vk))
+    assert p_gen.read_bytes() == ref
+    assert p_vk.read_bytes() == params_io.vk_bytes(ex)
+    bad = tmp_path / "bad.params"
+    bad.write_bytes(ref[:-1])
+    with pytest.raises(fg.FilGpuError):
+        fg.ProvingKey.load_params(ctx, gc, str(bad))
+
+
+def test_seal_commit_phase2_self_verifies(ctx, oracle):
+    """api/seal.hpp:296-313: partition proofs -> MultiProof -> batch self-verification; a partition
+    with an unsatisfied witness makes the whole C2 call fail instead of returning a bad proof."""
+    n_in, n_aux, rows, z = circuits.random_circuit(61, 500, n_in=5)
+    oc, gc = _load(ctx, oracle, n_in, n_aux, rows, z)
+    pk = fg.generate_random_parameters(ctx, gc, circuits.toxic())
+    zb = circuits.z_bytes(z)
+    blind = [(11 + k, 22 + k) for k in range(3)]
+    buf = fg.seal_commit_phase2_proofs(ctx, pk, gc, [zb] * 3, blind, n_in)
+    assert len(buf) == 3 * 192
+    vk, ic = pk.verifying_key()
+    for k in range(3):
+        assert fg.verify(vk, ic, zb[32:32 * n_in], buf[192 * k:192 * (k + 1)])
+    bad = bytearray(zb)
+    bad[-32] ^= 1
+    with pytest.raises(RuntimeError, match="sanity check failed"):
+        fg.seal_commit_phase2_proofs(ctx, pk, gc, [zb, bytes(bad), zb], blind, n_in)
