@@ -104,7 +104,7 @@ MI_HD XYZZ<F> xyzz_add_affine_inl(const XYZZ<F> &p, const Affine<F> &q) {
     F Q = p.X * PP;
     XYZZ<F> r;
     r.X = sqr(R) - PPP - dbl(Q);
-    r.Y = R * (Q - r.X) - p.Y * PPP;
+    r.Y = mul_add(R, Q - r.X, -p.Y, PPP);  // R (Q - X3) - Y1 PPP, one reduction
     r.ZZ = p.ZZ * PP;
     r.ZZZ = p.ZZZ * PPP;
     return r;
@@ -134,7 +134,7 @@ MI_HD XYZZ<F> xyzz_add_inl(const XYZZ<F> &p, const XYZZ<F> &q) {
     F Q = U1 * PP;
     XYZZ<F> r;
     r.X = sqr(R) - PPP - dbl(Q);
-    r.Y = R * (Q - r.X) - S1 * PPP;
+    r.Y = mul_add(R, Q - r.X, -S1, PPP);
     r.ZZ = p.ZZ * q.ZZ * PP;
     r.ZZZ = p.ZZZ * q.ZZZ * PPP;
     return r;

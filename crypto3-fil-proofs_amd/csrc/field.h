@@ -421,6 +421,40 @@ MI_HD fq_t operator*(const fq_t &a, const fq_t &b) {
 }
 MI_HD fq_t sqr(const fq_t &a) { return a * a; }
 
+// a*b + c*d with ONE Montgomery reduction (the group law's "X * Y - Z * W" with c = -Z in lazy
+// form): 392 + 196 MADs instead of 2 x 392 plus a subtraction.  Column sums stay below 2^64:
+// <= 28 products < 2^58 + 14 reduction products < 2^58 + a carry < 2^35 (42 * 2^58 < 2^63.4).
+// Output < (8p^2 + R p) / R < 2p for inputs in [0, 2p) since 8p < R = 2^406.
+MI_HD fq_t mul_add(const fq_t &a, const fq_t &b, const fq_t &c, const fq_t &d) {
+    constexpr int L = 14;
+    uint32_t m[L];
+    fq_t r;
+    uint64_t acc = 0;
+    MI_UNROLL for (int k = 0; k < L; k++) {
+        MI_UNROLL for (int i = 0; i < k; i++) {
+            acc += (uint64_t)a.v[i] * b.v[k - i];
+            acc += (uint64_t)c.v[i] * d.v[k - i];
+            acc += (uint64_t)m[i] * Fq29::P[k - i];
+        }
+        acc += (uint64_t)a.v[k] * b.v[0];
+        acc += (uint64_t)c.v[k] * d.v[0];
+        m[k] = ((uint32_t)acc * Fq29::INV) & Fq29::M;
+        acc += (uint64_t)m[k] * Fq29::P[0];
+        acc >>= 29;
+    }
+    MI_UNROLL for (int k = L; k < 2 * L - 1; k++) {
+        MI_UNROLL for (int i = k - L + 1; i < L; i++) {
+            acc += (uint64_t)a.v[i] * b.v[k - i];
+            acc += (uint64_t)c.v[i] * d.v[k - i];
+            acc += (uint64_t)m[i] * Fq29::P[k - i];
+        }
+        r.v[k - L] = (uint32_t)acc & Fq29::M;
+        acc >>= 29;
+    }
+    r.v[L - 1] = (uint32_t)acc;
+    return r;
+}
+
 // canonical 12 x 32-bit integer (< p) -> Montgomery
 MI_HD fq_t fq_from_raw(const fq32_t &raw) {
     fq_t t;
@@ -487,6 +521,7 @@ MI_HD fq2_t operator*(const fq2_t &a, const fq2_t &b) {  // Karatsuba, 3 Fq mult
     fq_t t = (a.c0 + a.c1) * (b.c0 + b.c1);
     return {v0 - v1, t - v0 - v1};
 }
+MI_HD fq2_t mul_add(const fq2_t &a, const fq2_t &b, const fq2_t &c, const fq2_t &d) { return a * b + c * d; }
 MI_HD fq2_t sqr(const fq2_t &a) {  // (a0 + a1)(a0 - a1), 2 a0 a1: 2 Fq mults
     fq_t t = a.c0 * a.c1;
     return {(a.c0 + a.c1) * (a.c0 - a.c1), t + t};
