@@ -48,6 +48,17 @@ def counter_per_dispatch(pmc_dir, counter, kernel_substr):
     return [v for _, v in vals]
 
 
+def step_launch_avg_ms(trace_dir, kernel_substr, bench):
+    """Average duration of the dominant kernel over the launches of the TIMED steps only (the
+    launch order is warmup proves, timed proves, standalone MSMs), to set beside bench.py's own
+    HIP-event average ("roofline.avg_launch_ms")."""
+    rows = [r for r in csv.DictReader(open(_one(trace_dir, "*kernel_trace.csv"))) if kernel_substr in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows]
+    lo, hi = 4 * bench["warmup"], 4 * (bench["warmup"] + bench["steps"])
+    return sum(d[lo:hi]) / max(hi - lo, 1), [round(x, 3) for x in d]
+
+
 def g1_launch_points(bench):
     """points processed by each k_accum_level0<G1> launch of `bench.py --warmup 1 --steps 1`:
     per prove H, L, A, B_G1; then the standalone MSM (1 warm + msm_reps)."""
@@ -76,6 +87,12 @@ def main():
     dom = next(k for k in out["kernels"] if args.kernel in k["kernel"])
     out["dominant_kernel"] = {"name": args.kernel, "calls": dom["calls"], "avg_ms": dom["avg_ms"],
                               "total_ms": dom["total_ms"]}
+    try:
+        avg, per = step_launch_avg_ms(args.trace, args.kernel, bench)
+        out["dominant_kernel"].update({"timed_step_launch_avg_ms": avg, "launch_ms": per,
+                                       "bench_hip_event_avg_launch_ms": bench["roofline"]["avg_launch_ms"]})
+    except FileNotFoundError:
+        pass
     if args.fetch and args.write:
         f = counter_per_dispatch(args.fetch, "FETCH_SIZE", args.kernel)
         w = counter_per_dispatch(args.write, "WRITE_SIZE", args.kernel)
