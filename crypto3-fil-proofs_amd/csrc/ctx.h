@@ -209,7 +209,21 @@ void scale_all(Ctx &c, fr_t *d, uint64_t n, const fr_t &s);
 void fr_to_mont_inplace(Ctx &c, fr_t *d, uint64_t n);
 void fr_from_mont_inplace(Ctx &c, fr_t *d, uint64_t n);
 
-// ---- MSM (msm.hip) ----
+// ---- MSM (msm_impl.h, msm_g1.hip, msm_g2.hip) ----
+// Scalar-side state of one MSM (digits sorted into buckets, chunked, chunk order): depends only on
+// the scalars, so MSMs over the same scalars with different bases (B_G1 and B_G2 of one prove)
+// share it.  Pointers are into the ctx scratch arena; valid until the next msm_prepare on the ctx.
+struct MsmPlan {
+    uint64_t n = 0;
+    unsigned cb = 0, nwin = 0;
+    uint32_t nbk = 0, nb = 0, L0 = 0, maxcnt = 0, total = 0;
+    const uint32_t *vals_s = nullptr, *off = nullptr, *cnt = nullptr, *coff = nullptr, *ccnt = nullptr,
+                   *chunk_bucket = nullptr, *order = nullptr;
+};
+// false when every scalar is zero (the MSM is the identity)
+bool msm_prepare(Ctx &c, const fr_t *scalars, const uint32_t *idx, uint64_t n, MsmPlan &plan);
+void msm_g1_planned(Ctx &c, const MsmPlan &plan, const g1_affine_t *bases, g1_xyzz_t *result_host);
+void msm_g2_planned(Ctx &c, const MsmPlan &plan, const g2_affine_t *bases, g2_xyzz_t *result_host);
 // result = sum_i scalar[idx ? idx[i] : i] * bases[i]; scalars canonical (raw) Fr.
 void msm_g1(Ctx &c, const g1_affine_t *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,
             g1_xyzz_t *result_host);

@@ -23,4 +23,17 @@ void msm_g1(Ctx &c, const g1_affine_t *bases, const fr_t *scalars, const uint32_
     msm_run<fq_t>(c, bases, scalars, idx, n, result_host);
 }
 
+bool msm_prepare(Ctx &c, const fr_t *scalars, const uint32_t *idx, uint64_t n, MsmPlan &plan) {
+    return msm_prepare_impl(c, scalars, idx, n, plan);
+}
+
+void msm_g1_planned(Ctx &c, const MsmPlan &plan, const g1_affine_t *bases, g1_xyzz_t *result_host) {
+    if (!plan.total) {
+        *result_host = g1_xyzz_t::inf();
+        return;
+    }
+    ScopedTimer whole(c, &c.stats.msm_g1, plan.n);  // scalar-side phase timed by msm_prepare's caller
+    msm_accumulate_impl<fq_t>(c, plan, bases, result_host);
+}
+
 }  // namespace mi

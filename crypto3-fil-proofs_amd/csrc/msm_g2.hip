@@ -8,4 +8,13 @@ void msm_g2(Ctx &c, const g2_affine_t *bases, const fr_t *scalars, const uint32_
     msm_run<fq2_t>(c, bases, scalars, idx, n, result_host);
 }
 
+void msm_g2_planned(Ctx &c, const MsmPlan &plan, const g2_affine_t *bases, g2_xyzz_t *result_host) {
+    if (!plan.total) {
+        *result_host = g2_xyzz_t::inf();
+        return;
+    }
+    ScopedTimer whole(c, &c.stats.msm_g2, plan.n);  // scalar-side phase timed by msm_prepare's caller
+    msm_accumulate_impl<fq2_t>(c, plan, bases, result_host);
+}
+
 }  // namespace mi

@@ -70,17 +70,36 @@ __global__ void k_digits(const fr_t *__restrict__ scalars, const uint32_t *__res
     }
 }
 
-// keys are window-local (sorted per window): global bucket = window * nbk + key
-__global__ void k_bounds(const uint32_t *__restrict__ keys, uint32_t np, uint32_t n, uint32_t nbk,
-                         uint32_t *__restrict__ start, uint32_t *__restrict__ cnt) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= np) return;
-    uint32_t k = keys[i];
-    if (k == nbk) return;  // zero digit
-    uint32_t w = i / n, lo = w * n, hi = lo + n;
-    uint32_t g = w * nbk + k;
-    if (i == lo || keys[i - 1] != k) start[g] = i;
-    if (i + 1 == hi || keys[i + 1] != k) cnt[g] = i + 1;  // end; converted to a count below
+// keys are window-local (sorted per window): global bucket = window * nbk + key.  Four sorted keys
+// per thread (one 16-byte load); the neighbours across the group edge are single loads (L2 hits).
+__global__ void k_bounds4(const uint32_t *__restrict__ keys, uint32_t np, uint32_t n, uint32_t nbk,
+                          uint32_t *__restrict__ start, uint32_t *__restrict__ cnt) {
+    uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t i0 = q * 4;
+    if (i0 >= np) return;
+    uint32_t k[6];
+    k[0] = i0 ? keys[i0 - 1] : 0xffffffffu;
+    if (i0 + 4 <= np) {
+        uint4 v = *reinterpret_cast<const uint4 *>(keys + i0);
+        k[1] = v.x, k[2] = v.y, k[3] = v.z, k[4] = v.w;
+    } else {
+        MI_UNROLL for (int j = 0; j < 4; j++) k[1 + j] = i0 + j < np ? keys[i0 + j] : 0xffffffffu;
+    }
+    k[5] = i0 + 4 < np ? keys[i0 + 4] : 0xffffffffu;
+    uint32_t w = i0 / n, lo = w * n;
+    MI_UNROLL for (int j = 0; j < 4; j++) {
+        uint32_t i = i0 + j;
+        if (i >= np) break;
+        if (i >= lo + n) {
+            w++;
+            lo += n;
+        }
+        uint32_t kk = k[1 + j];
+        if (kk == nbk) continue;  // zero digit
+        uint32_t g = w * nbk + kk;
+        if (i == lo || k[j] != kk) start[g] = i;
+        if (i + 1 == lo + n || k[2 + j] != kk) cnt[g] = i + 1;  // end; converted to a count below
+    }
 }
 
 __global__ void k_end_to_cnt(const uint32_t *__restrict__ start, uint32_t *__restrict__ cnt, uint32_t nb) {
@@ -292,15 +311,15 @@ inline void sort_pairs_u32(void *tmp, size_t &bytes, const uint32_t *k_in, uint3
 
 }  // namespace
 
-template <class F>
-void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,
-                    XYZZ<F> *result) {
-    if (n == 0) {
-        *result = XYZZ<F>::inf();
-        return;
-    }
+// ---- phase 1 (scalars only, shared by every MSM over the same scalars: B_G1 and B_G2) ----
+// digits -> per-window sort -> bucket bounds -> level-0 chunking -> length-sorted chunk order.
+// The plan's arrays live in scratch slots 3, 5-8, 16, 17 and stay valid until the next prepare on
+// this ctx; the accumulation phase only uses the other slots.
+inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, uint64_t n, MsmPlan &pl) {
+    pl = MsmPlan();
+    pl.n = n;
+    if (n == 0) return false;
     hipStream_t st = c.stream;
-    ScopedTimer whole(c, sizeof(F) == sizeof(fq_t) ? &c.stats.msm_g1 : &c.stats.msm_g2, n);
     const unsigned cb = msm_window_bits(n);
     const unsigned nwin = (256 + cb - 1) / cb;
     const uint32_t nbk = 1u << (cb - 1);
@@ -311,6 +330,10 @@ void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const uint32_t
     const uint32_t nb = (uint32_t)nb64, np = (uint32_t)np64, invalid = nbk;  // window-local keys
     unsigned key_bits = 1;
     while ((1ull << key_bits) <= invalid) key_bits++;  // cb bits: one fewer onesweep pass than global keys
+    pl.cb = cb;
+    pl.nwin = nwin;
+    pl.nbk = nbk;
+    pl.nb = nb;
 
     uint32_t *keys = c.scratch[0].as<uint32_t>(np);
     uint32_t *vals = c.scratch[1].as<uint32_t>(np);
@@ -326,7 +349,6 @@ void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const uint32_t
         ScopedTimer tsort(c, &c.stats.sort, n);
         k_digits<<<grid_for(n, 256), 256, 0, st>>>(scalars, idx, (uint32_t)n, cb, nwin, invalid, keys, vals);
         MI_LAUNCHED(c, "k_digits");
-        MI_HIP(hipGetLastError());
         size_t tmp_bytes = 0;
         sort_pairs_u32(nullptr, tmp_bytes, keys, keys_s, vals, vals_s, (uint32_t)n, key_bits, st);
         void *tmp = c.scratch[4].get(tmp_bytes);
@@ -336,11 +358,11 @@ void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const uint32_t
         }
         MI_HIP(hipMemsetAsync(offA, 0, sizeof(uint32_t) * nb, st));
         MI_HIP(hipMemsetAsync(cntA, 0, sizeof(uint32_t) * nb, st));
-        k_bounds<<<grid_for(np, 256), 256, 0, st>>>(keys_s, np, (uint32_t)n, nbk, offA, cntA);
-        MI_LAUNCHED(c, "k_bounds");
+        const uint32_t nq = (np + 3) / 4;
+        k_bounds4<<<grid_for(nq, 256), 256, 0, st>>>(keys_s, np, (uint32_t)n, nbk, offA, cntA);
+        MI_LAUNCHED(c, "k_bounds4");
         k_end_to_cnt<<<grid_for(nb, 256), 256, 0, st>>>(offA, cntA, nb);
         MI_LAUNCHED(c, "k_end_to_cnt");
-        MI_HIP(hipGetLastError());
     }
 
     // largest bucket decides the number of accumulation levels
@@ -353,59 +375,75 @@ void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const uint32_t
         MI_HIP(hipMemcpyAsync(&maxcnt, dmax, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         MI_HIP(hipStreamSynchronize(st));
     }
+    pl.maxcnt = maxcnt;
 
     static const uint32_t L0 = [] {
         const char *e = getenv("MI_MSM_L0");
         uint32_t v = e ? (uint32_t)atoi(e) : L0_DEFAULT;
         return v >= 2 && v <= 1024 ? v : L0_DEFAULT;
     }();
+    pl.L0 = L0;
     unsigned len_bits = 1;
     while ((1u << len_bits) <= L0) len_bits++;
     uint32_t *coff = offB, *ccnt = cntB;
-    XYZZ<F> *P0 = nullptr;
-    {  // level 0: buckets cut into chunks of <= L0 sorted entries; one mixed-add chain per chunk
-        k_chunk_count<<<grid_for(nb, 256), 256, 0, st>>>(cntA, nb, L0, ccnt);
-        MI_LAUNCHED(c, "k_chunk_count");
-        size_t tmp_bytes = 0;
-        MI_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, ccnt, coff, nb, st));
-        void *tmp = c.scratch[4].get(tmp_bytes);
-        MI_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, ccnt, coff, nb, st));
-        uint32_t tail[2];
-        MI_HIP(hipMemcpyAsync(&tail[0], coff + nb - 1, 4, hipMemcpyDeviceToHost, st));
-        MI_HIP(hipMemcpyAsync(&tail[1], ccnt + nb - 1, 4, hipMemcpyDeviceToHost, st));
-        MI_HIP(hipStreamSynchronize(st));
-        uint32_t total = tail[0] + tail[1];
-        if (total == 0) {  // every scalar is zero
-            *result = XYZZ<F>::inf();
-            return;
-        }
-        uint32_t *heads = c.scratch[15].as<uint32_t>(total + 1);
-        uint32_t *chunk_bucket = c.scratch[13].as<uint32_t>(total + 1);
-        MI_HIP(hipMemsetAsync(heads, 0, sizeof(uint32_t) * (total + 1), st));
-        k_chunk_heads<<<grid_for(nb, 256), 256, 0, st>>>(ccnt, coff, nb, heads);
-        MI_LAUNCHED(c, "k_chunk_heads");
-        tmp_bytes = 0;
-        MI_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tmp_bytes, heads, chunk_bucket, MaxOp(), total, st));
-        tmp = c.scratch[4].get(tmp_bytes);
-        MI_HIP(hipcub::DeviceScan::InclusiveScan(tmp, tmp_bytes, heads, chunk_bucket, MaxOp(), total, st));
-        P0 = c.scratch[10].as<XYZZ<F>>(total);
-        // length-sorted chunk order (keys/vals scratch of the main sort are free by now)
-        uint32_t *lkeys = c.scratch[0].as<uint32_t>(total), *lids = c.scratch[1].as<uint32_t>(total);
-        uint32_t *lkeys_s = c.scratch[2].as<uint32_t>(total), *order = c.scratch[16].as<uint32_t>(total);
-        k_chunk_len_keys<<<grid_for(total, 256), 256, 0, st>>>(chunk_bucket, coff, cntA, total, L0, lkeys, lids);
-        MI_LAUNCHED(c, "k_chunk_len_keys");
-        size_t tb = 0;
-        MI_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, lkeys, lkeys_s, lids, order, total, 0, len_bits, st));
-        void *tmp2 = c.scratch[4].get(tb);
-        MI_HIP(hipcub::DeviceRadixSort::SortPairs(tmp2, tb, lkeys, lkeys_s, lids, order, total, 0, len_bits, st));
-        ScopedTimer tacc(c, sizeof(F) == sizeof(fq_t) ? &c.stats.accum_g1 : &c.stats.accum_g2, n);
-        k_accum_level0<F><<<grid_for(total, 256), 256, 0, st>>>(order, chunk_bucket, coff, offA, cntA, total, L0,
-                                                                 vals_s, bases, P0);
+    // level 0: buckets cut into chunks of <= L0 sorted entries; one mixed-add chain per chunk
+    k_chunk_count<<<grid_for(nb, 256), 256, 0, st>>>(cntA, nb, L0, ccnt);
+    MI_LAUNCHED(c, "k_chunk_count");
+    size_t tmp_bytes = 0;
+    MI_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, ccnt, coff, nb, st));
+    void *tmp = c.scratch[4].get(tmp_bytes);
+    MI_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, ccnt, coff, nb, st));
+    uint32_t tail[2];
+    MI_HIP(hipMemcpyAsync(&tail[0], coff + nb - 1, 4, hipMemcpyDeviceToHost, st));
+    MI_HIP(hipMemcpyAsync(&tail[1], ccnt + nb - 1, 4, hipMemcpyDeviceToHost, st));
+    MI_HIP(hipStreamSynchronize(st));
+    uint32_t total = tail[0] + tail[1];
+    pl.total = total;
+    if (total == 0) return false;  // every scalar is zero
+    uint32_t *heads = c.scratch[15].as<uint32_t>(total + 1);
+    uint32_t *chunk_bucket = c.scratch[17].as<uint32_t>(total + 1);
+    MI_HIP(hipMemsetAsync(heads, 0, sizeof(uint32_t) * (total + 1), st));
+    k_chunk_heads<<<grid_for(nb, 256), 256, 0, st>>>(ccnt, coff, nb, heads);
+    MI_LAUNCHED(c, "k_chunk_heads");
+    tmp_bytes = 0;
+    MI_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tmp_bytes, heads, chunk_bucket, MaxOp(), total, st));
+    tmp = c.scratch[4].get(tmp_bytes);
+    MI_HIP(hipcub::DeviceScan::InclusiveScan(tmp, tmp_bytes, heads, chunk_bucket, MaxOp(), total, st));
+    // length-sorted chunk order (keys/vals scratch of the main sort are free by now)
+    uint32_t *lkeys = c.scratch[0].as<uint32_t>(total), *lids = c.scratch[1].as<uint32_t>(total);
+    uint32_t *lkeys_s = c.scratch[2].as<uint32_t>(total), *order = c.scratch[16].as<uint32_t>(total);
+    k_chunk_len_keys<<<grid_for(total, 256), 256, 0, st>>>(chunk_bucket, coff, cntA, total, L0, lkeys, lids);
+    MI_LAUNCHED(c, "k_chunk_len_keys");
+    size_t tb = 0;
+    MI_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, lkeys, lkeys_s, lids, order, total, 0, len_bits, st));
+    void *tmp2 = c.scratch[4].get(tb);
+    MI_HIP(hipcub::DeviceRadixSort::SortPairs(tmp2, tb, lkeys, lkeys_s, lids, order, total, 0, len_bits, st));
+    pl.vals_s = vals_s;
+    pl.off = offA;
+    pl.cnt = cntA;
+    pl.coff = coff;
+    pl.ccnt = ccnt;
+    pl.chunk_bucket = chunk_bucket;
+    pl.order = order;
+    return true;
+}
+
+// ---- phase 2 (per base set): accumulation, chunk tree, bucket reduction, window combination ----
+template <class F>
+void msm_accumulate_impl(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, XYZZ<F> *result) {
+    hipStream_t st = c.stream;
+    const unsigned cb = pl.cb, nwin = pl.nwin;
+    const uint32_t nbk = pl.nbk, nb = pl.nb, L0 = pl.L0;
+    const uint32_t *coff = pl.coff, *ccnt = pl.ccnt, *offA = pl.off, *cntA = pl.cnt;
+    XYZZ<F> *P0 = c.scratch[10].as<XYZZ<F>>(pl.total);
+    {
+        ScopedTimer tacc(c, sizeof(F) == sizeof(fq_t) ? &c.stats.accum_g1 : &c.stats.accum_g2, pl.n);
+        k_accum_level0<F><<<grid_for(pl.total, 256), 256, 0, st>>>(pl.order, pl.chunk_bucket, coff, offA, cntA,
+                                                                    pl.total, L0, pl.vals_s, bases, P0);
         MI_LAUNCHED(c, "k_accum_level0");
-        MI_HIP(hipGetLastError());
     }
 
-    const uint32_t maxchunks = (maxcnt + L0 - 1) / L0;
+    const uint32_t maxchunks = (pl.maxcnt + L0 - 1) / L0;
     if (maxchunks > 1) {  // in-place strided tree over the chunk partials of multi-chunk buckets only
         uint8_t *flag = c.scratch[1].as<uint8_t>(nb);
         uint32_t *mlist = c.scratch[0].as<uint32_t>(nb);
@@ -444,7 +482,6 @@ void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const uint32_t
             k_tree_level<F><<<grid_for(total, 256), 256, 0, st>>>(map, qoff, mlist, coff, ccnt, total,
                                                                    (uint32_t)stride, P0);
             MI_LAUNCHED(c, "k_tree_level");
-            MI_HIP(hipGetLastError());
         }
     }
 
@@ -468,7 +505,6 @@ void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const uint32_t
     MI_LAUNCHED(c, "k_bucket_reduce_dense");
     k_seg_fold<F><<<grid_for(totB, 256), 256, 0, st>>>(accB, runB, totB, nsegB, SB, foldB);
     MI_LAUNCHED(c, "k_seg_fold");
-    MI_HIP(hipGetLastError());
     // stacked per-row tree sum of nsegB (a power of two) entries, groups of <= 8 (shallow chains)
     const uint32_t rows = 3 * nwin;
     XYZZ<F> *tsum = c.scratch[11].as<XYZZ<F>>(2 * ((uint64_t)rows * nsegB / 2 + rows));
@@ -480,7 +516,6 @@ void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const uint32_t
         uint32_t outs = rows * (per / G);
         k_sum_groups<F><<<grid_for(outs, 256), 256, 0, st>>>(cur, outs, G, bufs[k]);
         MI_LAUNCHED(c, "k_sum_groups");
-        MI_HIP(hipGetLastError());
         per /= G;
         cur = bufs[k];
         k ^= 1;
@@ -504,5 +539,16 @@ void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const uint32_t
     c.timer.resolve();
 }
 
+template <class F>
+void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,
+             XYZZ<F> *result) {
+    ScopedTimer whole(c, sizeof(F) == sizeof(fq_t) ? &c.stats.msm_g1 : &c.stats.msm_g2, n);
+    MsmPlan pl;
+    if (!msm_prepare_impl(c, scalars, idx, n, pl)) {
+        *result = XYZZ<F>::inf();
+        return;
+    }
+    msm_accumulate_impl<F>(c, pl, bases, result);
+}
 
 }  // namespace mi

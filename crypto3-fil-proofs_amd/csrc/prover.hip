@@ -711,8 +711,11 @@ ProofPoints groth16_prove(Ctx &c, const Srs &srs, const Circuit &circ, const fr_
             try {
                 MI_HIP(hipSetDevice(c.device));
                 msm_g1(x, srs.l, z_dev + circ.n_in, nullptr, circ.n_aux, &Lq);
-                msm_g1(x, srs.b_g1, z_dev, circ.idx_b, circ.n_b, &B1);
-                msm_g2(x, srs.b_g2, z_dev, circ.idx_b, circ.n_b, &B2);
+                // B_G1 and B_G2 share the scalars (z over the B-density): sort them once
+                MsmPlan pb;
+                msm_prepare(x, z_dev, circ.idx_b, circ.n_b, pb);
+                msm_g1_planned(x, pb, srs.b_g1, &B1);
+                msm_g2_planned(x, pb, srs.b_g2, &B2);
                 MI_HIP(hipEventRecord(done, x.stream));
             } catch (...) {
                 err = std::current_exception();
