@@ -189,6 +189,29 @@ def main():
         pts.msm_dev(sc_dev.data_ptr(), msm_n)
     ctx.synchronize()
     msm_dt = (time.perf_counter() - tm) / args.msm_reps
+    # BASELINE configs[1]: 2^20-point G1 MSM + 2^20-element Fr NTT (device-resident inputs)
+    micro = {}
+    if msm_n >= (1 << 20):
+        m20 = 1 << 20
+        pts.msm_dev(sc_dev.data_ptr(), m20)
+        ctx.synchronize()
+        tm = time.perf_counter()
+        for _ in range(10):
+            pts.msm_dev(sc_dev.data_ptr(), m20)
+        ctx.synchronize()
+        t20 = (time.perf_counter() - tm) / 10
+        x = torch.from_numpy(sw[:m20].copy().view(np.uint8).reshape(-1)).to(device)
+        ctx.ntt_dev(x.data_ptr(), 20, False, False)
+        ctx.synchronize()
+        tm = time.perf_counter()
+        for _ in range(10):
+            ctx.ntt_dev(x.data_ptr(), 20, False, False)
+        ctx.synchronize()
+        n20 = (time.perf_counter() - tm) / 10
+        micro = {"workload": "BASELINE configs[1]: 2^20-point G1 MSM + 2^20-element Fr NTT, device-resident",
+                 "msm_g1_2e20_ms": t20 * 1e3, "msm_g1_2e20_mpoints_per_s": m20 / t20 / 1e6,
+                 "ntt_fr_2e20_ms": n20 * 1e3, "ntt_fr_2e20_melems_per_s": m20 / n20 / 1e6}
+        del x
     del sc_dev
 
     cpu = None
@@ -228,11 +251,13 @@ def main():
                         break
                 except Exception:
                     pass
-    # secondary (binding) roofline: Fq multiplications per second vs the MAD-issue bound
+    # secondary (binding) roofline: Fq multiplications per second vs the MAD-issue bound, over the mixed
+    # additions the accumulation actually issued (non-zero signed digits, counted by the library)
     c_bits = fg.msm_window_bits(int(units_per_launch))
     nwin = (256 + c_bits - 1) // c_bits
-    fq_muls = units_per_launch * nwin * FQ_MUL_PER_MIXED_ADD[grp]
-    valu_ach = fq_muls / (avg_ms * 1e-3) if avg_ms > 0 else None
+    madds_per_launch = dom.get("madds", 0) / max(dom["launches"], 1)
+    fq_muls = madds_per_launch * FQ_MUL_PER_MIXED_ADD[grp]
+    valu_ach = fq_muls / (avg_ms * 1e-3) if avg_ms > 0 and fq_muls else None
     valu_peak = MAD_RATE / FQ_MUL_MADS
     total_steps = args.steps * world
     value = n * total_steps / dt
@@ -256,6 +281,7 @@ def main():
                    "parallelism": f"partition-sharded x{world}"},
         "msm_g1_mpoints_per_s": msm_n / msm_dt / 1e6,
         "msm_g1_points": msm_n,
+        "config2_micro": micro,
         "roofline": {
             "bound": "hbm",
             "kernel": dom_name,
@@ -279,7 +305,9 @@ def main():
             "peak": valu_peak,
             "unit": "Fq-mul/s",
             "frac": valu_ach / valu_peak if valu_ach else None,
-            "model": f"{FQ_MUL_PER_MIXED_ADD[grp]} Fq-mul per mixed add x {nwin} windows (c={c_bits}) per point",
+            "madds_per_launch": madds_per_launch,
+            "model": f"{FQ_MUL_PER_MIXED_ADD[grp]} Fq-mul per mixed add x mixed adds issued (non-zero digits of "
+                     f"{nwin} windows, c={c_bits}); peak = v_mad_u64_u32 issue rate / {FQ_MUL_MADS} MADs",
         },
         "cpu_baseline": cpu,
         "timers_ms": {k: round(v["ms"], 3) for k, v in stats.items()},

@@ -633,6 +633,14 @@ int mi_ctx_reset_stats(mi_ctx *ctx) {
         ctx->c.stats = mi::Stats();
     });
 }
+int mi_ctx_get_work(mi_ctx *ctx, uint64_t out[2]) {
+    return guard([&] {
+        need(ctx && out, "null argument");
+        CtxLock l(ctx);
+        out[0] = ctx->c.stats.madds_g1;
+        out[1] = ctx->c.stats.madds_g2;
+    });
+}
 unsigned mi_msm_window_bits(uint64_t n) { return mi::msm_window_bits(n); }
 
 // ---- verification (host) ---------------------------------------------------------------------

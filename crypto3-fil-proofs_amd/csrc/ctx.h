@@ -80,7 +80,10 @@ struct Stats {
     KStat sort;                // digit extraction + radix sort + bucket bounds
     KStat ntt;                 // NTT passes (all launches of one transform)
     KStat prove;               // whole Groth16 prove (device part through host assembly)
+    uint64_t madds_g1 = 0, madds_g2 = 0;  // mixed additions issued by k_accum_level0 (non-zero digits)
     void merge(const Stats &o) {
+        madds_g1 += o.madds_g1;
+        madds_g2 += o.madds_g2;
         KStat *d[] = {&accum_g1, &accum_g2, &msm_g1, &msm_g2, &sort, &ntt, &prove};
         const KStat *x[] = {&o.accum_g1, &o.accum_g2, &o.msm_g1, &o.msm_g2, &o.sort, &o.ntt, &o.prove};
         for (int i = 0; i < 7; i++) {
@@ -217,6 +220,7 @@ struct MsmPlan {
     uint64_t n = 0;
     unsigned cb = 0, nwin = 0;
     uint32_t nbk = 0, nb = 0, L0 = 0, maxcnt = 0, total = 0;
+    uint64_t entries = 0;  // non-zero digits over all windows
     const uint32_t *vals_s = nullptr, *off = nullptr, *cnt = nullptr, *coff = nullptr, *ccnt = nullptr,
                    *chunk_bucket = nullptr, *order = nullptr;
 };

@@ -7,7 +7,7 @@
 //   1. k_digits     : every scalar -> ceil(256/c) signed c-bit digits; one (bucket key, point
 //                     index | sign) pair per non-zero digit, laid out [window][point] (coalesced).
 //   2. radix sort   : rocPRIM onesweep per window over the c window-local key bits.
-//   3. k_bounds     : bucket start / end from the sorted keys.
+//   3. k_bounds4    : bucket start / end (and the zero-digit tail of each window) from the sorted keys.
 //   4. accumulation : buckets are cut into chunks of <= L sorted entries, one thread per chunk,
 //                     chunks length-sorted (6-7 bit radix sort) so a wave runs equal-length chunks
 //                     (mixed XYZZ += affine adds, point gathered by index); the chunk partials
@@ -72,8 +72,9 @@ __global__ void k_digits(const fr_t *__restrict__ scalars, const uint32_t *__res
 
 // keys are window-local (sorted per window): global bucket = window * nbk + key.  Four sorted keys
 // per thread (one 16-byte load); the neighbours across the group edge are single loads (L2 hits).
+// zstart[w] = first sorted position of window w holding a zero digit (key nbk sorts last).
 __global__ void k_bounds4(const uint32_t *__restrict__ keys, uint32_t np, uint32_t n, uint32_t nbk,
-                          uint32_t *__restrict__ start, uint32_t *__restrict__ cnt) {
+                          uint32_t *__restrict__ start, uint32_t *__restrict__ cnt, uint32_t *__restrict__ zstart) {
     uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t i0 = q * 4;
     if (i0 >= np) return;
@@ -95,7 +96,10 @@ __global__ void k_bounds4(const uint32_t *__restrict__ keys, uint32_t np, uint32
             lo += n;
         }
         uint32_t kk = k[1 + j];
-        if (kk == nbk) continue;  // zero digit
+        if (kk == nbk) {  // zero digit: not a bucket entry
+            if (i == lo || k[j] != kk) zstart[w] = i;
+            continue;
+        }
         uint32_t g = w * nbk + kk;
         if (i == lo || k[j] != kk) start[g] = i;
         if (i + 1 == lo + n || k[2 + j] != kk) cnt[g] = i + 1;  // end; converted to a count below
@@ -343,7 +347,8 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
     uint32_t *cntA = c.scratch[6].as<uint32_t>(nb);
     uint32_t *offB = c.scratch[7].as<uint32_t>(nb);
     uint32_t *cntB = c.scratch[8].as<uint32_t>(nb);
-    uint32_t *dmax = c.scratch[9].as<uint32_t>(4);
+    uint32_t *dmax = c.scratch[9].as<uint32_t>(4 + nwin);  // [max bucket size, pad, zstart[nwin]]
+    uint32_t *zstart = dmax + 4;
 
     {
         ScopedTimer tsort(c, &c.stats.sort, n);
@@ -358,24 +363,28 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
         }
         MI_HIP(hipMemsetAsync(offA, 0, sizeof(uint32_t) * nb, st));
         MI_HIP(hipMemsetAsync(cntA, 0, sizeof(uint32_t) * nb, st));
+        MI_HIP(hipMemsetAsync(zstart, 0xff, sizeof(uint32_t) * nwin, st));
         const uint32_t nq = (np + 3) / 4;
-        k_bounds4<<<grid_for(nq, 256), 256, 0, st>>>(keys_s, np, (uint32_t)n, nbk, offA, cntA);
+        k_bounds4<<<grid_for(nq, 256), 256, 0, st>>>(keys_s, np, (uint32_t)n, nbk, offA, cntA, zstart);
         MI_LAUNCHED(c, "k_bounds4");
         k_end_to_cnt<<<grid_for(nb, 256), 256, 0, st>>>(offA, cntA, nb);
         MI_LAUNCHED(c, "k_end_to_cnt");
     }
 
     // largest bucket decides the number of accumulation levels
-    uint32_t maxcnt = 0;
+    std::vector<uint32_t> head(4 + nwin);
     {
         size_t tmp_bytes = 0;
         MI_HIP(hipcub::DeviceReduce::Max(nullptr, tmp_bytes, cntA, dmax, nb, st));
         void *tmp = c.scratch[4].get(tmp_bytes);
         MI_HIP(hipcub::DeviceReduce::Max(tmp, tmp_bytes, cntA, dmax, nb, st));
-        MI_HIP(hipMemcpyAsync(&maxcnt, dmax, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        MI_HIP(hipMemcpyAsync(head.data(), dmax, sizeof(uint32_t) * (4 + nwin), hipMemcpyDeviceToHost, st));
         MI_HIP(hipStreamSynchronize(st));
     }
-    pl.maxcnt = maxcnt;
+    pl.maxcnt = head[0];
+    pl.entries = 0;  // non-zero digits = mixed additions of the accumulation
+    for (unsigned w = 0; w < nwin; w++)
+        pl.entries += head[4 + w] == 0xffffffffu ? n : head[4 + w] - (uint64_t)w * n;
 
     static const uint32_t L0 = [] {
         const char *e = getenv("MI_MSM_L0");
@@ -436,6 +445,7 @@ void msm_accumulate_impl(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, XYZZ
     const uint32_t nbk = pl.nbk, nb = pl.nb, L0 = pl.L0;
     const uint32_t *coff = pl.coff, *ccnt = pl.ccnt, *offA = pl.off, *cntA = pl.cnt;
     XYZZ<F> *P0 = c.scratch[10].as<XYZZ<F>>(pl.total);
+    (sizeof(F) == sizeof(fq_t) ? c.stats.madds_g1 : c.stats.madds_g2) += pl.entries;
     {
         ScopedTimer tacc(c, sizeof(F) == sizeof(fq_t) ? &c.stats.accum_g1 : &c.stats.accum_g2, pl.n);
         k_accum_level0<F><<<grid_for(pl.total, 256), 256, 0, st>>>(pl.order, pl.chunk_bucket, coff, offA, cntA,

@@ -36,10 +36,43 @@ __device__ __forceinline__ uint32_t brev(uint32_t x, unsigned bits) {
     return bits ? (__builtin_bitreverse32(x) >> (32 - bits)) : 0;
 }
 
+// LDS tile: four planes of 64-bit words (limb pairs) so every access is a ds_read/write_b64 by
+// 32-lane groups; positions are XOR-swizzled inside 32-word rows (worst case 2-way bank conflicts
+// for every radix-4 access pattern and conflict-free for the contiguous load/store phases).
+struct LdsTile {
+    uint64_t p[4][TILE];
+};
+__device__ __forceinline__ unsigned swz(unsigned p) { return p ^ (((p >> 5) * 5u) & 31u); }
+__device__ __forceinline__ void lds_put(LdsTile &s, unsigned p, const fr_t &x) {
+    const unsigned q = swz(p);
+    MI_UNROLL for (int k = 0; k < 4; k++) s.p[k][q] = (uint64_t)x.v[2 * k] | ((uint64_t)x.v[2 * k + 1] << 32);
+}
+__device__ __forceinline__ fr_t lds_get(const LdsTile &s, unsigned p) {
+    const unsigned q = swz(p);
+    fr_t x;
+    MI_UNROLL for (int k = 0; k < 4; k++) {
+        uint64_t w = s.p[k][q];
+        x.v[2 * k] = (uint32_t)w;
+        x.v[2 * k + 1] = (uint32_t)(w >> 32);
+    }
+    return x;
+}
+// insert zero bits at positions p0 < p1 (p1 = p0 + 1 here) / at position p
+__device__ __forceinline__ unsigned ins2(unsigned q, unsigned p0) {
+    return (q & ((1u << p0) - 1)) | ((q >> p0) << (p0 + 2));
+}
+__device__ __forceinline__ unsigned ins1(unsigned q, unsigned p) {
+    return (q & ((1u << p) - 1)) | ((q >> p) << (p + 1));
+}
+__device__ __forceinline__ fr_t tw_b(const fr_t *__restrict__ tw10, unsigned j, unsigned b) {
+    return tw10[j << (TILE_LOG - b)];  // omega_{2^b}^j
+}
+
 // One pass.  DIF: load -> b DIF stages -> optional inter-pass twiddle -> [epilogue] -> store.
 //            DIT: load -> optional inter-pass twiddle -> b DIT stages (reverse) -> store.
-// In-tile twiddles omega_{2^b}^j come from the 512-entry omega_1024 table (16 KiB, L1-resident), so
-// the tile is the only LDS use (32 KiB: 5 workgroups per CU).
+// The b stages run as radix-4 rounds (two stages per LDS round trip: each thread holds the four
+// elements x, x + h/2, x + h, x + 3h/2 of one group in registers) plus one radix-2 round when b is
+// odd; in-tile twiddles omega_{2^b}^j come from the 512-entry omega_1024 table (L1-resident).
 // Epilogue (last DIF pass only): epi = 1 multiplies the element at global position pos by
 // G^bitrev_L(pos) * scale (coset shift of the bit-reversed coefficients, fused 1/d); epi = 2 also
 // converts to canonical form (icoset: H for the MSM).
@@ -51,7 +84,7 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(fr_t *__restrict__ d, 
                                                           const fr_t *__restrict__ tw10, int epi,
                                                           const fr_t *__restrict__ glo,
                                                           const fr_t *__restrict__ ghi, fr_t scale) {
-    __shared__ fr_t sh[TILE];
+    __shared__ LdsTile sh;
     const unsigned T = 1u << Tlog;
     const unsigned Slog = M - b;
     const uint64_t S = 1ull << Slog;
@@ -77,33 +110,70 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(fr_t *__restrict__ d, 
             uint32_t ex = (uint32_t)(((uint64_t)(i20 + t) * k1) << (32 - M));
             if (ex) x = x * tw_full(lo, hi, ex);
         }
-        sh[e] = x;
+        lds_put(sh, e, x);
     }
     __syncthreads();
-    const unsigned nbf = tile >> 1;
-    for (unsigned st = 0; st < b; st++) {
-        unsigned s = DIF ? st : (b - 1 - st);  // DIF stage index
-        unsigned hlog = b - 1 - s;
-        unsigned h = 1u << hlog;
-        for (unsigned q = threadIdx.x; q < nbf; q += NTT_THREADS) {
-            unsigned t = q & (T - 1);
-            unsigned r = q >> Tlog;
-            unsigned g = r >> (b - 1);
-            unsigned k = r & ((1u << (b - 1)) - 1);
-            unsigned i1 = ((k >> hlog) << (hlog + 1)) | (k & (h - 1));
-            unsigned j = (k & (h - 1)) << s;  // exponent of omega_{2^b}
-            unsigned base = (g << b);
-            unsigned e0 = ((base + i1) << Tlog) + t;
-            unsigned e1 = e0 + (h << Tlog);
-            fr_t u = sh[e0], v = sh[e1];
-            if (DIF) {
-                fr_t dd = u - v;
-                sh[e0] = u + v;
-                sh[e1] = j ? dd * tw10[j << (TILE_LOG - b)] : dd;
-            } else {
-                fr_t w = j ? v * tw10[j << (TILE_LOG - b)] : v;
-                sh[e0] = u + w;
-                sh[e1] = u - w;
+    const unsigned nquad = tile >> 2;
+    const unsigned nr4 = b >> 1;  // radix-4 rounds: DIF stage pairs (0,1), (2,3), ...
+    const bool odd = b & 1;       // + one radix-2 round for stage b - 1
+    const unsigned q = threadIdx.x;
+    for (unsigned rr = 0; rr < nr4 + (odd ? 1 : 0); rr++) {
+        // DIF runs rounds in order; DIT runs them in reverse (the radix-2 round first when b is odd)
+        const unsigned r = DIF ? rr : nr4 + (odd ? 1 : 0) - 1 - rr;
+        const unsigned s = 2 * r;  // first DIF stage of this round
+        if (r < nr4) {
+            if (q < nquad) {
+                const unsigned hs = b - 1 - s;  // i1 bit of stage s; stage s + 1 uses bit hs - 1
+                const unsigned p0 = Tlog + hs - 1;
+                const unsigned base = ins2(q, p0);
+                const unsigned o1 = 1u << p0, o2 = 2u << p0;
+                const unsigned i1 = (base >> Tlog) & bmask;
+                const unsigned h = 1u << hs;
+                const unsigned j0 = (i1 & (h - 1)) << s;        // stage s, pair (x0, x2)
+                const unsigned j1 = j0 + (1u << (b - 2));       // stage s, pair (x1, x3)
+                const unsigned jq = (i1 & ((h >> 1) - 1)) << (s + 1);  // stage s + 1, both pairs
+                fr_t x0 = lds_get(sh, base), x1 = lds_get(sh, base + o1);
+                fr_t x2 = lds_get(sh, base + o2), x3 = lds_get(sh, base + o2 + o1);
+                if (DIF) {
+                    fr_t a = x0 + x2, c = x0 - x2;
+                    fr_t bb = x1 + x3, dd = x1 - x3;
+                    if (j0) c = c * tw_b(tw10, j0, b);
+                    dd = dd * tw_b(tw10, j1, b);
+                    x0 = a + bb;
+                    x1 = a - bb;
+                    x2 = c + dd;
+                    x3 = c - dd;
+                    if (jq) {
+                        fr_t w = tw_b(tw10, jq, b);
+                        x1 = x1 * w;
+                        x3 = x3 * w;
+                    }
+                } else {
+                    if (jq) {
+                        fr_t w = tw_b(tw10, jq, b);
+                        x1 = x1 * w;
+                        x3 = x3 * w;
+                    }
+                    fr_t a = x0 + x1, bb = x0 - x1;
+                    fr_t c = x2 + x3, dd = x2 - x3;
+                    if (j0) c = c * tw_b(tw10, j0, b);
+                    dd = dd * tw_b(tw10, j1, b);
+                    x0 = a + c;
+                    x2 = a - c;
+                    x1 = bb + dd;
+                    x3 = bb - dd;
+                }
+                lds_put(sh, base, x0);
+                lds_put(sh, base + o1, x1);
+                lds_put(sh, base + o2, x2);
+                lds_put(sh, base + o2 + o1, x3);
+            }
+        } else {  // radix-2 round: DIF stage b - 1 (pairs at i1 bit 0, twiddle exponent 0)
+            for (unsigned u = q; u < (tile >> 1); u += NTT_THREADS) {
+                const unsigned base = ins1(u, Tlog);
+                fr_t x0 = lds_get(sh, base), x1 = lds_get(sh, base + T);
+                lds_put(sh, base, x0 + x1);
+                lds_put(sh, base + T, x0 - x1);
             }
         }
         __syncthreads();
@@ -112,7 +182,7 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(fr_t *__restrict__ d, 
     for (unsigned e = threadIdx.x; e < tile; e += NTT_THREADS) {
         unsigned t = e & (T - 1), i1 = (e >> Tlog) & bmask, g = e >> (Tlog + b);
         uint64_t gi = ((sub0 + g) << M) + ((uint64_t)i1 << Slog) + i20 + t;
-        fr_t x = sh[e];
+        fr_t x = lds_get(sh, e);
         if (DIF && twiddle) {
             uint32_t k1 = brev(i1, b);
             uint32_t ex = (uint32_t)(((uint64_t)(i20 + t) * k1) << (32 - M));

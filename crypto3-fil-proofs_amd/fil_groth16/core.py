@@ -85,8 +85,12 @@ class Context:
         out = (ctypes.c_double * 21)()
         check(lib().mi_ctx_get_stats(self.h, out))
         v = list(out)
-        return {k: {"ms": v[3 * i], "launches": int(v[3 * i + 1]), "units": int(v[3 * i + 2])}
-                for i, k in enumerate(self.STAT_KEYS)}
+        st = {k: {"ms": v[3 * i], "launches": int(v[3 * i + 1]), "units": int(v[3 * i + 2])}
+              for i, k in enumerate(self.STAT_KEYS)}
+        w = (ctypes.c_uint64 * 2)()
+        check(lib().mi_ctx_get_work(self.h, w))
+        st["accum_g1"]["madds"], st["accum_g2"]["madds"] = int(w[0]), int(w[1])
+        return st
 
     # ---- building blocks ----
     def msm_g1(self, bases96: bytes, scalars32: bytes) -> bytes:

@@ -207,6 +207,9 @@ void mi_synth_free(mi_synth *s);
  *   4 digits + sort + bucket bounds          5 NTT transforms (units = elements)   6 whole prove (units = constraints) */
 int mi_ctx_get_stats(mi_ctx *ctx, double out[21]);
 int mi_ctx_reset_stats(mi_ctx *ctx);
+/* work counters since the last reset: out[0] / out[1] = mixed additions (non-zero signed digits)
+ * issued by the G1 / G2 bucket accumulation -- the unit of the VALU roofline */
+int mi_ctx_get_work(mi_ctx *ctx, uint64_t out[2]);
 /* msm window size chosen for n points (exposed for tests / reports) */
 unsigned mi_msm_window_bits(uint64_t n);
 
