@@ -25,10 +25,15 @@
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include "ctx.h"
+#include "g2pair.h"
 
 namespace mi {
 
 namespace {
+
+// At least two waves per SIMD for the group-law kernels: without it the G2 (Fq2) instances take
+// all 512 unified registers (256 VGPR + 256 AGPR) and run one wave per SIMD.
+#define MI_WAVES2 __attribute__((amdgpu_waves_per_eu(2)))
 
 constexpr uint32_t L0_DEFAULT = 64;  // sorted entries per chunk at level 0 (mixed adds); MI_MSM_L0 overrides
 constexpr uint32_t L1 = 16;  // chunk partials summed per thread per tree level (full adds)
@@ -146,7 +151,7 @@ __global__ void k_chunk_len_keys(const uint32_t *__restrict__ chunk_bucket, cons
 }
 
 template <class F>
-__global__ void __launch_bounds__(256) k_accum_level0(const uint32_t *__restrict__ order,
+__global__ void __launch_bounds__(256) MI_WAVES2 k_accum_level0(const uint32_t *__restrict__ order,
                                                       const uint32_t *__restrict__ chunk_bucket,
                                                       const uint32_t *__restrict__ coff,
                                                       const uint32_t *__restrict__ off,
@@ -154,7 +159,9 @@ __global__ void __launch_bounds__(256) k_accum_level0(const uint32_t *__restrict
                                                       const uint32_t *__restrict__ vals,
                                                       const Affine<F> *__restrict__ bases,
                                                       XYZZ<F> *__restrict__ out) {
-    uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    using LP = Lane<F>;
+    using R = typename LP::R;
+    uint32_t u = (blockIdx.x * blockDim.x + threadIdx.x) / LP::K;  // a lane pair per chunk for G2
     if (u >= total) return;
     uint32_t t = order[u];  // chunk id, length-sorted
     uint32_t b = chunk_bucket[t];
@@ -162,14 +169,14 @@ __global__ void __launch_bounds__(256) k_accum_level0(const uint32_t *__restrict
     uint32_t beg = off[b] + local * L0;
     uint32_t lim = local * L0 + L0 < cnt[b] ? local * L0 + L0 : cnt[b];
     uint32_t end = off[b] + lim;
-    XYZZ<F> acc = XYZZ<F>::inf();
+    XYZZ<R> acc = XYZZ<R>::inf();
     for (uint32_t p = beg; p < end; p++) {
         uint32_t v = vals[p];
-        Affine<F> a = bases[v & 0x7fffffffu];
+        Affine<R> a = LP::lda(bases + (v & 0x7fffffffu));
         if (v >> 31) a.y = -a.y;
         acc = xyzz_add_affine_inl(acc, a);
     }
-    out[t] = acc;
+    LP::st(out + t, acc);
 }
 
 // Buckets that span several level-0 chunks: their chunk partials P0[coff[b] + j] (j < ccnt[b]) are
@@ -198,13 +205,15 @@ __global__ void k_tree_heads(const uint32_t *__restrict__ qcnt, const uint32_t *
 }
 
 template <class F>
-__global__ void __launch_bounds__(256) k_tree_level(const uint32_t *__restrict__ map,
+__global__ void __launch_bounds__(256) MI_WAVES2 k_tree_level(const uint32_t *__restrict__ map,
                                                     const uint32_t *__restrict__ qoff,
                                                     const uint32_t *__restrict__ mlist,
                                                     const uint32_t *__restrict__ coff,
                                                     const uint32_t *__restrict__ ccnt, uint32_t total,
                                                     uint32_t stride, XYZZ<F> *__restrict__ P) {
-    uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    using LP = Lane<F>;
+    using R = typename LP::R;
+    uint32_t u = (blockIdx.x * blockDim.x + threadIdx.x) / LP::K;
     if (u >= total) return;
     uint32_t i = map[u];
     uint32_t b = mlist[i];
@@ -212,72 +221,78 @@ __global__ void __launch_bounds__(256) k_tree_level(const uint32_t *__restrict__
     uint32_t n = ccnt[b];
     XYZZ<F> *base = P + coff[b];
     uint64_t first = (uint64_t)q * L1 * stride;
-    XYZZ<F> acc = base[first];
+    XYZZ<R> acc = LP::ld(base + first);
     for (uint32_t j = 1; j < L1; j++) {
         uint64_t idx = first + (uint64_t)j * stride;
-        if (idx < n) acc = xyzz_add_inl(acc, base[idx]);
+        if (idx < n) acc = xyzz_add_inl(acc, LP::ld(base + idx));
     }
-    base[first] = acc;
+    LP::st(base + first, acc);
 }
 
 // Running-sum reduction over one segment of seg_len buckets (all group-law code inlined):
 //   seg_run = sum_j B_j,  seg_acc = sum_j (j + 1) B_j   (j = bucket index inside the segment)
 // Bucket b's sum is P[off[b]] when cnt[b] != 0 (level-0 chunk slot of its first chunk).
 template <class F>
-__global__ void __launch_bounds__(256) k_bucket_reduce(const uint32_t *__restrict__ off,
+__global__ void __launch_bounds__(256) MI_WAVES2 k_bucket_reduce(const uint32_t *__restrict__ off,
                                                        const uint32_t *__restrict__ cnt,
                                                        const XYZZ<F> *__restrict__ P, uint32_t nseg_total,
                                                        unsigned seg_len, XYZZ<F> *__restrict__ seg_acc,
                                                        XYZZ<F> *__restrict__ seg_run) {
-    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    using LP = Lane<F>;
+    using R = typename LP::R;
+    uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) / LP::K;
     if (t >= nseg_total) return;
     uint32_t b0 = t * seg_len;  // buckets of one window are contiguous and nbk % seg_len == 0
-    XYZZ<F> run = XYZZ<F>::inf(), acc = XYZZ<F>::inf();
+    XYZZ<R> run = XYZZ<R>::inf(), acc = XYZZ<R>::inf();
     for (int j = (int)seg_len - 1; j >= 0; j--) {
         uint32_t b = b0 + j;
-        if (cnt[b]) run = xyzz_add_inl(run, P[off[b]]);
+        if (cnt[b]) run = xyzz_add_inl(run, LP::ld(P + off[b]));
         acc = xyzz_add_inl(acc, run);
     }
-    seg_acc[t] = acc;
-    seg_run[t] = run;
+    LP::st(seg_acc + t, acc);
+    LP::st(seg_run + t, run);
 }
 
 // The same over a dense array of points (second level: the first level's segment sums), also
 // summing the first level's accumulators over the segment (sum_acc).
 template <class F>
-__global__ void __launch_bounds__(256) k_bucket_reduce_dense(const XYZZ<F> *__restrict__ P,
+__global__ void __launch_bounds__(256) MI_WAVES2 k_bucket_reduce_dense(const XYZZ<F> *__restrict__ P,
                                                              const XYZZ<F> *__restrict__ A, uint32_t nseg_total,
                                                              unsigned seg_len, XYZZ<F> *__restrict__ seg_acc,
                                                              XYZZ<F> *__restrict__ seg_run,
                                                              XYZZ<F> *__restrict__ sum_acc) {
-    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    using LP = Lane<F>;
+    using R = typename LP::R;
+    uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) / LP::K;
     if (t >= nseg_total) return;
     const XYZZ<F> *p = P + (uint64_t)t * seg_len;
     const XYZZ<F> *a = A + (uint64_t)t * seg_len;
-    XYZZ<F> run = XYZZ<F>::inf(), acc = XYZZ<F>::inf(), sa = XYZZ<F>::inf();
+    XYZZ<R> run = XYZZ<R>::inf(), acc = XYZZ<R>::inf(), sa = XYZZ<R>::inf();
     for (int j = (int)seg_len - 1; j >= 0; j--) {
-        run = xyzz_add_inl(run, p[j]);
+        run = xyzz_add_inl(run, LP::ld(p + j));
         acc = xyzz_add_inl(acc, run);
-        sa = xyzz_add_inl(sa, a[j]);
+        sa = xyzz_add_inl(sa, LP::ld(a + j));
     }
-    seg_acc[t] = acc;
-    seg_run[t] = run;
-    sum_acc[t] = sa;
+    LP::st(seg_acc + t, acc);
+    LP::st(seg_run + t, run);
+    LP::st(sum_acc + t, sa);
 }
 
 // out[t] = seg_acc[t] + (s * seg_len) * seg_run[t], s = segment index inside its window
 template <class F>
-__global__ void __launch_bounds__(256) k_seg_fold(const XYZZ<F> *__restrict__ seg_acc,
+__global__ void __launch_bounds__(256) MI_WAVES2 k_seg_fold(const XYZZ<F> *__restrict__ seg_acc,
                                                   const XYZZ<F> *__restrict__ seg_run, uint32_t nseg_total,
                                                   uint32_t nseg, unsigned seg_len, XYZZ<F> *__restrict__ out) {
-    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    using LP = Lane<F>;
+    using R = typename LP::R;
+    uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) / LP::K;
     if (t >= nseg_total) return;
-    XYZZ<F> acc = seg_acc[t];
+    XYZZ<R> acc = LP::ld(seg_acc + t);
     uint32_t k = (t % nseg) * seg_len;
-    XYZZ<F> run = seg_run[t];
+    XYZZ<R> run = LP::ld(seg_run + t);
     if (k && !run.is_inf()) {
         // k * run, left-to-right double-and-add, group law inlined (no device calls)
-        XYZZ<F> m = run;
+        XYZZ<R> m = run;
         int top = 31 - __builtin_clz(k);
         for (int bit = top - 1; bit >= 0; bit--) {
             m = xyzz_dbl_inl(m);
@@ -285,18 +300,20 @@ __global__ void __launch_bounds__(256) k_seg_fold(const XYZZ<F> *__restrict__ se
         }
         acc = xyzz_add_inl(acc, m);
     }
-    out[t] = acc;
+    LP::st(out + t, acc);
 }
 
 // out[w * (n / G) + g] = sum of in[w * n + g * G ... + G)   (n % G == 0)
 template <class F>
-__global__ void __launch_bounds__(256) k_sum_groups(const XYZZ<F> *__restrict__ in, uint32_t total_out,
+__global__ void __launch_bounds__(256) MI_WAVES2 k_sum_groups(const XYZZ<F> *__restrict__ in, uint32_t total_out,
                                                     unsigned G, XYZZ<F> *__restrict__ out) {
-    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    using LP = Lane<F>;
+    using R = typename LP::R;
+    uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) / LP::K;
     if (t >= total_out) return;
-    XYZZ<F> acc = in[(uint64_t)t * G];
-    for (unsigned i = 1; i < G; i++) acc = xyzz_add_inl(acc, in[(uint64_t)t * G + i]);
-    out[t] = acc;
+    XYZZ<R> acc = LP::ld(in + (uint64_t)t * G);
+    for (unsigned i = 1; i < G; i++) acc = xyzz_add_inl(acc, LP::ld(in + (uint64_t)t * G + i));
+    LP::st(out + t, acc);
 }
 
 inline unsigned grid_for(uint64_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
@@ -441,6 +458,7 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
 template <class F>
 void msm_accumulate_impl(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, XYZZ<F> *result) {
     hipStream_t st = c.stream;
+    const unsigned K = Lane<F>::K;  // threads per group element (2 for G2: g2pair.h)
     const unsigned cb = pl.cb, nwin = pl.nwin;
     const uint32_t nbk = pl.nbk, nb = pl.nb, L0 = pl.L0;
     const uint32_t *coff = pl.coff, *ccnt = pl.ccnt, *offA = pl.off, *cntA = pl.cnt;
@@ -448,7 +466,7 @@ void msm_accumulate_impl(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, XYZZ
     (sizeof(F) == sizeof(fq_t) ? c.stats.madds_g1 : c.stats.madds_g2) += pl.entries;
     {
         ScopedTimer tacc(c, sizeof(F) == sizeof(fq_t) ? &c.stats.accum_g1 : &c.stats.accum_g2, pl.n);
-        k_accum_level0<F><<<grid_for(pl.total, 256), 256, 0, st>>>(pl.order, pl.chunk_bucket, coff, offA, cntA,
+        k_accum_level0<F><<<grid_for((uint64_t)pl.total * K, 256), 256, 0, st>>>(pl.order, pl.chunk_bucket, coff, offA, cntA,
                                                                     pl.total, L0, pl.vals_s, bases, P0);
         MI_LAUNCHED(c, "k_accum_level0");
     }
@@ -489,7 +507,7 @@ void msm_accumulate_impl(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, XYZZ
             MI_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, heads, map, MaxOp(), total, st));
             tmp = c.scratch[4].get(tb);
             MI_HIP(hipcub::DeviceScan::InclusiveScan(tmp, tb, heads, map, MaxOp(), total, st));
-            k_tree_level<F><<<grid_for(total, 256), 256, 0, st>>>(map, qoff, mlist, coff, ccnt, total,
+            k_tree_level<F><<<grid_for((uint64_t)total * K, 256), 256, 0, st>>>(map, qoff, mlist, coff, ccnt, total,
                                                                    (uint32_t)stride, P0);
             MI_LAUNCHED(c, "k_tree_level");
         }
@@ -509,11 +527,11 @@ void msm_accumulate_impl(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, XYZZ
     // [sumAccB | runB | foldB] contiguous (one stacked tree sum over 3 * nwin rows), then accB
     XYZZ<F> *sumB = c.scratch[14].as<XYZZ<F>>(4 * (uint64_t)totB), *runB = sumB + totB, *foldB = runB + totB,
             *accB = foldB + totB;
-    k_bucket_reduce<F><<<grid_for(totA, 256), 256, 0, st>>>(coff, cntA, P0, totA, SA, accA, runA);
+    k_bucket_reduce<F><<<grid_for((uint64_t)totA * K, 256), 256, 0, st>>>(coff, cntA, P0, totA, SA, accA, runA);
     MI_LAUNCHED(c, "k_bucket_reduce");
-    k_bucket_reduce_dense<F><<<grid_for(totB, 256), 256, 0, st>>>(runA, accA, totB, SB, accB, runB, sumB);
+    k_bucket_reduce_dense<F><<<grid_for((uint64_t)totB * K, 256), 256, 0, st>>>(runA, accA, totB, SB, accB, runB, sumB);
     MI_LAUNCHED(c, "k_bucket_reduce_dense");
-    k_seg_fold<F><<<grid_for(totB, 256), 256, 0, st>>>(accB, runB, totB, nsegB, SB, foldB);
+    k_seg_fold<F><<<grid_for((uint64_t)totB * K, 256), 256, 0, st>>>(accB, runB, totB, nsegB, SB, foldB);
     MI_LAUNCHED(c, "k_seg_fold");
     // stacked per-row tree sum of nsegB (a power of two) entries, groups of <= 8 (shallow chains)
     const uint32_t rows = 3 * nwin;
@@ -524,7 +542,7 @@ void msm_accumulate_impl(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, XYZZ
     for (uint32_t per = nsegB; per > 1;) {
         unsigned G = per >= 8 ? 8 : per;
         uint32_t outs = rows * (per / G);
-        k_sum_groups<F><<<grid_for(outs, 256), 256, 0, st>>>(cur, outs, G, bufs[k]);
+        k_sum_groups<F><<<grid_for((uint64_t)outs * K, 256), 256, 0, st>>>(cur, outs, G, bufs[k]);
         MI_LAUNCHED(c, "k_sum_groups");
         per /= G;
         cur = bufs[k];
