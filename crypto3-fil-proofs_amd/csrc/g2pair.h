@@ -5,7 +5,7 @@
 // scratch spills (2 waves per SIMD at best).  Here lane 2k holds the c0 halves and lane 2k + 1 the c1
 // halves of every Fq2 value of one chunk, so each lane carries Fq-sized state and the pair exchanges
 // halves with one DPP quad_perm move per register:
-//   mul: c0 = a0 b0 + a1 (2p - b1) (even lane), c1 = a1 b0 + a0 b1 (odd lane), each ONE fused
+//   mul: c0 = a0 b0 + a1 (2p - b1) (even lane), c1 = a0 b1 + a1 b0 (odd lane), each ONE fused
 //        product-scanning Montgomery pass over two products: 2 x 588 lane-MADs, the same MAD count
 //        as a 3-multiplication Karatsuba on one lane;
 //   sqr: c0 = (a0 + a1)(a0 - a1), c1 = 2 a1 a0: one Fq multiplication per lane;
@@ -42,17 +42,25 @@ __device__ __forceinline__ fq2h_t operator-(const fq2h_t &a, const fq2h_t &b) { 
 __device__ __forceinline__ fq2h_t operator-(const fq2h_t &a) { return {-a.v}; }
 __device__ __forceinline__ fq2h_t dbl(const fq2h_t &a) { return {a.v + a.v}; }
 __device__ __forceinline__ fq2h_t operator*(const fq2h_t &a, const fq2h_t &b) {
+    // even: a0 b0 + a1 (2p - b1)     odd: a0 b1 + a1 b0
+    // The odd lane sends 2p - b1 instead of b1 (sender-side negation), so the received halves are
+    // pa = a_partner, psb = (odd ? b0 : -b1) and both lanes run mul_add(X1, b, X3, psb) with
+    // (X1, X3) = (a, pa) on even lanes and (pa, a) on odd lanes: one unsigned fused REDC
+    // (field.h mul_add: column sums < 2^63.4, result < 2p).
+    __builtin_amdgcn_sched_barrier(0);  // one pair multiplication at a time (register pressure)
     const bool odd = pair_odd();
-    const fq_t pa = pair_swap(a.v), pb = pair_swap(b.v);
-    // even: a0 b0 + a1 (2p - b1)     odd: a1 b0 + a0 b1   (pa, pb = the partner's halves); both
-    // are one unsigned fused REDC (field.h mul_add: column sums < 2^63.4, result < 2p)
-    const fq_t npb = -pb;
-    fq_t y1, y2;
+    const fq_t nb = -b.v;
+    fq_t sb;
+    MI_UNROLL for (int i = 0; i < 14; i++) sb.v[i] = odd ? nb.v[i] : b.v.v[i];
+    const fq_t pa = pair_swap(a.v), psb = pair_swap(sb);
+    fq_t x1, x3;
     MI_UNROLL for (int i = 0; i < 14; i++) {
-        y1.v[i] = odd ? pb.v[i] : b.v.v[i];
-        y2.v[i] = odd ? b.v.v[i] : npb.v[i];
+        x1.v[i] = odd ? pa.v[i] : a.v.v[i];
+        x3.v[i] = odd ? a.v.v[i] : pa.v[i];
     }
-    return {mul_add(a.v, y1, pa, y2)};
+    fq2h_t r = {mul_add(x1, b.v, x3, psb)};
+    __builtin_amdgcn_sched_barrier(0);
+    return r;
 }
 __device__ __forceinline__ fq2h_t sqr(const fq2h_t &a) {
     // even: (a0 + a1)(a0 - a1)     odd: (a1 + a1) a0
@@ -97,5 +105,23 @@ struct Lane<fq2_t> {  // G2: a lane pair per element, this lane's Fq half of eve
         return {{f[0]}, {f[2]}};
     }
 };
+
+// Bucket-reduction kernels (full XYZZ + XYZZ additions, two or three live accumulators): the lane
+// pair or one thread per G2 element (MI_G2_RED_PAIR); G1 is unchanged.
+#ifndef MI_G2_RED_PAIR
+#define MI_G2_RED_PAIR 1
+#endif
+template <class F>
+struct LaneRed : Lane<F> {};
+#if !MI_G2_RED_PAIR
+template <>
+struct LaneRed<fq2_t> {
+    static constexpr unsigned K = 1;
+    using R = fq2_t;
+    __device__ static XYZZ<R> ld(const XYZZ<fq2_t> *p) { return *p; }
+    __device__ static void st(XYZZ<fq2_t> *p, const XYZZ<R> &v) { *p = v; }
+    __device__ static Affine<R> lda(const Affine<fq2_t> *p) { return *p; }
+};
+#endif
 
 }  // namespace mi

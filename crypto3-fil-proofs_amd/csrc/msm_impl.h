@@ -34,6 +34,14 @@ namespace {
 // At least two waves per SIMD for the group-law kernels: without it the G2 (Fq2) instances take
 // all 512 unified registers (256 VGPR + 256 AGPR) and run one wave per SIMD.
 #define MI_WAVES2 __attribute__((amdgpu_waves_per_eu(2)))
+#ifndef MI_RED_CAP
+#define MI_RED_CAP 1
+#endif
+#if MI_RED_CAP
+#define MI_WAVES_RED MI_WAVES2
+#else
+#define MI_WAVES_RED
+#endif
 
 constexpr uint32_t L0_DEFAULT = 64;  // sorted entries per chunk at level 0 (mixed adds); MI_MSM_L0 overrides
 constexpr uint32_t L1 = 16;  // chunk partials summed per thread per tree level (full adds)
@@ -45,7 +53,7 @@ MI_HD uint32_t word_of(const fr_t &s, unsigned k) {
 }
 
 __global__ void k_digits(const fr_t *__restrict__ scalars, const uint32_t *__restrict__ idx, uint32_t n,
-                         unsigned c, unsigned nwin, uint32_t invalid, uint32_t *__restrict__ keys,
+                         unsigned c, unsigned nwin, uint32_t invalid, uint32_t wk, uint32_t *__restrict__ keys,
                          uint32_t *__restrict__ vals) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -70,7 +78,8 @@ __global__ void k_digits(const fr_t *__restrict__ scalars, const uint32_t *__res
             carry = 0;
         }
         uint64_t o = (uint64_t)w * n + i;
-        keys[o] = d ? d - 1 : invalid;  // bucket within the window; windows are sorted separately
+        // bucket within the window (+ w * wk when all windows are sorted in one call)
+        keys[o] = (d ? d - 1 : invalid) + w * wk;
         vals[o] = i | (neg << 31);
     }
 }
@@ -78,7 +87,7 @@ __global__ void k_digits(const fr_t *__restrict__ scalars, const uint32_t *__res
 // keys are window-local (sorted per window): global bucket = window * nbk + key.  Four sorted keys
 // per thread (one 16-byte load); the neighbours across the group edge are single loads (L2 hits).
 // zstart[w] = first sorted position of window w holding a zero digit (key nbk sorts last).
-__global__ void k_bounds4(const uint32_t *__restrict__ keys, uint32_t np, uint32_t n, uint32_t nbk,
+__global__ void k_bounds4(const uint32_t *__restrict__ keys, uint32_t np, uint32_t n, uint32_t nbk, uint32_t wk,
                           uint32_t *__restrict__ start, uint32_t *__restrict__ cnt, uint32_t *__restrict__ zstart) {
     uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t i0 = q * 4;
@@ -100,14 +109,14 @@ __global__ void k_bounds4(const uint32_t *__restrict__ keys, uint32_t np, uint32
             w++;
             lo += n;
         }
-        uint32_t kk = k[1 + j];
+        uint32_t kk = k[1 + j] - w * wk;  // window-local key
         if (kk == nbk) {  // zero digit: not a bucket entry
-            if (i == lo || k[j] != kk) zstart[w] = i;
+            if (i == lo || k[j] != k[1 + j]) zstart[w] = i;
             continue;
         }
         uint32_t g = w * nbk + kk;
-        if (i == lo || k[j] != kk) start[g] = i;
-        if (i + 1 == lo + n || k[2 + j] != kk) cnt[g] = i + 1;  // end; converted to a count below
+        if (i == lo || k[j] != k[1 + j]) start[g] = i;
+        if (i + 1 == lo + n || k[2 + j] != k[1 + j]) cnt[g] = i + 1;  // end; converted to a count below
     }
 }
 
@@ -205,13 +214,13 @@ __global__ void k_tree_heads(const uint32_t *__restrict__ qcnt, const uint32_t *
 }
 
 template <class F>
-__global__ void __launch_bounds__(256) MI_WAVES2 k_tree_level(const uint32_t *__restrict__ map,
+__global__ void __launch_bounds__(256) MI_WAVES_RED k_tree_level(const uint32_t *__restrict__ map,
                                                     const uint32_t *__restrict__ qoff,
                                                     const uint32_t *__restrict__ mlist,
                                                     const uint32_t *__restrict__ coff,
                                                     const uint32_t *__restrict__ ccnt, uint32_t total,
                                                     uint32_t stride, XYZZ<F> *__restrict__ P) {
-    using LP = Lane<F>;
+    using LP = LaneRed<F>;
     using R = typename LP::R;
     uint32_t u = (blockIdx.x * blockDim.x + threadIdx.x) / LP::K;
     if (u >= total) return;
@@ -233,12 +242,12 @@ __global__ void __launch_bounds__(256) MI_WAVES2 k_tree_level(const uint32_t *__
 //   seg_run = sum_j B_j,  seg_acc = sum_j (j + 1) B_j   (j = bucket index inside the segment)
 // Bucket b's sum is P[off[b]] when cnt[b] != 0 (level-0 chunk slot of its first chunk).
 template <class F>
-__global__ void __launch_bounds__(256) MI_WAVES2 k_bucket_reduce(const uint32_t *__restrict__ off,
+__global__ void __launch_bounds__(256) MI_WAVES_RED k_bucket_reduce(const uint32_t *__restrict__ off,
                                                        const uint32_t *__restrict__ cnt,
                                                        const XYZZ<F> *__restrict__ P, uint32_t nseg_total,
                                                        unsigned seg_len, XYZZ<F> *__restrict__ seg_acc,
                                                        XYZZ<F> *__restrict__ seg_run) {
-    using LP = Lane<F>;
+    using LP = LaneRed<F>;
     using R = typename LP::R;
     uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) / LP::K;
     if (t >= nseg_total) return;
@@ -256,12 +265,12 @@ __global__ void __launch_bounds__(256) MI_WAVES2 k_bucket_reduce(const uint32_t 
 // The same over a dense array of points (second level: the first level's segment sums), also
 // summing the first level's accumulators over the segment (sum_acc).
 template <class F>
-__global__ void __launch_bounds__(256) MI_WAVES2 k_bucket_reduce_dense(const XYZZ<F> *__restrict__ P,
+__global__ void __launch_bounds__(256) MI_WAVES_RED k_bucket_reduce_dense(const XYZZ<F> *__restrict__ P,
                                                              const XYZZ<F> *__restrict__ A, uint32_t nseg_total,
                                                              unsigned seg_len, XYZZ<F> *__restrict__ seg_acc,
                                                              XYZZ<F> *__restrict__ seg_run,
                                                              XYZZ<F> *__restrict__ sum_acc) {
-    using LP = Lane<F>;
+    using LP = LaneRed<F>;
     using R = typename LP::R;
     uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) / LP::K;
     if (t >= nseg_total) return;
@@ -280,10 +289,10 @@ __global__ void __launch_bounds__(256) MI_WAVES2 k_bucket_reduce_dense(const XYZ
 
 // out[t] = seg_acc[t] + (s * seg_len) * seg_run[t], s = segment index inside its window
 template <class F>
-__global__ void __launch_bounds__(256) MI_WAVES2 k_seg_fold(const XYZZ<F> *__restrict__ seg_acc,
+__global__ void __launch_bounds__(256) MI_WAVES_RED k_seg_fold(const XYZZ<F> *__restrict__ seg_acc,
                                                   const XYZZ<F> *__restrict__ seg_run, uint32_t nseg_total,
                                                   uint32_t nseg, unsigned seg_len, XYZZ<F> *__restrict__ out) {
-    using LP = Lane<F>;
+    using LP = LaneRed<F>;
     using R = typename LP::R;
     uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) / LP::K;
     if (t >= nseg_total) return;
@@ -305,9 +314,9 @@ __global__ void __launch_bounds__(256) MI_WAVES2 k_seg_fold(const XYZZ<F> *__res
 
 // out[w * (n / G) + g] = sum of in[w * n + g * G ... + G)   (n % G == 0)
 template <class F>
-__global__ void __launch_bounds__(256) MI_WAVES2 k_sum_groups(const XYZZ<F> *__restrict__ in, uint32_t total_out,
+__global__ void __launch_bounds__(256) MI_WAVES_RED k_sum_groups(const XYZZ<F> *__restrict__ in, uint32_t total_out,
                                                     unsigned G, XYZZ<F> *__restrict__ out) {
-    using LP = Lane<F>;
+    using LP = LaneRed<F>;
     using R = typename LP::R;
     uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) / LP::K;
     if (t >= total_out) return;
@@ -351,6 +360,12 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
     const uint32_t nb = (uint32_t)nb64, np = (uint32_t)np64, invalid = nbk;  // window-local keys
     unsigned key_bits = 1;
     while ((1ull << key_bits) <= invalid) key_bits++;  // cb bits: one fewer onesweep pass than global keys
+    // Small MSMs sort every window in ONE call over keys w * (nbk + 1) + local when that still takes
+    // two 11-bit onesweep places (2^20: 2 launches instead of 32); large ones sort window by window.
+    unsigned all_bits = 1;
+    while ((1ull << all_bits) <= (uint64_t)nwin * (nbk + 1) - 1) all_bits++;
+    const bool one_sort = all_bits <= 22 && nwin > 1;
+    const uint32_t wk = one_sort ? nbk + 1 : 0;
     pl.cb = cb;
     pl.nwin = nwin;
     pl.nbk = nbk;
@@ -369,20 +384,27 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
 
     {
         ScopedTimer tsort(c, &c.stats.sort, n);
-        k_digits<<<grid_for(n, 256), 256, 0, st>>>(scalars, idx, (uint32_t)n, cb, nwin, invalid, keys, vals);
+        k_digits<<<grid_for(n, 256), 256, 0, st>>>(scalars, idx, (uint32_t)n, cb, nwin, invalid, wk, keys, vals);
         MI_LAUNCHED(c, "k_digits");
         size_t tmp_bytes = 0;
-        sort_pairs_u32(nullptr, tmp_bytes, keys, keys_s, vals, vals_s, (uint32_t)n, key_bits, st);
-        void *tmp = c.scratch[4].get(tmp_bytes);
-        for (unsigned w = 0; w < nwin; w++) {
-            uint64_t o = (uint64_t)w * n;
-            sort_pairs_u32(tmp, tmp_bytes, keys + o, keys_s + o, vals + o, vals_s + o, (uint32_t)n, key_bits, st);
+        if (one_sort) {
+            sort_pairs_u32(nullptr, tmp_bytes, keys, keys_s, vals, vals_s, np, all_bits, st);
+            void *tmp = c.scratch[4].get(tmp_bytes);
+            sort_pairs_u32(tmp, tmp_bytes, keys, keys_s, vals, vals_s, np, all_bits, st);
+        } else {
+            sort_pairs_u32(nullptr, tmp_bytes, keys, keys_s, vals, vals_s, (uint32_t)n, key_bits, st);
+            void *tmp = c.scratch[4].get(tmp_bytes);
+            for (unsigned w = 0; w < nwin; w++) {
+                uint64_t o = (uint64_t)w * n;
+                sort_pairs_u32(tmp, tmp_bytes, keys + o, keys_s + o, vals + o, vals_s + o, (uint32_t)n, key_bits,
+                               st);
+            }
         }
         MI_HIP(hipMemsetAsync(offA, 0, sizeof(uint32_t) * nb, st));
         MI_HIP(hipMemsetAsync(cntA, 0, sizeof(uint32_t) * nb, st));
         MI_HIP(hipMemsetAsync(zstart, 0xff, sizeof(uint32_t) * nwin, st));
         const uint32_t nq = (np + 3) / 4;
-        k_bounds4<<<grid_for(nq, 256), 256, 0, st>>>(keys_s, np, (uint32_t)n, nbk, offA, cntA, zstart);
+        k_bounds4<<<grid_for(nq, 256), 256, 0, st>>>(keys_s, np, (uint32_t)n, nbk, wk, offA, cntA, zstart);
         MI_LAUNCHED(c, "k_bounds4");
         k_end_to_cnt<<<grid_for(nb, 256), 256, 0, st>>>(offA, cntA, nb);
         MI_LAUNCHED(c, "k_end_to_cnt");
@@ -458,7 +480,8 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
 template <class F>
 void msm_accumulate_impl(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, XYZZ<F> *result) {
     hipStream_t st = c.stream;
-    const unsigned K = Lane<F>::K;  // threads per group element (2 for G2: g2pair.h)
+    const unsigned K = Lane<F>::K;      // threads per element in the accumulation (2 for G2: g2pair.h)
+    const unsigned KR = LaneRed<F>::K;  // ... and in the reduction kernels
     const unsigned cb = pl.cb, nwin = pl.nwin;
     const uint32_t nbk = pl.nbk, nb = pl.nb, L0 = pl.L0;
     const uint32_t *coff = pl.coff, *ccnt = pl.ccnt, *offA = pl.off, *cntA = pl.cnt;
@@ -507,7 +530,7 @@ void msm_accumulate_impl(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, XYZZ
             MI_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, heads, map, MaxOp(), total, st));
             tmp = c.scratch[4].get(tb);
             MI_HIP(hipcub::DeviceScan::InclusiveScan(tmp, tb, heads, map, MaxOp(), total, st));
-            k_tree_level<F><<<grid_for((uint64_t)total * K, 256), 256, 0, st>>>(map, qoff, mlist, coff, ccnt, total,
+            k_tree_level<F><<<grid_for((uint64_t)total * KR, 256), 256, 0, st>>>(map, qoff, mlist, coff, ccnt, total,
                                                                    (uint32_t)stride, P0);
             MI_LAUNCHED(c, "k_tree_level");
         }
@@ -527,11 +550,11 @@ void msm_accumulate_impl(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, XYZZ
     // [sumAccB | runB | foldB] contiguous (one stacked tree sum over 3 * nwin rows), then accB
     XYZZ<F> *sumB = c.scratch[14].as<XYZZ<F>>(4 * (uint64_t)totB), *runB = sumB + totB, *foldB = runB + totB,
             *accB = foldB + totB;
-    k_bucket_reduce<F><<<grid_for((uint64_t)totA * K, 256), 256, 0, st>>>(coff, cntA, P0, totA, SA, accA, runA);
+    k_bucket_reduce<F><<<grid_for((uint64_t)totA * KR, 256), 256, 0, st>>>(coff, cntA, P0, totA, SA, accA, runA);
     MI_LAUNCHED(c, "k_bucket_reduce");
-    k_bucket_reduce_dense<F><<<grid_for((uint64_t)totB * K, 256), 256, 0, st>>>(runA, accA, totB, SB, accB, runB, sumB);
+    k_bucket_reduce_dense<F><<<grid_for((uint64_t)totB * KR, 256), 256, 0, st>>>(runA, accA, totB, SB, accB, runB, sumB);
     MI_LAUNCHED(c, "k_bucket_reduce_dense");
-    k_seg_fold<F><<<grid_for((uint64_t)totB * K, 256), 256, 0, st>>>(accB, runB, totB, nsegB, SB, foldB);
+    k_seg_fold<F><<<grid_for((uint64_t)totB * KR, 256), 256, 0, st>>>(accB, runB, totB, nsegB, SB, foldB);
     MI_LAUNCHED(c, "k_seg_fold");
     // stacked per-row tree sum of nsegB (a power of two) entries, groups of <= 8 (shallow chains)
     const uint32_t rows = 3 * nwin;
@@ -542,7 +565,7 @@ void msm_accumulate_impl(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, XYZZ
     for (uint32_t per = nsegB; per > 1;) {
         unsigned G = per >= 8 ? 8 : per;
         uint32_t outs = rows * (per / G);
-        k_sum_groups<F><<<grid_for((uint64_t)outs * K, 256), 256, 0, st>>>(cur, outs, G, bufs[k]);
+        k_sum_groups<F><<<grid_for((uint64_t)outs * KR, 256), 256, 0, st>>>(cur, outs, G, bufs[k]);
         MI_LAUNCHED(c, "k_sum_groups");
         per /= G;
         cur = bufs[k];

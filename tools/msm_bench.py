@@ -19,6 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--log-rows", type=int, default=26)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--query", type=int, default=0, help="0 h, 1 l, 2 a, 3 b_g1, 4 b_g2")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -30,8 +31,8 @@ def main():
     sc = synth.SynthCircuit(a.log_rows, 4, 1)
     circ = sc.load(ctx)
     pk = fg.generate_random_parameters(ctx, circ, splitmix_frs(TOXIC_SEED, 5))
-    n = pk.n_h
-    pts = pk.points(0)
+    pts = pk.points(a.query)
+    n = pts.n
     rng = np.random.default_rng(7)
     sw = rng.integers(0, 2**64, size=(n, 4), dtype=np.uint64)
     sw[:, 3] &= np.uint64(0x3FFFFFFFFFFFFFFF)
@@ -45,8 +46,9 @@ def main():
     ctx.synchronize()
     dt = (time.perf_counter() - t) / a.reps * 1e3
     st = ctx.stats()
-    per = {k: round(st[k]["ms"] / a.reps, 2) for k in ("sort", "accum_g1", "msm_g1")}
-    print(f"G1 MSM n={n}: {dt:.1f} ms wall ({n / dt / 1e3:.1f} Mpts/s); per MSM {per}", flush=True)
+    grp = "g2" if a.query == 4 else "g1"
+    per = {k: round(st[k]["ms"] / a.reps, 2) for k in ("sort", "accum_" + grp, "msm_" + grp)}
+    print(f"{grp.upper()} MSM query={a.query} n={n}: {dt:.1f} ms wall ({n / dt / 1e3:.1f} Mpts/s); per MSM {per}", flush=True)
 
 
 if __name__ == "__main__":
