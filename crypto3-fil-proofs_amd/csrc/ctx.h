@@ -202,6 +202,9 @@ void ntt_dit(Ctx &c, fr_t *d, unsigned log_n, bool inverse);
 void bitrev_permute(Ctx &c, fr_t *d, unsigned log_n);
 // DIF NTT whose last pass also multiplies position pos by g^(+-bitrev(pos)) * scale (and optionally
 // converts to canonical): iNTT + coset shift (+ 1/d) in the same HBM passes
+// iNTT -> coset shift * scale -> NTT in natural order (a, b, c of the QAP), one pass fewer than the
+// two transforms separately
+void ntt_coset_roundtrip(Ctx &c, fr_t *d, unsigned log_n, const fr_t &scale);
 void ntt_dif_coset_epilogue(Ctx &c, fr_t *d, unsigned log_n, bool inverse, bool inverse_gen, const fr_t &scale,
                             bool to_canonical);
 // d[pos] *= g^(±bitrev(pos)) * scale (scale may be null)

@@ -68,55 +68,17 @@ __device__ __forceinline__ fr_t tw_b(const fr_t *__restrict__ tw10, unsigned j, 
     return tw10[j << (TILE_LOG - b)];  // omega_{2^b}^j
 }
 
-// One pass.  DIF: load -> b DIF stages -> optional inter-pass twiddle -> [epilogue] -> store.
-//            DIT: load -> optional inter-pass twiddle -> b DIT stages (reverse) -> store.
-// The b stages run as radix-4 rounds (two stages per LDS round trip: each thread holds the four
-// elements x, x + h/2, x + h, x + 3h/2 of one group in registers) plus one radix-2 round when b is
-// odd; in-tile twiddles omega_{2^b}^j come from the 512-entry omega_1024 table (L1-resident).
-// Epilogue (last DIF pass only): epi = 1 multiplies the element at global position pos by
-// G^bitrev_L(pos) * scale (coset shift of the bit-reversed coefficients, fused 1/d); epi = 2 also
-// converts to canonical form (icoset: H for the MSM).
+// The b stages of one tile: radix-4 register rounds (two stages per LDS round trip) plus one
+// radix-2 round when b is odd.  DIF runs rounds in order, DIT the transpose in reverse order.
 template <bool DIF>
-__global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(fr_t *__restrict__ d, unsigned L, unsigned M, unsigned b,
-                                                          unsigned Tlog, unsigned Glog, int twiddle,
-                                                          const fr_t *__restrict__ lo,
-                                                          const fr_t *__restrict__ hi,
-                                                          const fr_t *__restrict__ tw10, int epi,
-                                                          const fr_t *__restrict__ glo,
-                                                          const fr_t *__restrict__ ghi, fr_t scale) {
-    __shared__ LdsTile sh;
+__device__ __forceinline__ void ntt_rounds(LdsTile &sh, unsigned b, unsigned Tlog, unsigned tile,
+                                           const fr_t *__restrict__ tw10) {
     const unsigned T = 1u << Tlog;
-    const unsigned Slog = M - b;
-    const uint64_t S = 1ull << Slog;
-    const unsigned tile_log = Glog + b + Tlog;
-    const unsigned tile = 1u << tile_log;
-    uint64_t sub0, i20;
-    if (Glog > 0) {  // several whole sub-problems per workgroup (T == S)
-        sub0 = (uint64_t)blockIdx.x << Glog;
-        i20 = 0;
-    } else {
-        uint64_t blocks_per_sub = S >> Tlog;
-        sub0 = blockIdx.x / blocks_per_sub;
-        i20 = (blockIdx.x % blocks_per_sub) << Tlog;
-    }
-    const unsigned bmask = (1u << b) - 1;
-    // load
-    for (unsigned e = threadIdx.x; e < tile; e += NTT_THREADS) {
-        unsigned t = e & (T - 1), i1 = (e >> Tlog) & bmask, g = e >> (Tlog + b);
-        uint64_t gi = ((sub0 + g) << M) + ((uint64_t)i1 << Slog) + i20 + t;
-        fr_t x = d[gi];
-        if (!DIF && twiddle) {
-            uint32_t k1 = brev(i1, b);
-            uint32_t ex = (uint32_t)(((uint64_t)(i20 + t) * k1) << (32 - M));
-            if (ex) x = x * tw_full(lo, hi, ex);
-        }
-        lds_put(sh, e, x);
-    }
-    __syncthreads();
     const unsigned nquad = tile >> 2;
     const unsigned nr4 = b >> 1;  // radix-4 rounds: DIF stage pairs (0,1), (2,3), ...
     const bool odd = b & 1;       // + one radix-2 round for stage b - 1
     const unsigned q = threadIdx.x;
+    const unsigned bmask = (1u << b) - 1;
     for (unsigned rr = 0; rr < nr4 + (odd ? 1 : 0); rr++) {
         // DIF runs rounds in order; DIT runs them in reverse (the radix-2 round first when b is odd)
         const unsigned r = DIF ? rr : nr4 + (odd ? 1 : 0) - 1 - rr;
@@ -178,17 +140,78 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(fr_t *__restrict__ d, 
         }
         __syncthreads();
     }
+}
+
+// One pass.  DIF: load -> b DIF stages -> optional inter-pass twiddle -> [epilogue] -> store.
+//            DIT: load -> optional inter-pass twiddle -> b DIT stages (reverse) -> store.
+// The b stages run as radix-4 rounds (two stages per LDS round trip: each thread holds the four
+// elements x, x + h/2, x + h, x + 3h/2 of one group in registers) plus one radix-2 round when b is
+// odd; in-tile twiddles omega_{2^b}^j come from the 512-entry omega_1024 table (L1-resident).
+// Epilogue (last DIF pass only): epi = 1 multiplies the element at global position pos by
+// G^bitrev_L(pos) * scale (coset shift of the bit-reversed coefficients, fused 1/d); epi = 2 also
+// converts to canonical form (icoset: H for the MSM).
+template <bool DIF, bool FUSED = false>
+__global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(fr_t *__restrict__ d, unsigned L, unsigned M, unsigned b,
+                                                          unsigned Tlog, unsigned Glog, int twiddle,
+                                                          const fr_t *__restrict__ lo,
+                                                          const fr_t *__restrict__ hi,
+                                                          const fr_t *__restrict__ tw10, int epi,
+                                                          const fr_t *__restrict__ glo,
+                                                          const fr_t *__restrict__ ghi, fr_t scale,
+                                                          const fr_t *__restrict__ tw10b = nullptr) {
+    __shared__ LdsTile sh;
+    const unsigned T = 1u << Tlog;
+    const unsigned Slog = M - b;
+    const uint64_t S = 1ull << Slog;
+    const unsigned tile_log = Glog + b + Tlog;
+    const unsigned tile = 1u << tile_log;
+    uint64_t sub0, i20;
+    if (Glog > 0) {  // several whole sub-problems per workgroup (T == S)
+        sub0 = (uint64_t)blockIdx.x << Glog;
+        i20 = 0;
+    } else {
+        uint64_t blocks_per_sub = S >> Tlog;
+        sub0 = blockIdx.x / blocks_per_sub;
+        i20 = (blockIdx.x % blocks_per_sub) << Tlog;
+    }
+    const unsigned bmask = (1u << b) - 1;
+    // load
+    for (unsigned e = threadIdx.x; e < tile; e += NTT_THREADS) {
+        unsigned t = e & (T - 1), i1 = (e >> Tlog) & bmask, g = e >> (Tlog + b);
+        uint64_t gi = ((sub0 + g) << M) + ((uint64_t)i1 << Slog) + i20 + t;
+        fr_t x = d[gi];
+        if (!DIF && twiddle) {
+            uint32_t k1 = brev(i1, b);
+            uint32_t ex = (uint32_t)(((uint64_t)(i20 + t) * k1) << (32 - M));
+            if (ex) x = x * tw_full(lo, hi, ex);
+        }
+        lds_put(sh, e, x);
+    }
+    __syncthreads();
+    ntt_rounds<DIF>(sh, b, Tlog, tile, tw10);
+    if (FUSED) {  // middle of iNTT -> coset -> NTT: epilogue in LDS, then the DIT rounds of the same tile
+        for (unsigned e = threadIdx.x; e < tile; e += NTT_THREADS) {
+            unsigned t = e & (T - 1), i1 = (e >> Tlog) & bmask, g = e >> (Tlog + b);
+            uint64_t gi = ((sub0 + g) << M) + ((uint64_t)i1 << Slog) + i20 + t;
+            fr_t x = lds_get(sh, e);
+            uint32_t ex = brev((uint32_t)gi, L);
+            if (ex) x = x * tw_full(glo, ghi, ex);
+            lds_put(sh, e, x * scale);
+        }
+        __syncthreads();
+        ntt_rounds<false>(sh, b, Tlog, tile, tw10b);
+    }
     // store
     for (unsigned e = threadIdx.x; e < tile; e += NTT_THREADS) {
         unsigned t = e & (T - 1), i1 = (e >> Tlog) & bmask, g = e >> (Tlog + b);
         uint64_t gi = ((sub0 + g) << M) + ((uint64_t)i1 << Slog) + i20 + t;
         fr_t x = lds_get(sh, e);
-        if (DIF && twiddle) {
+        if (DIF && !FUSED && twiddle) {
             uint32_t k1 = brev(i1, b);
             uint32_t ex = (uint32_t)(((uint64_t)(i20 + t) * k1) << (32 - M));
             if (ex) x = x * tw_full(lo, hi, ex);
         }
-        if (DIF && epi) {
+        if (DIF && !FUSED && epi) {
             uint32_t ex = brev((uint32_t)gi, L);
             if (ex) x = x * tw_full(glo, ghi, ex);
             x = x * scale;
@@ -372,6 +395,40 @@ static void ntt_run(Ctx &c, fr_t *d, unsigned L, bool inverse, bool dif, int epi
                                                                                   p.twiddle, lo, hi, tw10, 0, glo,
                                                                                   ghi, scale);
         }
+    }
+    MI_HIP(hipGetLastError());
+}
+
+// iNTT (DIF, natural -> bit-reversed) -> * g^bitrev(pos) * scale -> NTT (DIT, -> natural): the QAP's
+// "evaluations on the domain -> evaluations on the coset" for a, b, c.  The innermost DIF pass and the
+// first DIT pass work on the same contiguous tiles, so they run as ONE kernel (k_ntt_pass<true, true>):
+// one HBM pass fewer per vector than ntt_dif_coset_epilogue + ntt_dit.
+void ntt_coset_roundtrip(Ctx &c, fr_t *d, unsigned L, const fr_t &scale) {
+    if (L > 32) throw std::runtime_error("ntt: domain larger than 2^32");
+    if (L == 0) {
+        scale_all(c, d, 1, scale);
+        return;
+    }
+    ScopedTimer tm(c, &c.stats.ntt, 1ull << L);
+    auto plan = plan_passes(L);
+    const size_t last = plan.size() - 1;
+    for (size_t i = 0; i < last; i++) {
+        auto &p = plan[i];
+        k_ntt_pass<true><<<(unsigned)p.blocks, NTT_THREADS, 0, c.stream>>>(d, L, p.M, p.b, p.Tlog, p.Glog, p.twiddle,
+                                                                             c.tw.iv_lo, c.tw.iv_hi, c.tw.iv_1024, 0,
+                                                                             c.tw.g_lo, c.tw.g_hi, scale);
+    }
+    {
+        auto &p = plan[last];
+        k_ntt_pass<true, true><<<(unsigned)p.blocks, NTT_THREADS, 0, c.stream>>>(
+            d, L, p.M, p.b, p.Tlog, p.Glog, 0, c.tw.iv_lo, c.tw.iv_hi, c.tw.iv_1024, 1, c.tw.g_lo, c.tw.g_hi, scale,
+            c.tw.fw_1024);
+    }
+    for (int i = (int)last - 1; i >= 0; i--) {
+        auto &p = plan[i];
+        k_ntt_pass<false><<<(unsigned)p.blocks, NTT_THREADS, 0, c.stream>>>(d, L, p.M, p.b, p.Tlog, p.Glog, p.twiddle,
+                                                                              c.tw.fw_lo, c.tw.fw_hi, c.tw.fw_1024, 0,
+                                                                              c.tw.g_lo, c.tw.g_hi, scale);
     }
     MI_HIP(hipGetLastError());
 }

@@ -736,8 +736,7 @@ ProofPoints groth16_prove(Ctx &c, const Srs &srs, const Circuit &circ, const fr_
             fr_t dinv = inverse(to_mont(dd));
             fr_t *vecs[3] = {a, b, cc};
             for (fr_t *v : vecs) {
-                ntt_dif_coset_epilogue(c, v, L, true, false, dinv, false);  // ifft, then * g^i / d (bit-reversed)
-                ntt_dit(c, v, L, false);                                    // fft on the coset (natural order)
+                ntt_coset_roundtrip(c, v, L, dinv);  // ifft, * g^i / d, fft on the coset (natural order)
             }
             fr_t g = fr_small_mont(7);
             fr_t zinv = inverse(pow_u64(g, d) - fr_t::one());
