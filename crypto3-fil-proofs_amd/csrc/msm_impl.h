@@ -22,6 +22,7 @@
 //   7. host         : Horner over windows (c doublings each) on the CPU.
 #pragma once
 #include <hipcub/hipcub.hpp>
+#include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include "ctx.h"
@@ -84,11 +85,80 @@ __global__ void k_digits(const fr_t *__restrict__ scalars, const uint32_t *__res
     }
 }
 
+// Large MSMs: the same digits, but only the NON-ZERO ones are written, compacted per window at
+// [w * n, w * n + wcount[w]) (wave ballots, one atomic per window per workgroup).  Witness scalars are
+// boolean-heavy (0/1 and small values): 43 % of the L/A/B digit slots of the synthetic 2^26 circuit
+// are zero, and none of them is sorted any more.  Order inside a window is arbitrary before the sort.
+constexpr unsigned MAXW_C = 32;  // c >= 8
+__global__ void __launch_bounds__(256) k_digits_c(const fr_t *__restrict__ scalars, const uint32_t *__restrict__ idx,
+                                                  uint32_t n, unsigned c, unsigned nwin,
+                                                  uint32_t *__restrict__ wcount, uint32_t *__restrict__ keys,
+                                                  uint32_t *__restrict__ vals) {
+    __shared__ uint32_t wc[4][MAXW_C];
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    fr_t s = fr_t::zero();
+    if (i < n) s = scalars[idx ? idx[i] : i];
+    const uint32_t nbk = 1u << (c - 1);
+    const uint32_t mask = (1u << c) - 1;
+    uint32_t dg[MAXW_C];  // digit | neg << 31; 0 = zero digit
+    uint32_t carry = 0;
+    MI_UNROLL for (unsigned w = 0; w < MAXW_C; w++) {
+        dg[w] = 0;
+        if (w >= nwin) continue;
+        unsigned bit = w * c, word = bit >> 5, sh = bit & 31;
+        uint32_t d = 0;
+        if (word < 8) {
+            d = word_of(s, word) >> sh;
+            if (sh + c > 32 && word + 1 < 8) d |= word_of(s, word + 1) << (32 - sh);
+        }
+        d = (d & mask) + carry;
+        uint32_t neg = 0;
+        if (d > nbk) {
+            d = (1u << c) - d;
+            neg = 1;
+            carry = 1;
+        } else {
+            carry = 0;
+        }
+        dg[w] = d ? d | (neg << 31) : 0;
+    }
+    const uint64_t below = (1ull << lane) - 1;
+    uint32_t rank[MAXW_C];
+    MI_UNROLL for (unsigned w = 0; w < MAXW_C; w++) {
+        if (w >= nwin) break;
+        uint64_t m = __ballot(dg[w] != 0);
+        rank[w] = (uint32_t)__popcll(m & below);
+        if (lane == 0) wc[wave][w] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (threadIdx.x < nwin) {
+        const unsigned w = threadIdx.x;
+        uint32_t c0 = wc[0][w], c1 = wc[1][w], c2 = wc[2][w], c3 = wc[3][w];
+        uint32_t base = atomicAdd(&wcount[w], c0 + c1 + c2 + c3);
+        wc[0][w] = base;
+        wc[1][w] = base + c0;
+        wc[2][w] = base + c0 + c1;
+        wc[3][w] = base + c0 + c1 + c2;
+    }
+    __syncthreads();
+    MI_UNROLL for (unsigned w = 0; w < MAXW_C; w++) {
+        if (w >= nwin) break;
+        if (dg[w]) {
+            uint64_t o = (uint64_t)w * n + wc[wave][w] + rank[w];
+            keys[o] = (dg[w] & 0x7fffffffu) - 1;
+            vals[o] = i | (dg[w] & 0x80000000u);
+        }
+    }
+}
+
 // keys are window-local (sorted per window): global bucket = window * nbk + key.  Four sorted keys
 // per thread (one 16-byte load); the neighbours across the group edge are single loads (L2 hits).
 // zstart[w] = first sorted position of window w holding a zero digit (key nbk sorts last).
+// wcnt (compacted digits, else null): window w holds wcnt[w] valid entries from w * n on.
 __global__ void k_bounds4(const uint32_t *__restrict__ keys, uint32_t np, uint32_t n, uint32_t nbk, uint32_t wk,
-                          uint32_t *__restrict__ start, uint32_t *__restrict__ cnt, uint32_t *__restrict__ zstart) {
+                          const uint32_t *__restrict__ wcnt, uint32_t *__restrict__ start, uint32_t *__restrict__ cnt,
+                          uint32_t *__restrict__ zstart) {
     uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t i0 = q * 4;
     if (i0 >= np) return;
@@ -109,6 +179,8 @@ __global__ void k_bounds4(const uint32_t *__restrict__ keys, uint32_t np, uint32
             w++;
             lo += n;
         }
+        const uint32_t lim = wcnt ? wcnt[w] : n;
+        if (i - lo >= lim) continue;  // beyond the compacted entries of this window
         uint32_t kk = k[1 + j] - w * wk;  // window-local key
         if (kk == nbk) {  // zero digit: not a bucket entry
             if (i == lo || k[j] != k[1 + j]) zstart[w] = i;
@@ -116,7 +188,7 @@ __global__ void k_bounds4(const uint32_t *__restrict__ keys, uint32_t np, uint32
         }
         uint32_t g = w * nbk + kk;
         if (i == lo || k[j] != k[1 + j]) start[g] = i;
-        if (i + 1 == lo + n || k[2 + j] != k[1 + j]) cnt[g] = i + 1;  // end; converted to a count below
+        if (i + 1 == lo + lim || k[2 + j] != k[1 + j]) cnt[g] = i + 1;  // end; converted to a count below
     }
 }
 
@@ -364,7 +436,11 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
     // two 11-bit onesweep places (2^20: 2 launches instead of 32); large ones sort window by window.
     unsigned all_bits = 1;
     while ((1ull << all_bits) <= (uint64_t)nwin * (nbk + 1) - 1) all_bits++;
-    const bool one_sort = all_bits <= 22 && nwin > 1;
+    // MI_MSM_SORT=windowed forces the per-window path (and with it the zero-digit compaction when
+    // nwin <= MAXW_C) at any size: tests use it to cover the large-MSM path at 2^20
+    const char *sort_env = getenv("MI_MSM_SORT");
+    const bool force_windowed = sort_env && strcmp(sort_env, "windowed") == 0;
+    const bool one_sort = !force_windowed && all_bits <= 22 && nwin > 1;
     const uint32_t wk = one_sort ? nbk + 1 : 0;
     pl.cb = cb;
     pl.nwin = nwin;
@@ -379,32 +455,50 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
     uint32_t *cntA = c.scratch[6].as<uint32_t>(nb);
     uint32_t *offB = c.scratch[7].as<uint32_t>(nb);
     uint32_t *cntB = c.scratch[8].as<uint32_t>(nb);
-    uint32_t *dmax = c.scratch[9].as<uint32_t>(4 + nwin);  // [max bucket size, pad, zstart[nwin]]
-    uint32_t *zstart = dmax + 4;
+    uint32_t *dmax = c.scratch[9].as<uint32_t>(4 + 2 * nwin);  // [max bucket size, pad, zstart[nwin], wcount[nwin]]
+    uint32_t *zstart = dmax + 4, *wcount = zstart + nwin;
+    const bool compact = !one_sort && nwin <= MAXW_C;  // large MSMs: only non-zero digits are sorted
+    std::vector<uint32_t> wn(nwin, 0);
 
     {
         ScopedTimer tsort(c, &c.stats.sort, n);
-        k_digits<<<grid_for(n, 256), 256, 0, st>>>(scalars, idx, (uint32_t)n, cb, nwin, invalid, wk, keys, vals);
-        MI_LAUNCHED(c, "k_digits");
         size_t tmp_bytes = 0;
-        if (one_sort) {
-            sort_pairs_u32(nullptr, tmp_bytes, keys, keys_s, vals, vals_s, np, all_bits, st);
-            void *tmp = c.scratch[4].get(tmp_bytes);
-            sort_pairs_u32(tmp, tmp_bytes, keys, keys_s, vals, vals_s, np, all_bits, st);
-        } else {
+        if (compact) {
+            MI_HIP(hipMemsetAsync(wcount, 0, sizeof(uint32_t) * nwin, st));
+            k_digits_c<<<grid_for(n, 256), 256, 0, st>>>(scalars, idx, (uint32_t)n, cb, nwin, wcount, keys, vals);
+            MI_LAUNCHED(c, "k_digits_c");
+            MI_HIP(hipMemcpyAsync(wn.data(), wcount, sizeof(uint32_t) * nwin, hipMemcpyDeviceToHost, st));
+            MI_HIP(hipStreamSynchronize(st));
             sort_pairs_u32(nullptr, tmp_bytes, keys, keys_s, vals, vals_s, (uint32_t)n, key_bits, st);
             void *tmp = c.scratch[4].get(tmp_bytes);
             for (unsigned w = 0; w < nwin; w++) {
                 uint64_t o = (uint64_t)w * n;
-                sort_pairs_u32(tmp, tmp_bytes, keys + o, keys_s + o, vals + o, vals_s + o, (uint32_t)n, key_bits,
-                               st);
+                if (wn[w])
+                    sort_pairs_u32(tmp, tmp_bytes, keys + o, keys_s + o, vals + o, vals_s + o, wn[w], key_bits, st);
+            }
+        } else {
+            k_digits<<<grid_for(n, 256), 256, 0, st>>>(scalars, idx, (uint32_t)n, cb, nwin, invalid, wk, keys, vals);
+            MI_LAUNCHED(c, "k_digits");
+            if (one_sort) {
+                sort_pairs_u32(nullptr, tmp_bytes, keys, keys_s, vals, vals_s, np, all_bits, st);
+                void *tmp = c.scratch[4].get(tmp_bytes);
+                sort_pairs_u32(tmp, tmp_bytes, keys, keys_s, vals, vals_s, np, all_bits, st);
+            } else {
+                sort_pairs_u32(nullptr, tmp_bytes, keys, keys_s, vals, vals_s, (uint32_t)n, key_bits, st);
+                void *tmp = c.scratch[4].get(tmp_bytes);
+                for (unsigned w = 0; w < nwin; w++) {
+                    uint64_t o = (uint64_t)w * n;
+                    sort_pairs_u32(tmp, tmp_bytes, keys + o, keys_s + o, vals + o, vals_s + o, (uint32_t)n, key_bits,
+                                   st);
+                }
             }
         }
         MI_HIP(hipMemsetAsync(offA, 0, sizeof(uint32_t) * nb, st));
         MI_HIP(hipMemsetAsync(cntA, 0, sizeof(uint32_t) * nb, st));
         MI_HIP(hipMemsetAsync(zstart, 0xff, sizeof(uint32_t) * nwin, st));
         const uint32_t nq = (np + 3) / 4;
-        k_bounds4<<<grid_for(nq, 256), 256, 0, st>>>(keys_s, np, (uint32_t)n, nbk, wk, offA, cntA, zstart);
+        k_bounds4<<<grid_for(nq, 256), 256, 0, st>>>(keys_s, np, (uint32_t)n, nbk, wk, compact ? wcount : nullptr,
+                                                      offA, cntA, zstart);
         MI_LAUNCHED(c, "k_bounds4");
         k_end_to_cnt<<<grid_for(nb, 256), 256, 0, st>>>(offA, cntA, nb);
         MI_LAUNCHED(c, "k_end_to_cnt");
@@ -423,7 +517,7 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
     pl.maxcnt = head[0];
     pl.entries = 0;  // non-zero digits = mixed additions of the accumulation
     for (unsigned w = 0; w < nwin; w++)
-        pl.entries += head[4 + w] == 0xffffffffu ? n : head[4 + w] - (uint64_t)w * n;
+        pl.entries += compact ? wn[w] : head[4 + w] == 0xffffffffu ? n : head[4 + w] - (uint64_t)w * n;
 
     static const uint32_t L0 = [] {
         const char *e = getenv("MI_MSM_L0");

@@ -127,7 +127,15 @@ def test_msm_rejects_bad_points(ctx, oracle):
         ctx.msm_g1(bytes(bases), rand_fr_bytes(4, 12))
 
 
-def test_msm_g1_linearity_2_20(ctx, oracle):
+@pytest.fixture(params=["auto", "windowed"])
+def sort_mode(request, monkeypatch):
+    """auto: 2^20 sorts every window in one call; windowed: the per-window sort with zero-digit
+    compaction that MSMs of 2^22+ points take (MI_MSM_SORT, read at every MSM)."""
+    monkeypatch.setenv("MI_MSM_SORT", request.param)
+    return request.param
+
+
+def test_msm_g1_linearity_2_20(ctx, oracle, sort_mode):
     """Size-independent check at the BASELINE config-2 size: bases k_i G with known k_i, so
     MSM(bases, s) == (sum s_i k_i) G.  The Fr dot product is computed in Python ints."""
     n = 1 << 20
@@ -148,7 +156,7 @@ def test_msm_g1_linearity_2_20(ctx, oracle):
     assert got == oracle.g1_mul(oracle.g1_generator(), acc)
 
 
-def test_msm_g1_boolean_heavy_2_20(ctx, oracle):
+def test_msm_g1_boolean_heavy_2_20(ctx, oracle, sort_mode):
     """Boolean-heavy scalars (Filecoin witnesses): ~2^19 entries land in bucket 1 of window 0, so
     the in-place chunk tree runs four levels.  Checked by linearity on bases k_i G."""
     n = 1 << 20
@@ -173,7 +181,7 @@ def test_msm_g1_boolean_heavy_2_20(ctx, oracle):
     assert got == oracle.g1_mul(oracle.g1_generator(), acc)
 
 
-def test_msm_g2_boolean_heavy(ctx, oracle):
+def test_msm_g2_boolean_heavy(ctx, oracle, sort_mode):
     """G2 with one huge bucket (three tree levels) next to random scalars, against the oracle."""
     n = 1 << 16
     bases = _bases_g2(oracle, n, 555)
