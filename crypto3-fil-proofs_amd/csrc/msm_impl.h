@@ -103,9 +103,11 @@ __global__ void __launch_bounds__(256) k_digits_c(const fr_t *__restrict__ scala
     const uint32_t mask = (1u << c) - 1;
     uint32_t dg[MAXW_C];  // digit | neg << 31; 0 = zero digit
     uint32_t carry = 0;
+    // every loop below is fully unrolled over MAXW_C with `if (w < nwin)` guards (no break/continue),
+    // so dg[] and rank[] stay in registers (a data-dependent exit spilled them to scratch: 70x slower)
+    MI_UNROLL for (unsigned w = 0; w < MAXW_C; w++) dg[w] = 0;
     MI_UNROLL for (unsigned w = 0; w < MAXW_C; w++) {
-        dg[w] = 0;
-        if (w >= nwin) continue;
+        if (w < nwin) {
         unsigned bit = w * c, word = bit >> 5, sh = bit & 31;
         uint32_t d = 0;
         if (word < 8) {
@@ -122,14 +124,17 @@ __global__ void __launch_bounds__(256) k_digits_c(const fr_t *__restrict__ scala
             carry = 0;
         }
         dg[w] = d ? d | (neg << 31) : 0;
+        }
     }
     const uint64_t below = (1ull << lane) - 1;
     uint32_t rank[MAXW_C];
     MI_UNROLL for (unsigned w = 0; w < MAXW_C; w++) {
-        if (w >= nwin) break;
-        uint64_t m = __ballot(dg[w] != 0);
-        rank[w] = (uint32_t)__popcll(m & below);
-        if (lane == 0) wc[wave][w] = (uint32_t)__popcll(m);
+        rank[w] = 0;
+        if (w < nwin) {
+            uint64_t m = __ballot(dg[w] != 0);
+            rank[w] = (uint32_t)__popcll(m & below);
+            if (lane == 0) wc[wave][w] = (uint32_t)__popcll(m);
+        }
     }
     __syncthreads();
     if (threadIdx.x < nwin) {
@@ -143,8 +148,7 @@ __global__ void __launch_bounds__(256) k_digits_c(const fr_t *__restrict__ scala
     }
     __syncthreads();
     MI_UNROLL for (unsigned w = 0; w < MAXW_C; w++) {
-        if (w >= nwin) break;
-        if (dg[w]) {
+        if (w < nwin && dg[w]) {
             uint64_t o = (uint64_t)w * n + wc[wave][w] + rank[w];
             keys[o] = (dg[w] & 0x7fffffffu) - 1;
             vals[o] = i | (dg[w] & 0x80000000u);
