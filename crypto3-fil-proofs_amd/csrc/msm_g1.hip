@@ -1,4 +1,5 @@
 // msm_g1.hip -- G1 instantiation of the Pippenger MSM (msm_impl.h) + window heuristic.
+#define MI_WAVES2  // G1: compiler-chosen occupancy (msm_impl.h)
 #include "msm_impl.h"
 
 namespace mi {

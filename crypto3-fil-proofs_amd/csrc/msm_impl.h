@@ -32,9 +32,13 @@ namespace mi {
 
 namespace {
 
-// At least two waves per SIMD for the group-law kernels: without it the G2 (Fq2) instances take
-// all 512 unified registers (256 VGPR + 256 AGPR) and run one wave per SIMD.
+// At least two waves per SIMD for the G2 group-law kernels: without it the Fq2 instances take all 512
+// unified registers (256 VGPR + 256 AGPR) and run one wave per SIMD.  msm_g1.hip defines it empty
+// before including this header: the G1 instances pick 96-180 VGPRs on their own, and the cap made
+// the compiler spill two of the G1 reduction kernels.
+#ifndef MI_WAVES2
 #define MI_WAVES2 __attribute__((amdgpu_waves_per_eu(2)))
+#endif
 #ifndef MI_RED_CAP
 #define MI_RED_CAP 1
 #endif
