@@ -39,6 +39,9 @@ namespace {
 #ifndef MI_WAVES2
 #define MI_WAVES2 __attribute__((amdgpu_waves_per_eu(2)))
 #endif
+#ifndef MI_WAVES_ACC
+#define MI_WAVES_ACC MI_WAVES2
+#endif
 #ifndef MI_RED_CAP
 #define MI_RED_CAP 1
 #endif
@@ -240,7 +243,7 @@ __global__ void k_chunk_len_keys(const uint32_t *__restrict__ chunk_bucket, cons
 }
 
 template <class F>
-__global__ void __launch_bounds__(256) MI_WAVES2 k_accum_level0(const uint32_t *__restrict__ order,
+__global__ void __launch_bounds__(256) MI_WAVES_ACC k_accum_level0(const uint32_t *__restrict__ order,
                                                       const uint32_t *__restrict__ chunk_bucket,
                                                       const uint32_t *__restrict__ coff,
                                                       const uint32_t *__restrict__ off,
