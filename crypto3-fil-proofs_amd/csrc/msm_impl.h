@@ -39,6 +39,9 @@ namespace {
 #ifndef MI_WAVES2
 #define MI_WAVES2 __attribute__((amdgpu_waves_per_eu(2)))
 #endif
+#ifndef MI_ACC_PREFETCH
+#define MI_ACC_PREFETCH 0
+#endif
 #ifndef MI_WAVES_ACC
 #define MI_WAVES_ACC MI_WAVES2
 #endif
@@ -262,12 +265,36 @@ __global__ void __launch_bounds__(256) MI_WAVES_ACC k_accum_level0(const uint32_
     uint32_t lim = local * L0 + L0 < cnt[b] ? local * L0 + L0 : cnt[b];
     uint32_t end = off[b] + lim;
     XYZZ<R> acc = XYZZ<R>::inf();
+#if MI_ACC_PREFETCH
+    // Software pipeline: the next point's loads (and the index after it) are issued before this
+    // addition, so a wave no longer waits out two dependent HBM round trips (index, then point) at
+    // the top of every iteration.
+    if (beg < end) {
+        uint32_t v = vals[beg];
+        uint32_t vn = beg + 1 < end ? vals[beg + 1] : 0u;
+        Affine<R> a = LP::lda(bases + (v & 0x7fffffffu));
+        for (uint32_t p = beg; p < end; p++) {
+            Affine<R> an = a;
+            uint32_t vnn = 0;
+            if (p + 1 < end) {
+                an = LP::lda(bases + (vn & 0x7fffffffu));
+                if (p + 2 < end) vnn = vals[p + 2];
+            }
+            if (v >> 31) a.y = -a.y;
+            acc = xyzz_add_affine_inl(acc, a);
+            a = an;
+            v = vn;
+            vn = vnn;
+        }
+    }
+#else
     for (uint32_t p = beg; p < end; p++) {
         uint32_t v = vals[p];
         Affine<R> a = LP::lda(bases + (v & 0x7fffffffu));
         if (v >> 31) a.y = -a.y;
         acc = xyzz_add_affine_inl(acc, a);
     }
+#endif
     LP::st(out + t, acc);
 }
 
@@ -412,9 +439,19 @@ inline unsigned grid_for(uint64_t n, unsigned block) { return (unsigned)((n + bl
 
 // (bucket key, point index) pair sort of one window: rocPRIM onesweep with 11-bit places, so the
 // 22-bit keys of a 2^26 MSM take 2 places instead of 3 at the gfx950 default of 8 (-8% sort time).
+#ifndef MI_SORT_BLOCK
+#define MI_SORT_BLOCK 1024
+#endif
+#ifndef MI_SORT_IPT
+#define MI_SORT_IPT 24  // measured: 20.2 vs 21.3 ms of digits+sort per 2^26 MSM at 16
+#endif
+#ifndef MI_SORT_RADIX
+#define MI_SORT_RADIX 11
+#endif
 using onesweep11_cfg = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>, 11,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<MI_SORT_BLOCK, MI_SORT_IPT>,
+                                        rocprim::kernel_config<MI_SORT_BLOCK, MI_SORT_IPT>, MI_SORT_RADIX,
                                         rocprim::block_radix_rank_algorithm::match>>;
 
 inline void sort_pairs_u32(void *tmp, size_t &bytes, const uint32_t *k_in, uint32_t *k_out, const uint32_t *v_in,

@@ -94,6 +94,22 @@ def test_groth16_random_vs_oracle_and_pairing(ctx, oracle, rows, seed):
     assert fg.prove(ctx, pk, gc, zb, 0, 0) == op.prove(zb, 0, 0)[0]
 
 
+def test_groth16_windowed_sort_vs_oracle(ctx, oracle, monkeypatch):
+    """The large-MSM path of every MSM of a prove (per-window sort of the compacted non-zero digits,
+    and the B_G1 / B_G2 plan shared in that mode), forced at a size the oracle proves in seconds."""
+    monkeypatch.setenv("MI_MSM_SORT", "windowed")
+    n_in, n_aux, rws, z = circuits.random_circuit(34, 5000, n_in=6, n_free=32)
+    oc, gc = _load(ctx, oracle, n_in, n_aux, rws, z)
+    tox = circuits.toxic(34)
+    pk = fg.generate_random_parameters(ctx, gc, tox)
+    op = oracle.OracleParams(oc, tox)
+    zb = circuits.z_bytes(z)
+    r, s = circuits.blinding(34)
+    proof, raw = fg.prove(ctx, pk, gc, zb, r, s, want_raw=True)
+    oproof, oraw, _ = op.prove(zb, r, s)
+    assert proof == oproof and raw == oraw
+
+
 def test_prove_batch_and_priority(ctx, oracle):
     n_in, n_aux, rws, z = circuits.random_circuit(41, 300)
     oc, gc = _load(ctx, oracle, n_in, n_aux, rws, z)
