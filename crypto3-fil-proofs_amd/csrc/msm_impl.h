@@ -683,7 +683,13 @@ void msm_accumulate_impl(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, XYZZ
     //   accA_s = sum_j (j+1) B_{sS+j},  runA_s = sum_j B_{sS+j},  R = sum_s runA_s,  V = sum_s (s+1) runA_s,
     // V by a second running-sum level over runA (segments of SB) whose few segment offsets are folded
     // by double-and-add (k_seg_fold).
-    const uint64_t segA_target = sizeof(F) == sizeof(fq_t) ? (1u << 20) : (1u << 18);
+    // first-level segment count target (threads of k_bucket_reduce); MI_MSM_SEGA_LOG overrides (tuning)
+    static const int sega_env = [] {
+        const char *e = getenv("MI_MSM_SEGA_LOG");
+        return e ? atoi(e) : 0;
+    }();
+    const uint64_t segA_target = sega_env > 0 ? (1ull << sega_env)
+                                              : sizeof(F) == sizeof(fq_t) ? (1u << 20) : (1u << 18);
     unsigned SA = 1;
     while (SA < nbk && (uint64_t)nb / (SA * 2) >= segA_target) SA *= 2;
     const uint32_t nsegA = nbk / SA, totA = nwin * nsegA;
