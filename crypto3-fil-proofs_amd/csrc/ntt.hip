@@ -64,15 +64,18 @@ __device__ __forceinline__ unsigned ins2(unsigned q, unsigned p0) {
 __device__ __forceinline__ unsigned ins1(unsigned q, unsigned p) {
     return (q & ((1u << p) - 1)) | ((q >> p) << (p + 1));
 }
-__device__ __forceinline__ fr_t tw_b(const fr_t *__restrict__ tw10, unsigned j, unsigned b) {
-    return tw10[j << (TILE_LOG - b)];  // omega_{2^b}^j
-}
+// In-tile twiddle omega_{2^b}^j = tw[j << sh]: sh = TILE_LOG - b on the 512-entry omega_1024 table,
+// 0 on the per-pass copy in LDS (MI_NTT_TWLDS).
+__device__ __forceinline__ fr_t tw_b(const fr_t *__restrict__ tw, unsigned j, unsigned sh) { return tw[j << sh]; }
+#ifndef MI_NTT_TWLDS
+#define MI_NTT_TWLDS 0  // same-box A/B: 11.7 (global, L1-resident) vs 11.8 ms (LDS copy) per 2^26 transform
+#endif
 
 // The b stages of one tile: radix-4 register rounds (two stages per LDS round trip) plus one
 // radix-2 round when b is odd.  DIF runs rounds in order, DIT the transpose in reverse order.
 template <bool DIF>
 __device__ __forceinline__ void ntt_rounds(LdsTile &sh, unsigned b, unsigned Tlog, unsigned tile,
-                                           const fr_t *__restrict__ tw10) {
+                                           const fr_t *__restrict__ tw10, unsigned tsh) {
     const unsigned T = 1u << Tlog;
     const unsigned nquad = tile >> 2;
     const unsigned nr4 = b >> 1;  // radix-4 rounds: DIF stage pairs (0,1), (2,3), ...
@@ -99,27 +102,27 @@ __device__ __forceinline__ void ntt_rounds(LdsTile &sh, unsigned b, unsigned Tlo
                 if (DIF) {
                     fr_t a = x0 + x2, c = x0 - x2;
                     fr_t bb = x1 + x3, dd = x1 - x3;
-                    if (j0) c = c * tw_b(tw10, j0, b);
-                    dd = dd * tw_b(tw10, j1, b);
+                    if (j0) c = c * tw_b(tw10, j0, tsh);
+                    dd = dd * tw_b(tw10, j1, tsh);
                     x0 = a + bb;
                     x1 = a - bb;
                     x2 = c + dd;
                     x3 = c - dd;
                     if (jq) {
-                        fr_t w = tw_b(tw10, jq, b);
+                        fr_t w = tw_b(tw10, jq, tsh);
                         x1 = x1 * w;
                         x3 = x3 * w;
                     }
                 } else {
                     if (jq) {
-                        fr_t w = tw_b(tw10, jq, b);
+                        fr_t w = tw_b(tw10, jq, tsh);
                         x1 = x1 * w;
                         x3 = x3 * w;
                     }
                     fr_t a = x0 + x1, bb = x0 - x1;
                     fr_t c = x2 + x3, dd = x2 - x3;
-                    if (j0) c = c * tw_b(tw10, j0, b);
-                    dd = dd * tw_b(tw10, j1, b);
+                    if (j0) c = c * tw_b(tw10, j0, tsh);
+                    dd = dd * tw_b(tw10, j1, tsh);
                     x0 = a + c;
                     x2 = a - c;
                     x1 = bb + dd;
@@ -160,6 +163,23 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(fr_t *__restrict__ d, 
                                                           const fr_t *__restrict__ ghi, fr_t scale,
                                                           const fr_t *__restrict__ tw10b = nullptr) {
     __shared__ LdsTile sh;
+#if MI_NTT_TWLDS
+    // this pass's in-tile twiddles omega_{2^b}^j, j < 2^(b-1), copied to LDS once per workgroup
+    // (and the forward table behind them for the fused pass): no global-load latency in the rounds
+    extern __shared__ fr_t twl[];
+    {
+        const unsigned half = b ? 1u << (b - 1) : 0, shft = TILE_LOG - b;
+        for (unsigned j = threadIdx.x; j < half; j += NTT_THREADS) {
+            twl[j] = tw10[j << shft];
+            if (FUSED) twl[half + j] = tw10b[j << shft];
+        }
+    }
+    const fr_t *twA = twl, *twB = twl + (b ? 1u << (b - 1) : 0);
+    const unsigned tsh = 0;
+#else
+    const fr_t *twA = tw10, *twB = tw10b;
+    const unsigned tsh = TILE_LOG - b;
+#endif
     const unsigned T = 1u << Tlog;
     const unsigned Slog = M - b;
     const uint64_t S = 1ull << Slog;
@@ -188,7 +208,7 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(fr_t *__restrict__ d, 
         lds_put(sh, e, x);
     }
     __syncthreads();
-    ntt_rounds<DIF>(sh, b, Tlog, tile, tw10);
+    ntt_rounds<DIF>(sh, b, Tlog, tile, twA, tsh);
     if (FUSED) {  // middle of iNTT -> coset -> NTT: epilogue in LDS, then the DIT rounds of the same tile
         for (unsigned e = threadIdx.x; e < tile; e += NTT_THREADS) {
             unsigned t = e & (T - 1), i1 = (e >> Tlog) & bmask, g = e >> (Tlog + b);
@@ -199,7 +219,7 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(fr_t *__restrict__ d, 
             lds_put(sh, e, x * scale);
         }
         __syncthreads();
-        ntt_rounds<false>(sh, b, Tlog, tile, tw10b);
+        ntt_rounds<false>(sh, b, Tlog, tile, twB, tsh);
     }
     // store
     for (unsigned e = threadIdx.x; e < tile; e += NTT_THREADS) {
@@ -219,6 +239,10 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(fr_t *__restrict__ d, 
         }
         d[gi] = x;
     }
+}
+
+inline size_t twl_bytes(unsigned b, bool fused) {
+    return MI_NTT_TWLDS && b ? (sizeof(fr_t) << (b - 1)) * (fused ? 2 : 1) : 0;
 }
 
 struct PassPlan {
@@ -384,14 +408,14 @@ static void ntt_run(Ctx &c, fr_t *d, unsigned L, bool inverse, bool dif, int epi
         for (size_t i = 0; i < plan.size(); i++) {
             auto &p = plan[i];
             int e = (i + 1 == plan.size()) ? epi : 0;
-            k_ntt_pass<true><<<(unsigned)p.blocks, NTT_THREADS, 0, c.stream>>>(d, L, p.M, p.b, p.Tlog, p.Glog,
+            k_ntt_pass<true><<<(unsigned)p.blocks, NTT_THREADS, twl_bytes(p.b, false), c.stream>>>(d, L, p.M, p.b, p.Tlog, p.Glog,
                                                                                  p.twiddle, lo, hi, tw10, e, glo,
                                                                                  ghi, scale);
         }
     } else {
         for (int i = (int)plan.size() - 1; i >= 0; i--) {
             auto &p = plan[i];
-            k_ntt_pass<false><<<(unsigned)p.blocks, NTT_THREADS, 0, c.stream>>>(d, L, p.M, p.b, p.Tlog, p.Glog,
+            k_ntt_pass<false><<<(unsigned)p.blocks, NTT_THREADS, twl_bytes(p.b, false), c.stream>>>(d, L, p.M, p.b, p.Tlog, p.Glog,
                                                                                   p.twiddle, lo, hi, tw10, 0, glo,
                                                                                   ghi, scale);
         }
@@ -414,19 +438,19 @@ void ntt_coset_roundtrip(Ctx &c, fr_t *d, unsigned L, const fr_t &scale) {
     const size_t last = plan.size() - 1;
     for (size_t i = 0; i < last; i++) {
         auto &p = plan[i];
-        k_ntt_pass<true><<<(unsigned)p.blocks, NTT_THREADS, 0, c.stream>>>(d, L, p.M, p.b, p.Tlog, p.Glog, p.twiddle,
+        k_ntt_pass<true><<<(unsigned)p.blocks, NTT_THREADS, twl_bytes(p.b, false), c.stream>>>(d, L, p.M, p.b, p.Tlog, p.Glog, p.twiddle,
                                                                              c.tw.iv_lo, c.tw.iv_hi, c.tw.iv_1024, 0,
                                                                              c.tw.g_lo, c.tw.g_hi, scale);
     }
     {
         auto &p = plan[last];
-        k_ntt_pass<true, true><<<(unsigned)p.blocks, NTT_THREADS, 0, c.stream>>>(
+        k_ntt_pass<true, true><<<(unsigned)p.blocks, NTT_THREADS, twl_bytes(p.b, true), c.stream>>>(
             d, L, p.M, p.b, p.Tlog, p.Glog, 0, c.tw.iv_lo, c.tw.iv_hi, c.tw.iv_1024, 1, c.tw.g_lo, c.tw.g_hi, scale,
             c.tw.fw_1024);
     }
     for (int i = (int)last - 1; i >= 0; i--) {
         auto &p = plan[i];
-        k_ntt_pass<false><<<(unsigned)p.blocks, NTT_THREADS, 0, c.stream>>>(d, L, p.M, p.b, p.Tlog, p.Glog, p.twiddle,
+        k_ntt_pass<false><<<(unsigned)p.blocks, NTT_THREADS, twl_bytes(p.b, false), c.stream>>>(d, L, p.M, p.b, p.Tlog, p.Glog, p.twiddle,
                                                                               c.tw.fw_lo, c.tw.fw_hi, c.tw.fw_1024, 0,
                                                                               c.tw.g_lo, c.tw.g_hi, scale);
     }
