@@ -145,7 +145,7 @@ struct Ctx {
     hipStream_t stream = nullptr;
     std::recursive_mutex mu;
     NttTables tw;
-    DevBuf scratch[24];  // 0-15: MSM / NTT / upload temporaries, 20-21: prover vectors / staging
+    DevBuf scratch[24];  // 0-19: MSM / NTT / upload temporaries (18-19: G2 second level), 20-21: prover vectors
     Stats stats;
     EventTimer timer;
     // Auxiliary lane: a second stream with its own scratch arena and timers, driven from a second

@@ -435,6 +435,70 @@ __global__ void __launch_bounds__(256) MI_WAVES_RED k_sum_groups(const XYZZ<F> *
     LP::st(out + t, acc);
 }
 
+// ---- G2 second-level bucket reduction (g2_second_level) ----
+// Bucket sums -> affine by Montgomery's trick over K consecutive buckets per thread (empty or
+// infinite buckets become the affine infinity (0, 0)).
+template <class F, int K>
+__global__ void __launch_bounds__(256) k_bucket_affine(const uint32_t *__restrict__ coff,
+                                                       const uint32_t *__restrict__ cnt,
+                                                       const XYZZ<F> *__restrict__ P0, uint32_t nb,
+                                                       F *__restrict__ pre, Affine<F> *__restrict__ out) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t beg = t * K;
+    if (beg >= nb) return;
+    const uint64_t end = beg + K < nb ? beg + K : nb;
+    F prod = F::one();
+    for (uint64_t i = beg; i < end; i++) {
+        pre[i] = prod;
+        if (cnt[i]) {
+            const XYZZ<F> p = P0[coff[i]];
+            if (!p.is_inf()) prod = prod * p.ZZZ;
+        }
+    }
+    F inv = inverse_inl(prod);
+    for (uint64_t i = end; i-- > beg;) {
+        if (!cnt[i]) {
+            out[i] = Affine<F>::inf();
+            continue;
+        }
+        const XYZZ<F> p = P0[coff[i]];
+        if (p.is_inf()) {
+            out[i] = Affine<F>::inf();
+            continue;
+        }
+        F izzz = inv * pre[i];
+        inv = inv * p.ZZZ;
+        F izz = sqr(p.ZZ * izzz);
+        out[i] = {p.X * izz, p.Y * izzz};
+    }
+}
+
+// Bucket g = w * 2^jbits + j of a non-empty bucket carries weight s = j + 1 < 2^(2 c2): entries
+// (window 2w, digit s mod 2^c2) and (window 2w + 1, digit s >> c2), keys window * 2^c2 + digit - 1.
+__global__ void k_l2_digits(const uint32_t *__restrict__ cnt, uint32_t nb, unsigned jbits, unsigned c2,
+                            uint32_t invalid, uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= nb) return;
+    const uint32_t w = g >> jbits, s = (g & ((1u << jbits) - 1)) + 1;
+    const uint32_t d0 = s & ((1u << c2) - 1), d1 = s >> c2;
+    const bool live = cnt[g] != 0;
+    keys[2 * (uint64_t)g] = live && d0 ? ((2 * w) << c2) + d0 - 1 : invalid;
+    keys[2 * (uint64_t)g + 1] = live && d1 ? ((2 * w + 1) << c2) + d1 - 1 : invalid;
+    vals[2 * (uint64_t)g] = g;
+    vals[2 * (uint64_t)g + 1] = g;
+}
+
+// bucket start / end of globally keyed sorted entries (invalid keys sort last and are skipped)
+__global__ void k_bounds_flat(const uint32_t *__restrict__ keys, uint32_t np, uint32_t invalid,
+                              uint32_t *__restrict__ start, uint32_t *__restrict__ endp) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= np) return;
+    const uint32_t k = keys[i];
+    if (k == invalid) return;
+    if (i == 0 || keys[i - 1] != k) start[k] = i;
+    if (i + 1 == np || keys[i + 1] != k) endp[k] = i + 1;
+}
+
 inline unsigned grid_for(uint64_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
 
 // (bucket key, point index) pair sort of one window: rocPRIM onesweep with 11-bit places, so the
@@ -463,6 +527,63 @@ inline void sort_pairs_u32(void *tmp, size_t &bytes, const uint32_t *k_in, uint3
 
 // ---- phase 1 (scalars only, shared by every MSM over the same scalars: B_G1 and B_G2) ----
 // digits -> per-window sort -> bucket bounds -> level-0 chunking -> length-sorted chunk order.
+// Level-0 chunking of a bucketed entry list (bucket b: entries [off[b], off[b] + cnt[b]) of vals_s;
+// pl.maxcnt set): chunk counts/offsets per bucket, chunk -> bucket map, length-sorted chunk order.
+// Fills the rest of the plan; false when there is no entry at all.
+inline bool plan_chunks(Ctx &c, MsmPlan &pl, uint32_t *offA, uint32_t *cntA, uint32_t *offB, uint32_t *cntB,
+                        uint32_t nb, const uint32_t *vals_s) {
+    hipStream_t st = c.stream;
+    static const uint32_t L0 = [] {
+        const char *e = getenv("MI_MSM_L0");
+        uint32_t v = e ? (uint32_t)atoi(e) : L0_DEFAULT;
+        return v >= 2 && v <= 1024 ? v : L0_DEFAULT;
+    }();
+    pl.L0 = L0;
+    unsigned len_bits = 1;
+    while ((1u << len_bits) <= L0) len_bits++;
+    uint32_t *coff = offB, *ccnt = cntB;
+    // level 0: buckets cut into chunks of <= L0 sorted entries; one mixed-add chain per chunk
+    k_chunk_count<<<grid_for(nb, 256), 256, 0, st>>>(cntA, nb, L0, ccnt);
+    MI_LAUNCHED(c, "k_chunk_count");
+    size_t tmp_bytes = 0;
+    MI_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, ccnt, coff, nb, st));
+    void *tmp = c.scratch[4].get(tmp_bytes);
+    MI_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, ccnt, coff, nb, st));
+    uint32_t tail[2];
+    MI_HIP(hipMemcpyAsync(&tail[0], coff + nb - 1, 4, hipMemcpyDeviceToHost, st));
+    MI_HIP(hipMemcpyAsync(&tail[1], ccnt + nb - 1, 4, hipMemcpyDeviceToHost, st));
+    MI_HIP(hipStreamSynchronize(st));
+    uint32_t total = tail[0] + tail[1];
+    pl.total = total;
+    if (total == 0) return false;  // every scalar is zero
+    uint32_t *heads = c.scratch[15].as<uint32_t>(total + 1);
+    uint32_t *chunk_bucket = c.scratch[17].as<uint32_t>(total + 1);
+    MI_HIP(hipMemsetAsync(heads, 0, sizeof(uint32_t) * (total + 1), st));
+    k_chunk_heads<<<grid_for(nb, 256), 256, 0, st>>>(ccnt, coff, nb, heads);
+    MI_LAUNCHED(c, "k_chunk_heads");
+    tmp_bytes = 0;
+    MI_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tmp_bytes, heads, chunk_bucket, MaxOp(), total, st));
+    tmp = c.scratch[4].get(tmp_bytes);
+    MI_HIP(hipcub::DeviceScan::InclusiveScan(tmp, tmp_bytes, heads, chunk_bucket, MaxOp(), total, st));
+    // length-sorted chunk order (keys/vals scratch of the main sort are free by now)
+    uint32_t *lkeys = c.scratch[0].as<uint32_t>(total), *lids = c.scratch[1].as<uint32_t>(total);
+    uint32_t *lkeys_s = c.scratch[2].as<uint32_t>(total), *order = c.scratch[16].as<uint32_t>(total);
+    k_chunk_len_keys<<<grid_for(total, 256), 256, 0, st>>>(chunk_bucket, coff, cntA, total, L0, lkeys, lids);
+    MI_LAUNCHED(c, "k_chunk_len_keys");
+    size_t tb = 0;
+    MI_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, lkeys, lkeys_s, lids, order, total, 0, len_bits, st));
+    void *tmp2 = c.scratch[4].get(tb);
+    MI_HIP(hipcub::DeviceRadixSort::SortPairs(tmp2, tb, lkeys, lkeys_s, lids, order, total, 0, len_bits, st));
+    pl.vals_s = vals_s;
+    pl.off = offA;
+    pl.cnt = cntA;
+    pl.coff = coff;
+    pl.ccnt = ccnt;
+    pl.chunk_bucket = chunk_bucket;
+    pl.order = order;
+    return true;
+}
+
 // The plan's arrays live in scratch slots 3, 5-8, 16, 17 and stay valid until the next prepare on
 // this ctx; the accumulation phase only uses the other slots.
 inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, uint64_t n, MsmPlan &pl) {
@@ -567,60 +688,14 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
     for (unsigned w = 0; w < nwin; w++)
         pl.entries += compact ? wn[w] : head[4 + w] == 0xffffffffu ? n : head[4 + w] - (uint64_t)w * n;
 
-    static const uint32_t L0 = [] {
-        const char *e = getenv("MI_MSM_L0");
-        uint32_t v = e ? (uint32_t)atoi(e) : L0_DEFAULT;
-        return v >= 2 && v <= 1024 ? v : L0_DEFAULT;
-    }();
-    pl.L0 = L0;
-    unsigned len_bits = 1;
-    while ((1u << len_bits) <= L0) len_bits++;
-    uint32_t *coff = offB, *ccnt = cntB;
-    // level 0: buckets cut into chunks of <= L0 sorted entries; one mixed-add chain per chunk
-    k_chunk_count<<<grid_for(nb, 256), 256, 0, st>>>(cntA, nb, L0, ccnt);
-    MI_LAUNCHED(c, "k_chunk_count");
-    size_t tmp_bytes = 0;
-    MI_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, ccnt, coff, nb, st));
-    void *tmp = c.scratch[4].get(tmp_bytes);
-    MI_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, ccnt, coff, nb, st));
-    uint32_t tail[2];
-    MI_HIP(hipMemcpyAsync(&tail[0], coff + nb - 1, 4, hipMemcpyDeviceToHost, st));
-    MI_HIP(hipMemcpyAsync(&tail[1], ccnt + nb - 1, 4, hipMemcpyDeviceToHost, st));
-    MI_HIP(hipStreamSynchronize(st));
-    uint32_t total = tail[0] + tail[1];
-    pl.total = total;
-    if (total == 0) return false;  // every scalar is zero
-    uint32_t *heads = c.scratch[15].as<uint32_t>(total + 1);
-    uint32_t *chunk_bucket = c.scratch[17].as<uint32_t>(total + 1);
-    MI_HIP(hipMemsetAsync(heads, 0, sizeof(uint32_t) * (total + 1), st));
-    k_chunk_heads<<<grid_for(nb, 256), 256, 0, st>>>(ccnt, coff, nb, heads);
-    MI_LAUNCHED(c, "k_chunk_heads");
-    tmp_bytes = 0;
-    MI_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tmp_bytes, heads, chunk_bucket, MaxOp(), total, st));
-    tmp = c.scratch[4].get(tmp_bytes);
-    MI_HIP(hipcub::DeviceScan::InclusiveScan(tmp, tmp_bytes, heads, chunk_bucket, MaxOp(), total, st));
-    // length-sorted chunk order (keys/vals scratch of the main sort are free by now)
-    uint32_t *lkeys = c.scratch[0].as<uint32_t>(total), *lids = c.scratch[1].as<uint32_t>(total);
-    uint32_t *lkeys_s = c.scratch[2].as<uint32_t>(total), *order = c.scratch[16].as<uint32_t>(total);
-    k_chunk_len_keys<<<grid_for(total, 256), 256, 0, st>>>(chunk_bucket, coff, cntA, total, L0, lkeys, lids);
-    MI_LAUNCHED(c, "k_chunk_len_keys");
-    size_t tb = 0;
-    MI_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, lkeys, lkeys_s, lids, order, total, 0, len_bits, st));
-    void *tmp2 = c.scratch[4].get(tb);
-    MI_HIP(hipcub::DeviceRadixSort::SortPairs(tmp2, tb, lkeys, lkeys_s, lids, order, total, 0, len_bits, st));
-    pl.vals_s = vals_s;
-    pl.off = offA;
-    pl.cnt = cntA;
-    pl.coff = coff;
-    pl.ccnt = ccnt;
-    pl.chunk_bucket = chunk_bucket;
-    pl.order = order;
-    return true;
+    return plan_chunks(c, pl, offA, cntA, offB, cntB, nb, vals_s);
 }
 
 // ---- phase 2 (per base set): accumulation, chunk tree, bucket reduction, window combination ----
+// Level-0 accumulation of the plan's chunks over `bases` and the in-place chunk tree: bucket b's sum
+// ends up in P0[coff[b]] (when cnt[b] != 0).  Returns P0 (scratch slot 10).
 template <class F>
-void msm_accumulate_impl(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, XYZZ<F> *result) {
+XYZZ<F> *accumulate_chunks(Ctx &c, const MsmPlan &pl, const Affine<F> *bases) {
     hipStream_t st = c.stream;
     const unsigned K = Lane<F>::K;      // threads per element in the accumulation (2 for G2: g2pair.h)
     const unsigned KR = LaneRed<F>::K;  // ... and in the reduction kernels
@@ -677,7 +752,17 @@ void msm_accumulate_impl(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, XYZZ
             MI_LAUNCHED(c, "k_tree_level");
         }
     }
+    return P0;
+}
 
+// Bucket reduction of every window of the plan: W[w] = sum_b (b + 1) B_{w,b} (window-local b).
+template <class F>
+void reduce_windows(Ctx &c, const MsmPlan &pl, XYZZ<F> *P0, std::vector<XYZZ<F>> &W) {
+    hipStream_t st = c.stream;
+    const unsigned KR = LaneRed<F>::K;  // threads per element in the reduction kernels
+    const unsigned nwin = pl.nwin;
+    const uint32_t nbk = pl.nbk, nb = pl.nb;
+    const uint32_t *coff = pl.coff, *cntA = pl.cnt;
     // Bucket reduction, two running-sum levels (no per-segment scalar multiplication on the big level):
     //   W = sum_b (b+1) B_b,  b = s*S + j:  W = sum_s accA_s + S * (V - R),
     //   accA_s = sum_j (j+1) B_{sS+j},  runA_s = sum_j B_{sS+j},  R = sum_s runA_s,  V = sum_s (s+1) runA_s,
@@ -722,13 +807,105 @@ void msm_accumulate_impl(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, XYZZ
     std::vector<XYZZ<F>> sums(rows);
     MI_HIP(hipMemcpyAsync(sums.data(), cur, sizeof(XYZZ<F>) * rows, hipMemcpyDeviceToHost, st));
     MI_HIP(hipStreamSynchronize(st));
-    std::vector<XYZZ<F>> W(nwin);
+    W.assign(nwin, XYZZ<F>::inf());
     for (unsigned w = 0; w < nwin; w++) {  // W = SumA + SA * (V - R)
         const XYZZ<F> &SumA = sums[w], &R = sums[nwin + w], &V = sums[2 * nwin + w];
         XYZZ<F> t = xyzz_add(V, xyzz_neg(R));
         for (unsigned sa = SA; sa > 1; sa >>= 1) t = xyzz_dbl(t);
         W[w] = xyzz_add(SumA, t);
     }
+}
+
+// G2 bucket reduction as a second-level MSM.  The lane-pair full addition (XYZZ + XYZZ) of the
+// running-sum reduction needs more than 256 registers (every measured build either spills or runs one
+// wave per SIMD), while the lane-pair MIXED addition runs at the accumulation's rate.  So for large
+// G2 instances: bucket sums -> affine (batch inversion), then each window's sum_j (j + 1) B_j is a
+// Pippenger over those affine points with the small scalars j + 1 split into two c2-bit digits
+// (windows 2w, 2w + 1; about 2 mixed additions per bucket, ~2^c2 second-level buckets per window),
+// and W_w = W'_{2w} + 2^c2 W'_{2w+1}.  Reuses the level-1 plan's scratch: the plan is consumed.
+// MI_G2_L2=0 turns it off (the plain reduction), MI_G2_L2=2 forces it at any size (tests).
+template <class F>
+bool g2_second_level(Ctx &c, const MsmPlan &pl, XYZZ<F> *P0, std::vector<XYZZ<F>> &W) {
+    if constexpr (sizeof(F) != sizeof(fq2_t)) {
+        return false;
+    } else {
+        // MI_G2_L2: 0 off, 1 (default) from 2^20 level-1 buckets on, 2 always (tests); read per call
+        const char *e = getenv("MI_G2_L2");
+        const int mode = e ? atoi(e) : 1;
+        if (mode == 0 || (mode == 1 && pl.nb < (1u << 20))) return false;
+        hipStream_t st = c.stream;
+        const unsigned nwin = pl.nwin, cb = pl.cb;
+        const uint32_t nb = pl.nb;
+        const unsigned c2 = (cb + 1) / 2;  // s = j + 1 <= 2^(cb - 1) < 2^(2 c2)
+        const uint32_t nbk2 = 1u << c2, nwin2 = 2 * nwin, nb2 = nwin2 * nbk2, invalid2 = nb2;
+        // 1. bucket sums -> affine
+        Affine<F> *Baff = c.scratch[18].as<Affine<F>>(nb);
+        F *pre = c.scratch[19].as<F>(nb);
+        k_bucket_affine<F, 32><<<grid_for(((uint64_t)nb + 31) / 32, 256), 256, 0, st>>>(pl.coff, pl.cnt, P0, nb,
+                                                                                       pre, Baff);
+        MI_LAUNCHED(c, "k_bucket_affine");
+        // 2. two digit entries per non-empty bucket, one sort over all of them
+        const uint32_t np2 = 2 * nb;
+        uint32_t *keys = c.scratch[0].as<uint32_t>(np2), *vals = c.scratch[1].as<uint32_t>(np2);
+        uint32_t *keys_s = c.scratch[2].as<uint32_t>(np2), *vals_s = c.scratch[3].as<uint32_t>(np2);
+        k_l2_digits<<<grid_for(nb, 256), 256, 0, st>>>(pl.cnt, nb, cb - 1, c2, invalid2, keys, vals);
+        MI_LAUNCHED(c, "k_l2_digits");
+        unsigned bits = 1;
+        while ((1ull << bits) <= invalid2) bits++;
+        size_t tmp_bytes = 0;
+        sort_pairs_u32(nullptr, tmp_bytes, keys, keys_s, vals, vals_s, np2, bits, st);
+        void *tmp = c.scratch[4].get(tmp_bytes);
+        sort_pairs_u32(tmp, tmp_bytes, keys, keys_s, vals, vals_s, np2, bits, st);
+        // 3. buckets of the second level
+        uint32_t *off2 = c.scratch[5].as<uint32_t>(nb2), *cnt2 = c.scratch[6].as<uint32_t>(nb2);
+        MI_HIP(hipMemsetAsync(off2, 0, sizeof(uint32_t) * nb2, st));
+        MI_HIP(hipMemsetAsync(cnt2, 0, sizeof(uint32_t) * nb2, st));
+        k_bounds_flat<<<grid_for(np2, 256), 256, 0, st>>>(keys_s, np2, invalid2, off2, cnt2);
+        MI_LAUNCHED(c, "k_bounds_flat");
+        k_end_to_cnt<<<grid_for(nb2, 256), 256, 0, st>>>(off2, cnt2, nb2);
+        MI_LAUNCHED(c, "k_end_to_cnt");
+        uint32_t *dm = c.scratch[9].as<uint32_t>(4);
+        uint32_t head[2] = {0, 0};
+        tmp_bytes = 0;
+        MI_HIP(hipcub::DeviceReduce::Max(nullptr, tmp_bytes, cnt2, dm, nb2, st));
+        size_t tb2 = 0;
+        MI_HIP(hipcub::DeviceReduce::Sum(nullptr, tb2, cnt2, dm + 1, nb2, st));
+        tmp = c.scratch[4].get(tmp_bytes > tb2 ? tmp_bytes : tb2);
+        MI_HIP(hipcub::DeviceReduce::Max(tmp, tmp_bytes, cnt2, dm, nb2, st));
+        MI_HIP(hipcub::DeviceReduce::Sum(tmp, tb2, cnt2, dm + 1, nb2, st));
+        MI_HIP(hipMemcpyAsync(head, dm, sizeof(head), hipMemcpyDeviceToHost, st));
+        MI_HIP(hipStreamSynchronize(st));
+        MsmPlan p2;
+        p2.n = head[1];
+        p2.cb = c2;
+        p2.nwin = nwin2;
+        p2.nbk = nbk2;
+        p2.nb = nb2;
+        p2.maxcnt = head[0];
+        p2.entries = head[1];
+        W.assign(nwin, XYZZ<F>::inf());
+        if (!plan_chunks(c, p2, off2, cnt2, c.scratch[7].as<uint32_t>(nb2), c.scratch[8].as<uint32_t>(nb2), nb2,
+                         vals_s))
+            return true;  // every bucket empty
+        // 4. second-level accumulation over the affine buckets, reduction, recombination
+        XYZZ<F> *Q0 = accumulate_chunks<F>(c, p2, Baff);
+        std::vector<XYZZ<F>> W2;
+        reduce_windows<F>(c, p2, Q0, W2);
+        for (unsigned w = 0; w < nwin; w++) {
+            XYZZ<F> t = W2[2 * w + 1];
+            for (unsigned i = 0; i < c2; i++) t = xyzz_dbl(t);
+            W[w] = xyzz_add(W2[2 * w], t);
+        }
+        return true;
+    }
+}
+
+template <class F>
+void msm_accumulate_impl(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, XYZZ<F> *result) {
+    XYZZ<F> *P0 = accumulate_chunks<F>(c, pl, bases);
+    std::vector<XYZZ<F>> W;
+    if (!g2_second_level<F>(c, pl, P0, W)) reduce_windows<F>(c, pl, P0, W);
+    const unsigned nwin = pl.nwin, cb = pl.cb;
     XYZZ<F> acc = W[nwin - 1];
     for (int w = (int)nwin - 2; w >= 0; w--) {
         for (unsigned i = 0; i < cb; i++) acc = xyzz_dbl(acc);

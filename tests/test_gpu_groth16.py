@@ -95,9 +95,11 @@ def test_groth16_random_vs_oracle_and_pairing(ctx, oracle, rows, seed):
 
 
 def test_groth16_windowed_sort_vs_oracle(ctx, oracle, monkeypatch):
-    """The large-MSM path of every MSM of a prove (per-window sort of the compacted non-zero digits,
-    and the B_G1 / B_G2 plan shared in that mode), forced at a size the oracle proves in seconds."""
+    """The large-MSM paths of a prove (per-window sort of the compacted non-zero digits, the B_G1 / B_G2
+    plan shared in that mode, G2 second-level bucket reduction), forced at a size the oracle proves in
+    seconds."""
     monkeypatch.setenv("MI_MSM_SORT", "windowed")
+    monkeypatch.setenv("MI_G2_L2", "2")  # and B_G2's bucket reduction as the second-level MSM
     n_in, n_aux, rws, z = circuits.random_circuit(34, 5000, n_in=6, n_free=32)
     oc, gc = _load(ctx, oracle, n_in, n_aux, rws, z)
     tox = circuits.toxic(34)

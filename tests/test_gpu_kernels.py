@@ -80,8 +80,16 @@ def test_msm_g1_random(ctx, oracle, n):
     assert ctx.msm_g1(bases, scal) == oracle.msm_g1(bases, scal)
 
 
+@pytest.fixture(params=["0", "2"])
+def g2_level2(request, monkeypatch):
+    """G2 bucket reduction: "0" the running-sum kernels, "2" the second-level MSM over affine buckets
+    (forced at every size; by default it takes over from 2^20 level-1 buckets, MI_G2_L2)."""
+    monkeypatch.setenv("MI_G2_L2", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("n", [1, 5, 100, 1500])
-def test_msm_g2_random(ctx, oracle, n):
+def test_msm_g2_random(ctx, oracle, n, g2_level2):
     bases = _bases_g2(oracle, n, 3000 + n)
     scal = rand_fr_bytes(n, 4000 + n)
     assert ctx.msm_g2(bases, scal) == oracle.msm_g2(bases, scal)
@@ -181,7 +189,7 @@ def test_msm_g1_boolean_heavy_2_20(ctx, oracle, sort_mode):
     assert got == oracle.g1_mul(oracle.g1_generator(), acc)
 
 
-def test_msm_g2_boolean_heavy(ctx, oracle, sort_mode):
+def test_msm_g2_boolean_heavy(ctx, oracle, sort_mode, g2_level2):
     """G2 with one huge bucket (three tree levels) next to random scalars, against the oracle."""
     n = 1 << 16
     bases = _bases_g2(oracle, n, 555)
