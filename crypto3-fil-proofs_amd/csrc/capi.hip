@@ -431,6 +431,40 @@ int mi_groth16_prove_batch(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *cir
     });
 }
 
+static void share_impl(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circ, const mi::fr_t *z_dev, uint32_t rank,
+                       uint32_t world, uint8_t *share) {
+    need(world > 0 && rank < world, "share rank out of range (rank < world)");
+    mi::sums_encode(mi::groth16_sums(ctx->c, *srs->p, *circ->p, z_dev, rank, world), share);
+}
+
+int mi_groth16_prove_share(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circ, const uint8_t *z, uint32_t rank,
+                           uint32_t world, int priority, uint8_t *share) {
+    return guard([&] {
+        need(ctx && srs && circ && z && share, "null argument");
+        CtxLock l(ctx, priority);
+        uint64_t nv = circ->p->n_in + circ->p->n_aux;
+        share_impl(ctx, srs, circ, upload_fr(ctx->c, 21, z, nv), rank, world, share);
+    });
+}
+
+int mi_groth16_prove_share_dev(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circ, const void *z_dev,
+                               uint32_t rank, uint32_t world, int priority, uint8_t *share) {
+    return guard([&] {
+        need(ctx && srs && circ && z_dev && share, "null argument");
+        CtxLock l(ctx, priority);
+        share_impl(ctx, srs, circ, (const mi::fr_t *)z_dev, rank, world, share);
+    });
+}
+
+int mi_groth16_assemble(const uint8_t *vk, const uint8_t *shares, uint64_t count, const uint8_t r[32],
+                        const uint8_t s[32], uint8_t *proof, uint8_t *raw) {
+    return guard([&] {
+        need(vk && shares && r && s && proof, "null argument");
+        need(count > 0, "no proof shares");
+        proof_bytes(mi::groth16_assemble_shares(vk, shares, count, fr_checked(r), fr_checked(s)), proof, raw);
+    });
+}
+
 int mi_groth16_trapdoor_dlogs(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circ, const void *z_dev,
                               const uint8_t r[32], const uint8_t s[32], uint8_t out[96]) {
     return guard([&] {

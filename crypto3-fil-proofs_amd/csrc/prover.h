@@ -65,9 +65,34 @@ struct ProofPoints {
     g1_affine_t A, C;
     g2_affine_t B;
 };
+// The five MSM results of one proof: sum_i h_i H_i, sum_i z_aux,i L_i, sum_i z_i A_i, sum_i z_i B1_i (G1) and
+// sum_i z_i B2_i (G2).  With world > 1 each is one rank's share: the sum over the rank's contiguous slice
+// of every query (h in its bit-reversed device order; single-proof latency mode); the shares of
+// all ranks add up to the full sums.
+struct ProofSums {
+    g1_xyzz_t H, L, A, B1;
+    g2_xyzz_t B2;
+};
+// The verifying-key points the assembly adds (scheme_params vk: alpha_g1, beta_g1, beta_g2, delta_g1, delta_g2).
+struct AssemblyKey {
+    g1_affine_t alpha_g1, beta_g1, delta_g1;
+    g2_affine_t beta_g2, delta_g2;
+};
 // z_dev: (n_in + n_aux) canonical Fr on the device (z[0] must be ONE).  r, s canonical.
 ProofPoints groth16_prove(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, const fr_t &r,
                           const fr_t &s);
+// rank's share of the MSMs (rank < world); the witness map and NTT chain run in full on every rank
+ProofSums groth16_sums(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, unsigned rank = 0,
+                       unsigned world = 1);
+// A = alpha + A_sum + r delta, B = beta + B2_sum + s delta, C = H + L + s A + r B1 - r s delta (host)
+ProofPoints groth16_assemble(const AssemblyKey &k, const ProofSums &sums, const fr_t &r, const fr_t &s);
+AssemblyKey assembly_key(const Srs &srs);
+// share wire format (MI_SHARE_BYTES = 576): H | L | A | B_G1 (96 B each) | B_G2 (192 B), zcash uncompressed
+void sums_encode(const ProofSums &sums, uint8_t out[576]);
+// sum `count` encoded shares and assemble the proof against the uncompressed vk (verify.hip); throws on a
+// share or vk point that does not decode onto the curve
+ProofPoints groth16_assemble_shares(const uint8_t *vk, const uint8_t *shares, uint64_t count, const fr_t &r,
+                                    const fr_t &s);
 // trapdoor dlogs of the unique proof for (z, r, s) (requires srs.has_trapdoor): A, B, C in Fr (canonical)
 void groth16_trapdoor_dlogs(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, const fr_t &r,
                             const fr_t &s, fr_t out[3]);

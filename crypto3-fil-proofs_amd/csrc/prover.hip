@@ -688,18 +688,24 @@ Srs *srs_generate(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5]) {
 }
 
 // ================================================================================ prove
-ProofPoints groth16_prove(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, const fr_t &r,
-                          const fr_t &s) {
+ProofSums groth16_sums(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, unsigned rank,
+                       unsigned world) {
     if (srs.d != circ.d || srs.n_l != circ.n_aux || srs.n_a != circ.n_a || srs.n_b != circ.n_b)
         throw std::invalid_argument("SRS does not match circuit");
+    if (world == 0 || rank >= world) throw std::invalid_argument("share rank out of range");
     hipStream_t st = c.stream;
     const uint64_t d = circ.d, nv = circ.n_in + circ.n_aux;
     const unsigned L = circ.log_d;
-    ProofPoints out;
+    // this rank's contiguous slice [lo, lo + cnt) of a query of n points
+    auto slice = [&](uint64_t n, uint64_t &lo) {
+        lo = n * rank / world;
+        return n * (rank + 1) / world - lo;
+    };
+    ProofSums out;
+    g1_xyzz_t &H = out.H, &Lq = out.L, &As = out.A, &B1 = out.B1;
+    g2_xyzz_t &B2 = out.B2;
     {
     ScopedTimer whole(c, &c.stats.prove, circ.n);
-    g1_xyzz_t H, Lq, As, B1;
-    g2_xyzz_t B2;
     {
         // L, B_G1 and B_G2 do not depend on the QAP: they run on the auxiliary lane (second stream,
         // second host thread) while this stream runs the witness map, the NTT chain, H and A.
@@ -713,10 +719,11 @@ ProofPoints groth16_prove(Ctx &c, const Srs &srs, const Circuit &circ, const fr_
                 MI_HIP(hipSetDevice(c.device));
                 // B_G1 and B_G2 share the scalars (z over the B-density): sort them once
                 auto run_b = [&] {
+                    uint64_t lo, cnt = slice(circ.n_b, lo);
                     MsmPlan pb;
-                    msm_prepare(x, z_dev, circ.idx_b, circ.n_b, pb);
-                    msm_g1_planned(x, pb, srs.b_g1, &B1);
-                    msm_g2_planned(x, pb, srs.b_g2, &B2);
+                    msm_prepare(x, z_dev, circ.idx_b + lo, cnt, pb);
+                    msm_g1_planned(x, pb, srs.b_g1 + lo, &B1);
+                    msm_g2_planned(x, pb, srs.b_g2 + lo, &B2);
                 };
                 // aux-lane order: B before L (same-box A/B at 2^26: -2 ms per proof; MI_AUX_ORDER=l_first
                 // restores L first)
@@ -725,7 +732,8 @@ ProofPoints groth16_prove(Ctx &c, const Srs &srs, const Circuit &circ, const fr_
                     return !(e && strcmp(e, "l_first") == 0);
                 }();
                 if (b_first) run_b();
-                msm_g1(x, srs.l, z_dev + circ.n_in, nullptr, circ.n_aux, &Lq);
+                uint64_t l_lo, l_cnt = slice(circ.n_aux, l_lo);
+                msm_g1(x, srs.l + l_lo, z_dev + circ.n_in + l_lo, nullptr, l_cnt, &Lq);
                 if (!b_first) run_b();
                 MI_HIP(hipEventRecord(done, x.stream));
             } catch (...) {
@@ -753,8 +761,9 @@ ProofPoints groth16_prove(Ctx &c, const Srs &srs, const Circuit &circ, const fr_
             fr_t zinv = inverse(pow_u64(g, d) - fr_t::one());
             k_qap_divide<<<grid1(d), 256, 0, st>>>(a, b, cc, d, zinv);
             ntt_dif_coset_epilogue(c, a, L, true, true, dinv, true);  // icoset, canonical H (bit-reversed order)
-            msm_g1(c, srs.h_perm, a, nullptr, d - 1, &H);
-            msm_g1(c, srs.a, z_dev, circ.idx_a, circ.n_a, &As);
+            uint64_t h_lo, h_cnt = slice(d - 1, h_lo), a_lo, a_cnt = slice(circ.n_a, a_lo);
+            msm_g1(c, srs.h_perm + h_lo, a + h_lo, nullptr, h_cnt, &H);
+            msm_g1(c, srs.a + a_lo, z_dev, circ.idx_a + a_lo, a_cnt, &As);
         } catch (...) {
             err_main = std::current_exception();
         }
@@ -768,24 +777,49 @@ ProofPoints groth16_prove(Ctx &c, const Srs &srs, const Circuit &circ, const fr_
         c.stats.merge(x.stats);
         x.stats = Stats();
     }
-    // assembly on the host
-    fr_t rs = from_mont(to_mont(r) * to_mont(s));
-    g1_xyzz_t A = xyzz_add(xyzz_add_affine(As, srs.alpha_g1), xyzz_mul(xyzz_from_affine(srs.delta_g1), r.v, 8));
-    g2_xyzz_t B = xyzz_add(xyzz_add_affine(B2, srs.beta_g2), xyzz_mul(xyzz_from_affine(srs.delta_g2), s.v, 8));
-    g1_xyzz_t C = xyzz_mul(xyzz_from_affine(srs.delta_g1), rs.v, 8);
-    C = xyzz_add(C, xyzz_mul(xyzz_from_affine(srs.alpha_g1), s.v, 8));
-    C = xyzz_add(C, xyzz_mul(xyzz_from_affine(srs.beta_g1), r.v, 8));
-    C = xyzz_add(C, xyzz_mul(As, s.v, 8));
-    C = xyzz_add(C, xyzz_mul(B1, r.v, 8));
-    C = xyzz_add(C, H);
-    C = xyzz_add(C, Lq);
-    out.A = xyzz_to_affine(A);
-    out.B = xyzz_to_affine(B);
-    out.C = xyzz_to_affine(C);
     }
     MI_HIP(hipStreamSynchronize(st));
     c.timer.resolve();
     return out;
+}
+
+AssemblyKey assembly_key(const Srs &srs) {
+    return AssemblyKey{srs.alpha_g1, srs.beta_g1, srs.delta_g1, srs.beta_g2, srs.delta_g2};
+}
+
+// libsnark r1cs_gg_ppzksnark_prover / bellman create_proof: the blinded proof from the five MSM sums
+ProofPoints groth16_assemble(const AssemblyKey &k, const ProofSums &m, const fr_t &r, const fr_t &s) {
+    fr_t rs = from_mont(to_mont(r) * to_mont(s));
+    // A = alpha + sum z_i A_i + r delta;  B = beta + sum z_i B_i + s delta (G2), B1 likewise in G1
+    g1_xyzz_t A = xyzz_add(xyzz_add_affine(m.A, k.alpha_g1), xyzz_mul(xyzz_from_affine(k.delta_g1), r.v, 8));
+    g2_xyzz_t B = xyzz_add(xyzz_add_affine(m.B2, k.beta_g2), xyzz_mul(xyzz_from_affine(k.delta_g2), s.v, 8));
+    // C = H + L + s A + r B1 - r s delta, expanded so that A and B1 enter without their blinding:
+    //   s (alpha + A_sum + r delta) + r (beta + B1_sum + s delta) - r s delta = s alpha + r beta + s A_sum + r B1_sum + r s delta
+    g1_xyzz_t C = xyzz_mul(xyzz_from_affine(k.delta_g1), rs.v, 8);
+    C = xyzz_add(C, xyzz_mul(xyzz_from_affine(k.alpha_g1), s.v, 8));
+    C = xyzz_add(C, xyzz_mul(xyzz_from_affine(k.beta_g1), r.v, 8));
+    C = xyzz_add(C, xyzz_mul(m.A, s.v, 8));
+    C = xyzz_add(C, xyzz_mul(m.B1, r.v, 8));
+    C = xyzz_add(C, m.H);
+    C = xyzz_add(C, m.L);
+    ProofPoints out;
+    out.A = xyzz_to_affine(A);
+    out.B = xyzz_to_affine(B);
+    out.C = xyzz_to_affine(C);
+    return out;
+}
+
+ProofPoints groth16_prove(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, const fr_t &r,
+                          const fr_t &s) {
+    return groth16_assemble(assembly_key(srs), groth16_sums(c, srs, circ, z_dev), r, s);
+}
+
+void sums_encode(const ProofSums &m, uint8_t out[576]) {
+    g1_encode(xyzz_to_affine(m.H), out);
+    g1_encode(xyzz_to_affine(m.L), out + 96);
+    g1_encode(xyzz_to_affine(m.A), out + 192);
+    g1_encode(xyzz_to_affine(m.B1), out + 288);
+    g2_encode(xyzz_to_affine(m.B2), out + 384);
 }
 
 Ctx &ctx_aux(Ctx &c) {

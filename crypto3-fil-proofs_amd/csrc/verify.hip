@@ -511,6 +511,28 @@ bool groth16_verify(const uint8_t *vk, const uint8_t *ic, uint64_t n_ic, const u
     return fq12_is_one(final_exponentiation_verify(multi_miller_loop(P, Q)));
 }
 
+// single-proof latency mode: add the ranks' shares, then assemble as groth16_prove does
+ProofPoints groth16_assemble_shares(const uint8_t *vk, const uint8_t *shares, uint64_t count, const fr_t &r,
+                                    const fr_t &s) {
+    if (count == 0) throw std::invalid_argument("no proof shares");
+    DecodedVk V = decode_vk(vk, nullptr, 0);
+    ProofSums m{g1_xyzz_t::inf(), g1_xyzz_t::inf(), g1_xyzz_t::inf(), g1_xyzz_t::inf(), g2_xyzz_t::inf()};
+    g1_xyzz_t *g1[4] = {&m.H, &m.L, &m.A, &m.B1};
+    for (uint64_t k = 0; k < count; k++) {
+        const uint8_t *sh = shares + 576 * k;
+        for (int j = 0; j < 4; j++) {
+            g1_affine_t p;
+            if (!g1_decode_host(sh + 96 * j, p) || !g1_on_curve_host(p))
+                throw std::domain_error("proof share: invalid G1 point");
+            *g1[j] = xyzz_add_affine(*g1[j], p);
+        }
+        g2_affine_t q;
+        if (!g2_decode_host(sh + 384, q) || !g2_on_curve_host(q)) throw std::domain_error("proof share: invalid G2 point");
+        m.B2 = xyzz_add_affine(m.B2, q);
+    }
+    return groth16_assemble(AssemblyKey{V.alpha, V.beta1, V.delta1, V.beta2, V.delta2}, m, r, s);
+}
+
 // bellman verify_proofs_batch: random 128-bit weights rho_i;
 //   prod e(rho_i A_i, B_i) * e(-sum rho_i acc_i, gamma) * e(-sum rho_i C_i, delta) * e(-(sum rho_i) alpha, beta) == 1
 bool groth16_verify_batch(const uint8_t *vk, const uint8_t *ic, uint64_t n_ic, uint64_t count, const uint8_t *inputs,

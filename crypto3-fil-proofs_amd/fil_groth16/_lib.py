@@ -22,6 +22,7 @@ EXPORTS = [
     "mi_synth_generate", "mi_synth_r1cs", "mi_synth_witness", "mi_synth_free",
     "mi_params_inspect", "mi_params_load", "mi_params_write", "mi_vk_write",
     "mi_groth16_verify", "mi_groth16_verify_batch", "mi_pairing",
+    "mi_groth16_prove_share", "mi_groth16_prove_share_dev", "mi_groth16_assemble",
 ]
 
 _lib = None
@@ -77,6 +78,9 @@ def lib():
         "mi_groth16_prove": ([vp, vp, vp, u8p, u8p, u8p, c_int, vp, vp], c_int),
         "mi_groth16_prove_dev": ([vp, vp, vp, vp, u8p, u8p, c_int, vp, vp], c_int),
         "mi_groth16_prove_batch": ([vp, vp, vp, u64, vp, u8p, c_int, vp], c_int),
+        "mi_groth16_prove_share": ([vp, vp, vp, u8p, ctypes.c_uint32, ctypes.c_uint32, c_int, vp], c_int),
+        "mi_groth16_prove_share_dev": ([vp, vp, vp, vp, ctypes.c_uint32, ctypes.c_uint32, c_int, vp], c_int),
+        "mi_groth16_assemble": ([u8p, u8p, u64, u8p, u8p, vp, vp], c_int),
         "mi_groth16_trapdoor_dlogs": ([vp, vp, vp, vp, u8p, u8p, vp], c_int),
         "mi_msm_g1": ([vp, u8p, u8p, u64, vp], c_int),
         "mi_msm_g2": ([vp, u8p, u8p, u64, vp], c_int),

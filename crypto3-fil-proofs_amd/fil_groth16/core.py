@@ -21,6 +21,7 @@ from ._lib import check, lib
 
 FR_MODULUS = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 PROOF_BYTES = 192
+SHARE_BYTES = 576
 VK_BYTES = 864
 
 
@@ -334,6 +335,31 @@ def prove_batch(ctx: Context, pk: ProvingKey, circuit: Circuit, zs, rs, priority
     out = ctypes.create_string_buffer(PROOF_BYTES * count)
     check(lib().mi_groth16_prove_batch(ctx.h, pk.h, circuit.h, count, arr, rsb, int(priority), out))
     return [out.raw[i * PROOF_BYTES:(i + 1) * PROOF_BYTES] for i in range(count)]
+
+
+def prove_share(ctx: Context, pk: ProvingKey, circuit: Circuit, z, rank: int, world: int, priority=False) -> bytes:
+    """Single-proof latency mode: this rank's share of the five MSMs of one proof
+    (SHARE_BYTES). z as for ``prove``. The shares of ranks 0..world-1 go to ``assemble``."""
+    out = ctypes.create_string_buffer(SHARE_BYTES)
+    if isinstance(z, int):
+        check(lib().mi_groth16_prove_share_dev(ctx.h, pk.h, circuit.h, ctypes.c_void_p(z), rank, world,
+                                               int(priority), out))
+    else:
+        assert len(z) == 32 * circuit.num_vars, "witness length must be (num_inputs + num_aux) * 32"
+        check(lib().mi_groth16_prove_share(ctx.h, pk.h, circuit.h, bytes(z), rank, world, int(priority), out))
+    return out.raw
+
+
+def assemble(vk: bytes, shares, r: int, s: int, want_raw=False):
+    """Add the ranks' shares and blind: the proof ``prove`` returns for the same (z, r, s). Host only."""
+    shares = [bytes(x) for x in shares]
+    if not shares or any(len(x) != SHARE_BYTES for x in shares):
+        raise ValueError(f"shares are {SHARE_BYTES} bytes each, at least one")
+    assert len(vk) == VK_BYTES
+    proof = ctypes.create_string_buffer(PROOF_BYTES)
+    raw = ctypes.create_string_buffer(384) if want_raw else None
+    check(lib().mi_groth16_assemble(bytes(vk), b"".join(shares), len(shares), fr_bytes(r), fr_bytes(s), proof, raw))
+    return (proof.raw, raw.raw) if want_raw else proof.raw
 
 
 def trapdoor_dlogs(ctx: Context, pk: ProvingKey, circuit: Circuit, z_dev_ptr: int, r: int, s: int):

@@ -10,7 +10,7 @@ one all-gather of the finished proofs (RCCL over xGMI with backend "nccl"; gloo 
 import numpy as np
 
 from .compound import shard_partitions
-from .core import PROOF_BYTES
+from .core import PROOF_BYTES, SHARE_BYTES
 
 
 def gather_multiproof(local_proofs, num_partitions: int, rank: int, world: int, device="cpu"):
@@ -39,3 +39,31 @@ def gather_multiproof(local_proofs, num_partitions: int, rank: int, world: int, 
     for p in range(num_partitions):
         out += allp[p % world][p // world].tobytes()
     return bytes(out)
+
+
+def gather_shares(share: bytes, world: int, device="cpu"):
+    """All-gather one MI_SHARE_BYTES record per rank (the latency mode's only exchange, 576 B per GPU)."""
+    import torch
+    import torch.distributed as dist
+
+    if len(share) != SHARE_BYTES:
+        raise ValueError(f"shares are {SHARE_BYTES} bytes")
+    t = torch.from_numpy(np.frombuffer(share, dtype=np.uint8).copy()).to(device)
+    if world == 1:
+        return [share]
+    bufs = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(bufs, t)
+    return [b.cpu().numpy().tobytes() for b in bufs]
+
+
+def prove_split(ctx, pk, circuit, z, r, s, rank: int, world: int, device="cpu", want_raw=False):
+    """Single-proof latency mode: one proof over `world` ranks, one GPU each.
+
+    Every rank holds the full proving key and witness, runs the witness map and NTT chain itself
+    (no 2 GB H broadcast), and computes its contiguous slice of each MSM; the 576-byte shares are
+    all-gathered and every rank assembles the same 192-byte proof as ``prove`` on one GPU."""
+    from .core import assemble, prove_share
+
+    vk, _ = pk.verifying_key()
+    shares = gather_shares(prove_share(ctx, pk, circuit, z, rank, world), world, device)
+    return assemble(vk, shares, r, s, want_raw=want_raw)

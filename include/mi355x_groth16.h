@@ -57,6 +57,7 @@ extern "C" {
 #define MI_ERR_NO_DEVICE (-6)
 
 #define MI_PROOF_BYTES 192
+#define MI_SHARE_BYTES 576 /* mi_groth16_prove_share: H | L | A | B_G1 (96 B each) | B_G2 (192 B) */
 #define MI_VK_BYTES 864 /* alpha_g1 | beta_g1 | beta_g2 | gamma_g2 | delta_g1 | delta_g2 (uncompressed) */
 
 typedef struct mi_ctx mi_ctx;         /* one per GPU: stream, twiddle tables, scratch */
@@ -167,6 +168,20 @@ int mi_groth16_prove_dev(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circu
 int mi_groth16_prove_batch(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circuit, uint64_t count,
                            const uint8_t *const *z, const uint8_t *rs /* count x 64 B: r | s */, int priority,
                            uint8_t *proofs_out);
+/* Single-proof latency mode (one proof split over `world` GPUs).  Rank `rank` runs the
+ * witness map and NTT chain in full and the MSMs over its contiguous slice of each query (h in the
+ * bit-reversed coefficient order the device keeps it in; l, a, b_g1/b_g2 in key order), writing the five partial sums, zcash-uncompressed, to share_out.  The callers exchange
+ * the shares (an all-gather of MI_SHARE_BYTES per rank) and any of them calls mi_groth16_assemble,
+ * which adds the shares and applies the blinding exactly as mi_groth16_prove does: the proof bytes are
+ * identical for every world size.  Replaces the single crypto3 prove call of compound_proof::prove
+ * (compound_proof.hpp:89-95) when one partition must finish sooner than one GPU can prove it. */
+int mi_groth16_prove_share(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circuit, const uint8_t *z,
+                           uint32_t rank, uint32_t world, int priority, uint8_t share_out[MI_SHARE_BYTES]);
+int mi_groth16_prove_share_dev(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circuit, const void *z_dev,
+                               uint32_t rank, uint32_t world, int priority, uint8_t share_out[MI_SHARE_BYTES]);
+/* host only (no device): vk = MI_VK_BYTES uncompressed, shares = count x MI_SHARE_BYTES (any order) */
+int mi_groth16_assemble(const uint8_t *vk, const uint8_t *shares, uint64_t count, const uint8_t r[32],
+                        const uint8_t s[32], uint8_t proof_out[MI_PROOF_BYTES], uint8_t *raw_out);
 /* discrete logs (canonical Fr, 3 x 32 B) of the unique valid A, B, C for (z, r, s) under a key
  * produced by mi_srs_generate -- the size-independent trapdoor check used by the tests */
 int mi_groth16_trapdoor_dlogs(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circuit, const void *z_dev,

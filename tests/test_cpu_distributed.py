@@ -60,3 +60,47 @@ def test_gloo_world2_gather(tmp_path, oracle, num_partitions):
     zb = circuits.z_bytes(z)
     serial = b"".join(P.prove(zb, 100 + p, 200 + p)[0] for p in range(num_partitions))
     assert outs[0] == serial
+
+
+def _split_worker(rank, world, port, outdir):
+    """Latency mode over gloo: rank k's share (oracle MSMs over its slices), all-gather, host assembly
+    through the C ABI (mi_groth16_assemble needs no device)."""
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "crypto3-fil-proofs_amd"), os.path.join(root, "oracle"),
+              os.path.join(root, "tests", "golden"), os.path.join(root, "tests")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+
+    import circuits
+    import fil_groth16 as fg
+    import oracle_py
+    import split_oracle
+    from fil_groth16.distributed import gather_shares
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n_in, n_aux, rows, z = circuits.random_circuit(71, 60)
+    mats = circuits.to_csr(rows)
+    P = oracle_py.OracleParams(oracle_py.OracleCircuit(len(rows), n_in, n_aux, mats), circuits.toxic())
+    mine = split_oracle.shares(oracle_py, P, n_in, n_aux, mats, circuits.z_bytes(z), world)[rank]
+    shares = gather_shares(mine, world)
+    proof = fg.assemble(P.export()["vk"], shares, 17, 19)
+    with open(os.path.join(outdir, f"s{rank}.bin"), "wb") as f:
+        f.write(proof)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_split_proof(tmp_path, oracle):
+    """SURVEY.md 8e single-proof latency mode: two ranks' shares, one all-gather, the same proof bytes
+    on both ranks as the serial prove."""
+    import circuits
+
+    world = 2
+    mp.spawn(_split_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    outs = [open(tmp_path / f"s{r}.bin", "rb").read() for r in range(world)]
+    n_in, n_aux, rows, z = circuits.random_circuit(71, 60)
+    P = oracle.OracleParams(oracle.OracleCircuit(len(rows), n_in, n_aux, circuits.to_csr(rows)), circuits.toxic())
+    assert outs[0] == outs[1] == P.prove(circuits.z_bytes(z), 17, 19)[0]

@@ -1,6 +1,7 @@
 """CPU: the product-side Groth16 verifier (mi_groth16_verify / _batch, host code in verify.hip --
 bellman verify_proof semantics, the C2 self-check of api/seal.hpp:310-313) against the golden
-proofs and oracle-made proofs, plus pairing bilinearity.  No device is needed."""
+proofs and oracle-made proofs, plus pairing bilinearity and the latency mode's share assembly
+(mi_groth16_assemble).  No device is needed."""
 import random
 
 import pytest
@@ -85,3 +86,39 @@ def test_pairing_bilinear(oracle):
     one = bytes(47) + b"\x01" + bytes(48 * 11)
     assert e1 != one  # non-degenerate
     assert fg.pairing(oracle.g1_mul(g1, R - 1), g2) != e1
+
+
+@pytest.mark.parametrize("world", [1, 3, 50])
+def test_assemble_shares_matches_oracle(oracle, world):
+    """mi_groth16_assemble (host): oracle shares of any split -- 50 ranks leave some slices empty --
+    add up and blind to the oracle's proof."""
+    import split_oracle
+
+    n_in, n_aux, rows, z = circuits.random_circuit(72, 30)
+    mats = circuits.to_csr(rows)
+    P = oracle.OracleParams(oracle.OracleCircuit(len(rows), n_in, n_aux, mats), circuits.toxic())
+    zb = circuits.z_bytes(z)
+    sh = split_oracle.shares(oracle, P, n_in, n_aux, mats, zb, world)
+    vk = P.export()["vk"]
+    proof, raw = fg.assemble(vk, sh, 3, 4, want_raw=True)
+    oproof, oraw, _ = P.prove(zb, 3, 4)
+    assert proof == oproof and raw == oraw
+    assert fg.assemble(vk, sh[::-1], 3, 4) == oproof  # order-free
+
+
+def test_assemble_rejects_bad_shares(oracle):
+    import split_oracle
+
+    n_in, n_aux, rows, z = circuits.random_circuit(73, 20)
+    mats = circuits.to_csr(rows)
+    P = oracle.OracleParams(oracle.OracleCircuit(len(rows), n_in, n_aux, mats), circuits.toxic())
+    sh = split_oracle.shares(oracle, P, n_in, n_aux, mats, circuits.z_bytes(z), 2)
+    vk = P.export()["vk"]
+    bad = bytearray(sh[0])
+    bad[100] ^= 1  # L's x coordinate: off the curve
+    with pytest.raises(fg.FilGpuError):
+        fg.assemble(vk, [bytes(bad), sh[1]], 1, 2)
+    with pytest.raises(ValueError):
+        fg.assemble(vk, [], 1, 2)
+    with pytest.raises(fg.FilGpuError):
+        fg.assemble(vk, sh, fg.FR_MODULUS.to_bytes(32, "little"), 2)  # r >= r_mod

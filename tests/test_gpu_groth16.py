@@ -207,3 +207,87 @@ def test_seal_commit_phase2_self_verifies(ctx, oracle):
     bad[-32] ^= 1
     with pytest.raises(RuntimeError, match="sanity check failed"):
         fg.seal_commit_phase2_proofs(ctx, pk, gc, [zb, bytes(bad), zb], blind, n_in)
+
+
+@pytest.mark.parametrize("rows,seed,worlds", [(700, 81, (1, 2, 3, 7)), (16000, 82, (4,))])
+def test_prove_share_vs_oracle_shares(ctx, oracle, rows, seed, worlds):
+    """Single-proof latency mode: every rank's GPU share is byte-identical to the oracle's
+    sums over the same slices, and the assembled proof equals the one-GPU proof and the oracle's."""
+    import split_oracle
+
+    n_in, n_aux, rws, z = circuits.random_circuit(seed, rows, n_in=6, n_free=32)
+    mats = circuits.to_csr(rws)
+    oc, gc = _load(ctx, oracle, n_in, n_aux, rws, z)
+    tox = circuits.toxic(seed)
+    pk = fg.generate_random_parameters(ctx, gc, tox)
+    op = oracle.OracleParams(oc, tox)
+    zb = circuits.z_bytes(z)
+    r, s = circuits.blinding(seed)
+    vk, _ = pk.verifying_key()
+    one = fg.prove(ctx, pk, gc, zb, r, s)
+    assert one == op.prove(zb, r, s)[0]
+    for world in worlds:
+        shares = [fg.prove_share(ctx, pk, gc, zb, k, world) for k in range(world)]
+        assert shares == split_oracle.shares(oracle, op, n_in, n_aux, mats, zb, world), world
+        assert fg.assemble(vk, shares, r, s) == one, world
+    with pytest.raises(fg.FilGpuError):
+        fg.prove_share(ctx, pk, gc, zb, 2, 2)  # rank >= world
+
+
+def test_prove_share_device_witness(ctx, oracle):
+    import torch
+
+    n_in, n_aux, rws, z = circuits.random_circuit(83, 900, n_in=6, n_free=32)
+    oc, gc = _load(ctx, oracle, n_in, n_aux, rws, z)
+    pk = fg.generate_random_parameters(ctx, gc, circuits.toxic())
+    zb = circuits.z_bytes(z)
+    zd = torch.from_numpy(np.frombuffer(zb, dtype=np.uint8).copy()).cuda()
+    vk, _ = pk.verifying_key()
+    shares = [fg.prove_share(ctx, pk, gc, zd.data_ptr(), k, 3) for k in range(3)]
+    assert fg.assemble(vk, shares, 9, 10) == fg.prove(ctx, pk, gc, zb, 9, 10)
+
+
+def _split_gpu_worker(rank, world, port, outdir):
+    import os
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "crypto3-fil-proofs_amd"), os.path.join(root, "tests", "golden")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+
+    import circuits
+    import fil_groth16 as fg
+    from fil_groth16.distributed import prove_split
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    c = fg.Context(0)
+    n_in, n_aux, rws, z = circuits.random_circuit(84, 3000, n_in=6, n_free=32)
+    gc = fg.Circuit(c, len(rws), n_in, n_aux, circuits.to_csr(rws))
+    pk = fg.generate_random_parameters(c, gc, circuits.toxic())
+    proof = prove_split(c, pk, gc, circuits.z_bytes(z), 21, 22, rank, world)
+    with open(os.path.join(outdir, f"p{rank}.bin"), "wb") as f:
+        f.write(proof)
+    dist.barrier()
+    dist.destroy_process_group()
+    del pk, gc
+    c.close()
+
+
+def test_prove_split_two_processes(oracle, tmp_path):
+    """fil_groth16.distributed.prove_split with one process per rank (both on this box's GPU, gloo for
+    the 576-byte all-gather; RCCL on a multi-GPU node): every rank ends with the oracle's proof."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    mp.spawn(_split_gpu_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    outs = [open(tmp_path / f"p{k}.bin", "rb").read() for k in range(2)]
+    n_in, n_aux, rws, z = circuits.random_circuit(84, 3000, n_in=6, n_free=32)
+    op = oracle.OracleParams(oracle.OracleCircuit(len(rws), n_in, n_aux, circuits.to_csr(rws)), circuits.toxic())
+    assert outs[0] == outs[1] == op.prove(circuits.z_bytes(z), 21, 22)[0]
