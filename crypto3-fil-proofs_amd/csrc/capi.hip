@@ -30,6 +30,7 @@ struct mi_points {
     uint64_t n;
     int is_g2;
     int owns;
+    const void *hi = nullptr;  // 2^128 multiples (split-mode MSM table), proving-key queries h, l, a only
 };
 
 namespace {
@@ -524,9 +525,9 @@ int mi_points_from_srs(mi_ctx *ctx, const mi_srs *srs, int which, mi_points **ou
         need(ctx && srs && out, "null argument");
         const mi::Srs &s = *srs->p;
         switch (which) {
-            case 0: *out = new mi_points{s.h_perm, s.n_h, 0, 0}; break;
-            case 1: *out = new mi_points{s.l, s.n_l, 0, 0}; break;
-            case 2: *out = new mi_points{s.a, s.n_a, 0, 0}; break;
+            case 0: *out = new mi_points{s.h_perm, s.n_h, 0, 0, s.h_hi}; break;
+            case 1: *out = new mi_points{s.l, s.n_l, 0, 0, s.l_hi}; break;
+            case 2: *out = new mi_points{s.a, s.n_a, 0, 0, s.a_hi}; break;
             case 3: *out = new mi_points{s.b_g1, s.n_b, 0, 0}; break;
             case 4: *out = new mi_points{s.b_g2, s.n_b, 1, 0}; break;
             default: throw std::invalid_argument("which must be 0..4");
@@ -547,7 +548,8 @@ int mi_msm_g1_dev(mi_ctx *ctx, const mi_points *bases, const void *scalars_dev, 
         need(n <= bases->n, "n exceeds the number of bases");
         CtxLock l(ctx);
         mi::g1_xyzz_t r;
-        mi::msm_g1(ctx->c, (const mi::g1_affine_t *)bases->dev, (const mi::fr_t *)scalars_dev, nullptr, n, &r);
+        mi::msm_g1(ctx->c, (const mi::g1_affine_t *)bases->dev, (const mi::fr_t *)scalars_dev, nullptr, n, &r,
+                   (const mi::g1_affine_t *)bases->hi);
         mi::g1_encode(mi::xyzz_to_affine(r), out96);
     });
 }

@@ -220,24 +220,37 @@ void fr_from_mont_inplace(Ctx &c, fr_t *d, uint64_t n);
 // the scalars, so MSMs over the same scalars with different bases (B_G1 and B_G2 of one prove)
 // share it.  Pointers are into the ctx scratch arena; valid until the next msm_prepare on the ctx.
 struct MsmPlan {
-    uint64_t n = 0;
+    uint64_t n = 0;      // points of the plan (2 x the real points in split mode)
+    uint64_t nreal = 0;  // split mode (non-zero): point j >= nreal is 2^128 * base[j - nreal], scalar halves
     unsigned cb = 0, nwin = 0;
     uint32_t nbk = 0, nb = 0, L0 = 0, maxcnt = 0, total = 0;
     uint64_t entries = 0;  // non-zero digits over all windows
     const uint32_t *vals_s = nullptr, *off = nullptr, *cnt = nullptr, *coff = nullptr, *ccnt = nullptr,
                    *chunk_bucket = nullptr, *order = nullptr;
 };
-// false when every scalar is zero (the MSM is the identity)
-bool msm_prepare(Ctx &c, const fr_t *scalars, const uint32_t *idx, uint64_t n, MsmPlan &plan);
-void msm_g1_planned(Ctx &c, const MsmPlan &plan, const g1_affine_t *bases, g1_xyzz_t *result_host);
+// false when every scalar is zero (the MSM is the identity).  split: plan the 2n half-scalar points of
+// the 2^128-shifted base table (msm_g1 with bases_hi); the plan then needs bases_hi too.
+bool msm_prepare(Ctx &c, const fr_t *scalars, const uint32_t *idx, uint64_t n, MsmPlan &plan, bool split = false);
+void msm_g1_planned(Ctx &c, const MsmPlan &plan, const g1_affine_t *bases, g1_xyzz_t *result_host,
+                    const g1_affine_t *bases_hi = nullptr);
 void msm_g2_planned(Ctx &c, const MsmPlan &plan, const g2_affine_t *bases, g2_xyzz_t *result_host);
 // result = sum_i scalar[idx ? idx[i] : i] * bases[i]; scalars canonical (raw) Fr.
+// bases_hi (optional): bases_hi[i] = 2^128 bases[i].  With it, large MSMs run in split mode: scalar
+// k_i = lo_i + 2^128 hi_i becomes two 128-bit scalars over bases[i] and bases_hi[i], which halves the
+// windows (and the bucket reduction) for the same number of mixed additions (MI_MSM_SPLIT: 0 off,
+// 1 default from 2^16 points, 2 always).
 void msm_g1(Ctx &c, const g1_affine_t *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,
-            g1_xyzz_t *result_host);
+            g1_xyzz_t *result_host, const g1_affine_t *bases_hi = nullptr);
+// whether msm_g1 with a bases_hi table takes the split path for n points
+bool msm_use_split(uint64_t n);
+// bases_hi table: out[i] = 2^128 in[i] (128 doublings, batch-normalised to affine); scratch slots 10, 11
+void g1_shift128(Ctx &c, const g1_affine_t *in, uint64_t n, g1_affine_t *out);
 void msm_g2(Ctx &c, const g2_affine_t *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,
             g2_xyzz_t *result_host);
 // host-side window-size heuristic (exposed for tests)
 unsigned msm_window_bits(uint64_t n);
+// same for `n` points with scalars of `sbits` bits including the signed-digit carry (256 plain, 129 split)
+unsigned msm_window_bits_for(uint64_t n, unsigned sbits);
 
 // ---- encodings (encode.hip) ----
 // zcash uncompressed big-endian -> device Montgomery affine; returns count of invalid points

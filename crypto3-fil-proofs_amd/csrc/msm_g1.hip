@@ -5,12 +5,16 @@
 
 namespace mi {
 
-unsigned msm_window_bits(uint64_t n) {
-    // minimise (mixed adds) + 1.4 x (bucket-reduction full adds) over c
-    unsigned best = 4;
+unsigned msm_window_bits(uint64_t n) { return msm_window_bits_for(n, 256); }
+
+unsigned msm_window_bits_for(uint64_t n, unsigned sbits) {
+    // minimise (mixed adds) + 1.4 x (bucket-reduction full adds) over c; split plans (129-bit scalars)
+    // keep c >= 5 so their ceil(129 / c) windows fit the compacted digit kernel (MAXW_C)
+    const unsigned cmin = sbits < 256 ? 5 : 4;
+    unsigned best = cmin;
     double best_cost = 1e300;
-    for (unsigned c = 4; c <= 22; c++) {
-        unsigned nwin = (256 + c - 1) / c;
+    for (unsigned c = cmin; c <= 22; c++) {
+        unsigned nwin = (sbits + c - 1) / c;
         double cost = (double)n * nwin + 1.4 * 2.0 * nwin * (double)(1u << (c - 1)) + 64.0 * nwin * c;
         if (cost < best_cost) {
             best_cost = cost;
@@ -20,22 +24,30 @@ unsigned msm_window_bits(uint64_t n) {
     return best;
 }
 
+bool msm_use_split(uint64_t n) {
+    // MI_MSM_SPLIT: 0 off, 1 (default) from 2^16 points, 2 always (tests); read per call
+    const char *e = getenv("MI_MSM_SPLIT");
+    const int mode = e ? atoi(e) : 1;
+    return mode == 2 || (mode == 1 && n >= (1u << 16));
+}
+
 void msm_g1(Ctx &c, const g1_affine_t *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,
-            g1_xyzz_t *result_host) {
-    msm_run<fq_t>(c, bases, scalars, idx, n, result_host);
+            g1_xyzz_t *result_host, const g1_affine_t *bases_hi) {
+    msm_run<fq_t>(c, bases, scalars, idx, n, result_host, bases_hi);
 }
 
-bool msm_prepare(Ctx &c, const fr_t *scalars, const uint32_t *idx, uint64_t n, MsmPlan &plan) {
-    return msm_prepare_impl(c, scalars, idx, n, plan);
+bool msm_prepare(Ctx &c, const fr_t *scalars, const uint32_t *idx, uint64_t n, MsmPlan &plan, bool split) {
+    return msm_prepare_impl(c, scalars, idx, n, plan, split);
 }
 
-void msm_g1_planned(Ctx &c, const MsmPlan &plan, const g1_affine_t *bases, g1_xyzz_t *result_host) {
+void msm_g1_planned(Ctx &c, const MsmPlan &plan, const g1_affine_t *bases, g1_xyzz_t *result_host,
+                    const g1_affine_t *bases_hi) {
     if (!plan.total) {
         *result_host = g1_xyzz_t::inf();
         return;
     }
     ScopedTimer whole(c, &c.stats.msm_g1, plan.n);  // scalar-side phase timed by msm_prepare's caller
-    msm_accumulate_impl<fq_t>(c, plan, bases, result_host);
+    msm_accumulate_impl<fq_t>(c, plan, bases, result_host, bases_hi);
 }
 
 }  // namespace mi

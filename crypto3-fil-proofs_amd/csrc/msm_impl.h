@@ -100,15 +100,27 @@ __global__ void k_digits(const fr_t *__restrict__ scalars, const uint32_t *__res
 // boolean-heavy (0/1 and small values): 43 % of the L/A/B digit slots of the synthetic 2^26 circuit
 // are zero, and none of them is sorted any more.  Order inside a window is arbitrary before the sort.
 constexpr unsigned MAXW_C = 32;  // c >= 8
+// Split mode (nreal != 0, n = 2 nreal): point i < nreal takes bits [0, 128) of scalar i, point
+// nreal + i bits [128, 256) of the same scalar (its base is 2^128 times as large).
 __global__ void __launch_bounds__(256) k_digits_c(const fr_t *__restrict__ scalars, const uint32_t *__restrict__ idx,
-                                                  uint32_t n, unsigned c, unsigned nwin,
+                                                  uint32_t n, unsigned c, unsigned nwin, uint32_t nreal,
                                                   uint32_t *__restrict__ wcount, uint32_t *__restrict__ keys,
                                                   uint32_t *__restrict__ vals) {
     __shared__ uint32_t wc[4][MAXW_C];
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     fr_t s = fr_t::zero();
-    if (i < n) s = scalars[idx ? idx[i] : i];
+    if (i < n) {
+        const bool hi = nreal && i >= nreal;
+        const uint32_t src = hi ? i - nreal : i;
+        s = scalars[idx ? idx[src] : src];
+        if (nreal) {
+            MI_UNROLL for (int j = 0; j < 4; j++) {
+                s.v[j] = hi ? s.v[j + 4] : s.v[j];
+                s.v[j + 4] = 0;
+            }
+        }
+    }
     const uint32_t nbk = 1u << (c - 1);
     const uint32_t mask = (1u << c) - 1;
     uint32_t dg[MAXW_C];  // digit | neg << 31; 0 = zero digit
@@ -253,8 +265,18 @@ __global__ void __launch_bounds__(256) MI_WAVES_ACC k_accum_level0(const uint32_
                                                       const uint32_t *__restrict__ cnt, uint32_t total, uint32_t L0,
                                                       const uint32_t *__restrict__ vals,
                                                       const Affine<F> *__restrict__ bases,
+                                                      const Affine<F> *__restrict__ bases_hi, uint32_t nreal,
                                                       XYZZ<F> *__restrict__ out) {
     using LP = Lane<F>;
+    // point j of the plan: bases[j], or in split mode bases_hi[j - nreal] from j = nreal on
+    // (G1 only: split mode has no G2 table, and the select costs the G2 lane-pair kernel registers)
+    auto src = [&](uint32_t v) {
+        const uint32_t j = v & 0x7fffffffu;
+        if constexpr (sizeof(F) == sizeof(fq_t))
+            return j < nreal ? bases + j : bases_hi + (j - nreal);
+        else
+            return bases + j;
+    };
     using R = typename LP::R;
     uint32_t u = (blockIdx.x * blockDim.x + threadIdx.x) / LP::K;  // a lane pair per chunk for G2
     if (u >= total) return;
@@ -272,12 +294,12 @@ __global__ void __launch_bounds__(256) MI_WAVES_ACC k_accum_level0(const uint32_
     if (beg < end) {
         uint32_t v = vals[beg];
         uint32_t vn = beg + 1 < end ? vals[beg + 1] : 0u;
-        Affine<R> a = LP::lda(bases + (v & 0x7fffffffu));
+        Affine<R> a = LP::lda(src(v));
         for (uint32_t p = beg; p < end; p++) {
             Affine<R> an = a;
             uint32_t vnn = 0;
             if (p + 1 < end) {
-                an = LP::lda(bases + (vn & 0x7fffffffu));
+                an = LP::lda(src(vn));
                 if (p + 2 < end) vnn = vals[p + 2];
             }
             if (v >> 31) a.y = -a.y;
@@ -290,7 +312,7 @@ __global__ void __launch_bounds__(256) MI_WAVES_ACC k_accum_level0(const uint32_
 #else
     for (uint32_t p = beg; p < end; p++) {
         uint32_t v = vals[p];
-        Affine<R> a = LP::lda(bases + (v & 0x7fffffffu));
+        Affine<R> a = LP::lda(src(v));
         if (v >> 31) a.y = -a.y;
         acc = xyzz_add_affine_inl(acc, a);
     }
@@ -586,13 +608,18 @@ inline bool plan_chunks(Ctx &c, MsmPlan &pl, uint32_t *offA, uint32_t *cntA, uin
 
 // The plan's arrays live in scratch slots 3, 5-8, 16, 17 and stay valid until the next prepare on
 // this ctx; the accumulation phase only uses the other slots.
-inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, uint64_t n, MsmPlan &pl) {
+inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, uint64_t nscal, MsmPlan &pl,
+                             bool split = false) {
     pl = MsmPlan();
+    if (nscal == 0) return false;
+    // split mode: 2 nscal points with 128-bit scalars (+1 carry bit), always on the compacted path
+    const uint64_t n = split ? 2 * nscal : nscal;
+    const unsigned sbits = split ? 129 : 256;
     pl.n = n;
-    if (n == 0) return false;
+    pl.nreal = split ? nscal : 0;
     hipStream_t st = c.stream;
-    const unsigned cb = msm_window_bits(n);
-    const unsigned nwin = (256 + cb - 1) / cb;
+    const unsigned cb = msm_window_bits_for(n, sbits);
+    const unsigned nwin = (sbits + cb - 1) / cb;
     const uint32_t nbk = 1u << (cb - 1);
     const uint64_t nb64 = (uint64_t)nwin * nbk;
     const uint64_t np64 = (uint64_t)nwin * n;
@@ -609,7 +636,7 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
     // nwin <= MAXW_C) at any size: tests use it to cover the large-MSM path at 2^20
     const char *sort_env = getenv("MI_MSM_SORT");
     const bool force_windowed = sort_env && strcmp(sort_env, "windowed") == 0;
-    const bool one_sort = !force_windowed && all_bits <= 22 && nwin > 1;
+    const bool one_sort = !force_windowed && !split && all_bits <= 22 && nwin > 1;
     const uint32_t wk = one_sort ? nbk + 1 : 0;
     pl.cb = cb;
     pl.nwin = nwin;
@@ -627,6 +654,7 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
     uint32_t *dmax = c.scratch[9].as<uint32_t>(4 + 2 * nwin);  // [max bucket size, pad, zstart[nwin], wcount[nwin]]
     uint32_t *zstart = dmax + 4, *wcount = zstart + nwin;
     const bool compact = !one_sort && nwin <= MAXW_C;  // large MSMs: only non-zero digits are sorted
+    if (split && !compact) throw std::logic_error("msm: split mode needs the compacted digit path");
     std::vector<uint32_t> wn(nwin, 0);
 
     {
@@ -634,7 +662,8 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
         size_t tmp_bytes = 0;
         if (compact) {
             MI_HIP(hipMemsetAsync(wcount, 0, sizeof(uint32_t) * nwin, st));
-            k_digits_c<<<grid_for(n, 256), 256, 0, st>>>(scalars, idx, (uint32_t)n, cb, nwin, wcount, keys, vals);
+            k_digits_c<<<grid_for(n, 256), 256, 0, st>>>(scalars, idx, (uint32_t)n, cb, nwin, (uint32_t)pl.nreal,
+                                                          wcount, keys, vals);
             MI_LAUNCHED(c, "k_digits_c");
             MI_HIP(hipMemcpyAsync(wn.data(), wcount, sizeof(uint32_t) * nwin, hipMemcpyDeviceToHost, st));
             MI_HIP(hipStreamSynchronize(st));
@@ -695,7 +724,8 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
 // Level-0 accumulation of the plan's chunks over `bases` and the in-place chunk tree: bucket b's sum
 // ends up in P0[coff[b]] (when cnt[b] != 0).  Returns P0 (scratch slot 10).
 template <class F>
-XYZZ<F> *accumulate_chunks(Ctx &c, const MsmPlan &pl, const Affine<F> *bases) {
+XYZZ<F> *accumulate_chunks(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, const Affine<F> *bases_hi = nullptr) {
+    if (pl.nreal && !bases_hi) throw std::logic_error("msm: split plan without the 2^128 base table");
     hipStream_t st = c.stream;
     const unsigned K = Lane<F>::K;      // threads per element in the accumulation (2 for G2: g2pair.h)
     const unsigned KR = LaneRed<F>::K;  // ... and in the reduction kernels
@@ -707,7 +737,8 @@ XYZZ<F> *accumulate_chunks(Ctx &c, const MsmPlan &pl, const Affine<F> *bases) {
     {
         ScopedTimer tacc(c, sizeof(F) == sizeof(fq_t) ? &c.stats.accum_g1 : &c.stats.accum_g2, pl.n);
         k_accum_level0<F><<<grid_for((uint64_t)pl.total * K, 256), 256, 0, st>>>(pl.order, pl.chunk_bucket, coff, offA, cntA,
-                                                                    pl.total, L0, pl.vals_s, bases, P0);
+                                                                    pl.total, L0, pl.vals_s, bases, bases_hi,
+                                                                    pl.nreal ? (uint32_t)pl.nreal : 0xffffffffu, P0);
         MI_LAUNCHED(c, "k_accum_level0");
     }
 
@@ -901,8 +932,9 @@ bool g2_second_level(Ctx &c, const MsmPlan &pl, XYZZ<F> *P0, std::vector<XYZZ<F>
 }
 
 template <class F>
-void msm_accumulate_impl(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, XYZZ<F> *result) {
-    XYZZ<F> *P0 = accumulate_chunks<F>(c, pl, bases);
+void msm_accumulate_impl(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, XYZZ<F> *result,
+                         const Affine<F> *bases_hi = nullptr) {
+    XYZZ<F> *P0 = accumulate_chunks<F>(c, pl, bases, bases_hi);
     std::vector<XYZZ<F>> W;
     if (!g2_second_level<F>(c, pl, P0, W)) reduce_windows<F>(c, pl, P0, W);
     const unsigned nwin = pl.nwin, cb = pl.cb;
@@ -917,14 +949,15 @@ void msm_accumulate_impl(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, XYZZ
 
 template <class F>
 void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,
-             XYZZ<F> *result) {
+             XYZZ<F> *result, const Affine<F> *bases_hi = nullptr) {
     ScopedTimer whole(c, sizeof(F) == sizeof(fq_t) ? &c.stats.msm_g1 : &c.stats.msm_g2, n);
     MsmPlan pl;
-    if (!msm_prepare_impl(c, scalars, idx, n, pl)) {
+    const bool split = bases_hi && msm_use_split(n);
+    if (!msm_prepare_impl(c, scalars, idx, n, pl, split)) {
         *result = XYZZ<F>::inf();
         return;
     }
-    msm_accumulate_impl<F>(c, pl, bases, result);
+    msm_accumulate_impl<F>(c, pl, bases, result, split ? bases_hi : nullptr);
 }
 
 }  // namespace mi

@@ -31,6 +31,8 @@ struct Srs {
     unsigned log_d = 0;
     uint64_t n_h = 0, n_l = 0, n_a = 0, n_b = 0, n_ic = 0;
     g1_affine_t *h_perm = nullptr, *l = nullptr, *a = nullptr, *b_g1 = nullptr;
+    // 2^128 multiples of h_perm, l and a: the split-mode MSM tables (msm_g1 bases_hi), built at load
+    g1_affine_t *h_hi = nullptr, *l_hi = nullptr, *a_hi = nullptr;
     g2_affine_t *b_g2 = nullptr;
     g1_affine_t alpha_g1, beta_g1, delta_g1;
     g2_affine_t beta_g2, gamma_g2, delta_g2;

@@ -221,6 +221,15 @@ __global__ void __launch_bounds__(256) k_batch_affine(const XYZZ<F> *__restrict_
     }
 }
 
+// 2^128 * P, XYZZ (128 doublings); batch-normalised by k_batch_affine
+__global__ void __launch_bounds__(256) k_shift128(const g1_affine_t *__restrict__ in, uint64_t n, g1_xyzz_t *__restrict__ out) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    g1_xyzz_t p = xyzz_from_affine(in[i]);
+    for (int k = 0; k < 128; k++) p = xyzz_dbl_inl(p);
+    out[i] = p;
+}
+
 // block-level partial dot products sum z_i * e_i (z canonical -> montgomery on the fly)
 __global__ void k_dot(const fr_t *__restrict__ z, const fr_t *__restrict__ e, uint64_t off, uint64_t n,
                       fr_t *__restrict__ partial) {
@@ -358,7 +367,7 @@ Circuit::~Circuit() {
     if (idx_b) hipFree(idx_b);
 }
 Srs::~Srs() {
-    void *ps[] = {h_perm, l, a, b_g1, b_g2, at, bt, ct};
+    void *ps[] = {h_perm, l, a, b_g1, b_g2, at, bt, ct, h_hi, l_hi, a_hi};
     for (void *p : ps)
         if (p) hipFree(p);
 }
@@ -463,6 +472,10 @@ static A *upload_points(Ctx &c, const uint8_t *bytes, uint64_t n, bool is_g2, bo
     return out;
 }
 
+namespace {
+void build_hi_tables(Ctx &c, Srs &S);
+}
+
 Srs *srs_load(Ctx &c, const Circuit *circ, const SrsHost &h, bool checked) {
     Srs *S = new Srs();
     try {
@@ -501,6 +514,7 @@ Srs *srs_load(Ctx &c, const Circuit *circ, const SrsHost &h, bool checked) {
         S->ic.resize(h.n_ic);
         for (uint64_t i = 0; i < h.n_ic; i++)
             if (!g1_decode_host(h.ic + 96 * i, S->ic[i])) throw std::invalid_argument("bad ic encoding");
+        build_hi_tables(c, *S);
     } catch (...) {
         delete S;
         throw;
@@ -523,6 +537,37 @@ static void fixed_base_affine(Ctx &c, const Affine<F> *table, const fr_t *k_dev,
         MI_HIP(hipGetLastError());
     }
 }
+
+void g1_shift128(Ctx &c, const g1_affine_t *in, uint64_t n, g1_affine_t *out) {
+    const uint64_t chunk = 1ull << 24;
+    g1_xyzz_t *tmp = c.scratch[10].as<g1_xyzz_t>(n < chunk ? (n ? n : 1) : chunk);
+    fq_t *pre = c.scratch[11].as<fq_t>(n < chunk ? (n ? n : 1) : chunk);
+    for (uint64_t o = 0; o < n; o += chunk) {
+        uint64_t m = n - o < chunk ? n - o : chunk;
+        k_shift128<<<grid1(m), 256, 0, c.stream>>>(in + o, m, tmp);
+        constexpr int K = 32;
+        k_batch_affine<fq_t, K><<<grid1((m + K - 1) / K), 256, 0, c.stream>>>(tmp, m, pre, out + o);
+        MI_HIP(hipGetLastError());
+    }
+    MI_HIP(hipStreamSynchronize(c.stream));
+}
+
+namespace {
+// split-mode tables of the three G1 queries whose MSMs run alone (B_G1 shares B_G2's plan, which has
+// no table on the G2 side, so b_g1 gets none)
+void build_hi_tables(Ctx &c, Srs &S) {
+    struct Q {
+        const g1_affine_t *src;
+        uint64_t n;
+        g1_affine_t **dst;
+    } qs[] = {{S.h_perm, S.n_h, &S.h_hi}, {S.l, S.n_l, &S.l_hi}, {S.a, S.n_a, &S.a_hi}};
+    for (auto &q : qs) {
+        if (!q.src || !q.n) continue;
+        *q.dst = dalloc<g1_affine_t>(q.n);
+        g1_shift128(c, q.src, q.n, *q.dst);
+    }
+}
+}  // namespace
 
 Srs *srs_generate(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5]) {
     Srs *S = new Srs();
@@ -680,6 +725,7 @@ Srs *srs_generate(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5]) {
         S->beta_g2 = host_mul_affine(g2, toxic_canonical[2]);
         S->gamma_g2 = host_mul_affine(g2, toxic_canonical[3]);
         S->delta_g2 = host_mul_affine(g2, toxic_canonical[4]);
+        build_hi_tables(c, *S);
     } catch (...) {
         delete S;
         throw;
@@ -733,7 +779,8 @@ ProofSums groth16_sums(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *
                 }();
                 if (b_first) run_b();
                 uint64_t l_lo, l_cnt = slice(circ.n_aux, l_lo);
-                msm_g1(x, srs.l + l_lo, z_dev + circ.n_in + l_lo, nullptr, l_cnt, &Lq);
+                msm_g1(x, srs.l + l_lo, z_dev + circ.n_in + l_lo, nullptr, l_cnt, &Lq,
+                       srs.l_hi ? srs.l_hi + l_lo : nullptr);
                 if (!b_first) run_b();
                 MI_HIP(hipEventRecord(done, x.stream));
             } catch (...) {
@@ -762,8 +809,8 @@ ProofSums groth16_sums(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *
             k_qap_divide<<<grid1(d), 256, 0, st>>>(a, b, cc, d, zinv);
             ntt_dif_coset_epilogue(c, a, L, true, true, dinv, true);  // icoset, canonical H (bit-reversed order)
             uint64_t h_lo, h_cnt = slice(d - 1, h_lo), a_lo, a_cnt = slice(circ.n_a, a_lo);
-            msm_g1(c, srs.h_perm + h_lo, a + h_lo, nullptr, h_cnt, &H);
-            msm_g1(c, srs.a + a_lo, z_dev, circ.idx_a + a_lo, a_cnt, &As);
+            msm_g1(c, srs.h_perm + h_lo, a + h_lo, nullptr, h_cnt, &H, srs.h_hi ? srs.h_hi + h_lo : nullptr);
+            msm_g1(c, srs.a + a_lo, z_dev, circ.idx_a + a_lo, a_cnt, &As, srs.a_hi ? srs.a_hi + a_lo : nullptr);
         } catch (...) {
             err_main = std::current_exception();
         }

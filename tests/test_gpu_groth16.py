@@ -112,6 +112,24 @@ def test_groth16_windowed_sort_vs_oracle(ctx, oracle, monkeypatch):
     assert proof == oproof and raw == oraw
 
 
+@pytest.mark.parametrize("split", ["0", "2"])
+def test_groth16_split_msm_vs_oracle(ctx, oracle, monkeypatch, split):
+    """H, L and A through the split-mode MSM (2^128 base tables, two 128-bit half scalars per point)
+    forced at a size the oracle proves in seconds; "0" is the plain path at the same size."""
+    monkeypatch.setenv("MI_MSM_SPLIT", split)
+    n_in, n_aux, rws, z = circuits.random_circuit(35, 5000, n_in=6, n_free=32)
+    oc, gc = _load(ctx, oracle, n_in, n_aux, rws, z)
+    tox = circuits.toxic(35)
+    pk = fg.generate_random_parameters(ctx, gc, tox)
+    op = oracle.OracleParams(oc, tox)
+    zb = circuits.z_bytes(z)
+    r, s = circuits.blinding(35)
+    assert fg.prove(ctx, pk, gc, zb, r, s) == op.prove(zb, r, s)[0]
+    vk, _ = pk.verifying_key()
+    shares = [fg.prove_share(ctx, pk, gc, zb, k, 3) for k in range(3)]  # latency-mode slices, same path
+    assert fg.assemble(vk, shares, r, s) == op.prove(zb, r, s)[0]
+
+
 def test_prove_batch_and_priority(ctx, oracle):
     n_in, n_aux, rws, z = circuits.random_circuit(41, 300)
     oc, gc = _load(ctx, oracle, n_in, n_aux, rws, z)

@@ -197,3 +197,54 @@ def test_msm_g2_boolean_heavy(ctx, oracle, sort_mode, g2_level2):
     sc = [1 if rng.random() < 0.8 else rng.randrange(R) for _ in range(n)]
     sb = b"".join(s.to_bytes(32, "little") for s in sc)
     assert ctx.msm_g2(bases, sb) == oracle.msm_g2(bases, sb)
+
+
+def _split_scalars(n, seed):
+    """full-width, zero, one, R - 1, 128-bit-only (empty high half) and high-half-only scalars"""
+    rng = np.random.default_rng(seed)
+    w = rng.integers(0, 2**64, size=(n, 4), dtype=np.uint64)
+    w[:, 3] &= np.uint64(0x3FFFFFFFFFFFFFFF)
+    kind = rng.integers(0, 8, size=n)
+    w[kind == 1] = 0
+    w[kind == 2] = np.array([1, 0, 0, 0], dtype=np.uint64)
+    w[kind == 3] = np.frombuffer((R - 1).to_bytes(32, "little"), dtype=np.uint64)
+    w[kind == 4, 2:] = 0
+    w[kind == 5, :2] = 0
+    return w.tobytes()
+
+
+@pytest.mark.parametrize("split", ["0", "2"])
+def test_msm_split_tables_vs_oracle(ctx, oracle, monkeypatch, split):
+    """Split mode (MI_MSM_SPLIT=2 forces it at any size): the l and a queries' MSMs over their 2^128
+    tables, against the oracle's MSM over the same points."""
+    import torch
+
+    monkeypatch.setenv("MI_MSM_SPLIT", split)
+    n_in, n_aux, rws, z = circuits.random_circuit(91, 3000, n_in=6, n_free=32)
+    gc = fg.Circuit(ctx, len(rws), n_in, n_aux, circuits.to_csr(rws))
+    pk = fg.generate_random_parameters(ctx, gc, circuits.toxic())
+    for which in (1, 2):
+        pts, q = pk.points(which), pk.query(which)
+        n = len(q) // 96
+        for seed in (1, 2):
+            sb = _split_scalars(n, 100 * which + seed)
+            sd = torch.from_numpy(np.frombuffer(sb, dtype=np.uint8).copy()).cuda()
+            assert pts.msm_dev(sd.data_ptr(), n) == oracle.msm_g1(q, sb), (which, seed)
+            torch.cuda.synchronize()
+
+
+def test_msm_split_default_2_17(ctx, oracle):
+    """Default selection (split from 2^16 points on) on the l query of a 2^17-row synthetic circuit."""
+    import torch
+
+    from fil_groth16 import synth
+
+    sc = synth.SynthCircuit(log_rows=17, n_in=4, seed=3)
+    gc = sc.load(ctx)
+    pk = fg.generate_random_parameters(ctx, gc, circuits.toxic())
+    pts, q = pk.points(1), pk.query(1)
+    n = len(q) // 96
+    assert n >= 1 << 16
+    sb = _split_scalars(n, 5)
+    sd = torch.from_numpy(np.frombuffer(sb, dtype=np.uint8).copy()).cuda()
+    assert pts.msm_dev(sd.data_ptr(), n) == oracle.msm_g1(q, sb)
