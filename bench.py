@@ -253,8 +253,6 @@ def main():
                     pass
     # secondary (binding) roofline: Fq multiplications per second vs the MAD-issue bound, over the mixed
     # additions the accumulation actually issued (non-zero signed digits, counted by the library)
-    c_bits = fg.msm_window_bits(int(units_per_launch))
-    nwin = (256 + c_bits - 1) // c_bits
     madds_per_launch = dom.get("madds", 0) / max(dom["launches"], 1)
     fq_muls = madds_per_launch * FQ_MUL_PER_MIXED_ADD[grp]
     valu_ach = fq_muls / (avg_ms * 1e-3) if avg_ms > 0 and fq_muls else None
@@ -306,8 +304,9 @@ def main():
             "unit": "Fq-mul/s",
             "frac": valu_ach / valu_peak if valu_ach else None,
             "madds_per_launch": madds_per_launch,
-            "model": f"{FQ_MUL_PER_MIXED_ADD[grp]} Fq-mul per mixed add x mixed adds issued (non-zero digits of "
-                     f"{nwin} windows, c={c_bits}); peak = v_mad_u64_u32 issue rate / {FQ_MUL_MADS} MADs",
+            "model": f"{FQ_MUL_PER_MIXED_ADD[grp]} Fq-mul per mixed add x mixed adds issued (non-zero signed digits "
+                     f"counted by the library; split-mode MSMs: 2n half-scalar points over 6 windows); "
+                     f"peak = v_mad_u64_u32 issue rate / {FQ_MUL_MADS} MADs",
         },
         "cpu_baseline": cpu,
         "timers_ms": {k: round(v["ms"], 3) for k, v in stats.items()},

@@ -46,7 +46,7 @@ void msm_g1_planned(Ctx &c, const MsmPlan &plan, const g1_affine_t *bases, g1_xy
         *result_host = g1_xyzz_t::inf();
         return;
     }
-    ScopedTimer whole(c, &c.stats.msm_g1, plan.n);  // scalar-side phase timed by msm_prepare's caller
+    ScopedTimer whole(c, &c.stats.msm_g1, plan.nreal ? plan.nreal : plan.n);  // scalar-side phase timed by msm_prepare's caller
     msm_accumulate_impl<fq_t>(c, plan, bases, result_host, bases_hi);
 }
 

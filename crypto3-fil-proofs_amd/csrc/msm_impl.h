@@ -735,7 +735,9 @@ XYZZ<F> *accumulate_chunks(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, co
     XYZZ<F> *P0 = c.scratch[10].as<XYZZ<F>>(pl.total);
     (sizeof(F) == sizeof(fq_t) ? c.stats.madds_g1 : c.stats.madds_g2) += pl.entries;
     {
-        ScopedTimer tacc(c, sizeof(F) == sizeof(fq_t) ? &c.stats.accum_g1 : &c.stats.accum_g2, pl.n);
+        // units = input points (the split plan's 2n half-scalar points are n of them)
+        ScopedTimer tacc(c, sizeof(F) == sizeof(fq_t) ? &c.stats.accum_g1 : &c.stats.accum_g2,
+                         pl.nreal ? pl.nreal : pl.n);
         k_accum_level0<F><<<grid_for((uint64_t)pl.total * K, 256), 256, 0, st>>>(pl.order, pl.chunk_bucket, coff, offA, cntA,
                                                                     pl.total, L0, pl.vals_s, bases, bases_hi,
                                                                     pl.nreal ? (uint32_t)pl.nreal : 0xffffffffu, P0);
