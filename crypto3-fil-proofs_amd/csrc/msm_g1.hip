@@ -9,8 +9,8 @@ unsigned msm_window_bits(uint64_t n) { return msm_window_bits_for(n, 256); }
 
 unsigned msm_window_bits_for(uint64_t n, unsigned sbits) {
     // minimise (mixed adds) + 1.4 x (bucket-reduction full adds) over c; split plans (129-bit scalars)
-    // keep c >= 5 so their ceil(129 / c) windows fit the compacted digit kernel (MAXW_C)
-    const unsigned cmin = sbits < 256 ? 5 : 4;
+    // keep c >= 9 so their ceil(129 / c) windows fit the split digit kernel (MAXW_S = 16)
+    const unsigned cmin = sbits < 256 ? 9 : 4;
     unsigned best = cmin;
     double best_cost = 1e300;
     for (unsigned c = cmin; c <= 22; c++) {

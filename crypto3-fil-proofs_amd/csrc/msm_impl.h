@@ -178,6 +178,93 @@ __global__ void __launch_bounds__(256) k_digits_c(const fr_t *__restrict__ scala
     }
 }
 
+// Split plans: one thread per INPUT scalar writes the digits of both 128-bit halves -- point i (low half)
+// and point nreal + i (high half, 2^128-shifted base) -- so the plan costs the same digit work as the
+// plain 12-window one (a thread per half-scalar point measured +2.3 ms per 2^26 MSM).  c >= 9 keeps
+// ceil(129 / c) <= MAXW_S windows.
+constexpr unsigned MAXW_S = 16;
+MI_HD uint32_t word4_of(const uint32_t *v, unsigned k) {
+    uint32_t r = 0;
+    MI_UNROLL for (int j = 0; j < 4; j++) r = (k == (unsigned)j) ? v[j] : r;
+    return r;
+}
+// signed c-bit digits (| neg << 31, 0 = zero digit) of the 128-bit value v[0..3]
+MI_HD void digits128(const uint32_t *v, unsigned c, unsigned nwin, uint32_t *dg) {
+    const uint32_t nbk = 1u << (c - 1), mask = (1u << c) - 1;
+    uint32_t carry = 0;
+    MI_UNROLL for (unsigned w = 0; w < MAXW_S; w++) {
+        dg[w] = 0;
+        if (w < nwin) {
+            unsigned bit = w * c, word = bit >> 5, sh = bit & 31;
+            uint32_t d = 0;
+            if (word < 4) {
+                d = word4_of(v, word) >> sh;
+                if (sh + c > 32 && word + 1 < 4) d |= word4_of(v, word + 1) << (32 - sh);
+            }
+            d = (d & mask) + carry;
+            uint32_t neg = 0;
+            if (d > nbk) {
+                d = (1u << c) - d;
+                neg = 1;
+                carry = 1;
+            } else {
+                carry = 0;
+            }
+            dg[w] = d ? d | (neg << 31) : 0;
+        }
+    }
+}
+__global__ void __launch_bounds__(256) k_digits_split(const fr_t *__restrict__ scalars,
+                                                      const uint32_t *__restrict__ idx, uint32_t nreal, unsigned c,
+                                                      unsigned nwin, uint32_t *__restrict__ wcount,
+                                                      uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+    __shared__ uint32_t wc[4][MAXW_S];
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t n = 2ull * nreal;  // window stride of keys / vals
+    fr_t s = fr_t::zero();
+    if (i < nreal) s = scalars[idx ? idx[i] : i];
+    uint32_t dlo[MAXW_S], dhi[MAXW_S];
+    digits128(s.v, c, nwin, dlo);
+    digits128(s.v + 4, c, nwin, dhi);
+    const uint64_t below = (1ull << lane) - 1;
+    uint32_t rlo[MAXW_S], rhi[MAXW_S];
+    MI_UNROLL for (unsigned w = 0; w < MAXW_S; w++) {
+        rlo[w] = rhi[w] = 0;
+        if (w < nwin) {
+            uint64_t mlo = __ballot(dlo[w] != 0), mhi = __ballot(dhi[w] != 0);
+            uint32_t clo = (uint32_t)__popcll(mlo);
+            rlo[w] = (uint32_t)__popcll(mlo & below);
+            rhi[w] = clo + (uint32_t)__popcll(mhi & below);
+            if (lane == 0) wc[wave][w] = clo + (uint32_t)__popcll(mhi);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < nwin) {
+        const unsigned w = threadIdx.x;
+        uint32_t c0 = wc[0][w], c1 = wc[1][w], c2 = wc[2][w], c3 = wc[3][w];
+        uint32_t base = atomicAdd(&wcount[w], c0 + c1 + c2 + c3);
+        wc[0][w] = base;
+        wc[1][w] = base + c0;
+        wc[2][w] = base + c0 + c1;
+        wc[3][w] = base + c0 + c1 + c2;
+    }
+    __syncthreads();
+    MI_UNROLL for (unsigned w = 0; w < MAXW_S; w++) {
+        if (w < nwin) {
+            const uint64_t o = (uint64_t)w * n + wc[wave][w];
+            if (dlo[w]) {
+                keys[o + rlo[w]] = (dlo[w] & 0x7fffffffu) - 1;
+                vals[o + rlo[w]] = i | (dlo[w] & 0x80000000u);
+            }
+            if (dhi[w]) {
+                keys[o + rhi[w]] = (dhi[w] & 0x7fffffffu) - 1;
+                vals[o + rhi[w]] = (i + nreal) | (dhi[w] & 0x80000000u);
+            }
+        }
+    }
+}
+
 // keys are window-local (sorted per window): global bucket = window * nbk + key.  Four sorted keys
 // per thread (one 16-byte load); the neighbours across the group edge are single loads (L2 hits).
 // zstart[w] = first sorted position of window w holding a zero digit (key nbk sorts last).
@@ -662,9 +749,16 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
         size_t tmp_bytes = 0;
         if (compact) {
             MI_HIP(hipMemsetAsync(wcount, 0, sizeof(uint32_t) * nwin, st));
-            k_digits_c<<<grid_for(n, 256), 256, 0, st>>>(scalars, idx, (uint32_t)n, cb, nwin, (uint32_t)pl.nreal,
-                                                          wcount, keys, vals);
-            MI_LAUNCHED(c, "k_digits_c");
+            if (split) {
+                if (nwin > MAXW_S) throw std::logic_error("msm: split plan with more than MAXW_S windows");
+                k_digits_split<<<grid_for(nscal, 256), 256, 0, st>>>(scalars, idx, (uint32_t)nscal, cb, nwin, wcount,
+                                                                      keys, vals);
+                MI_LAUNCHED(c, "k_digits_split");
+            } else {
+                k_digits_c<<<grid_for(n, 256), 256, 0, st>>>(scalars, idx, (uint32_t)n, cb, nwin, 0u, wcount, keys,
+                                                              vals);
+                MI_LAUNCHED(c, "k_digits_c");
+            }
             MI_HIP(hipMemcpyAsync(wn.data(), wcount, sizeof(uint32_t) * nwin, hipMemcpyDeviceToHost, st));
             MI_HIP(hipStreamSynchronize(st));
             sort_pairs_u32(nullptr, tmp_bytes, keys, keys_s, vals, vals_s, (uint32_t)n, key_bits, st);
