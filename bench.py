@@ -2,20 +2,25 @@
 """bench.py -- BASELINE metric: Groth16 constraints/sec (BLS12-381), plus MSM G1 Mpoints/s at 2^26.
 
 Workload (BASELINE.json configs[2]): "Synthetic 2^26-constraint R1CS full Groth16 prove, 1 x MI355X".
-A step = one full Groth16 prove of that circuit: witness map (R1CS evaluation), 7 NTTs, QAP
-division, 4 G1 MSMs (H, L, A, B_G1) + 1 G2 MSM (B_G2) and proof assembly, proof bytes returned
-to the host.  Inputs (witness, R1CS, proving key) are resident in HBM when the timed region
-starts; the 192-byte proofs of all ranks are gathered to rank 0 over RCCL inside the timed region
-(the MultiProof assembly of api/seal.hpp:306-308).
+A step = one full Groth16 prove of that circuit as the metric defines it ("witness and
+R1CS in host memory, SRS resident on device" -> "192 B proof in host memory"): the witness upload from
+page-locked host memory (overlapped with the previous step's proof, mi_groth16_prove_batch), witness
+map, 7 NTTs, QAP division, 4 G1 MSMs (H, L, A, B_G1) + 1 G2 MSM (B_G2), proof assembly.  The 192-byte
+proofs of all ranks are gathered to rank 0 over RCCL inside the timed region (the MultiProof assembly
+of api/seal.hpp:306-308).  After the timer, every timed proof is pairing-verified (the C2 self-check
+policy, api/seal.hpp:310-313) and the line carries "verified".
 
-Multi-GPU: one process per GPU; each rank proves its own partition every step (PoSt / PoRep
-partitions are independent proofs -- SURVEY.md §8e), so per-GPU work is fixed: weak scaling.
+Multi-GPU: one process per GPU; by default each rank proves its own partition every step (PoSt /
+PoRep partitions are independent proofs -- SURVEY.md 8e), so per-GPU work is fixed: weak scaling.
+--partitions P runs BASELINE config 5's shape instead: every step proves P partitions round-robin over
+the ranks (10 over 8 GPUs: two rounds on ranks 0 and 1) and all-gathers the P x 192-byte multi-proof.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--log-rows 26]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--log-rows 26] [--partitions P]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -37,9 +42,13 @@ FQ_MUL_PER_MIXED_ADD = {"G1": 10, "G2": 28}  # madd-2008-s: 8M + 2S over Fq / Fq
 TOXIC_SEED = 0x5EED
 
 
-def workload_name(log_rows):
+def workload_name(log_rows, partitions=0, world=1):
     cfg = {26: " (BASELINE config 3)", 27: " (BASELINE config 4 shape: 32 GiB PoRep-sized, d = 2^27)"}
-    return f"synthetic 2^{log_rows}-constraint R1CS full Groth16 prove" + cfg.get(log_rows, "")
+    base = f"synthetic 2^{log_rows}-constraint R1CS full Groth16 prove"
+    if partitions:
+        return (f"{partitions}-partition batch of the {base} (BASELINE config 5 shape: partitions "
+                f"round-robin over {world} GPU(s))")
+    return base + cfg.get(log_rows, "")
 
 
 def splitmix_frs(seed, n):
@@ -63,37 +72,75 @@ def log(rank, *a):
         print("[bench]", *a, file=sys.stderr, flush=True)
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(args, fg, synth_mod, ctx):
-    """The oracle (oracle/, a CPU restatement of the same prover) on a bounded sample of the same
-    workload family: a 2^cpu_log_rows-constraint synthetic circuit, params generated on the GPU
-    and exported, witness in host memory -> proof, timed with OpenMP threads = OMP_NUM_THREADS."""
+    """The oracle (oracle/, a CPU restatement of the same prover, OpenMP) on bounded samples of the
+    same workload family: 2^a- and 2^b-constraint synthetic circuits (params generated on the GPU and
+    exported, witness in host memory -> proof).  The rate at the target size is extrapolated from the
+    two samples' measured scaling exponent and labelled as such.  Threads: OMP_NUM_THREADS (the GPU
+    box allots each GPU a 16-CPU share and sets it to 16), else every CPU this process may run on."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    affinity = len(os.sched_getaffinity(0))
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or affinity
     oracle_py.set_threads(threads)
-    sc = synth_mod.SynthCircuit(args.cpu_log_rows, args.n_in, args.seed)
-    circ = sc.load(ctx)
-    pk = fg.generate_random_parameters(ctx, circ, splitmix_frs(TOXIC_SEED, 5))
-    vk, ic = pk.verifying_key()
-    q = dict(h=pk.query(0), l=pk.query(1), a=pk.query(2), b_g1=pk.query(3), b_g2=pk.query(4), vk=vk, ic=ic)
-    oc = oracle_py.OracleCircuit(sc.n, sc.n_in, sc.n_aux, sc.csr())
-    op = oracle_py.OracleParams(oc, queries=q)
-    zb = sc.z_bytes()
-    r, s = splitmix_frs(77, 2)
-    t0 = time.perf_counter()
-    proof_cpu = op.prove(zb, r, s)[0]
-    dt = time.perf_counter() - t0
-    proof_gpu = fg.prove(ctx, pk, circ, zb, r, s)
-    return {
-        "value": sc.n / dt,
+    samples = []
+    for lr in sorted(int(x) for x in str(args.cpu_log_rows).split(",")):
+        sc = synth_mod.SynthCircuit(lr, args.n_in, args.seed)
+        circ = sc.load(ctx)
+        pk = fg.generate_random_parameters(ctx, circ, splitmix_frs(TOXIC_SEED, 5))
+        vk, ic = pk.verifying_key()
+        q = dict(h=pk.query(0), l=pk.query(1), a=pk.query(2), b_g1=pk.query(3), b_g2=pk.query(4), vk=vk, ic=ic)
+        oc = oracle_py.OracleCircuit(sc.n, sc.n_in, sc.n_aux, sc.csr())
+        op = oracle_py.OracleParams(oc, queries=q)
+        zb = sc.z_bytes()
+        r, s = splitmix_frs(77, 2)
+        t0 = time.perf_counter()
+        proof_cpu = op.prove(zb, r, s)[0]
+        dt = time.perf_counter() - t0
+        proof_gpu = fg.prove(ctx, pk, circ, zb, r, s)
+        samples.append({"log_rows": lr, "constraints": sc.n, "seconds": dt, "constraints_per_s": sc.n / dt,
+                        "gpu_proof_bytes_identical": proof_cpu == proof_gpu})
+        del op, oc, q, pk, circ, sc
+    big = samples[-1]
+    out = {
+        "value": big["constraints_per_s"],
         "unit": "constraints/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"oracle prove of the 2^{args.cpu_log_rows}-row synthetic circuit ({sc.n} constraints), "
-                  f"{dt:.2f} s with {threads} OpenMP threads; GPU proof bytes identical: {proof_cpu == proof_gpu}",
-        "seconds": dt,
+        "sample": f"oracle prove of the 2^{big['log_rows']}-row synthetic circuit ({big['constraints']} constraints), "
+                  f"{big['seconds']:.2f} s with {threads} OpenMP threads on {cpu_model()}; GPU proof bytes identical: "
+                  f"{all(x['gpu_proof_bytes_identical'] for x in samples)}",
+        "cpu_model": cpu_model(),
+        "host_cpus": os.cpu_count(),
+        "affinity_cpus": affinity,
+        "samples": samples,
     }
+    if len(samples) >= 2:
+        a, b = samples[-2], samples[-1]
+        alpha = math.log(b["seconds"] / a["seconds"]) / math.log(b["constraints"] / a["constraints"])
+        n_t = (1 << args.log_rows) - args.n_in
+        t_t = b["seconds"] * (n_t / b["constraints"]) ** alpha
+        out["extrapolated"] = {
+            "label": "extrapolated",
+            "log_rows": args.log_rows,
+            "constraints": n_t,
+            "seconds": t_t,
+            "constraints_per_s": n_t / t_t,
+            "model": f"t(n) = t(2^{b['log_rows']}) (n / n_{b['log_rows']})^alpha, alpha = {alpha:.3f} fitted on "
+                     f"the 2^{a['log_rows']} and 2^{b['log_rows']} samples, {threads} threads",
+        }
+    return out
 
 
 def main():
@@ -104,9 +151,14 @@ def main():
     ap.add_argument("--log-rows", type=int, default=26, help="log2 of the evaluation domain (config 3: 26)")
     ap.add_argument("--n-in", type=int, default=4)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--partitions", type=int, default=0,
+                    help="config-5 mode: P partitions per step, round-robin over the ranks (0: one per rank)")
+    ap.add_argument("--params", default=None,
+                    help="load the proving key from a bellman/filecoin params file (mmap) instead of generating it")
     ap.add_argument("--msm-reps", type=int, default=3, help="reps of the standalone 2^log-rows G1 MSM")
-    ap.add_argument("--cpu-log-rows", type=int, default=21)
+    ap.add_argument("--cpu-log-rows", default="21,22", help="oracle sample sizes (comma-separated log2 rows)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-device-resident", action="store_true", help="skip the secondary HBM-resident run")
     ap.add_argument("--stats-json", default=None, help="write per-kernel timers here")
     args = ap.parse_args()
 
@@ -126,6 +178,8 @@ def main():
 
     import fil_groth16 as fg
     from fil_groth16 import synth as synth_mod
+    from fil_groth16.compound import shard_partitions
+    from fil_groth16.distributed import gather_multiproof, prove_partitions
 
     t_setup = time.perf_counter()
     ctx = fg.Context(local_rank)
@@ -133,37 +187,56 @@ def main():
     t_synth = time.perf_counter() - t_setup
     circ = sc.load(ctx)
     t_load = time.perf_counter() - t_setup - t_synth
-    pk = fg.generate_random_parameters(ctx, circ, splitmix_frs(TOXIC_SEED, 5))
+    if args.params:
+        pk = fg.ProvingKey.load_params(ctx, circ, args.params, checked=False)
+    else:
+        pk = fg.generate_random_parameters(ctx, circ, splitmix_frs(TOXIC_SEED, 5))
     ctx.synchronize()
     t_srs = time.perf_counter() - t_setup - t_synth - t_load
-    z = torch.from_numpy(sc.z_array().copy()).to(device)  # witness resident in HBM
-    torch.cuda.synchronize()
+    # the witness in page-locked host memory, where a synthesiser would write it (mi_host_alloc)
+    zhost = fg.HostBuffer(32 * sc.num_vars)
+    np.copyto(zhost.array, sc.z_array())
     n = sc.n
-    log(rank, f"setup: synth {t_synth:.1f}s circuit load {t_load:.1f}s srs gen {t_srs:.1f}s; n={n} d={circ.d} "
-              f"|a|={circ.n_a} |b|={circ.n_b}")
+    vk, ic = pk.verifying_key()
+    pub_inputs = zhost.array[32:32 * sc.n_in].tobytes()
+    log(rank, f"setup: synth {t_synth:.1f}s circuit load {t_load:.1f}s srs {'load' if args.params else 'gen'} "
+              f"{t_srs:.1f}s; n={n} d={circ.d} |a|={circ.n_a} |b|={circ.n_b}")
 
-    blind = splitmix_frs(1000 + rank, 2 * (args.warmup + args.steps))
-    for w in range(args.warmup):
-        fg.prove(ctx, pk, circ, z.data_ptr(), blind[2 * w], blind[2 * w + 1])
+    P = args.partitions
+    mine = shard_partitions(P, rank, world) if P else [rank]
+    per_step = len(mine)
+    blind = splitmix_frs(1000, 2 * (args.warmup + args.steps) * max(P, world))
+
+    def blinding(step, part):
+        i = step * max(P, world) + part
+        return blind[2 * i], blind[2 * i + 1]
+
+    if args.warmup:
+        fg.prove_batch(ctx, pk, circ, [zhost] * (args.warmup * per_step),
+                       [blinding(w, p) for w in range(args.warmup) for p in mine])
     ctx.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     ctx.reset_stats()
 
+    gdev = device if dist else "cpu"
     t0 = time.perf_counter()
-    proofs = []
-    for k in range(args.steps):
-        i = args.warmup + k
-        proofs.append(fg.prove(ctx, pk, circ, z.data_ptr(), blind[2 * i], blind[2 * i + 1]))
-    # MultiProof assembly: gather every rank's 192-byte proofs to rank 0 over RCCL
-    local = torch.from_numpy(np.frombuffer(b"".join(proofs), dtype=np.uint8).copy()).to(device)
-    if dist:
-        bufs = [torch.empty_like(local) for _ in range(world)]
-        dist.all_gather(bufs, local)
-        gathered = torch.cat(bufs).cpu().numpy().tobytes() if rank == 0 else None
+    if P:
+        multiproofs = []
+        for k in range(args.steps):
+            step = args.warmup + k
+            multiproofs.append(prove_partitions(
+                lambda ids: fg.prove_batch(ctx, pk, circ, [zhost] * len(ids), [blinding(step, p) for p in ids]),
+                P, rank, world, gdev))
+        proofs = [mp_[192 * i:192 * (i + 1)] for mp_ in multiproofs for i in range(P)]
     else:
-        gathered = local.cpu().numpy().tobytes()
+        # K partitions of this rank in one batch: partition k + 1's upload overlaps proof k
+        local = fg.prove_batch(ctx, pk, circ, [zhost] * args.steps,
+                               [blinding(args.warmup + k, rank) for k in range(args.steps)])
+        # MultiProof assembly: every rank's proofs gathered in (step, rank) order over RCCL
+        proofs = gather_multiproof(local, args.steps * world, rank, world, gdev) if dist else b"".join(local)
+        proofs = [proofs[192 * i:192 * (i + 1)] for i in range(len(proofs) // 192)]
     ctx.synchronize()
     if dist:
         dist.barrier()
@@ -174,6 +247,30 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     stats = ctx.stats()
+    proofs_total = args.steps * (P if P else world)
+
+    # the C2 self-check policy (api/seal.hpp:310-313), outside the timer: every gathered proof is
+    # pairing-verified (one batch multi-pairing with OS-random weights) and the last one singly
+    t_ver = time.perf_counter()
+    verified = bool(fg.verify_batch(vk, ic, [pub_inputs] * len(proofs), proofs)) and \
+        bool(fg.verify(vk, ic, pub_inputs, proofs[-1]))
+    t_ver = time.perf_counter() - t_ver
+
+    # secondary: the same proof with the witness already resident in HBM (no upload)
+    resident = None
+    if not args.no_device_resident:
+        zdev = torch.from_numpy(sc.z_array().copy()).to(device)
+        k2 = max(2, args.steps // 4)
+        fg.prove(ctx, pk, circ, zdev.data_ptr(), *blinding(0, 0))
+        ctx.synchronize()
+        tr = time.perf_counter()
+        for k in range(k2):
+            fg.prove(ctx, pk, circ, zdev.data_ptr(), *blinding(k, 0))
+        ctx.synchronize()
+        tr = (time.perf_counter() - tr) / k2
+        resident = {"value": n / tr, "unit": "constraints/s", "ms_per_proof": tr * 1e3, "proofs": k2,
+                    "note": "witness resident in HBM before the timer (no H2D): the round-1 definition"}
+        del zdev
 
     # secondary metric: standalone G1 MSM over the resident 2^log_rows - 1 h-query points
     msm_n = pk.n_h
@@ -212,7 +309,7 @@ def main():
                  "msm_g1_2e20_ms": t20 * 1e3, "msm_g1_2e20_mpoints_per_s": m20 / t20 / 1e6,
                  "ntt_fr_2e20_ms": n20 * 1e3, "ntt_fr_2e20_melems_per_s": m20 / n20 / 1e6}
         del x
-    del sc_dev
+    del sc_dev, pts
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -257,8 +354,8 @@ def main():
     fq_muls = madds_per_launch * FQ_MUL_PER_MIXED_ADD[grp]
     valu_ach = fq_muls / (avg_ms * 1e-3) if avg_ms > 0 and fq_muls else None
     valu_peak = MAD_RATE / FQ_MUL_MADS
-    total_steps = args.steps * world
-    value = n * total_steps / dt
+    value = n * proofs_total / dt
+    h2d = stats["h2d"]
     out = {
         "metric": "Groth16 constraints/sec (BLS12-381); MSM G1 Mpoints/s at 2^26",
         "value": value,
@@ -271,12 +368,20 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32 limbs (Fq 381-bit / Fr 255-bit Montgomery)",
-        "data": "synthetic R1CS + satisfying witness (csrc/synth.hip), proving key generated on device from "
-                "fixed toxic waste",
-        "config": {"workload": workload_name(args.log_rows),
+        "data": "synthetic R1CS + satisfying witness (csrc/synth.hip) in page-locked host memory, proving key "
+                + ("loaded from " + args.params if args.params else "generated on device from fixed toxic waste"),
+        "config": {"workload": workload_name(args.log_rows, P, world),
                    "constraints": n, "domain": circ.d, "num_inputs": sc.n_in, "num_aux": sc.n_aux,
-                   "a_query": circ.n_a, "b_query": circ.n_b, "proofs_per_step": world,
+                   "a_query": circ.n_a, "b_query": circ.n_b, "proofs_per_step": P if P else world,
+                   "partitions_per_rank": per_step,
                    "parallelism": f"partition-sharded x{world}"},
+        "verified": verified,
+        "verified_proofs": len(proofs),
+        "verify_s": t_ver,
+        "witness": "host (pinned), H2D of partition k + 1 overlapped with proof k",
+        "h2d": {"ms_per_proof": h2d["ms"] / max(h2d["launches"], 1),
+                "gb_per_s": h2d["units"] / max(h2d["ms"], 1e-9) / 1e6, "bytes_per_proof": 32 * sc.num_vars},
+        "device_resident": resident,
         "msm_g1_mpoints_per_s": msm_n / msm_dt / 1e6,
         "msm_g1_points": msm_n,
         "config2_micro": micro,
@@ -288,8 +393,8 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS if achieved else None,
             "traffic": traffic,
-            "traffic_source": f"profiles/{traffic_src} (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, per point x "
-                              f"points per launch)" if traffic_src else None,
+            "traffic_source": f"profiles/{traffic_src} (FETCH_SIZE + WRITE_SIZE per point x points per launch; "
+                              f"see the summary for the gfx950 correction applied)" if traffic_src else None,
             "avg_launch_ms": avg_ms,
             "units_per_launch": units_per_launch,
             "algorithmic_bytes_per_unit": bytes_per_unit,
@@ -310,12 +415,14 @@ def main():
         },
         "cpu_baseline": cpu,
         "timers_ms": {k: round(v["ms"], 3) for k, v in stats.items()},
-        "setup_s": {"synth": t_synth, "circuit_load": t_load, "srs_generate": t_srs},
-        "multiproof_bytes": len(gathered),
+        "setup_s": {"synth": t_synth, "circuit_load": t_load, "srs": t_srs},
+        "multiproof_bytes": 192 * len(proofs),
         "msm_reps": args.msm_reps,
     }
     if cpu and cpu.get("value"):
         out["gpu_over_cpu"] = value / cpu["value"]
+        if cpu.get("extrapolated"):
+            out["gpu_over_cpu_extrapolated_same_size"] = value / cpu["extrapolated"]["constraints_per_s"]
     if args.stats_json:
         with open(args.stats_json, "w") as f:
             json.dump(stats, f, indent=1)

@@ -9,13 +9,46 @@
 #include <unistd.h>
 
 #include <string>
+#include <thread>
 
 #include "../../include/mi355x_groth16.h"
 #include "prover.h"
 
+// Witness uploads (host z -> HBM) run on their own stream into one of two device slots, so the copy
+// of partition k + 1 overlaps the proof of partition k (mi_groth16_prove_batch).  Pinned witnesses
+// (mi_host_alloc, or memory the caller registered) go up in one DMA; pageable ones through two pinned
+// staging buffers.  Each upload is followed on the same stream by the canonical-Fr check of its entries.
+struct WitnessUploader {
+    static constexpr uint64_t STAGE = 64ull << 20;
+    hipStream_t copy = nullptr;
+    int *flags_host = nullptr;  // pinned: [slot] = entries >= r
+    int *flags_dev = nullptr;
+    hipEvent_t done[2] = {nullptr, nullptr}, t0[2] = {nullptr, nullptr};
+    uint8_t *stage[2] = {nullptr, nullptr};
+    hipEvent_t stage_free[2] = {nullptr, nullptr};
+    void release() {
+        if (copy) hipStreamSynchronize(copy);
+        for (int k = 0; k < 2; k++) {
+            if (done[k]) hipEventDestroy(done[k]);
+            if (t0[k]) hipEventDestroy(t0[k]);
+            if (stage_free[k]) hipEventDestroy(stage_free[k]);
+            if (stage[k]) hipHostFree(stage[k]);
+            done[k] = t0[k] = stage_free[k] = nullptr;
+            stage[k] = nullptr;
+        }
+        if (flags_host) hipHostFree(flags_host);
+        if (flags_dev) hipFree(flags_dev);
+        if (copy) hipStreamDestroy(copy);
+        flags_host = nullptr;
+        flags_dev = nullptr;
+        copy = nullptr;
+    }
+};
+
 struct mi_ctx {
     mi::Ctx c;
     hipStream_t normal = nullptr, high = nullptr;
+    WitnessUploader up;
 };
 struct mi_circuit {
     mi::Circuit *p;
@@ -160,7 +193,7 @@ mi::fr_t fr_checked(const uint8_t *b) {
     return x;
 }
 
-// upload z (host) to a device scratch buffer and reduce it mod r
+// upload z (host) to a device scratch buffer and reduce it mod r (building blocks: MSM scalars, NTT data)
 mi::fr_t *upload_fr(mi::Ctx &c, int slot, const uint8_t *bytes, uint64_t n) {
     mi::fr_t *d = c.scratch[slot].as<mi::fr_t>(n ? n : 1);
     if (n) {
@@ -169,6 +202,100 @@ mi::fr_t *upload_fr(mi::Ctx &c, int slot, const uint8_t *bytes, uint64_t n) {
     }
     return d;
 }
+
+WitnessUploader &uploader(mi_ctx *ctx) {
+    WitnessUploader &u = ctx->up;
+    if (!u.copy) {
+        try {
+            MI_HIP(hipStreamCreateWithFlags(&u.copy, hipStreamNonBlocking));
+            MI_HIP(hipHostMalloc((void **)&u.flags_host, 2 * sizeof(int), hipHostMallocDefault));
+            MI_HIP(hipMalloc((void **)&u.flags_dev, 2 * sizeof(int)));
+            for (int k = 0; k < 2; k++) {
+                MI_HIP(hipEventCreate(&u.done[k]));
+                MI_HIP(hipEventCreate(&u.t0[k]));
+                MI_HIP(hipEventCreateWithFlags(&u.stage_free[k], hipEventDisableTiming));
+            }
+        } catch (...) {
+            u.release();
+            throw;
+        }
+    }
+    return u;
+}
+
+bool is_pinned(const void *p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory: clear the error the query recorded
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+// Witness slot k (0 / 1) lives in ctx scratch 21 + k.  Queues the H2D copy of z and the canonical check
+// on the copy stream and records done[k]; pageable inputs are staged by the calling thread.
+mi::fr_t *witness_upload(mi_ctx *ctx, int k, const uint8_t *z, uint64_t n) {
+    WitnessUploader &u = uploader(ctx);
+    mi::Ctx &c = ctx->c;
+    mi::fr_t *d = c.scratch[21 + k].as<mi::fr_t>(n ? n : 1);
+    const uint64_t bytes = 32 * n;
+    MI_HIP(hipEventRecord(u.t0[k], u.copy));
+    MI_HIP(hipMemsetAsync(u.flags_dev + k, 0, sizeof(int), u.copy));
+    if (bytes && is_pinned(z)) {
+        MI_HIP(hipMemcpyAsync(d, z, bytes, hipMemcpyHostToDevice, u.copy));
+    } else if (bytes) {
+        for (int b = 0; b < 2; b++)
+            if (!u.stage[b]) MI_HIP(hipHostMalloc((void **)&u.stage[b], WitnessUploader::STAGE, hipHostMallocDefault));
+        uint64_t i = 0;
+        for (uint64_t o = 0; o < bytes; o += WitnessUploader::STAGE, i++) {
+            const uint64_t m = bytes - o < WitnessUploader::STAGE ? bytes - o : WitnessUploader::STAGE;
+            const int b = (int)(i & 1);
+            if (i >= 2) MI_HIP(hipEventSynchronize(u.stage_free[b]));  // its previous DMA has drained
+            memcpy(u.stage[b], z + o, m);
+            MI_HIP(hipMemcpyAsync((uint8_t *)d + o, u.stage[b], m, hipMemcpyHostToDevice, u.copy));
+            MI_HIP(hipEventRecord(u.stage_free[b], u.copy));
+        }
+    }
+    mi::fr_count_noncanonical(c, d, n, u.flags_dev + k, u.copy);
+    MI_HIP(hipMemcpyAsync(u.flags_host + k, u.flags_dev + k, sizeof(int), hipMemcpyDeviceToHost, u.copy));
+    MI_HIP(hipEventRecord(u.done[k], u.copy));
+    return d;
+}
+
+// Waits for slot k's upload (the proof before it has normally hidden it), books its time, refuses a
+// witness holding non-canonical entries (MI_ERR_ARG: an Fr32 "MUST represent a valid Fr",
+// core/fr32.hpp:36-40) and orders the ctx stream after the copy.
+void witness_ready(mi_ctx *ctx, int k, uint64_t n) {
+    WitnessUploader &u = ctx->up;
+    MI_HIP(hipEventSynchronize(u.done[k]));
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, u.t0[k], u.done[k]) == hipSuccess) {
+        ctx->c.stats.h2d.ms += ms;
+        ctx->c.stats.h2d.launches += 1;
+        ctx->c.stats.h2d.units += 32 * n;
+    }
+    if (u.flags_host[k])
+        throw std::invalid_argument("witness entry is not a canonical Fr element (>= r): " +
+                                    std::to_string(u.flags_host[k]) + " of " + std::to_string(n));
+    MI_HIP(hipStreamWaitEvent(ctx->c.stream, u.done[k], 0));
+}
+
+// Device-resident witness: the same check on the ctx stream; read after the proof's final sync.
+struct DevWitnessCheck {
+    mi_ctx *ctx;
+    DevWitnessCheck(mi_ctx *x, const mi::fr_t *z, uint64_t n) : ctx(x) {
+        WitnessUploader &u = uploader(x);
+        MI_HIP(hipMemsetAsync(u.flags_dev, 0, sizeof(int), x->c.stream));
+        mi::fr_count_noncanonical(x->c, z, n, u.flags_dev, x->c.stream);
+        MI_HIP(hipMemcpyAsync(u.flags_host, u.flags_dev, sizeof(int), hipMemcpyDeviceToHost, x->c.stream));
+    }
+    void verdict(uint64_t n) {
+        MI_HIP(hipStreamSynchronize(ctx->c.stream));
+        if (ctx->up.flags_host[0])
+            throw std::invalid_argument("witness entry is not a canonical Fr element (>= r): " +
+                                        std::to_string(ctx->up.flags_host[0]) + " of " + std::to_string(n));
+    }
+};
 
 }  // namespace
 
@@ -218,6 +345,7 @@ void mi_ctx_destroy(mi_ctx *ctx) {
     if (!ctx) return;
     hipSetDevice(ctx->c.device);
     hipDeviceSynchronize();
+    ctx->up.release();
     mi::ntt_free_tables(ctx->c);
     mi::ctx_aux_free(ctx->c);
     for (auto &b : ctx->c.scratch) b.release();
@@ -241,6 +369,19 @@ int mi_ctx_synchronize(mi_ctx *ctx) {
         MI_HIP(hipStreamSynchronize(ctx->high));
         ctx->c.timer.resolve();
     });
+}
+
+int mi_host_alloc(uint64_t bytes, void **out) {
+    return guard([&] {
+        need(out != nullptr, "null out");
+        *out = nullptr;
+        need(bytes > 0, "zero-byte host allocation");
+        MI_HIP(hipHostMalloc(out, bytes, hipHostMallocDefault));
+    });
+}
+
+void mi_host_free(void *p) {
+    if (p) hipHostFree(p);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -404,7 +545,8 @@ int mi_groth16_prove(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circ, con
         need(ctx && srs && circ && z && r && s && proof, "null argument");
         CtxLock l(ctx, priority);
         uint64_t nv = circ->p->n_in + circ->p->n_aux;
-        mi::fr_t *zd = upload_fr(ctx->c, 21, z, nv);
+        mi::fr_t *zd = witness_upload(ctx, 0, z, nv);
+        witness_ready(ctx, 0, nv);
         prove_impl(ctx, srs, circ, zd, r, s, proof, raw);
     });
 }
@@ -414,7 +556,13 @@ int mi_groth16_prove_dev(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circ,
     return guard([&] {
         need(ctx && srs && circ && z_dev && r && s && proof, "null argument");
         CtxLock l(ctx, priority);
-        prove_impl(ctx, srs, circ, (const mi::fr_t *)z_dev, r, s, proof, raw);
+        uint64_t nv = circ->p->n_in + circ->p->n_aux;
+        DevWitnessCheck chk(ctx, (const mi::fr_t *)z_dev, nv);
+        uint8_t p[MI_PROOF_BYTES], w[384];
+        prove_impl(ctx, srs, circ, (const mi::fr_t *)z_dev, r, s, p, raw ? w : nullptr);
+        chk.verdict(nv);
+        memcpy(proof, p, MI_PROOF_BYTES);
+        if (raw) memcpy(raw, w, 384);
     });
 }
 
@@ -422,12 +570,37 @@ int mi_groth16_prove_batch(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *cir
                            const uint8_t *const *z, const uint8_t *rs, int priority, uint8_t *proofs_out) {
     return guard([&] {
         need(ctx && srs && circ && z && rs && proofs_out, "null argument");
+        for (uint64_t k = 0; k < count; k++) need(z[k] != nullptr, "null witness");
         CtxLock l(ctx, priority);
         uint64_t nv = circ->p->n_in + circ->p->n_aux;
+        // partition k + 1's upload (and, for pageable witnesses, its host staging on a helper thread)
+        // runs while partition k is proven; witness_ready(k) then finds it finished
+        mi::fr_t *zd[2] = {witness_upload(ctx, 0, z[0], nv), nullptr};
         for (uint64_t k = 0; k < count; k++) {
-            need(z[k] != nullptr, "null witness");
-            mi::fr_t *zd = upload_fr(ctx->c, 21, z[k], nv);
-            prove_impl(ctx, srs, circ, zd, rs + 64 * k, rs + 64 * k + 32, proofs_out + 192 * k, nullptr);
+            const int slot = (int)(k & 1);
+            witness_ready(ctx, slot, nv);
+            std::thread next;
+            std::exception_ptr up_err;
+            if (k + 1 < count) {
+                const int ns = slot ^ 1;
+                const uint8_t *zn = z[k + 1];
+                next = std::thread([&, ns, zn] {
+                    try {
+                        MI_HIP(hipSetDevice(ctx->c.device));
+                        zd[ns] = witness_upload(ctx, ns, zn, nv);
+                    } catch (...) {
+                        up_err = std::current_exception();
+                    }
+                });
+            }
+            try {
+                prove_impl(ctx, srs, circ, zd[slot], rs + 64 * k, rs + 64 * k + 32, proofs_out + 192 * k, nullptr);
+            } catch (...) {
+                if (next.joinable()) next.join();
+                throw;
+            }
+            if (next.joinable()) next.join();
+            if (up_err) std::rethrow_exception(up_err);
         }
     });
 }
@@ -444,7 +617,9 @@ int mi_groth16_prove_share(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *cir
         need(ctx && srs && circ && z && share, "null argument");
         CtxLock l(ctx, priority);
         uint64_t nv = circ->p->n_in + circ->p->n_aux;
-        share_impl(ctx, srs, circ, upload_fr(ctx->c, 21, z, nv), rank, world, share);
+        mi::fr_t *zd = witness_upload(ctx, 0, z, nv);
+        witness_ready(ctx, 0, nv);
+        share_impl(ctx, srs, circ, zd, rank, world, share);
     });
 }
 
@@ -453,7 +628,12 @@ int mi_groth16_prove_share_dev(mi_ctx *ctx, const mi_srs *srs, const mi_circuit 
     return guard([&] {
         need(ctx && srs && circ && z_dev && share, "null argument");
         CtxLock l(ctx, priority);
-        share_impl(ctx, srs, circ, (const mi::fr_t *)z_dev, rank, world, share);
+        uint64_t nv = circ->p->n_in + circ->p->n_aux;
+        DevWitnessCheck chk(ctx, (const mi::fr_t *)z_dev, nv);
+        uint8_t sh[MI_SHARE_BYTES];
+        share_impl(ctx, srs, circ, (const mi::fr_t *)z_dev, rank, world, sh);
+        chk.verdict(nv);
+        memcpy(share, sh, MI_SHARE_BYTES);
     });
 }
 
@@ -485,7 +665,7 @@ static mi_points *points_upload(mi_ctx *ctx, const uint8_t *bytes, uint64_t n, b
     void *dev = nullptr;
     MI_HIP(hipMalloc(&dev, dsz * (n ? n : 1)));
     int *bad = c.scratch[9].as<int>(4);
-    MI_HIP(hipMemsetAsync(bad, 0, sizeof(int), c.stream));
+    MI_HIP(hipMemsetAsync(bad, 0, 3 * sizeof(int), c.stream));
     const uint64_t chunk = 1ull << 22;
     uint8_t *stage = c.scratch[0].as<uint8_t>(esz * (n < chunk ? (n ? n : 1) : chunk));
     for (uint64_t o = 0; o < n; o += chunk) {
@@ -501,7 +681,7 @@ static mi_points *points_upload(mi_ctx *ctx, const uint8_t *bytes, uint64_t n, b
     MI_HIP(hipStreamSynchronize(c.stream));
     if (nbad) {
         hipFree(dev);
-        throw std::invalid_argument("point encoding invalid (non-canonical or not on curve)");
+        throw std::invalid_argument("point encoding invalid (flags, non-canonical or not on curve)");
     }
     return new mi_points{dev, n, g2 ? 1 : 0, 1};
 }
@@ -643,7 +823,7 @@ int mi_ntt_fr(mi_ctx *ctx, uint8_t *data32, unsigned log_n, int inverse, int cos
 }
 
 // ------------------------------------------------------------------------------------------
-int mi_ctx_get_stats(mi_ctx *ctx, double out[21]) {
+int mi_ctx_get_stats(mi_ctx *ctx, double out[24]) {
     return guard([&] {
         need(ctx && out, "null argument");
         CtxLock l(ctx);
@@ -651,8 +831,8 @@ int mi_ctx_get_stats(mi_ctx *ctx, double out[21]) {
         MI_HIP(hipStreamSynchronize(ctx->high));
         ctx->c.timer.resolve();
         const mi::Stats &s = ctx->c.stats;
-        const mi::KStat *ks[7] = {&s.accum_g1, &s.accum_g2, &s.msm_g1, &s.msm_g2, &s.sort, &s.ntt, &s.prove};
-        for (int i = 0; i < 7; i++) {
+        const mi::KStat *ks[8] = {&s.accum_g1, &s.accum_g2, &s.msm_g1, &s.msm_g2, &s.sort, &s.ntt, &s.prove, &s.h2d};
+        for (int i = 0; i < 8; i++) {
             out[3 * i] = ks[i]->ms;
             out[3 * i + 1] = (double)ks[i]->launches;
             out[3 * i + 2] = (double)ks[i]->units;
@@ -665,6 +845,7 @@ int mi_ctx_reset_stats(mi_ctx *ctx) {
         CtxLock l(ctx);
         MI_HIP(hipStreamSynchronize(ctx->normal));
         MI_HIP(hipStreamSynchronize(ctx->high));
+        if (ctx->up.copy) MI_HIP(hipStreamSynchronize(ctx->up.copy));
         ctx->c.timer.resolve();
         ctx->c.stats = mi::Stats();
     });
@@ -690,9 +871,20 @@ int mi_groth16_verify(const uint8_t *vk, const uint8_t *ic, uint64_t n_ic, const
 }
 
 int mi_groth16_verify_batch(const uint8_t *vk, const uint8_t *ic, uint64_t n_ic, uint64_t count,
-                            const uint8_t *inputs, const uint8_t *proofs, const uint8_t *seed32, int *valid) {
+                            const uint8_t *inputs, const uint8_t *proofs, int *valid) {
     return guard([&] {
         need(vk && ic && valid && (count == 0 || proofs) && (count == 0 || n_ic <= 1 || inputs), "null argument");
+        *valid = 0;
+        *valid = mi::groth16_verify_batch(vk, ic, n_ic, count, inputs, proofs, nullptr) ? 1 : 0;
+    });
+}
+
+int mi_groth16_verify_batch_seeded(const uint8_t *vk, const uint8_t *ic, uint64_t n_ic, uint64_t count,
+                                   const uint8_t *inputs, const uint8_t *proofs, const uint8_t seed32[32],
+                                   int *valid) {
+    return guard([&] {
+        need(vk && ic && valid && seed32 && (count == 0 || proofs) && (count == 0 || n_ic <= 1 || inputs),
+             "null argument");
         *valid = 0;
         *valid = mi::groth16_verify_batch(vk, ic, n_ic, count, inputs, proofs, seed32) ? 1 : 0;
     });

@@ -80,13 +80,14 @@ struct Stats {
     KStat sort;                // digit extraction + radix sort + bucket bounds
     KStat ntt;                 // NTT passes (all launches of one transform)
     KStat prove;               // whole Groth16 prove (device part through host assembly)
+    KStat h2d;                 // witness upload + canonical check on the copy stream (units = bytes)
     uint64_t madds_g1 = 0, madds_g2 = 0;  // mixed additions issued by k_accum_level0 (non-zero digits)
     void merge(const Stats &o) {
         madds_g1 += o.madds_g1;
         madds_g2 += o.madds_g2;
-        KStat *d[] = {&accum_g1, &accum_g2, &msm_g1, &msm_g2, &sort, &ntt, &prove};
-        const KStat *x[] = {&o.accum_g1, &o.accum_g2, &o.msm_g1, &o.msm_g2, &o.sort, &o.ntt, &o.prove};
-        for (int i = 0; i < 7; i++) {
+        KStat *d[] = {&accum_g1, &accum_g2, &msm_g1, &msm_g2, &sort, &ntt, &prove, &h2d};
+        const KStat *x[] = {&o.accum_g1, &o.accum_g2, &o.msm_g1, &o.msm_g2, &o.sort, &o.ntt, &o.prove, &o.h2d};
+        for (int i = 0; i < 8; i++) {
             d[i]->ms += x[i]->ms;
             d[i]->launches += x[i]->launches;
             d[i]->units += x[i]->units;
@@ -145,7 +146,8 @@ struct Ctx {
     hipStream_t stream = nullptr;
     std::recursive_mutex mu;
     NttTables tw;
-    DevBuf scratch[24];  // 0-19: MSM / NTT / upload temporaries (18-19: G2 second level), 20-21: prover vectors
+    DevBuf scratch[24];  // 0-19: MSM / NTT / upload temporaries (18-19: G2 second level), 20: prover vectors,
+                         // 21-22: witness slots (capi.hip uploader; 21 also building-block inputs)
     Stats stats;
     EventTimer timer;
     // Auxiliary lane: a second stream with its own scratch arena and timers, driven from a second
@@ -253,9 +255,17 @@ unsigned msm_window_bits(uint64_t n);
 unsigned msm_window_bits_for(uint64_t n, unsigned sbits);
 
 // ---- encodings (encode.hip) ----
-// zcash uncompressed big-endian -> device Montgomery affine; returns count of invalid points
-void g1_decode_uncompressed(Ctx &c, const uint8_t *dev_bytes, g1_affine_t *out, uint64_t n, int *bad_dev);
-void g2_decode_uncompressed(Ctx &c, const uint8_t *dev_bytes, g2_affine_t *out, uint64_t n, int *bad_dev);
+// zcash uncompressed big-endian -> device Montgomery affine (zcash from_uncompressed flag rules).
+// bad_dev[0] += malformed / non-canonical / off-curve points; with reject_inf, bad_dev[1] += infinities
+void g1_decode_uncompressed(Ctx &c, const uint8_t *dev_bytes, g1_affine_t *out, uint64_t n, int *bad_dev,
+                            bool reject_inf = false);
+void g2_decode_uncompressed(Ctx &c, const uint8_t *dev_bytes, g2_affine_t *out, uint64_t n, int *bad_dev,
+                            bool reject_inf = false);
+// bad_dev[2] += points P with r P != O (the checked load's subgroup test)
+void g1_subgroup_check(Ctx &c, const g1_affine_t *pts, uint64_t n, int *bad_dev);
+void g2_subgroup_check(Ctx &c, const g2_affine_t *pts, uint64_t n, int *bad_dev);
+// *bad_dev += entries >= r (witness validation: an Fr32 must represent a valid Fr, core/fr32.hpp:36-40)
+void fr_count_noncanonical(Ctx &c, const fr_t *d, uint64_t n, int *bad_dev, hipStream_t st);
 // device affine -> zcash uncompressed bytes (device buffer); perm_log != 0 un-bit-reverses the source
 void g1_encode_uncompressed(Ctx &c, const g1_affine_t *in, uint8_t *dev_out, uint64_t n, unsigned perm_log);
 void g2_encode_uncompressed(Ctx &c, const g2_affine_t *in, uint8_t *dev_out, uint64_t n);

@@ -180,4 +180,21 @@ typedef Affine<fq2_t> g2_affine_t;
 typedef XYZZ<fq_t> g1_xyzz_t;
 typedef XYZZ<fq2_t> g2_xyzz_t;
 
+// y^2 = x^3 + 4 (G1) and y^2 = x^3 + 4 (u + 1) (G2); the affine infinity (0, 0) is not on the curve,
+// callers handle it by its flag
+MI_HD bool g1_on_curve(const g1_affine_t &a) { return sqr(a.y) == sqr(a.x) * a.x + fq_small(4); }
+MI_HD bool g2_on_curve(const g2_affine_t &a) {
+    const fq2_t b = {fq_small(4), fq_small(4)};
+    return sqr(a.y) == sqr(a.x) * a.x + b;
+}
+// r * a == O: membership in the prime-order subgroup, the check zcash/bellman's checked
+// from_uncompressed adds to the curve equation (Parameters::read with checked = true)
+template <class F>
+MI_HD bool in_prime_subgroup(const Affine<F> &a) {
+    if (a.is_inf()) return true;
+    uint32_t r[8];
+    MI_UNROLL for (int i = 0; i < 8; i++) r[i] = FrDesc::MOD[i];
+    return xyzz_mul_inl(xyzz_from_affine(a), r, 8).is_inf();
+}
+
 }  // namespace mi

@@ -32,45 +32,73 @@ __device__ __forceinline__ bool fq_from_be48(const uint8_t *p, bool mask_flags, 
     return !geq_raw(raw, fq32_t::modulus_raw());
 }
 
-__device__ bool g1_on_curve(const g1_affine_t &a) {
-    fq_t four = fq_small(4);
-    return sqr(a.y) == sqr(a.x) * a.x + four;
-}
-__device__ bool g2_on_curve(const g2_affine_t &a) {
-    fq_t four = fq_small(4);
-    fq2_t b = {four, four};
-    return sqr(a.y) == sqr(a.x) * a.x + b;
+// zcash/bellman from_uncompressed flag rules for byte 0 of an uncompressed point: the compression
+// bit (0x80) is clear; infinity (0x40) has every other bit of the encoding zero; otherwise the sort
+// bit (0x20) is clear.  Returns 0 = finite point, 1 = valid infinity, -1 = malformed.
+__device__ __forceinline__ int uncompressed_flags(const uint8_t *p, int len) {
+    const uint8_t f = p[0];
+    if (f & 0x80) return -1;
+    if (f & 0x40) {
+        uint32_t any = f & 0x3f;
+        for (int k = 1; k < len; k++) any |= p[k];
+        return any ? -1 : 1;
+    }
+    return (f & 0x20) ? -1 : 0;
 }
 
+// bad[0]: malformed / non-canonical / off-curve points, bad[1]: infinities when reject_inf (bellman's
+// Parameters::read refuses the identity in every query: "point at infinity")
 __global__ void k_g1_decode(const uint8_t *__restrict__ in, g1_affine_t *__restrict__ out, uint64_t n,
-                            int *__restrict__ bad) {
+                            int *__restrict__ bad, int reject_inf) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint8_t *p = in + 96 * i;
-    if (p[0] & 0x40) {
+    const int f = uncompressed_flags(p, 96);
+    if (f != 0) {
+        if (f < 0) atomicAdd(&bad[0], 1);
+        else if (reject_inf) atomicAdd(&bad[1], 1);
         out[i] = g1_affine_t::inf();
         return;
     }
     g1_affine_t a;
     bool ok = fq_from_be48(p, true, a.x) & fq_from_be48(p + 48, false, a.y);
-    if (!ok || !g1_on_curve(a)) atomicAdd(bad, 1);
+    if (!ok || !g1_on_curve(a)) atomicAdd(&bad[0], 1);
     out[i] = a;
 }
 
 __global__ void k_g2_decode(const uint8_t *__restrict__ in, g2_affine_t *__restrict__ out, uint64_t n,
-                            int *__restrict__ bad) {
+                            int *__restrict__ bad, int reject_inf) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint8_t *p = in + 192 * i;
-    if (p[0] & 0x40) {
+    const int f = uncompressed_flags(p, 192);
+    if (f != 0) {
+        if (f < 0) atomicAdd(&bad[0], 1);
+        else if (reject_inf) atomicAdd(&bad[1], 1);
         out[i] = g2_affine_t::inf();
         return;
     }
     g2_affine_t a;
     bool ok = fq_from_be48(p, true, a.x.c1) & fq_from_be48(p + 48, false, a.x.c0) &
               fq_from_be48(p + 96, false, a.y.c1) & fq_from_be48(p + 144, false, a.y.c0);
-    if (!ok || !g2_on_curve(a)) atomicAdd(bad, 1);
+    if (!ok || !g2_on_curve(a)) atomicAdd(&bad[0], 1);
     out[i] = a;
+}
+
+// r * P == O for every decoded point (the checked load); bad[2] counts points outside the subgroup
+template <class F>
+__global__ void __launch_bounds__(256) k_subgroup(const Affine<F> *__restrict__ pts, uint64_t n,
+                                                  int *__restrict__ bad) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (!in_prime_subgroup(pts[i])) atomicAdd(&bad[2], 1);
+}
+
+// entries >= r (not a valid Fr: core/fr32.hpp:36-40) -> *bad += 1
+__global__ void k_fr_check(const fr_t *__restrict__ d, uint64_t n, int *__restrict__ bad) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (geq_raw(d[i], fr_t::modulus_raw())) atomicAdd(bad, 1);
 }
 
 __device__ __forceinline__ void fq_to_be48_dev(const fq_t &a, uint8_t *out) {
@@ -147,14 +175,31 @@ void debug_sync(Ctx &c, const char *what) {
     if (e != hipSuccess) throw hip_error(e, std::string("kernel ") + what + " failed: " + hipGetErrorString(e));
 }
 
-void g1_decode_uncompressed(Ctx &c, const uint8_t *dev_bytes, g1_affine_t *out, uint64_t n, int *bad_dev) {
+void g1_decode_uncompressed(Ctx &c, const uint8_t *dev_bytes, g1_affine_t *out, uint64_t n, int *bad_dev,
+                            bool reject_inf) {
     if (!n) return;
-    k_g1_decode<<<grid1(n), 256, 0, c.stream>>>(dev_bytes, out, n, bad_dev);
+    k_g1_decode<<<grid1(n), 256, 0, c.stream>>>(dev_bytes, out, n, bad_dev, reject_inf ? 1 : 0);
     MI_HIP(hipGetLastError());
 }
-void g2_decode_uncompressed(Ctx &c, const uint8_t *dev_bytes, g2_affine_t *out, uint64_t n, int *bad_dev) {
+void g2_decode_uncompressed(Ctx &c, const uint8_t *dev_bytes, g2_affine_t *out, uint64_t n, int *bad_dev,
+                            bool reject_inf) {
     if (!n) return;
-    k_g2_decode<<<grid1(n), 256, 0, c.stream>>>(dev_bytes, out, n, bad_dev);
+    k_g2_decode<<<grid1(n), 256, 0, c.stream>>>(dev_bytes, out, n, bad_dev, reject_inf ? 1 : 0);
+    MI_HIP(hipGetLastError());
+}
+void g1_subgroup_check(Ctx &c, const g1_affine_t *pts, uint64_t n, int *bad_dev) {
+    if (!n) return;
+    k_subgroup<fq_t><<<grid1(n), 256, 0, c.stream>>>(pts, n, bad_dev);
+    MI_HIP(hipGetLastError());
+}
+void g2_subgroup_check(Ctx &c, const g2_affine_t *pts, uint64_t n, int *bad_dev) {
+    if (!n) return;
+    k_subgroup<fq2_t><<<grid1(n), 256, 0, c.stream>>>(pts, n, bad_dev);
+    MI_HIP(hipGetLastError());
+}
+void fr_count_noncanonical(Ctx &c, const fr_t *d, uint64_t n, int *bad_dev, hipStream_t st) {
+    if (!n) return;
+    k_fr_check<<<grid1(n), 256, 0, st>>>(d, n, bad_dev);
     MI_HIP(hipGetLastError());
 }
 void g1_encode_uncompressed(Ctx &c, const g1_affine_t *in, uint8_t *dev_out, uint64_t n, unsigned perm_log) {

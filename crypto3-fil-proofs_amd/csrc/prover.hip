@@ -334,15 +334,31 @@ void g2_compress(const g2_affine_t &a, uint8_t out[96]) {
     bool largest = a.y.c1.is_zero() ? fq_lex_largest(a.y.c0) : fq_lex_largest(a.y.c1);
     if (largest) out[0] |= 0x20;
 }
+// zcash from_uncompressed flag rules (see k_g1_decode): 0x80 clear; infinity = 0x40 with every other
+// bit zero; the sort bit 0x20 clear on finite points.  The curve equation is the caller's check.
+static int uncompressed_flags_host(const uint8_t *p, int len) {
+    const uint8_t f = p[0];
+    if (f & 0x80) return -1;
+    if (f & 0x40) {
+        uint32_t any = f & 0x3f;
+        for (int k = 1; k < len; k++) any |= p[k];
+        return any ? -1 : 1;
+    }
+    return (f & 0x20) ? -1 : 0;
+}
 bool g1_decode_host(const uint8_t in[96], g1_affine_t &out) {
-    if (in[0] & 0x40) {
+    const int f = uncompressed_flags_host(in, 96);
+    if (f < 0) return false;
+    if (f == 1) {
         out = g1_affine_t::inf();
         return true;
     }
     return fq_from_be48_host(in, true, out.x) && fq_from_be48_host(in + 48, false, out.y);
 }
 bool g2_decode_host(const uint8_t in[192], g2_affine_t &out) {
-    if (in[0] & 0x40) {
+    const int f = uncompressed_flags_host(in, 192);
+    if (f < 0) return false;
+    if (f == 1) {
         out = g2_affine_t::inf();
         return true;
     }
@@ -440,34 +456,41 @@ Circuit *circuit_load(Ctx &c, const R1csHost &cs) {
     return C;
 }
 
+// One proving-key query, streamed through a bounded staging buffer and decoded on the device with
+// bellman's Parameters::read rules: canonical coordinates, on the curve, the identity refused in every
+// query ("point at infinity"), and with checked = true also r P = O (from_uncompressed vs _unchecked).
 template <class A>
-static A *upload_points(Ctx &c, const uint8_t *bytes, uint64_t n, bool is_g2, bool checked) {
+static A *upload_points(Ctx &c, const uint8_t *bytes, uint64_t n, bool is_g2, bool checked, const char *name) {
     if (!n) return nullptr;
     const size_t esz = is_g2 ? 192 : 96;
     A *out = dalloc<A>(n);
     int *bad = c.scratch[9].as<int>(4);
-    MI_HIP(hipMemsetAsync(bad, 0, sizeof(int), c.stream));
-    // stream through a bounded staging buffer
+    MI_HIP(hipMemsetAsync(bad, 0, 3 * sizeof(int), c.stream));
     const uint64_t chunk = 1ull << 22;
     uint8_t *stage = c.scratch[0].as<uint8_t>(esz * (n < chunk ? n : chunk));
     for (uint64_t o = 0; o < n; o += chunk) {
         uint64_t m = n - o < chunk ? n - o : chunk;
         MI_HIP(hipMemcpyAsync(stage, bytes + esz * o, esz * m, hipMemcpyHostToDevice, c.stream));
         if (is_g2)
-            g2_decode_uncompressed(c, stage, (g2_affine_t *)out + o, m, bad);
+            g2_decode_uncompressed(c, stage, (g2_affine_t *)out + o, m, bad, true);
         else
-            g1_decode_uncompressed(c, stage, (g1_affine_t *)out + o, m, bad);
+            g1_decode_uncompressed(c, stage, (g1_affine_t *)out + o, m, bad, true);
     }
-    int nbad = 0;
-    MI_HIP(hipMemcpyAsync(&nbad, bad, sizeof(int), hipMemcpyDeviceToHost, c.stream));
+    if (checked) {
+        if (is_g2)
+            g2_subgroup_check(c, (const g2_affine_t *)out, n, bad);
+        else
+            g1_subgroup_check(c, (const g1_affine_t *)out, n, bad);
+    }
+    int nbad[3] = {0, 0, 0};
+    MI_HIP(hipMemcpyAsync(nbad, bad, sizeof(nbad), hipMemcpyDeviceToHost, c.stream));
     MI_HIP(hipStreamSynchronize(c.stream));
-    if (nbad && checked) {
+    if (nbad[0] || nbad[1] || nbad[2]) {
         hipFree(out);
-        throw std::invalid_argument("SRS contains points that are not on the curve / not canonical");
-    }
-    if (nbad) {
-        hipFree(out);
-        throw std::invalid_argument("SRS contains non-canonical coordinates");
+        std::string q = std::string("SRS ") + name + " query: ";
+        if (nbad[0]) throw std::invalid_argument(q + std::to_string(nbad[0]) + " malformed or off-curve point(s)");
+        if (nbad[1]) throw std::invalid_argument(q + std::to_string(nbad[1]) + " point(s) at infinity");
+        throw std::invalid_argument(q + std::to_string(nbad[2]) + " point(s) outside the prime-order subgroup");
     }
     return out;
 }
@@ -497,23 +520,33 @@ Srs *srs_load(Ctx &c, const Circuit *circ, const SrsHost &h, bool checked) {
         S->n_a = h.n_a;
         S->n_b = h.n_b_g1;
         if (h.n_b_g1 != h.n_b_g2) throw std::invalid_argument("|b_g1| != |b_g2|");
-        g1_affine_t *hnat = upload_points<g1_affine_t>(c, h.h, h.n_h, false, checked);
+        g1_affine_t *hnat = upload_points<g1_affine_t>(c, h.h, h.n_h, false, checked, "h");
         S->h_perm = dalloc<g1_affine_t>(h.n_h);
         k_permute_h<<<grid1(h.n_h), 256, 0, c.stream>>>(hnat, S->h_perm, S->log_d, h.n_h);
         MI_HIP(hipStreamSynchronize(c.stream));
         hipFree(hnat);
-        S->l = upload_points<g1_affine_t>(c, h.l, h.n_l, false, checked);
-        S->a = upload_points<g1_affine_t>(c, h.a, h.n_a, false, checked);
-        S->b_g1 = upload_points<g1_affine_t>(c, h.b_g1, h.n_b_g1, false, checked);
-        S->b_g2 = upload_points<g2_affine_t>(c, h.b_g2, h.n_b_g2, true, checked);
+        S->l = upload_points<g1_affine_t>(c, h.l, h.n_l, false, checked, "l");
+        S->a = upload_points<g1_affine_t>(c, h.a, h.n_a, false, checked, "a");
+        S->b_g1 = upload_points<g1_affine_t>(c, h.b_g1, h.n_b_g1, false, checked, "b_g1");
+        S->b_g2 = upload_points<g2_affine_t>(c, h.b_g2, h.n_b_g2, true, checked, "b_g2");
+        // verifying key and ic on the host: curve equation always, subgroup when checked; ic points are
+        // refused at infinity like the queries (bellman VerifyingKey::read)
+        auto g1_ok = [&](const g1_affine_t &p) { return p.is_inf() || (g1_on_curve(p) && (!checked || in_prime_subgroup(p))); };
+        auto g2_ok = [&](const g2_affine_t &p) { return p.is_inf() || (g2_on_curve(p) && (!checked || in_prime_subgroup(p))); };
         bool ok = g1_decode_host(h.vk, S->alpha_g1) && g1_decode_host(h.vk + 96, S->beta_g1) &&
                   g2_decode_host(h.vk + 192, S->beta_g2) && g2_decode_host(h.vk + 384, S->gamma_g2) &&
                   g1_decode_host(h.vk + 576, S->delta_g1) && g2_decode_host(h.vk + 672, S->delta_g2);
         if (!ok) throw std::invalid_argument("bad verifying key encoding");
+        if (!g1_ok(S->alpha_g1) || !g1_ok(S->beta_g1) || !g1_ok(S->delta_g1) || !g2_ok(S->beta_g2) ||
+            !g2_ok(S->gamma_g2) || !g2_ok(S->delta_g2))
+            throw std::invalid_argument("verifying key point not on the curve / outside the subgroup");
         S->n_ic = h.n_ic;
         S->ic.resize(h.n_ic);
-        for (uint64_t i = 0; i < h.n_ic; i++)
+        for (uint64_t i = 0; i < h.n_ic; i++) {
             if (!g1_decode_host(h.ic + 96 * i, S->ic[i])) throw std::invalid_argument("bad ic encoding");
+            if (S->ic[i].is_inf()) throw std::invalid_argument("ic point at infinity");
+            if (!g1_ok(S->ic[i])) throw std::invalid_argument("ic point not on the curve / outside the subgroup");
+        }
         build_hi_tables(c, *S);
     } catch (...) {
         delete S;

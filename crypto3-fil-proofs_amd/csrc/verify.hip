@@ -17,9 +17,10 @@
 // Final exponentiation: f^((p^6 - 1)(p^2 + 1)) by conjugation, inversion and Frobenius, then the
 // hard part: exact f^((p^4 - p^2 + 1) / r) by square-and-multiply for mi_pairing, and for the
 // verifier the cube of it through the BLS12 z-chain (identity checked with big integers at start).
+#include <errno.h>
 #include <string.h>
+#include <sys/random.h>
 
-#include <random>
 #include <vector>
 
 #include "prover.h"
@@ -533,6 +534,53 @@ ProofPoints groth16_assemble_shares(const uint8_t *vk, const uint8_t *shares, ui
     return groth16_assemble(AssemblyKey{V.alpha, V.beta1, V.delta1, V.beta2, V.delta2}, m, r, s);
 }
 
+// ChaCha20 block (RFC 8439) keyed by a 32-byte seed: the deterministic weight stream of the seeded
+// batch verifier (tests).  Production batch verification draws its weights from getrandom().
+static inline uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
+static void chacha20_block(const uint32_t key[8], uint32_t counter, uint8_t out[64]) {
+    uint32_t st[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, key[0], key[1], key[2], key[3],
+                       key[4],      key[5],      key[6],      key[7],      counter, 0u,     0u,     0u};
+    uint32_t x[16];
+    memcpy(x, st, sizeof x);
+    auto qr = [&](int a, int b, int c, int d) {
+        x[a] += x[b]; x[d] = rotl32(x[d] ^ x[a], 16);
+        x[c] += x[d]; x[b] = rotl32(x[b] ^ x[c], 12);
+        x[a] += x[b]; x[d] = rotl32(x[d] ^ x[a], 8);
+        x[c] += x[d]; x[b] = rotl32(x[b] ^ x[c], 7);
+    };
+    for (int r = 0; r < 10; r++) {
+        qr(0, 4, 8, 12), qr(1, 5, 9, 13), qr(2, 6, 10, 14), qr(3, 7, 11, 15);
+        qr(0, 5, 10, 15), qr(1, 6, 11, 12), qr(2, 7, 8, 13), qr(3, 4, 9, 14);
+    }
+    for (int i = 0; i < 16; i++) {
+        uint32_t v = x[i] + st[i];
+        memcpy(out + 4 * i, &v, 4);
+    }
+}
+// 16 bytes of weight per proof: OS randomness (bellman draws rho from OsRng), or the ChaCha20 stream
+// of seed32 when the caller asked for a reproducible check
+static std::vector<uint8_t> batch_weights(uint64_t count, const uint8_t *seed32) {
+    std::vector<uint8_t> w(16 * count + 64);
+    if (seed32) {
+        uint32_t key[8];
+        memcpy(key, seed32, 32);
+        for (uint64_t o = 0, blk = 0; o < 16 * count; o += 64, blk++) {
+            if (blk >> 32) throw std::length_error("batch too large for one ChaCha20 stream");
+            chacha20_block(key, (uint32_t)blk, w.data() + o);
+        }
+    } else {
+        for (size_t o = 0; o < 16 * count;) {
+            ssize_t got = getrandom(w.data() + o, 16 * count - o, 0);
+            if (got < 0) {
+                if (errno == EINTR) continue;
+                throw std::runtime_error("getrandom failed");
+            }
+            o += (size_t)got;
+        }
+    }
+    return w;
+}
+
 // bellman verify_proofs_batch: random 128-bit weights rho_i;
 //   prod e(rho_i A_i, B_i) * e(-sum rho_i acc_i, gamma) * e(-sum rho_i C_i, delta) * e(-(sum rho_i) alpha, beta) == 1
 bool groth16_verify_batch(const uint8_t *vk, const uint8_t *ic, uint64_t n_ic, uint64_t count, const uint8_t *inputs,
@@ -540,17 +588,7 @@ bool groth16_verify_batch(const uint8_t *vk, const uint8_t *ic, uint64_t n_ic, u
     if (n_ic == 0) throw std::invalid_argument("verifying key has no IC points");
     if (count == 0) return true;
     DecodedVk V = decode_vk(vk, ic, n_ic);
-    std::seed_seq seq = [&] {
-        std::vector<uint32_t> s(8);
-        if (seed32) {
-            memcpy(s.data(), seed32, 32);
-        } else {
-            std::random_device rd;
-            for (auto &x : s) x = rd();
-        }
-        return std::seed_seq(s.begin(), s.end());
-    }();
-    std::mt19937_64 rng(seq);
+    std::vector<uint8_t> weights = batch_weights(count, seed32);
     std::vector<g1_affine_t> P;
     std::vector<g2_affine_t> Q;
     g1_xyzz_t sacc = g1_xyzz_t::inf(), sc = g1_xyzz_t::inf();
@@ -558,11 +596,8 @@ bool groth16_verify_batch(const uint8_t *vk, const uint8_t *ic, uint64_t n_ic, u
     for (uint64_t i = 0; i < count; i++) {
         DecodedProof pr = decode_proof(proofs + 192 * i);
         fr_t rho = fr_t::zero();
-        uint64_t a = rng() | 1, b = rng();
-        rho.v[0] = (uint32_t)a;
-        rho.v[1] = (uint32_t)(a >> 32);
-        rho.v[2] = (uint32_t)b;
-        rho.v[3] = (uint32_t)(b >> 32);
+        memcpy(rho.v, weights.data() + 16 * i, 16);
+        rho.v[0] |= 1;  // non-zero
         rsum = rsum + to_mont(rho);
         P.push_back(xyzz_to_affine(xyzz_mul(xyzz_from_affine(pr.A), rho.v, 4)));
         Q.push_back(pr.B);

@@ -23,6 +23,7 @@ EXPORTS = [
     "mi_params_inspect", "mi_params_load", "mi_params_write", "mi_vk_write",
     "mi_groth16_verify", "mi_groth16_verify_batch", "mi_pairing",
     "mi_groth16_prove_share", "mi_groth16_prove_share_dev", "mi_groth16_assemble",
+    "mi_host_alloc", "mi_host_free", "mi_groth16_verify_batch_seeded",
 ]
 
 _lib = None
@@ -106,7 +107,10 @@ def lib():
         "mi_params_write": ([vp, vp, u8p], c_int),
         "mi_vk_write": ([vp, u8p], c_int),
         "mi_groth16_verify": ([u8p, u8p, u64, u8p, u8p, ctypes.POINTER(c_int)], c_int),
-        "mi_groth16_verify_batch": ([u8p, u8p, u64, u64, u8p, u8p, u8p, ctypes.POINTER(c_int)], c_int),
+        "mi_groth16_verify_batch": ([u8p, u8p, u64, u64, u8p, u8p, ctypes.POINTER(c_int)], c_int),
+        "mi_groth16_verify_batch_seeded": ([u8p, u8p, u64, u64, u8p, u8p, u8p, ctypes.POINTER(c_int)], c_int),
+        "mi_host_alloc": ([u64, pp], c_int),
+        "mi_host_free": ([vp], None),
         "mi_pairing": ([u8p, u8p, vp], c_int),
     }
     for name, (args, res) in sig.items():

@@ -77,13 +77,13 @@ class Context:
         return s.value or 0
 
     # ---- device timers (HIP events inside the library; always on) ----
-    STAT_KEYS = ["accum_g1", "accum_g2", "msm_g1", "msm_g2", "sort", "ntt", "prove"]
+    STAT_KEYS = ["accum_g1", "accum_g2", "msm_g1", "msm_g2", "sort", "ntt", "prove", "h2d"]
 
     def reset_stats(self):
         check(lib().mi_ctx_reset_stats(self.h))
 
     def stats(self) -> dict:
-        out = (ctypes.c_double * 21)()
+        out = (ctypes.c_double * (3 * len(self.STAT_KEYS)))()
         check(lib().mi_ctx_get_stats(self.h, out))
         v = list(out)
         st = {k: {"ms": v[3 * i], "launches": int(v[3 * i + 1]), "units": int(v[3 * i + 2])}
@@ -281,13 +281,18 @@ def verify(vk: bytes, ic: bytes, inputs: bytes, proof: bytes) -> bool:
 
 def verify_batch(vk: bytes, ic: bytes, inputs, proofs, seed: bytes = None) -> bool:
     """bellman verify_proofs_batch (verify_batch_seal, api/seal.hpp:339-485): one multi-pairing with
-    random 128-bit weights drawn from ``seed`` (32 B; None = OS randomness)."""
+    random 128-bit weights from getrandom() (bellman: OsRng).  ``seed`` (32 B, tests only) makes the
+    weights a reproducible ChaCha20 stream instead (mi_groth16_verify_batch_seeded)."""
     n_ic = len(ic) // 96
     assert len(inputs) == len(proofs) and all(len(x) == 32 * (n_ic - 1) for x in inputs)
     assert seed is None or len(seed) == 32
     ok = ctypes.c_int(0)
-    check(lib().mi_groth16_verify_batch(vk, ic, n_ic, len(proofs), b"".join(inputs) or None,
-                                        b"".join(proofs) or None, seed, ctypes.byref(ok)))
+    ins, prs = b"".join(inputs) or None, b"".join(proofs) or None
+    if seed is None:
+        check(lib().mi_groth16_verify_batch(vk, ic, n_ic, len(proofs), ins, prs, ctypes.byref(ok)))
+    else:
+        check(lib().mi_groth16_verify_batch_seeded(vk, ic, n_ic, len(proofs), ins, prs, bytes(seed),
+                                                   ctypes.byref(ok)))
     return bool(ok.value)
 
 
@@ -327,10 +332,46 @@ def prove(ctx: Context, pk: ProvingKey, circuit: Circuit, z, r: int, s: int, pri
     return (proof.raw, raw.raw) if want_raw else proof.raw
 
 
+class HostBuffer:
+    """Page-locked host memory from mi_host_alloc: a witness written here goes to the GPU at full DMA
+    rate (and prove_batch overlaps the next partition's copy with the current proof)."""
+
+    def __init__(self, nbytes: int):
+        p = ctypes.c_void_p()
+        check(lib().mi_host_alloc(nbytes, ctypes.byref(p)))
+        self.ptr, self.nbytes = p.value, nbytes
+        self.array = np.frombuffer((ctypes.c_uint8 * nbytes).from_address(self.ptr), dtype=np.uint8)
+
+    def __del__(self):
+        try:
+            self.array = None
+            lib().mi_host_free(ctypes.c_void_p(self.ptr))
+        except Exception:
+            pass
+
+
+def _host_ptr(z, nbytes):
+    """(address, keepalive) of a host witness without copying it: HostBuffer, numpy array or bytes."""
+    if isinstance(z, HostBuffer):
+        assert z.nbytes >= nbytes
+        return z.ptr, z
+    if isinstance(z, np.ndarray):
+        assert z.flags.c_contiguous and z.nbytes >= nbytes
+        return z.ctypes.data, z
+    b = bytes(z)
+    assert len(b) >= nbytes
+    arr = np.frombuffer(b, dtype=np.uint8)
+    return arr.ctypes.data, arr
+
+
 def prove_batch(ctx: Context, pk: ProvingKey, circuit: Circuit, zs, rs, priority=False):
-    """count independent partition proofs -> list of 192-byte proofs."""
+    """count independent partition proofs -> list of 192-byte proofs.  Witnesses stay in host memory
+    (HostBuffer, numpy arrays or bytes; never copied here): the library uploads partition k + 1 while
+    it proves partition k."""
     count = len(zs)
-    arr = (ctypes.c_char_p * count)(*[bytes(z) for z in zs])
+    nbytes = 32 * circuit.num_vars
+    keep = [_host_ptr(z, nbytes) for z in zs]
+    arr = (ctypes.c_void_p * count)(*[p for p, _ in keep])
     rsb = b"".join(fr_bytes(r) + fr_bytes(s) for r, s in rs)
     out = ctypes.create_string_buffer(PROOF_BYTES * count)
     check(lib().mi_groth16_prove_batch(ctx.h, pk.h, circuit.h, count, arr, rsb, int(priority), out))

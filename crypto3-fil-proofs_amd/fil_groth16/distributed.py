@@ -41,6 +41,18 @@ def gather_multiproof(local_proofs, num_partitions: int, rank: int, world: int, 
     return bytes(out)
 
 
+def prove_partitions(prove_fn, num_partitions: int, rank: int, world: int, device="cpu"):
+    """Config-5 runner (Window-PoSt batch / PoRep C2 partitions over the GPUs of one node): this rank
+    proves its round-robin share shard_partitions(P, rank, world) with ``prove_fn(partition_ids) ->
+    list of 192-byte proofs`` (on a GPU: one fg.prove_batch over its witnesses, so partition k + 1's
+    upload overlaps proof k), then the P x 192-byte multi-proof is all-gathered in partition order
+    (api/seal.hpp:306-308; FallbackPoStCompound::prove per partition, api/post.hpp:305-348).
+    10 partitions on 8 GPUs leave two rounds on ranks 0 and 1 (post.cpp:37-46, constants.hpp:88)."""
+    mine = shard_partitions(num_partitions, rank, world)
+    local = list(prove_fn(mine)) if mine else []
+    return gather_multiproof(local, num_partitions, rank, world, device)
+
+
 def gather_shares(share: bytes, world: int, device="cpu"):
     """All-gather one MI_SHARE_BYTES record per rank (the latency mode's only exchange, 576 B per GPU)."""
     import torch

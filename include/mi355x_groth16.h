@@ -100,6 +100,12 @@ const char *mi_last_error(void);
 /* stream handle (hipStream_t) the context launches on; external work may be ordered against it */
 int mi_ctx_stream(mi_ctx *ctx, void **stream_out);
 int mi_ctx_synchronize(mi_ctx *ctx);
+/* Page-locked host memory for witnesses.  The reference hands the prover host-side assignments
+ * (api/seal.hpp:298-301); a synthesiser that writes z into such a buffer lets the prover's H2D copy
+ * run at full DMA rate, and mi_groth16_prove_batch overlaps partition k + 1's copy with partition k's
+ * proof.  Pageable witnesses work too (staged through pinned buffers). */
+int mi_host_alloc(uint64_t bytes, void **out);
+void mi_host_free(void *p);
 
 /* ---- circuits and proving keys ---- */
 int mi_circuit_load(mi_ctx *ctx, const mi_r1cs *cs, mi_circuit **out);
@@ -107,7 +113,10 @@ int mi_circuit_load(mi_ctx *ctx, const mi_r1cs *cs, mi_circuit **out);
 int mi_circuit_info(const mi_circuit *c, uint64_t out[9]);
 void mi_circuit_free(mi_circuit *c);
 
-/* checked != 0 additionally verifies every point is on its curve (mapped_scheme_params::checked) */
+/* Every point is decoded with zcash/bellman from_uncompressed rules (flag bits, canonical coordinates,
+ * on the curve) and, like bellman's Parameters::read, a point at infinity in h, l, a, b_g1, b_g2 or ic
+ * is refused.  checked != 0 (Parameters::read(checked = true), mapped_scheme_params::checked)
+ * additionally verifies r * P == O for every point (prime-order subgroup).  Failures: MI_ERR_ARG. */
 int mi_srs_load(mi_ctx *ctx, const mi_circuit *circuit_or_null, const mi_srs_host *host, int checked,
                 mi_srs **out);
 /* toxic waste tau, alpha, beta, gamma, delta: 5 x 32 B LE canonical; generators = standard G1/G2 */
@@ -123,8 +132,12 @@ void mi_srs_free(mi_srs *srs);
 /* ---- verification (host CPU; no device needed) ----
  *   mi_groth16_verify       <- crypto3 r1cs_gg_ppzksnark verify / bellman verify_proof, used by the
  *                              self-check of every C2 proof (api/seal.hpp:310-313) and verify_seal
- *   mi_groth16_verify_batch <- bellman verify_proofs_batch behind verify_batch_seal (api/seal.hpp:339-485);
- *                              seed32 = randomness of the linear combination (NULL: std::random_device)
+ *   mi_groth16_verify_batch <- bellman verify_proofs_batch behind verify_batch_seal (api/seal.hpp:339-485):
+ *                              one multi-pairing over random 128-bit weights drawn from getrandom()
+ *                              (bellman: OsRng); soundness against adversarial proofs needs weights the
+ *                              prover cannot predict
+ *   mi_groth16_verify_batch_seeded  the same with the weights from a ChaCha20 stream keyed by seed32:
+ *                              reproducible, for tests only (a known seed lets a forger cancel terms)
  * vk: MI_VK_BYTES, ic: n_ic x 96 B (uncompressed); inputs: (n_ic - 1) x 32 B LE canonical public
  * inputs WITHOUT the implicit ONE (generate_public_inputs order), per proof; proofs: 192 B each.
  * *valid = 1 / 0.  Undecodable, off-curve or non-subgroup proof points: MI_ERR_INVALID_POINT;
@@ -134,7 +147,10 @@ void mi_srs_free(mi_srs *srs);
 int mi_groth16_verify(const uint8_t *vk, const uint8_t *ic, uint64_t n_ic, const uint8_t *inputs,
                       const uint8_t proof[MI_PROOF_BYTES], int *valid);
 int mi_groth16_verify_batch(const uint8_t *vk, const uint8_t *ic, uint64_t n_ic, uint64_t count,
-                            const uint8_t *inputs, const uint8_t *proofs, const uint8_t *seed32, int *valid);
+                            const uint8_t *inputs, const uint8_t *proofs, int *valid);
+int mi_groth16_verify_batch_seeded(const uint8_t *vk, const uint8_t *ic, uint64_t n_ic, uint64_t count,
+                                   const uint8_t *inputs, const uint8_t *proofs, const uint8_t seed32[32],
+                                   int *valid);
 int mi_pairing(const uint8_t g1_96[96], const uint8_t g2_192[192], uint8_t out[576]);
 
 /* ---- parameter files (bellman Parameters::write layout = filecoin v28-*.params) ----
@@ -153,7 +169,9 @@ int mi_params_write(mi_ctx *ctx, const mi_srs *srs, const char *path);
 int mi_vk_write(const mi_srs *srs, const char *path);
 
 /* ---- Groth16 ---- */
-/* z: (num_inputs + num_aux) x 32 B, z[0] = ONE.  r, s: injected blinding (tests / parity);
+/* z: (num_inputs + num_aux) x 32 B, z[0] = ONE.  Every entry must be canonical (< r): a witness holding
+ * a non-canonical entry is refused with MI_ERR_ARG (an Fr32 "MUST represent a valid Fr",
+ * core/fr32.hpp:36-40), for host and device witnesses alike.  r, s: injected blinding (tests / parity);
  * priority != 0 runs on the context's high-priority stream (post_config.priority,
  * libs/filecoin/include/nil/filecoin/proofs/types/post_config.hpp:41-42).
  * raw_out (optional, may be NULL): uncompressed A (96) | B (192) | C (96). */
@@ -164,7 +182,8 @@ int mi_groth16_prove(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circuit, 
 int mi_groth16_prove_dev(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circuit, const void *z_dev,
                          const uint8_t r[32], const uint8_t s[32], int priority, uint8_t proof_out[MI_PROOF_BYTES],
                          uint8_t *raw_out);
-/* count independent partitions (compound_proof::circuit_proofs loop); proofs_out = count x 192 B */
+/* count independent partitions (compound_proof::circuit_proofs loop); proofs_out = count x 192 B.
+ * Partition k + 1's witness upload overlaps partition k's proof (copy stream, two device slots). */
 int mi_groth16_prove_batch(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circuit, uint64_t count,
                            const uint8_t *const *z, const uint8_t *rs /* count x 64 B: r | s */, int priority,
                            uint8_t *proofs_out);
@@ -217,10 +236,11 @@ int mi_synth_witness(const mi_synth *s, const uint8_t **z, uint64_t *num_vars);
 void mi_synth_free(mi_synth *s);
 
 /* ---- device timers (HIP events on the launching stream, resolved at existing sync points, so they
- * stay on inside timed regions).  out = 7 records x {ms, launches, units}:
+ * stay on inside timed regions).  out = 8 records x {ms, launches, units}:
  *   0 k_accum_level0<G1> (units = points)   1 k_accum_level0<G2>   2 whole G1 MSM   3 whole G2 MSM
- *   4 digits + sort + bucket bounds          5 NTT transforms (units = elements)   6 whole prove (units = constraints) */
-int mi_ctx_get_stats(mi_ctx *ctx, double out[21]);
+ *   4 digits + sort + bucket bounds          5 NTT transforms (units = elements)   6 whole prove (units = constraints)
+ *   7 witness H2D upload + canonical check on the copy stream (units = bytes) */
+int mi_ctx_get_stats(mi_ctx *ctx, double out[24]);
 int mi_ctx_reset_stats(mi_ctx *ctx);
 /* work counters since the last reset: out[0] / out[1] = mixed additions (non-zero signed digits)
  * issued by the G1 / G2 bucket accumulation -- the unit of the VALU roofline */

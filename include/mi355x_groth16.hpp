@@ -138,7 +138,8 @@ struct multi_proof {
     std::vector<proof_bytes> circuit_proofs;
     std::vector<uint8_t> verifying_key;
     std::vector<uint8_t> ic;
-    // verify_seal's batch check over all partitions (api/seal.hpp:339-485); seed: 32 B or nullptr
+    // verify_seal's batch check over all partitions (api/seal.hpp:339-485); weights from getrandom(),
+    // or from the ChaCha20 stream of seed32 (32 B, tests only) when given
     bool verify(const std::vector<std::vector<fr32>> &public_inputs, const uint8_t *seed32 = nullptr) const {
         if (public_inputs.size() != circuit_proofs.size()) throw error(MI_ERR_ARG, "one input vector per partition");
         std::vector<uint8_t> in, pr;
@@ -148,9 +149,13 @@ struct multi_proof {
         }
         for (auto &p : circuit_proofs) pr.insert(pr.end(), p.begin(), p.end());
         int ok = 0;
-        check(mi_groth16_verify_batch(verifying_key.data(), ic.data(), ic.size() / 96, circuit_proofs.size(),
-                                      in.empty() ? nullptr : in.data(), pr.empty() ? nullptr : pr.data(), seed32,
-                                      &ok));
+        const uint8_t *ins = in.empty() ? nullptr : in.data(), *prs = pr.empty() ? nullptr : pr.data();
+        if (seed32)
+            check(mi_groth16_verify_batch_seeded(verifying_key.data(), ic.data(), ic.size() / 96,
+                                                 circuit_proofs.size(), ins, prs, seed32, &ok));
+        else
+            check(mi_groth16_verify_batch(verifying_key.data(), ic.data(), ic.size() / 96, circuit_proofs.size(),
+                                          ins, prs, &ok));
         return ok != 0;
     }
     std::vector<uint8_t> write() const {  // api/seal.hpp:306-308

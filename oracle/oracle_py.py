@@ -9,7 +9,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+# ORACLE_LIB selects another build of the same sources, e.g. the ASan/UBSan one (make -C oracle asan)
+LIB_PATH = os.environ.get("ORACLE_LIB", os.path.join(_HERE, "build", "liboracle.so"))
 
 R_MOD = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 P_MOD = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB

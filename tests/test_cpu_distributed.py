@@ -104,3 +104,58 @@ def test_gloo_world2_split_proof(tmp_path, oracle):
     n_in, n_aux, rows, z = circuits.random_circuit(71, 60)
     P = oracle.OracleParams(oracle.OracleCircuit(len(rows), n_in, n_aux, circuits.to_csr(rows)), circuits.toxic())
     assert outs[0] == outs[1] == P.prove(circuits.z_bytes(z), 17, 19)[0]
+
+
+def _partitions_worker(rank, world, port, num_partitions, outdir):
+    """bench.py --partitions P, with the oracle standing in for the GPU prover: the same runner
+    (fil_groth16.distributed.prove_partitions) and gather over gloo instead of RCCL."""
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "crypto3-fil-proofs_amd"), os.path.join(root, "oracle"),
+              os.path.join(root, "tests", "golden")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+
+    import circuits
+    import oracle_py
+    from fil_groth16.distributed import prove_partitions
+
+    oracle_py.set_threads(1)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n_in, n_aux, rows, z = circuits.random_circuit(62, 40)
+    P = oracle_py.OracleParams(oracle_py.OracleCircuit(len(rows), n_in, n_aux, circuits.to_csr(rows)),
+                               circuits.toxic())
+    zb = circuits.z_bytes(z)
+    proven = []
+
+    def prove_fn(ids):
+        proven.extend(ids)
+        return [P.prove(zb, 300 + p, 400 + p)[0] for p in ids]
+
+    buf = prove_partitions(prove_fn, num_partitions, rank, world)
+    with open(os.path.join(outdir, f"p{rank}.bin"), "wb") as f:
+        f.write(buf)
+    with open(os.path.join(outdir, f"ids{rank}.txt"), "w") as f:
+        f.write(",".join(map(str, proven)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,num_partitions", [(2, 10), (8, 10), (3, 2)])
+def test_gloo_partition_runner(tmp_path, oracle, world, num_partitions):
+    """Config 5 shape: 10 Window-PoSt partitions over 8 ranks (two rounds on ranks 0 and 1), and fewer
+    partitions than ranks; every rank ends with the serial multi-proof."""
+    import circuits
+
+    mp.spawn(_partitions_worker, args=(world, _free_port(), num_partitions, str(tmp_path)), nprocs=world,
+             join=True)
+    outs = [open(tmp_path / f"p{r}.bin", "rb").read() for r in range(world)]
+    ids = [open(tmp_path / f"ids{r}.txt").read() for r in range(world)]
+    assert ids == [",".join(map(str, range(r, num_partitions, world))) for r in range(world)]
+    n_in, n_aux, rows, z = circuits.random_circuit(62, 40)
+    P = oracle.OracleParams(oracle.OracleCircuit(len(rows), n_in, n_aux, circuits.to_csr(rows)), circuits.toxic())
+    zb = circuits.z_bytes(z)
+    serial = b"".join(P.prove(zb, 300 + p, 400 + p)[0] for p in range(num_partitions))
+    assert all(o == serial for o in outs)

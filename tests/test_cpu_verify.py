@@ -74,6 +74,9 @@ def test_verify_batch(oracle):
     assert not fg.verify_batch(ex["vk"], ex["ic"], [inputs] * 4, bad, seed)
     wrong = inputs[:-32] + b"\x05" + bytes(31)
     assert not fg.verify_batch(ex["vk"], ex["ic"], [wrong] + [inputs] * 3, proofs, seed)
+    # production mode: weights from getrandom() (bellman OsRng), no caller-chosen seed
+    assert fg.verify_batch(ex["vk"], ex["ic"], [inputs] * 4, proofs)
+    assert not fg.verify_batch(ex["vk"], ex["ic"], [inputs] * 4, bad)
 
 
 def test_pairing_bilinear(oracle):
