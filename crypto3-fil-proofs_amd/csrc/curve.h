@@ -83,6 +83,18 @@ MI_NOINL XYZZ<F> xyzz_dbl_affine(const Affine<F> &a) {
     return xyzz_dbl_affine_inl(a);
 }
 
+// Lazy-reduction hooks of the additions (field.h "lazy forms"): Fq takes the unreduced forms, every
+// other coordinate type (Fq2, the G2 lane-pair halves) the plain reduced operators.
+template <class F>
+MI_HD F lazy_sub(const F &a, const F &b) { return a - b; }
+template <class F>
+MI_HD F lazy_neg(const F &a) { return -a; }
+template <class F>
+MI_HD F x3_of(const F &r2, const F &ppp, const F &q) { return r2 - ppp - dbl(q); }
+MI_HD fq_t lazy_sub(const fq_t &a, const fq_t &b) { return fq_sub_lazy(a, b); }
+MI_HD fq_t lazy_neg(const fq_t &a) { return fq_neg_lazy(a); }
+MI_HD fq_t x3_of(const fq_t &r2, const fq_t &ppp, const fq_t &q) { return fq_x3(r2, ppp, q); }
+
 // *_inl: force-inlined bodies for the hot kernels (no call ABI, no scratch); the plain names
 // are noinline wrappers for cold code (host assembly, table builds, reductions).
 
@@ -103,8 +115,8 @@ MI_HD XYZZ<F> xyzz_add_affine_inl(const XYZZ<F> &p, const Affine<F> &q) {
     F PPP = P * PP;
     F Q = p.X * PP;
     XYZZ<F> r;
-    r.X = sqr(R) - PPP - dbl(Q);
-    r.Y = mul_add(R, Q - r.X, -p.Y, PPP);  // R (Q - X3) - Y1 PPP, one reduction
+    r.X = x3_of(sqr(R), PPP, Q);
+    r.Y = mul_add(R, lazy_sub(Q, r.X), lazy_neg(p.Y), PPP);  // R (Q - X3) - Y1 PPP, one reduction
     r.ZZ = p.ZZ * PP;
     r.ZZZ = p.ZZZ * PPP;
     return r;
@@ -133,8 +145,8 @@ MI_HD XYZZ<F> xyzz_add_inl(const XYZZ<F> &p, const XYZZ<F> &q) {
     F PPP = P * PP;
     F Q = U1 * PP;
     XYZZ<F> r;
-    r.X = sqr(R) - PPP - dbl(Q);
-    r.Y = mul_add(R, Q - r.X, -S1, PPP);
+    r.X = x3_of(sqr(R), PPP, Q);
+    r.Y = mul_add(R, lazy_sub(Q, r.X), lazy_neg(S1), PPP);
     r.ZZ = p.ZZ * q.ZZ * PP;
     r.ZZZ = p.ZZZ * q.ZZZ * PPP;
     return r;

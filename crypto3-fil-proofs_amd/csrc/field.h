@@ -371,6 +371,72 @@ MI_HD fq_t operator-(const fq_t &a, const fq_t &b) {  // a - b + 2p, then reduce
 MI_HD fq_t operator-(const fq_t &a) { return fq_t::zero() - a; }
 MI_HD fq_t dbl(const fq_t &a) { return a + a; }
 
+// ---- lazy forms: values that only feed multiplications skip the conditional subtraction ----
+// REDC(a b) = (a b + m p) / R < a b / R + p, so a product is < 2p whenever a b < p R; with
+// R = 2^406 > 2^25 p that holds for operands up to ~2^12 p each.  The column-sum bound of operator*
+// and mul_add (<= 42 products per column) needs carry-normalised 29-bit limbs, not values < 2p, so
+// an unreduced but normalised operand in [0, 4p) costs nothing.  (The group law keeps every value it
+// tests with is_zero or stores reduced to [0, 2p).)
+struct Fq29L {
+    static constexpr uint32_t P4[14] = {0x1ffeaaacu, 0x1fdfffffu, 0x13ffffb9u, 0x1ffff58au, 0x1d8907aau,
+                                        0x0541ed61u, 0x0bf6730du, 0x0279c289u, 0x1d91dd2eu, 0x0869759au,
+                                        0x0b1ba7b6u, 0x0bff34d2u, 0x00447a8eu, 0x00000034u};
+    static constexpr uint32_t P6[14] = {0x1ffe0002u, 0x1fcfffffu, 0x1dffff96u, 0x0ffff04fu, 0x1c4d8b80u,
+                                        0x17e2e412u, 0x01f1ac93u, 0x03b6a3ceu, 0x0c5acbc5u, 0x0c9e3068u,
+                                        0x10a97b91u, 0x11fecf3bu, 0x0066b7d5u, 0x0000004eu};
+};
+
+// a - b + 2p for b <= 2p: normalised limbs, value in [0, a + 2p) (not reduced)
+MI_HD fq_t fq_sub_lazy(const fq_t &a, const fq_t &b) {
+    fq_t s;
+    int32_t c = 0;
+    MI_UNROLL for (int i = 0; i < 13; i++) {
+        int32_t t = (int32_t)a.v[i] - (int32_t)b.v[i] + (int32_t)Fq29::P2[i] + c;
+        s.v[i] = (uint32_t)t & Fq29::M;
+        c = t >> 29;
+    }
+    s.v[13] = (uint32_t)((int32_t)a.v[13] - (int32_t)b.v[13] + (int32_t)Fq29::P2[13] + c);
+    return s;
+}
+
+// -y of an affine coordinate y in [0, 2p] as 2p - y (in [0, 2p]); the raw zero stays zero so the
+// (0, 0) infinity encoding survives negation
+MI_HD fq_t fq_neg_lazy(const fq_t &y) {
+    uint32_t z = 0;
+    MI_UNROLL for (int i = 0; i < 14; i++) z |= y.v[i];
+    const fq_t s = fq_sub_lazy(fq_t::zero(), y);
+    fq_t r;
+    MI_UNROLL for (int i = 0; i < 14; i++) r.v[i] = z ? s.v[i] : 0u;
+    return r;
+}
+
+// X3 = R^2 - PPP - 2Q of the XYZZ additions, reduced to [0, 2p): one signed limb pass computes
+// R^2 + 6p - PPP - 2Q in [0, 8p) (all three inputs < 2p), then 4p and 2p are conditionally subtracted
+// (instead of three add/sub passes with a conditional subtraction each).
+MI_HD fq_t fq_x3(const fq_t &r2, const fq_t &ppp, const fq_t &q) {
+    uint32_t s[14];
+    int32_t c = 0;
+    MI_UNROLL for (int i = 0; i < 13; i++) {
+        int32_t t = (int32_t)r2.v[i] + (int32_t)Fq29L::P6[i] - (int32_t)ppp.v[i] - 2 * (int32_t)q.v[i] + c;
+        s[i] = (uint32_t)t & Fq29::M;
+        c = t >> 29;
+    }
+    s[13] = (uint32_t)((int32_t)r2.v[13] + (int32_t)Fq29L::P6[13] - (int32_t)ppp.v[13] - 2 * (int32_t)q.v[13] + c);
+    uint32_t d[14];
+    int32_t bw = 0;
+    MI_UNROLL for (int i = 0; i < 13; i++) {
+        int32_t t = (int32_t)s[i] - (int32_t)Fq29L::P4[i] + bw;
+        d[i] = (uint32_t)t & Fq29::M;
+        bw = t >> 29;
+    }
+    const int32_t top = (int32_t)s[13] - (int32_t)Fq29L::P4[13] + bw;
+    d[13] = (uint32_t)top;
+    if (top < 0) {
+        MI_UNROLL for (int i = 0; i < 14; i++) d[i] = s[i];
+    }
+    return fq_sub_2p_if_ge(d);
+}
+
 // canonical representative in [0, p)
 MI_HD fq_t fq_canon(const fq_t &a) {
     fq_t d;

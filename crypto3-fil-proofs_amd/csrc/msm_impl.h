@@ -389,7 +389,7 @@ __global__ void __launch_bounds__(256) MI_WAVES_ACC k_accum_level0(const uint32_
                 an = LP::lda(src(vn));
                 if (p + 2 < end) vnn = vals[p + 2];
             }
-            if (v >> 31) a.y = -a.y;
+            if (v >> 31) a.y = lazy_neg(a.y);
             acc = xyzz_add_affine_inl(acc, a);
             a = an;
             v = vn;
@@ -400,7 +400,7 @@ __global__ void __launch_bounds__(256) MI_WAVES_ACC k_accum_level0(const uint32_
     for (uint32_t p = beg; p < end; p++) {
         uint32_t v = vals[p];
         Affine<R> a = LP::lda(src(v));
-        if (v >> 31) a.y = -a.y;
+        if (v >> 31) a.y = lazy_neg(a.y);
         acc = xyzz_add_affine_inl(acc, a);
     }
 #endif

@@ -1,0 +1,242 @@
+// grouplaw_check.cpp -- TEST INFRASTRUCTURE: the device group law (csrc/field.h, csrc/curve.h) compiled
+// for the host, checked against the CPU oracle (oracle/, linked) under ASan/UBSan.
+//
+// The XYZZ additions the MSM kernels inline use lazily reduced intermediates (field.h "lazy forms":
+// unreduced subtractions feeding multiplications, one-pass X3).  This program runs exactly that code
+// on the host over sequences that hit every branch -- distinct points with random signs, P + P
+// (doubling), P + (-P) (infinity), infinity operands, non-canonical representatives v + p of every
+// coordinate -- and compares each result with the oracle's affine group law.  It also checks the lazy
+// field forms against the reduced operators on random and extreme (near 2p) values.
+// Build/run: tests/test_cpu_grouplaw.py (hipcc host-only, -fsanitize=address,undefined).
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+
+#include "curve.h"
+#include "oracle.h"
+
+using namespace mi;
+
+static std::mt19937_64 rng(12345);
+static int failures = 0;
+#define CHECK(cond, ...)                        \
+    do {                                        \
+        if (!(cond)) {                          \
+            std::printf("FAIL %s:%d ", __FILE__, __LINE__); \
+            std::printf(__VA_ARGS__);           \
+            std::printf("\n");                  \
+            failures++;                         \
+        }                                       \
+    } while (0)
+
+static fq_t fq_from_be(const uint8_t *p) {
+    fq32_t raw;
+    for (int i = 0; i < 12; i++) {
+        const uint8_t *q = p + 4 * (11 - i);
+        raw.v[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+    }
+    return fq_from_raw(raw);
+}
+static void fq_to_be(const fq_t &a, uint8_t *p) {
+    fq32_t raw = fq_to_raw(a);
+    for (int i = 0; i < 12; i++) {
+        uint32_t w = raw.v[i];
+        uint8_t *q = p + 4 * (11 - i);
+        q[0] = w >> 24, q[1] = w >> 16, q[2] = w >> 8, q[3] = w;
+    }
+}
+// the other representative of the same residue: v + p when v < p (limbs stay normalised)
+static fq_t alt_rep(const fq_t &a) {
+    fq_t c = fq_canon(a), r;
+    uint32_t carry = 0;
+    for (int i = 0; i < 14; i++) {
+        uint32_t t = c.v[i] + Fq29::P[i] + carry;
+        r.v[i] = i < 13 ? (t & Fq29::M) : t;
+        carry = i < 13 ? t >> 29 : 0;
+    }
+    return r;
+}
+static fq_t rand_fq() {  // uniform-ish value in [0, 2p) (random residue, random representative)
+    uint8_t b[48];
+    for (int i = 0; i < 48; i++) b[i] = (uint8_t)rng();
+    b[0] &= 0x0f;  // < 2^380 < p
+    fq_t a = fq_from_be(b);
+    return (rng() & 1) ? alt_rep(a) : fq_canon(a);
+}
+
+static void g1_to_bytes(const g1_affine_t &a, uint8_t out[96]) {
+    if (a.is_inf()) {
+        std::memset(out, 0, 96);
+        out[0] = 0x40;
+        return;
+    }
+    fq_to_be(a.x, out);
+    fq_to_be(a.y, out + 48);
+}
+static g1_affine_t g1_from_bytes(const uint8_t in[96]) {
+    if (in[0] & 0x40) return g1_affine_t::inf();
+    return {fq_from_be(in), fq_from_be(in + 48)};
+}
+static void rand_scalar(uint8_t s[32]) {
+    for (int i = 0; i < 32; i++) s[i] = (uint8_t)rng();
+    s[31] &= 0x3f;
+}
+static void neg_scalar(const uint8_t s[32], uint8_t out[32]) {  // r - s
+    static const uint32_t R[8] = {0x00000001u, 0xffffffffu, 0xfffe5bfeu, 0x53bda402u,
+                                  0x09a1d805u, 0x3339d808u, 0x299d7d48u, 0x73eda753u};
+    uint64_t bw = 0;
+    for (int i = 0; i < 8; i++) {
+        uint32_t si;
+        std::memcpy(&si, s + 4 * i, 4);
+        uint64_t d = (uint64_t)R[i] - si - bw;
+        uint32_t o = (uint32_t)d;
+        std::memcpy(out + 4 * i, &o, 4);
+        bw = (d >> 63) & 1;
+    }
+}
+
+static bool same_point(const g1_xyzz_t &acc, const uint8_t expect[96]) {
+    g1_affine_t a = xyzz_to_affine_inl(acc);
+    uint8_t got[96];
+    g1_to_bytes(a, got);
+    return std::memcmp(got, expect, 96) == 0;
+}
+
+static void check_fields() {
+    for (int it = 0; it < 20000; it++) {
+        fq_t a = rand_fq(), b = rand_fq(), c = rand_fq(), d = rand_fq();
+        if (it < 64) {  // extremes: 2p - 1 - small, 0, p
+            fq_t two_p_m1;
+            for (int i = 0; i < 14; i++) two_p_m1.v[i] = Fq29::P2[i];
+            two_p_m1.v[0] -= 1 + (it & 7);
+            if (it & 8) a = two_p_m1;
+            if (it & 16) b = two_p_m1;
+            if (it & 32) c = fq_t::zero();
+        }
+        // lazy subtraction / negation feed a multiplication exactly like the reduced forms
+        CHECK(fq_canon(fq_sub_lazy(a, b) * c) == fq_canon((a - b) * c), "sub_lazy it=%d", it);
+        CHECK(fq_canon(fq_neg_lazy(a) * c) == fq_canon((-a) * c), "neg_lazy it=%d", it);
+        CHECK(fq_canon(mul_add(a, fq_sub_lazy(b, c), fq_neg_lazy(d), a)) ==
+                  fq_canon(a * (b - c) - d * a), "mul_add lazy it=%d", it);
+        // one-pass X3 equals the three reduced operations, and stays in [0, 2p)
+        fq_t x3 = fq_x3(a, b, c);
+        CHECK(x3 == a - b - dbl(c), "x3 it=%d", it);
+        fq_t lim;
+        for (int i = 0; i < 14; i++) lim.v[i] = Fq29::P2[i];
+        bool below = false;
+        for (int i = 13; i >= 0; i--)
+            if (x3.v[i] != lim.v[i]) {
+                below = x3.v[i] < lim.v[i];
+                break;
+            }
+        CHECK(below, "x3 not reduced it=%d", it);
+        for (int i = 0; i < 13; i++) CHECK(x3.v[i] <= Fq29::M, "x3 limb it=%d", it);
+    }
+}
+
+static void check_g1_sequences() {
+    uint8_t gen[96];
+    or_g1_generator(gen);
+    for (int seq = 0; seq < 200; seq++) {
+        const int n = 1 + (int)(rng() % 24);
+        g1_xyzz_t acc = g1_xyzz_t::inf();
+        uint8_t expect[96];
+        std::memset(expect, 0, 96);
+        expect[0] = 0x40;
+        uint8_t prev_s[32];
+        bool have_prev = false;
+        for (int i = 0; i < n; i++) {
+            uint8_t s[32];
+            const int kind = (int)(rng() % 8);
+            if (kind == 0 && have_prev) std::memcpy(s, prev_s, 32);   // same point again: doubling branch
+            else if (kind == 1 && have_prev) neg_scalar(prev_s, s);    // its negation: infinity branch
+            else rand_scalar(s);
+            const bool inf = kind == 2;
+            const bool neg = rng() & 1;
+            uint8_t pt[96];
+            if (inf) {
+                std::memset(pt, 0, 96);
+                pt[0] = 0x40;
+            } else {
+                or_g1_mul(gen, s, pt);
+            }
+            g1_affine_t q = g1_from_bytes(pt);
+            if (rng() & 1) q.x = alt_rep(q.x);
+            if (rng() & 1 && !q.is_inf()) q.y = alt_rep(q.y);
+            if (neg) q.y = lazy_neg(q.y);  // what k_accum_level0 does for a negative digit
+            acc = xyzz_add_affine_inl(acc, q);
+            if (!inf) {
+                uint8_t term[96], sum[96];
+                if (neg) {
+                    uint8_t ns[32];
+                    neg_scalar(s, ns);
+                    or_g1_mul(gen, ns, term);
+                } else {
+                    std::memcpy(term, pt, 96);
+                }
+                or_g1_add(expect, term, sum);
+                std::memcpy(expect, sum, 96);
+                if (neg) neg_scalar(s, prev_s);  // prev_s = scalar of the point actually added
+                else std::memcpy(prev_s, s, 32);
+                have_prev = true;
+            }
+            CHECK(same_point(acc, expect), "g1 madd seq=%d step=%d kind=%d neg=%d", seq, i, kind, (int)neg);
+        }
+        // full XYZZ + XYZZ: acc + acc (doubling), acc + (-acc) (infinity), acc + fresh sum
+        g1_xyzz_t d = xyzz_add_inl(acc, acc);
+        uint8_t e2[96];
+        or_g1_add(expect, expect, e2);
+        CHECK(same_point(d, e2), "g1 add dbl seq=%d", seq);
+        g1_xyzz_t z = xyzz_add_inl(acc, xyzz_neg(acc));
+        CHECK(z.is_inf(), "g1 add inverse seq=%d", seq);
+        uint8_t s[32], pt[96], e3[96];
+        rand_scalar(s);
+        or_g1_mul(gen, s, pt);
+        g1_xyzz_t other = xyzz_add_affine_inl(g1_xyzz_t::inf(), g1_from_bytes(pt));
+        other = xyzz_dbl_inl(other);
+        uint8_t pt2[96];
+        or_g1_add(pt, pt, pt2);
+        or_g1_add(expect, pt2, e3);
+        CHECK(same_point(xyzz_add_inl(acc, other), e3), "g1 add seq=%d", seq);
+    }
+}
+
+// G2 through the generic (reduced) path the host uses for the window combination
+static void check_g2() {
+    uint8_t gen[192];
+    or_g2_generator(gen);
+    auto from = [](const uint8_t *p) -> g2_affine_t {
+        if (p[0] & 0x40) return g2_affine_t::inf();
+        return {{fq_from_be(p + 48), fq_from_be(p)}, {fq_from_be(p + 144), fq_from_be(p + 96)}};
+    };
+    for (int seq = 0; seq < 20; seq++) {
+        g2_xyzz_t acc = g2_xyzz_t::inf();
+        uint8_t expect[192];
+        std::memset(expect, 0, 192);
+        expect[0] = 0x40;
+        for (int i = 0; i < 6; i++) {
+            uint8_t s[32], pt[192], sum[192];
+            rand_scalar(s);
+            or_g2_mul(gen, s, pt);
+            acc = xyzz_add_affine_inl(acc, from(pt));
+            if (i == 3) acc = xyzz_add_affine_inl(acc, from(pt)), or_g2_add(expect, pt, sum), std::memcpy(expect, sum, 192);
+            or_g2_add(expect, pt, sum);
+            std::memcpy(expect, sum, 192);
+        }
+        g2_affine_t a = xyzz_to_affine_inl(acc), e = from(expect);
+        CHECK(a.x == e.x && a.y == e.y, "g2 seq=%d", seq);
+    }
+}
+
+int main() {
+    check_fields();
+    check_g1_sequences();
+    check_g2();
+    if (failures) {
+        std::printf("%d failures\n", failures);
+        return 1;
+    }
+    std::printf("grouplaw OK\n");
+    return 0;
+}
