@@ -12,6 +12,7 @@
 #include <thread>
 
 #include "../../include/mi355x_groth16.h"
+#include "poseidon_math.h"
 #include "prover.h"
 
 // Witness uploads (host z -> HBM) run on their own stream into one of two device slots, so the copy
@@ -348,6 +349,7 @@ void mi_ctx_destroy(mi_ctx *ctx) {
     ctx->up.release();
     mi::ntt_free_tables(ctx->c);
     mi::ctx_aux_free(ctx->c);
+    mi::poseidon_free(ctx->c);
     for (auto &b : ctx->c.scratch) b.release();
     if (ctx->normal) hipStreamDestroy(ctx->normal);
     if (ctx->high) hipStreamDestroy(ctx->high);
@@ -823,7 +825,7 @@ int mi_ntt_fr(mi_ctx *ctx, uint8_t *data32, unsigned log_n, int inverse, int cos
 }
 
 // ------------------------------------------------------------------------------------------
-int mi_ctx_get_stats(mi_ctx *ctx, double out[24]) {
+int mi_ctx_get_stats(mi_ctx *ctx, double out[30]) {
     return guard([&] {
         need(ctx && out, "null argument");
         CtxLock l(ctx);
@@ -831,8 +833,9 @@ int mi_ctx_get_stats(mi_ctx *ctx, double out[24]) {
         MI_HIP(hipStreamSynchronize(ctx->high));
         ctx->c.timer.resolve();
         const mi::Stats &s = ctx->c.stats;
-        const mi::KStat *ks[8] = {&s.accum_g1, &s.accum_g2, &s.msm_g1, &s.msm_g2, &s.sort, &s.ntt, &s.prove, &s.h2d};
-        for (int i = 0; i < 8; i++) {
+        const mi::KStat *ks[mi::Stats::NK] = {&s.accum_g1, &s.accum_g2, &s.msm_g1, &s.msm_g2, &s.sort,
+                                              &s.ntt,      &s.prove,    &s.h2d,    &s.poseidon, &s.tree_h2d};
+        for (int i = 0; i < mi::Stats::NK; i++) {
             out[3 * i] = ks[i]->ms;
             out[3 * i + 1] = (double)ks[i]->launches;
             out[3 * i + 2] = (double)ks[i]->units;
@@ -992,6 +995,283 @@ int mi_vk_write(const mi_srs *srs, const char *path) {
             throw;
         }
         if (fclose(f) != 0) throw std::runtime_error("close failed");
+    });
+}
+
+}  // extern "C"
+
+// ---- Poseidon and the stacked-PoRep Merkle trees -------------------------
+namespace {
+
+// Input uploads of the tree builders: columns / leaves go up in batches on a copy stream into two
+// device staging slots (scratch 21, 22), so batch k + 1's copy overlaps batch k's hashing.  Every
+// uploaded entry is checked canonical (< r) on the device (an Fr32 must represent a valid Fr,
+// core/fr32.hpp:36-40); the count is read once at the end.
+struct TreeUploads {
+    mi::Ctx &c;
+    hipStream_t cp = nullptr;
+    hipEvent_t ready[2] = {nullptr, nullptr}, freed[2] = {nullptr, nullptr};
+    bool used[2] = {false, false};
+    int *bad = nullptr;
+    explicit TreeUploads(mi::Ctx &ctx) : c(ctx) {
+        MI_HIP(hipStreamCreateWithFlags(&cp, hipStreamNonBlocking));
+        for (int k = 0; k < 2; k++) {
+            MI_HIP(hipEventCreateWithFlags(&ready[k], hipEventDisableTiming));
+            MI_HIP(hipEventCreateWithFlags(&freed[k], hipEventDisableTiming));
+        }
+        bad = c.scratch[23].as<int>(1);
+        MI_HIP(hipMemsetAsync(bad, 0, sizeof(int), c.stream));
+    }
+    ~TreeUploads() {
+        if (cp) hipStreamSynchronize(cp);
+        for (int k = 0; k < 2; k++) {
+            if (ready[k]) hipEventDestroy(ready[k]);
+            if (freed[k]) hipEventDestroy(freed[k]);
+        }
+        if (cp) hipStreamDestroy(cp);
+    }
+    // copy the n entries of each source (host) into slot k at [j * stride], then make the compute
+    // stream wait for them and check them
+    void put(int k, const uint8_t *const *src, unsigned nsrc, uint64_t first, uint64_t n, mi::fr_t *dst,
+             uint64_t stride) {
+        if (used[k]) MI_HIP(hipStreamWaitEvent(cp, freed[k], 0));
+        {
+            hipStream_t keep = c.stream;
+            c.stream = cp;
+            mi::ScopedTimer t(c, &c.stats.tree_h2d, 32ull * n * nsrc);
+            for (unsigned j = 0; j < nsrc; j++)
+                MI_HIP(hipMemcpyAsync(dst + j * stride, src[j] + 32 * first, 32 * n, hipMemcpyHostToDevice, cp));
+            c.stream = keep;
+        }
+        MI_HIP(hipEventRecord(ready[k], cp));
+        MI_HIP(hipStreamWaitEvent(c.stream, ready[k], 0));
+        for (unsigned j = 0; j < nsrc; j++) mi::fr_count_noncanonical(c, dst + j * stride, n, bad, c.stream);
+    }
+    void release(int k) {  // slot k may be overwritten once the compute stream is past this point
+        MI_HIP(hipEventRecord(freed[k], c.stream));
+        used[k] = true;
+    }
+    void check(const char *what) {
+        int h = 0;
+        MI_HIP(hipMemcpyAsync(&h, bad, sizeof(int), hipMemcpyDeviceToHost, c.stream));
+        MI_HIP(hipStreamSynchronize(c.stream));
+        if (h) throw std::invalid_argument(std::string(what) + ": entry is not a canonical Fr (>= r)");
+    }
+};
+
+uint64_t tree_batch() {  // columns / leaves per upload batch (MI_TREE_BATCH overrides, for tests)
+    const char *e = getenv("MI_TREE_BATCH");
+    const uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
+    return v ? v : (1ull << 21);
+}
+
+void check_dev_canonical(mi::Ctx &c, const mi::fr_t *d, uint64_t n, const char *what) {
+    int *bad = c.scratch[23].as<int>(1);
+    MI_HIP(hipMemsetAsync(bad, 0, sizeof(int), c.stream));
+    mi::fr_count_noncanonical(c, d, n, bad, c.stream);
+    int h = 0;
+    MI_HIP(hipMemcpyAsync(&h, bad, sizeof(int), hipMemcpyDeviceToHost, c.stream));
+    MI_HIP(hipStreamSynchronize(c.stream));
+    if (h) throw std::invalid_argument(std::string(what) + ": entry is not a canonical Fr (>= r)");
+}
+
+void need_tree_arity(unsigned a) { need(a == 2 || a == 4 || a == 8 || a == 11, "arity must be 2, 4, 8 or 11"); }
+
+}  // namespace
+
+extern "C" {
+
+int mi_poseidon_constants(unsigned arity, uint8_t *round_constants, uint8_t *mds, uint32_t shape[3]) {
+    return guard([&] {
+        need(shape != nullptr, "null shape");
+        need_tree_arity(arity);
+        const mi::PoseidonHost h = mi::poseidon_derive(arity, mi::poseidon_sbox_field());
+        shape[0] = h.t;
+        shape[1] = (uint32_t)h.rf;
+        shape[2] = (uint32_t)h.rp;
+        if (round_constants)
+            for (size_t i = 0; i < h.plain_rc.size(); i++) mi::fr_to_le(h.plain_rc[i], round_constants + 32 * i);
+        if (mds)
+            for (size_t i = 0; i < h.plain_mds.size(); i++) mi::fr_to_le(h.plain_mds[i], mds + 32 * i);
+    });
+}
+
+int mi_poseidon_hash_dev(mi_ctx *ctx, unsigned arity, const void *preimages_dev, uint64_t count, void *digests_dev) {
+    return guard([&] {
+        need(ctx && (count == 0 || (preimages_dev && digests_dev)), "null argument");
+        need_tree_arity(arity);
+        CtxLock l(ctx);
+        check_dev_canonical(ctx->c, (const mi::fr_t *)preimages_dev, count * arity, "poseidon preimage");
+        mi::poseidon_hash_dev(ctx->c, arity, (const mi::fr_t *)preimages_dev, count, arity, 1,
+                              (mi::fr_t *)digests_dev);
+    });
+}
+
+int mi_poseidon_hash(mi_ctx *ctx, unsigned arity, const uint8_t *preimages, uint64_t count, uint8_t *digests) {
+    return guard([&] {
+        need(ctx && (count == 0 || (preimages && digests)), "null argument");
+        need_tree_arity(arity);
+        CtxLock l(ctx);
+        if (!count) return;
+        mi::fr_t *in = ctx->c.scratch[21].as<mi::fr_t>(count * arity);
+        mi::fr_t *out = ctx->c.scratch[22].as<mi::fr_t>(count);
+        MI_HIP(hipMemcpyAsync(in, preimages, 32 * count * arity, hipMemcpyHostToDevice, ctx->c.stream));
+        check_dev_canonical(ctx->c, in, count * arity, "poseidon preimage");
+        mi::poseidon_hash_dev(ctx->c, arity, in, count, arity, 1, out);
+        MI_HIP(hipMemcpyAsync(digests, out, 32 * count, hipMemcpyDeviceToHost, ctx->c.stream));
+        MI_HIP(hipStreamSynchronize(ctx->c.stream));
+    });
+}
+
+int mi_tree_cache_size(uint64_t leaves, unsigned arity, unsigned rows_to_discard, uint64_t *out) {
+    return guard([&] {
+        need(out != nullptr, "null out");
+        *out = mi::tree_rows_size(leaves, arity, rows_to_discard);
+    });
+}
+
+int mi_tree_build_dev(mi_ctx *ctx, unsigned arity, const void *leaves_dev, uint64_t leaves, unsigned rows_to_discard,
+                      void *tree_dev) {
+    return guard([&] {
+        need(ctx && leaves_dev && tree_dev, "null argument");
+        need_tree_arity(arity);
+        CtxLock l(ctx);
+        mi::tree_rows_size(leaves, arity, rows_to_discard);
+        check_dev_canonical(ctx->c, (const mi::fr_t *)leaves_dev, leaves, "tree leaf");
+        mi::fr_t *tmp = ctx->c.scratch[22].as<mi::fr_t>(2 * (leaves / arity) + 1);
+        mi::tree_build_dev(ctx->c, arity, (const mi::fr_t *)leaves_dev, leaves, rows_to_discard,
+                           (mi::fr_t *)tree_dev, tmp);
+        MI_HIP(hipStreamSynchronize(ctx->c.stream));
+    });
+}
+
+int mi_tree_build(mi_ctx *ctx, unsigned arity, const uint8_t *leaves, uint64_t n, unsigned rows_to_discard,
+                  uint8_t *tree_out) {
+    return guard([&] {
+        need(ctx && leaves && tree_out, "null argument");
+        need_tree_arity(arity);
+        CtxLock l(ctx);
+        mi::Ctx &c = ctx->c;
+        const uint64_t tsz = mi::tree_rows_size(n, arity, rows_to_discard);
+        mi::fr_t *leaf_dev = c.scratch[20].as<mi::fr_t>(n + tsz);
+        mi::fr_t *rows = leaf_dev + n;
+        {
+            TreeUploads up(c);
+            const uint64_t B = tree_batch();
+            int k = 0;
+            for (uint64_t b = 0; b < n; b += B, k ^= 1) {
+                const uint64_t nb = std::min(B, n - b);
+                const uint8_t *src[1] = {leaves};
+                up.put(k, src, 1, b, nb, leaf_dev + b, 0);
+                up.release(k);
+            }
+            up.check("tree leaf");
+        }
+        mi::fr_t *tmp = c.scratch[22].as<mi::fr_t>(2 * (n / arity) + 1);
+        mi::tree_build_dev(c, arity, leaf_dev, n, rows_to_discard, rows, tmp);
+        MI_HIP(hipMemcpyAsync(tree_out, rows, 32 * tsz, hipMemcpyDeviceToHost, c.stream));
+        MI_HIP(hipStreamSynchronize(c.stream));
+    });
+}
+
+// ColumnTreeBuilder::add_final_columns: base = column hashes (nodes), tree = every row above the base
+int mi_tree_c_build_dev(mi_ctx *ctx, unsigned layers, uint64_t nodes, const void *labels_dev, unsigned tree_arity,
+                        void *base_dev, void *tree_dev) {
+    return guard([&] {
+        need(ctx && labels_dev && base_dev && tree_dev, "null argument");
+        need_tree_arity(layers);
+        need_tree_arity(tree_arity);
+        CtxLock l(ctx);
+        mi::Ctx &c = ctx->c;
+        mi::tree_rows_size(nodes, tree_arity, 0);
+        check_dev_canonical(c, (const mi::fr_t *)labels_dev, nodes * layers, "layer label");
+        mi::poseidon_hash_dev(c, layers, (const mi::fr_t *)labels_dev, nodes, 1, nodes, (mi::fr_t *)base_dev);
+        mi::tree_build_dev(c, tree_arity, (const mi::fr_t *)base_dev, nodes, 0, (mi::fr_t *)tree_dev, nullptr);
+        MI_HIP(hipStreamSynchronize(c.stream));
+    });
+}
+
+int mi_tree_c_build(mi_ctx *ctx, unsigned layers, uint64_t nodes, const uint8_t *const *layer_labels,
+                    unsigned tree_arity, uint8_t *base_out, uint8_t *tree_out) {
+    return guard([&] {
+        need(ctx && layer_labels && base_out && tree_out, "null argument");
+        need_tree_arity(layers);
+        need_tree_arity(tree_arity);
+        for (unsigned j = 0; j < layers; j++) need(layer_labels[j] != nullptr, "null layer");
+        CtxLock l(ctx);
+        mi::Ctx &c = ctx->c;
+        const uint64_t tsz = mi::tree_rows_size(nodes, tree_arity, 0);
+        mi::fr_t *base = c.scratch[20].as<mi::fr_t>(nodes + tsz);
+        mi::fr_t *rows = base + nodes;
+        const uint64_t B = std::min<uint64_t>(tree_batch(), nodes);
+        mi::fr_t *stage[2] = {c.scratch[21].as<mi::fr_t>(B * layers), c.scratch[22].as<mi::fr_t>(B * layers)};
+        {
+            TreeUploads up(c);
+            int k = 0;
+            for (uint64_t b = 0; b < nodes; b += B, k ^= 1) {
+                const uint64_t nb = std::min(B, nodes - b);
+                up.put(k, layer_labels, layers, b, nb, stage[k], B);
+                mi::poseidon_hash_dev(c, layers, stage[k], nb, 1, B, base + b);
+                up.release(k);
+            }
+            up.check("layer label");
+        }
+        mi::tree_build_dev(c, tree_arity, base, nodes, 0, rows, nullptr);
+        MI_HIP(hipMemcpyAsync(base_out, base, 32 * nodes, hipMemcpyDeviceToHost, c.stream));
+        MI_HIP(hipMemcpyAsync(tree_out, rows, 32 * tsz, hipMemcpyDeviceToHost, c.stream));
+        MI_HIP(hipStreamSynchronize(c.stream));
+    });
+}
+
+// generate_tree_r_last: replica = label + data (written back over data), then TreeBuilder over it
+int mi_tree_r_last_build_dev(mi_ctx *ctx, uint64_t nodes, const void *labels_dev, void *data_dev, unsigned tree_arity,
+                             unsigned rows_to_discard, void *tree_dev) {
+    return guard([&] {
+        need(ctx && labels_dev && data_dev && tree_dev, "null argument");
+        need_tree_arity(tree_arity);
+        CtxLock l(ctx);
+        mi::Ctx &c = ctx->c;
+        mi::tree_rows_size(nodes, tree_arity, rows_to_discard);
+        check_dev_canonical(c, (const mi::fr_t *)labels_dev, nodes, "last-layer label");
+        check_dev_canonical(c, (const mi::fr_t *)data_dev, nodes, "sector data node");
+        mi::encode_dev(c, (const mi::fr_t *)labels_dev, (mi::fr_t *)data_dev, nodes);
+        mi::fr_t *tmp = c.scratch[22].as<mi::fr_t>(2 * (nodes / tree_arity) + 1);
+        mi::tree_build_dev(c, tree_arity, (const mi::fr_t *)data_dev, nodes, rows_to_discard, (mi::fr_t *)tree_dev, tmp);
+        MI_HIP(hipStreamSynchronize(c.stream));
+    });
+}
+
+int mi_tree_r_last_build(mi_ctx *ctx, uint64_t nodes, const uint8_t *last_layer_labels, uint8_t *data,
+                         unsigned tree_arity, unsigned rows_to_discard, uint8_t *tree_out) {
+    return guard([&] {
+        need(ctx && last_layer_labels && data && tree_out, "null argument");
+        need_tree_arity(tree_arity);
+        CtxLock l(ctx);
+        mi::Ctx &c = ctx->c;
+        const uint64_t tsz = mi::tree_rows_size(nodes, tree_arity, rows_to_discard);
+        mi::fr_t *leaves = c.scratch[20].as<mi::fr_t>(nodes + tsz);
+        mi::fr_t *rows = leaves + nodes;
+        const uint64_t B = std::min<uint64_t>(tree_batch(), nodes);
+        mi::fr_t *stage[2] = {c.scratch[21].as<mi::fr_t>(B), c.scratch[22].as<mi::fr_t>(B)};
+        {
+            TreeUploads up(c);
+            int k = 0;
+            for (uint64_t b = 0; b < nodes; b += B, k ^= 1) {
+                const uint64_t nb = std::min(B, nodes - b);
+                const uint8_t *lab[1] = {last_layer_labels}, *dat[1] = {data};
+                up.put(k, lab, 1, b, nb, stage[k], 0);
+                up.put(k, dat, 1, b, nb, leaves + b, 0);
+                mi::encode_dev(c, stage[k], leaves + b, nb);
+                up.release(k);
+            }
+            up.check("last-layer label / sector data node");
+        }
+        // the replica goes back to the caller (the reference overwrites the data buffer in place)
+        MI_HIP(hipMemcpyAsync(data, leaves, 32 * nodes, hipMemcpyDeviceToHost, c.stream));
+        mi::fr_t *tmp = c.scratch[22].as<mi::fr_t>(2 * (nodes / tree_arity) + 1);
+        mi::tree_build_dev(c, tree_arity, leaves, nodes, rows_to_discard, rows, tmp);
+        MI_HIP(hipMemcpyAsync(tree_out, rows, 32 * tsz, hipMemcpyDeviceToHost, c.stream));
+        MI_HIP(hipStreamSynchronize(c.stream));
     });
 }
 

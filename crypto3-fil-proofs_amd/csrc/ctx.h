@@ -81,13 +81,17 @@ struct Stats {
     KStat ntt;                 // NTT passes (all launches of one transform)
     KStat prove;               // whole Groth16 prove (device part through host assembly)
     KStat h2d;                 // witness upload + canonical check on the copy stream (units = bytes)
+    KStat poseidon;            // k_poseidon launches (units = hashes)
+    KStat tree_h2d;            // tree builders' label / data uploads (units = bytes)
     uint64_t madds_g1 = 0, madds_g2 = 0;  // mixed additions issued by k_accum_level0 (non-zero digits)
+    static constexpr int NK = 10;
     void merge(const Stats &o) {
         madds_g1 += o.madds_g1;
         madds_g2 += o.madds_g2;
-        KStat *d[] = {&accum_g1, &accum_g2, &msm_g1, &msm_g2, &sort, &ntt, &prove, &h2d};
-        const KStat *x[] = {&o.accum_g1, &o.accum_g2, &o.msm_g1, &o.msm_g2, &o.sort, &o.ntt, &o.prove, &o.h2d};
-        for (int i = 0; i < 8; i++) {
+        KStat *d[] = {&accum_g1, &accum_g2, &msm_g1, &msm_g2, &sort, &ntt, &prove, &h2d, &poseidon, &tree_h2d};
+        const KStat *x[] = {&o.accum_g1, &o.accum_g2, &o.msm_g1, &o.msm_g2, &o.sort, &o.ntt, &o.prove, &o.h2d,
+                            &o.poseidon, &o.tree_h2d};
+        for (int i = 0; i < NK; i++) {
             d[i]->ms += x[i]->ms;
             d[i]->launches += x[i]->launches;
             d[i]->units += x[i]->units;

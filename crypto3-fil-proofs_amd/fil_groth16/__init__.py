@@ -10,3 +10,4 @@ from .core import (FR_MODULUS, PROOF_BYTES, SHARE_BYTES, VK_BYTES, Circuit, Cont
                    params_inspect, pairing, prove, prove_batch, prove_share, trapdoor_dlogs, verify, verify_batch)
 from .compound import (MultiProof, partition_count, get_partitions_for_window_post,  # noqa: F401
                        circuit_proofs, seal_commit_phase2_proofs)
+from . import tree  # noqa: F401  (Poseidon + tree C / tree R-last builders)

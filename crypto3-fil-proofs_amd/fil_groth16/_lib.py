@@ -24,6 +24,9 @@ EXPORTS = [
     "mi_groth16_verify", "mi_groth16_verify_batch", "mi_pairing",
     "mi_groth16_prove_share", "mi_groth16_prove_share_dev", "mi_groth16_assemble",
     "mi_host_alloc", "mi_host_free", "mi_groth16_verify_batch_seeded",
+    "mi_poseidon_constants", "mi_poseidon_hash", "mi_poseidon_hash_dev", "mi_tree_cache_size",
+    "mi_tree_build", "mi_tree_build_dev", "mi_tree_c_build", "mi_tree_c_build_dev",
+    "mi_tree_r_last_build", "mi_tree_r_last_build_dev",
 ]
 
 _lib = None
@@ -112,6 +115,16 @@ def lib():
         "mi_host_alloc": ([u64, pp], c_int),
         "mi_host_free": ([vp], None),
         "mi_pairing": ([u8p, u8p, vp], c_int),
+        "mi_poseidon_constants": ([ctypes.c_uint, vp, vp, vp], c_int),
+        "mi_poseidon_hash": ([vp, ctypes.c_uint, vp, u64, vp], c_int),
+        "mi_poseidon_hash_dev": ([vp, ctypes.c_uint, vp, u64, vp], c_int),
+        "mi_tree_cache_size": ([u64, ctypes.c_uint, ctypes.c_uint, vp], c_int),
+        "mi_tree_build": ([vp, ctypes.c_uint, vp, u64, ctypes.c_uint, vp], c_int),
+        "mi_tree_build_dev": ([vp, ctypes.c_uint, vp, u64, ctypes.c_uint, vp], c_int),
+        "mi_tree_c_build": ([vp, ctypes.c_uint, u64, vp, ctypes.c_uint, vp, vp], c_int),
+        "mi_tree_c_build_dev": ([vp, ctypes.c_uint, u64, vp, ctypes.c_uint, vp, vp], c_int),
+        "mi_tree_r_last_build": ([vp, u64, vp, vp, ctypes.c_uint, ctypes.c_uint, vp], c_int),
+        "mi_tree_r_last_build_dev": ([vp, u64, vp, vp, ctypes.c_uint, ctypes.c_uint, vp], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -239,14 +239,62 @@ void mi_synth_free(mi_synth *s);
  * stay on inside timed regions).  out = 8 records x {ms, launches, units}:
  *   0 k_accum_level0<G1> (units = points)   1 k_accum_level0<G2>   2 whole G1 MSM   3 whole G2 MSM
  *   4 digits + sort + bucket bounds          5 NTT transforms (units = elements)   6 whole prove (units = constraints)
- *   7 witness H2D upload + canonical check on the copy stream (units = bytes) */
-int mi_ctx_get_stats(mi_ctx *ctx, double out[24]);
+ *   7 witness H2D upload + canonical check on the copy stream (units = bytes)
+ *   8 k_poseidon launches (units = hashes)  9 tree builders' label / data uploads (units = bytes) */
+int mi_ctx_get_stats(mi_ctx *ctx, double out[30]);
 int mi_ctx_reset_stats(mi_ctx *ctx);
 /* work counters since the last reset: out[0] / out[1] = mixed additions (non-zero signed digits)
  * issued by the G1 / G2 bucket accumulation -- the unit of the VALU roofline */
 int mi_ctx_get_work(mi_ctx *ctx, uint64_t out[2]);
 /* msm window size chosen for n points (exposed for tests / reports) */
 unsigned mi_msm_window_bits(uint64_t n);
+
+/* ---- Poseidon and the stacked-PoRep Merkle trees ---------------------------
+ * Poseidon over Fr (BLS12-381 scalar field): state [2^arity - 1, x_1 .. x_arity], x^5, 8 full rounds and
+ * 55 / 56 / 57 / 57 partial rounds for arity 2 / 4 / 8 / 11, Cauchy MDS 1 / (i + j + t), Grain-LFSR round
+ * constants; digest = state[1].  Inputs must be canonical Fr (< r), MI_ERR_ARG otherwise.  Trees are
+ * stored row by row, bottom-up (base row excluded), the layout of the reference's DiskTree / LCTree
+ * stores.  Replaces:
+ *   mi_poseidon_hash      <- crypto3::hash<crypto3::hashes::poseidon<FieldType, A, A>> as called by
+ *                            hash_single_column (libs/storage/include/nil/filecoin/storage/proofs/porep/
+ *                            stacked/vanilla/hash.hpp:37-47) and the tree hasher ([NOT IN TREE])
+ *   mi_tree_c_build       <- generate_tree_c_gpu / ColumnTreeBuilder<ColumnArity, TreeArity>::
+ *                            add_final_columns -> (base_data, tree_data)  (porep/stacked/vanilla/proof.hpp:
+ *                            383-590; use_gpu_column_builder, core/configuration.hpp:51-56)
+ *   mi_tree_r_last_build  <- generate_tree_r_last with use_gpu_tree_builder: encode(key, data) per node,
+ *                            then TreeBuilder<Arity>::add_final_leaves -> tree_data of
+ *                            get_merkle_tree_cache_size(leafs, arity, rows_to_discard) entries
+ *                            (proof.hpp:630-760)
+ *   mi_tree_build         <- TreeBuilder<Arity>::add_final_leaves over given leaves (same file)
+ *   mi_tree_cache_size    <- get_merkle_tree_cache_size (merkletree; called at proof.hpp:717) */
+/* (t, R_F, R_P) in shape; with non-null buffers also the (R_F + R_P) * t round constants and the t * t MDS
+ * matrix, canonical 32-byte LE (tests / external checks) */
+int mi_poseidon_constants(unsigned arity, uint8_t *round_constants, uint8_t *mds, uint32_t shape[3]);
+/* digests[i] = Poseidon_arity(preimages[i * arity .. i * arity + arity - 1]) (32 B LE each) */
+int mi_poseidon_hash(mi_ctx *ctx, unsigned arity, const uint8_t *preimages, uint64_t count, uint8_t *digests);
+int mi_poseidon_hash_dev(mi_ctx *ctx, unsigned arity, const void *preimages_dev, uint64_t count, void *digests_dev);
+/* entries of the cached rows: every row above the base except the rows_to_discard lowest of them */
+int mi_tree_cache_size(uint64_t leaves, unsigned arity, unsigned rows_to_discard, uint64_t *out);
+int mi_tree_build(mi_ctx *ctx, unsigned arity, const uint8_t *leaves, uint64_t leaf_count, unsigned rows_to_discard,
+                  uint8_t *tree_out);
+int mi_tree_build_dev(mi_ctx *ctx, unsigned arity, const void *leaves_dev, uint64_t leaf_count,
+                      unsigned rows_to_discard, void *tree_dev);
+/* tree C: column j = (layer_labels[0][j], .., layer_labels[layers - 1][j]) hashed with Poseidon_layers
+ * (layers = 2 or 11 in Filecoin) into base_out[j]; tree_out = all rows above the base of the
+ * tree_arity-ary Poseidon tree over them (mi_tree_cache_size(nodes, tree_arity, 0) entries).
+ * Host variant: labels are streamed up in batches overlapped with the hashing.
+ * Device variant: labels_dev is layer-major (layer l at entry l * nodes). */
+int mi_tree_c_build(mi_ctx *ctx, unsigned layers, uint64_t nodes, const uint8_t *const *layer_labels,
+                    unsigned tree_arity, uint8_t *base_out, uint8_t *tree_out);
+int mi_tree_c_build_dev(mi_ctx *ctx, unsigned layers, uint64_t nodes, const void *labels_dev, unsigned tree_arity,
+                        void *base_dev, void *tree_dev);
+/* tree R-last: data[j] <- last_layer_labels[j] + data[j] (mod r: the replica, written back over data),
+ * then the tree_arity-ary Poseidon tree over the replica; tree_out receives
+ * mi_tree_cache_size(nodes, tree_arity, rows_to_discard) entries */
+int mi_tree_r_last_build(mi_ctx *ctx, uint64_t nodes, const uint8_t *last_layer_labels, uint8_t *data,
+                         unsigned tree_arity, unsigned rows_to_discard, uint8_t *tree_out);
+int mi_tree_r_last_build_dev(mi_ctx *ctx, uint64_t nodes, const void *labels_dev, void *data_dev, unsigned tree_arity,
+                             unsigned rows_to_discard, void *tree_dev);
 
 #ifdef __cplusplus
 }

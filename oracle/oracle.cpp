@@ -940,6 +940,54 @@ unsigned domain_log(uint64_t rows) {
 
 extern "C" {
 
+/* Poseidon, literal form (oracle/poseidon_ref.py restated with 64-bit-limb Montgomery Fr and OpenMP, for
+ * the tree builders' CPU baseline and large checks).  PARITY UNPINNED.  rc: (rf + rp) * t canonical
+ * constants, mds: t * t (state' = state * M), tag = 2^arity - 1, digest = state[1];
+ * out[i] = hash(in[i * arity .. i * arity + arity - 1]).  Returns -1 on a non-canonical input. */
+int or_poseidon_hash(unsigned arity, const uint8_t *rc32, const uint8_t *mds32, unsigned rf, unsigned rp,
+                     const uint8_t *in32, uint64_t n, uint8_t *out32) {
+    const unsigned t = arity + 1;
+    if (t > 17) return -1;
+    std::vector<fr> rc((size_t)(rf + rp) * t), m((size_t)t * t);
+    for (size_t i = 0; i < rc.size(); i++) rc[i] = fr_from_le(rc32 + 32 * i);
+    for (size_t i = 0; i < m.size(); i++) m[i] = fr_from_le(mds32 + 32 * i);
+    uint8_t tagb[32] = {0};
+    const uint64_t tag = (1ull << arity) - 1;
+    memcpy(tagb, &tag, 8);
+    const fr ftag = fr_from_le(tagb);
+    int bad = 0;
+    const int nt = nthreads();
+#pragma omp parallel for num_threads(nt) schedule(static) reduction(| : bad) if (n >= 64)
+    for (int64_t i = 0; i < (int64_t)n; i++) {
+        fr s[17], nx[17];
+        s[0] = ftag;
+        for (unsigned j = 0; j < arity; j++) {
+            uint64_t raw[4];
+            memcpy(raw, in32 + 32 * ((uint64_t)i * arity + j), 32);
+            if (!FR::is_canonical(raw)) bad |= 1;
+            s[j + 1] = FR::from_raw(raw);
+        }
+        unsigned k = 0;
+        for (unsigned r = 0; r < rf + rp; r++) {
+            const bool full = r < rf / 2 || r >= rf / 2 + rp;
+            for (unsigned j = 0; j < t; j++) s[j] = FR::add(s[j], rc[k + j]);
+            k += t;
+            for (unsigned j = 0; j < (full ? t : 1u); j++) {
+                fr x2 = FR::mul(s[j], s[j]);
+                s[j] = FR::mul(FR::mul(x2, x2), s[j]);
+            }
+            for (unsigned j = 0; j < t; j++) {
+                fr acc = FR::zero();
+                for (unsigned q = 0; q < t; q++) acc = FR::add(acc, FR::mul(s[q], m[(size_t)q * t + j]));
+                nx[j] = acc;
+            }
+            for (unsigned j = 0; j < t; j++) s[j] = nx[j];
+        }
+        fr_to_le(s[1], out32 + 32 * (uint64_t)i);
+    }
+    return bad ? -1 : 0;
+}
+
 void or_set_threads(int n) { g_threads = n; }
 int or_get_threads(void) { return nthreads(); }
 

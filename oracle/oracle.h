@@ -109,6 +109,9 @@ int or_groth16_verify(const uint8_t vk864[864], const uint8_t *ic96, uint64_t nu
                       const uint8_t *inputs32 /* num_inputs*32 incl. ONE */, const uint8_t raw[384]);
 
 /* threads used by the oracle (OpenMP); 0 = library default */
+/* Poseidon, literal form (constants from oracle/poseidon_ref.py); out[i] = hash of in[i*arity ..] */
+int or_poseidon_hash(unsigned arity, const uint8_t *rc32, const uint8_t *mds32, unsigned rf, unsigned rp,
+                     const uint8_t *in32, uint64_t n, uint8_t *out32);
 void or_set_threads(int n);
 int or_get_threads(void);
 

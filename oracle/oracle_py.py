@@ -167,6 +167,25 @@ def set_threads(n):
     lib().or_set_threads(n)
 
 
+def poseidon_hash(arity: int, preimages: bytes) -> bytes:
+    """C restatement of oracle/poseidon_ref.py (literal rounds, OpenMP): digests of consecutive groups of
+    `arity` canonical 32-byte LE inputs."""
+    import poseidon_ref as P
+
+    h = P.poseidon(arity)
+    rc = b"".join(P.fr_to_bytes(x) for x in h.rc)
+    mds = b"".join(P.fr_to_bytes(x) for row in h.m for x in row)
+    n = len(preimages) // (32 * arity)
+    out = _buf(32 * max(n, 1))
+    L = lib()
+    L.or_poseidon_hash.argtypes = [ctypes.c_uint, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint, ctypes.c_uint,
+                                   ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p]
+    rc_ = L.or_poseidon_hash(arity, rc, mds, h.r_f, h.r_p, bytes(preimages), n, out)
+    if rc_ != 0:
+        raise ValueError("non-canonical Poseidon input")
+    return out.raw[:32 * n]
+
+
 # ------------------------------------------------------------------ R1CS / Groth16
 class R1CS(ctypes.Structure):
     _fields_ = [
