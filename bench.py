@@ -143,6 +143,61 @@ def cpu_baseline(args, fg, synth_mod, ctx):
     return out
 
 
+def tree_c_leg(args, fg, ctx, device, world):
+    """tree C of one sub-tree (device-resident labels): column hashes + arity-8 tree, with its VALU
+    roofline (v_mad_u64_u32 issue over the MADs of every Poseidon it runs) and the oracle's CPU rate."""
+    import numpy as np
+    import torch
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from tree_bench import MAD_RATE as TREE_MAD_RATE, mads_per_hash
+
+    n, L = 1 << args.tree_log_nodes, 11
+    g = torch.Generator(device=device)
+    g.manual_seed(3)
+    labels = torch.randint(0, 2 ** 62, (L * n, 4), dtype=torch.int64, device=device, generator=g)
+    labels[:, 3] &= 0x0FFFFFFFFFFFFFFF  # < 2^252: canonical Fr
+    base = torch.empty((n, 4), dtype=torch.int64, device=device)
+    tree = torch.empty((fg.tree.get_merkle_tree_cache_size(n, 8, 0), 4), dtype=torch.int64, device=device)
+    b = fg.tree.ColumnTreeBuilder(ctx, L, 8)
+    b.add_final_columns_dev(labels.data_ptr(), n, base.data_ptr(), tree.data_ptr())
+    ctx.synchronize()
+    ctx.reset_stats()
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        b.add_final_columns_dev(labels.data_ptr(), n, base.data_ptr(), tree.data_ptr())
+    ctx.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    st = ctx.stats()["poseidon"]
+    node_hashes = (n - 1) // 7  # arity-8 tree over n leaves
+    mads = n * mads_per_hash(11) + node_hashes * mads_per_hash(8)
+    kern_s = st["ms"] * 1e-3 / reps
+    out = {"workload": f"tree C of one sub-tree: 2^{args.tree_log_nodes} columns x 11 layers -> Poseidon-11 "
+                       f"column hashes -> arity-8 Poseidon tree (device-resident labels)",
+           "columns_per_s": n / dt, "ms_per_tree": dt * 1e3, "kernel_ms_per_tree": kern_s * 1e3,
+           "valu_roofline": {"kernel": "k_poseidon<12> + k_poseidon<9>", "bound": "valu (v_mad_u64_u32 issue)",
+                             "mads_per_tree": mads, "achieved_mads_per_s": mads / kern_s,
+                             "peak_mads_per_s": TREE_MAD_RATE, "frac": mads / kern_s / TREE_MAD_RATE},
+           "hbm_algorithmic_GBps": (n * (32 * L + 32) + node_hashes * 9 * 32) / kern_s / 1e9}
+    if world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle_py
+
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+        oracle_py.set_threads(threads)
+        m = 4096
+        sample = labels.view(L, n, 4)[:, :m].permute(1, 0, 2).contiguous().cpu().numpy().view(np.uint8).tobytes()
+        t0 = time.perf_counter()
+        oracle_py.poseidon_hash(11, sample)
+        dtc = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": m / dtc, "unit": "column hashes/s", "cores": threads, "kind": "port",
+                               "sample": f"{m} Poseidon-11 column hashes of the same labels by the oracle (literal "
+                                         f"rounds, 64-bit-limb Montgomery, OpenMP) on {cpu_model()}"}
+    del labels, base, tree
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -160,6 +215,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-device-resident", action="store_true", help="skip the secondary HBM-resident run")
     ap.add_argument("--stats-json", default=None, help="write per-kernel timers here")
+    ap.add_argument("--tree-log-nodes", type=int, default=21,
+                    help="secondary: tree C over 2^N columns x 11 layers (N a multiple of 3; 0 skips)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -311,6 +368,12 @@ def main():
         del x
     del sc_dev, pts
 
+    # tree C over one 2^tree_log_nodes-node sub-tree (device-resident labels), and the
+    # oracle's CPU Poseidon on a sample of the same columns
+    tree = None
+    if args.tree_log_nodes and rank == 0:
+        tree = tree_c_leg(args, fg, ctx, device, world)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
@@ -414,6 +477,7 @@ def main():
                      f"peak = v_mad_u64_u32 issue rate / {FQ_MUL_MADS} MADs",
         },
         "cpu_baseline": cpu,
+        "tree_c": tree,
         "timers_ms": {k: round(v["ms"], 3) for k, v in stats.items()},
         "setup_s": {"synth": t_synth, "circuit_load": t_load, "srs": t_srs},
         "multiproof_bytes": 192 * len(proofs),

@@ -9,6 +9,9 @@
   seal_commit_phase2_proofs       the C2 tail (api/seal.hpp:296-313): circuit_proofs -> MultiProof ->
                                   self-verification ("post-seal verification sanity check failed")
   get_partitions_for_window_post  libs/filecoin/src/api/post.cpp:37-46
+  generate_window_post_proofs     generate_window_post (api/post.hpp:305-348): partitions from the sector
+                                  count, FallbackPoStCompound::prove over them with post_config.priority
+  generate_winning_post_proof     generate_winning_post (api/post.hpp:178-230): one partition
   shard_partitions                one process per GPU: partition k goes to rank k % world
 """
 from .core import PROOF_BYTES, prove, verify_batch
@@ -86,3 +89,33 @@ def seal_commit_phase2_proofs(ctx, pk, circuit, witnesses, blindings, num_inputs
 def shard_partitions(num_partitions: int, rank: int, world: int):
     """Partition indices proven by ``rank`` (round-robin: 10 partitions on 8 GPUs -> 2 rounds on 2)."""
     return list(range(rank, num_partitions, world))
+
+
+def _post_partitions(num_sectors: int, sector_count: int) -> int:
+    """The partition count FallbackPoStCompound::setup receives: get_partitions_for_window_post's
+    optional, unset (None) meaning one partition (compound_proof.hpp:85-87 partition_count(-1) = 1)."""
+    p = get_partitions_for_window_post(num_sectors, sector_count)
+    return partition_count(-1 if p is None else p)
+
+
+def generate_window_post_proofs(ctx, pk, circuit, num_sectors: int, sector_count: int, witnesses, blindings,
+                                priority: bool = True) -> bytes:
+    """api/post.hpp:305-348: the Window-PoSt SNARK.  ``witnesses`` holds one synthesised assignment per
+    partition (circuit synthesis is upstream of the boundary); their number must equal the partition
+    count derived from (num_sectors, sector_count) exactly as the reference derives it.  Proofs are made
+    on the high-priority stream when ``priority`` (post_config.priority, types/post_config.hpp:41-42) and
+    returned as the P x 192-byte proof vector (proof.to_vec())."""
+    parts = _post_partitions(num_sectors, sector_count)
+    if len(witnesses) != parts:
+        raise ValueError(f"window post: {parts} partition(s) for {num_sectors} sectors of {sector_count}, "
+                         f"got {len(witnesses)} witness(es)")
+    return MultiProof(circuit_proofs(ctx, pk, circuit, witnesses, blindings, priority=priority)).to_bytes()
+
+
+def generate_winning_post_proof(ctx, pk, circuit, num_replicas: int, sector_count: int, witness, blinding,
+                                priority: bool = False) -> bytes:
+    """api/post.hpp:178-230: the Winning-PoSt SNARK -- exactly ``sector_count`` replicas ("invalid amount
+    of replicas"), partitions unset (one partition), one 192-byte proof."""
+    if num_replicas != sector_count:
+        raise ValueError("invalid amount of replicas")
+    return MultiProof(circuit_proofs(ctx, pk, circuit, [witness], [blinding], priority=priority)).to_bytes()

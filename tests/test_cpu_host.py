@@ -141,3 +141,13 @@ def test_cpp_host_layer_builds_and_fails_loudly_without_gpu():
         pytest.skip("GPU present (covered by tests/test_gpu_cpp.py)")
     r = subprocess.run([exe, "8", "2"], capture_output=True, text=True)
     assert r.returncode == 3 and "no HIP device" in r.stderr
+
+
+def test_post_partition_derivation():
+    # generate_window_post: get_partitions_for_window_post's optional -> FallbackPoStCompound partitions
+    # (unset = partition_count(-1) = 1); api/post.hpp:319-322, src/api/post.cpp:37-46
+    from fil_groth16.compound import _post_partitions
+    assert _post_partitions(10 * 2349, 2349) == 10
+    assert _post_partitions(10 * 2349 + 2348, 2349) == 10
+    assert _post_partitions(2349, 2349) == 1
+    assert _post_partitions(5, 2349) == 1

@@ -227,6 +227,31 @@ def test_seal_commit_phase2_self_verifies(ctx, oracle):
         fg.seal_commit_phase2_proofs(ctx, pk, gc, [zb, bytes(bad), zb], blind, n_in)
 
 
+def test_window_and_winning_post_drivers(ctx, oracle):
+    """api/post.hpp:305-348 / :178-230: the Window-PoSt driver proves one partition per
+    get_partitions_for_window_post (sectors / 2349 per partition), on the high-priority stream, and
+    each proof equals the oracle's; Winning-PoSt proves exactly one partition."""
+    n_in, n_aux, rows, z = circuits.random_circuit(63, 400, n_in=4)
+    oc, gc = _load(ctx, oracle, n_in, n_aux, rows, z)
+    tox = circuits.toxic()
+    pk = fg.generate_random_parameters(ctx, gc, tox)
+    op = oracle.OracleParams(oc, tox)
+    zb = circuits.z_bytes(z)
+    blind = [(31 + k, 41 + k) for k in range(3)]
+    buf = fg.generate_window_post_proofs(ctx, pk, gc, 3 * 2349 + 7, 2349, [zb] * 3, blind)
+    assert len(buf) == 3 * 192
+    for k, (r, s) in enumerate(blind):
+        assert buf[192 * k:192 * (k + 1)] == op.prove(zb, r, s)[0]
+    with pytest.raises(ValueError, match="partition"):
+        fg.generate_window_post_proofs(ctx, pk, gc, 3 * 2349, 2349, [zb] * 2, blind[:2])
+    one = fg.generate_window_post_proofs(ctx, pk, gc, 2349, 2349, [zb], blind[:1])  # <= 1 -> one partition
+    assert one == buf[:192]
+    win = fg.generate_winning_post_proof(ctx, pk, gc, 1, 1, zb, blind[0])
+    assert win == buf[:192]
+    with pytest.raises(ValueError, match="invalid amount of replicas"):
+        fg.generate_winning_post_proof(ctx, pk, gc, 2, 1, zb, blind[0])
+
+
 @pytest.mark.parametrize("rows,seed,worlds", [(700, 81, (1, 2, 3, 7)), (16000, 82, (4,))])
 def test_prove_share_vs_oracle_shares(ctx, oracle, rows, seed, worlds):
     """Single-proof latency mode: every rank's GPU share is byte-identical to the oracle's
