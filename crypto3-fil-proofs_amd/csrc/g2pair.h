@@ -106,22 +106,13 @@ struct Lane<fq2_t> {  // G2: a lane pair per element, this lane's Fq half of eve
     }
 };
 
-// Bucket-reduction kernels (full XYZZ + XYZZ additions, two or three live accumulators): the lane
-// pair or one thread per G2 element (MI_G2_RED_PAIR); G1 is unchanged.
-#ifndef MI_G2_RED_PAIR
-#define MI_G2_RED_PAIR 1
-#endif
+// Bucket-reduction kernels (full XYZZ + XYZZ additions, two or three live accumulators) use the same
+// lane pairs.  A one-thread-per-G2-element reduction variant existed in round 1 for an A/B; built without
+// the two-wave cap it took all 512 unified registers and returned a wrong G2 sum at n = 1 on the GPU
+// (tools/g2_variants.sh variant C), while the identical group-law code compiled for the host is correct
+// under ASan/UBSan against the oracle (tests/test_cpu_grouplaw.py, G2 sequences).  The fault is in that
+// AGPR-heavy device build, not in the arithmetic; the variant lost the A/B anyway, so it was removed.
 template <class F>
 struct LaneRed : Lane<F> {};
-#if !MI_G2_RED_PAIR
-template <>
-struct LaneRed<fq2_t> {
-    static constexpr unsigned K = 1;
-    using R = fq2_t;
-    __device__ static XYZZ<R> ld(const XYZZ<fq2_t> *p) { return *p; }
-    __device__ static void st(XYZZ<fq2_t> *p, const XYZZ<R> &v) { *p = v; }
-    __device__ static Affine<R> lda(const Affine<fq2_t> *p) { return *p; }
-};
-#endif
 
 }  // namespace mi

@@ -45,14 +45,7 @@ namespace {
 #ifndef MI_WAVES_ACC
 #define MI_WAVES_ACC MI_WAVES2
 #endif
-#ifndef MI_RED_CAP
-#define MI_RED_CAP 1
-#endif
-#if MI_RED_CAP
-#define MI_WAVES_RED MI_WAVES2
-#else
-#define MI_WAVES_RED
-#endif
+#define MI_WAVES_RED MI_WAVES2  // the reduction kernels keep the two-wave cap (see g2pair.h LaneRed)
 
 constexpr uint32_t L0_DEFAULT = 64;  // sorted entries per chunk at level 0 (mixed adds); MI_MSM_L0 overrides
 constexpr uint32_t L1 = 16;  // chunk partials summed per thread per tree level (full adds)

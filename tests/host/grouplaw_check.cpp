@@ -226,6 +226,26 @@ static void check_g2() {
         }
         g2_affine_t a = xyzz_to_affine_inl(acc), e = from(expect);
         CHECK(a.x == e.x && a.y == e.y, "g2 seq=%d", seq);
+        // the bucket-reduction operations: full XYZZ additions (doubling and inverse branches too) and the
+        // k_seg_fold double-and-add k * P
+        uint8_t e2[192], ek[192], ks[32];
+        or_g2_add(expect, expect, e2);
+        g2_affine_t d = xyzz_to_affine_inl(xyzz_add_inl(acc, acc)), de = from(e2);
+        CHECK(d.x == de.x && d.y == de.y, "g2 full add dbl seq=%d", seq);
+        CHECK(xyzz_add_inl(acc, xyzz_neg(acc)).is_inf(), "g2 full add inverse seq=%d", seq);
+        g2_affine_t d2 = xyzz_to_affine_inl(xyzz_dbl_inl(acc));
+        CHECK(d2.x == de.x && d2.y == de.y, "g2 dbl seq=%d", seq);
+        const uint32_t k = 1 + (uint32_t)(rng() % 5000000);
+        std::memset(ks, 0, 32);
+        std::memcpy(ks, &k, 4);
+        or_g2_mul(expect, ks, ek);
+        g2_xyzz_t m = acc;
+        for (int bit = 30 - __builtin_clz(k); bit >= 0; bit--) {
+            m = xyzz_dbl_inl(m);
+            if ((k >> bit) & 1) m = xyzz_add_inl(m, acc);
+        }
+        g2_affine_t km = xyzz_to_affine_inl(m), kme = from(ek);
+        CHECK(km.x == kme.x && km.y == kme.y, "g2 k*P seq=%d k=%u", seq, k);
     }
 }
 
