@@ -198,6 +198,43 @@ def tree_c_leg(args, fg, ctx, device, world):
     return out
 
 
+def config4_leg(args, fg, synth_mod, ctx):
+    """BASELINE config 4 (the north-star target: a 32 GiB Seal-PoRep-sized circuit, ~1.3e8 constraints,
+    d = 2^27) on the same GPU after the config-3 objects are freed: host (pinned) witness, one warm-up and
+    `config4_steps` timed proofs with overlapped uploads, every proof pairing-verified."""
+    import gc
+
+    import numpy as np
+
+    lr = args.config4_log_rows
+    t0 = time.perf_counter()
+    sc = synth_mod.SynthCircuit(lr, args.n_in, args.seed)
+    circ = sc.load(ctx)
+    pk = fg.generate_random_parameters(ctx, circ, splitmix_frs(TOXIC_SEED, 5))
+    ctx.synchronize()
+    t_setup = time.perf_counter() - t0
+    z = fg.HostBuffer(32 * sc.num_vars)
+    np.copyto(z.array, sc.z_array())
+    blind = splitmix_frs(4000, 2 * (1 + args.config4_steps))
+    fg.prove_batch(ctx, pk, circ, [z], [(blind[0], blind[1])])
+    ctx.synchronize()
+    t1 = time.perf_counter()
+    proofs = fg.prove_batch(ctx, pk, circ, [z] * args.config4_steps,
+                            [(blind[2 * k + 2], blind[2 * k + 3]) for k in range(args.config4_steps)])
+    ctx.synchronize()
+    dt = (time.perf_counter() - t1) / args.config4_steps
+    vk, ic = pk.verifying_key()
+    pub = z.array[32:32 * sc.n_in].tobytes()
+    verified = bool(fg.verify_batch(vk, ic, [pub] * len(proofs), proofs))
+    out = {"workload": f"BASELINE config 4 shape: synthetic 2^{lr}-domain R1CS ({sc.n} constraints, 32 GiB "
+                       f"Seal-PoRep-sized), host (pinned) witness",
+           "value": sc.n / dt, "unit": "constraints/s", "ms_per_proof": dt * 1e3, "proofs": len(proofs),
+           "verified": verified, "setup_s": t_setup, "domain": circ.d, "a_query": circ.n_a, "b_query": circ.n_b}
+    del proofs, z, pk, circ, sc
+    gc.collect()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -215,6 +252,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-device-resident", action="store_true", help="skip the secondary HBM-resident run")
     ap.add_argument("--stats-json", default=None, help="write per-kernel timers here")
+    ap.add_argument("--config4-log-rows", type=int, default=27,
+                    help="secondary: BASELINE config 4 (2^N domain) after the main run on one GPU (0 skips)")
+    ap.add_argument("--config4-steps", type=int, default=2)
     ap.add_argument("--tree-log-nodes", type=int, default=21,
                     help="secondary: tree C over 2^N columns x 11 layers (N a multiple of 3; 0 skips)")
     args = ap.parse_args()
@@ -254,6 +294,8 @@ def main():
     zhost = fg.HostBuffer(32 * sc.num_vars)
     np.copyto(zhost.array, sc.z_array())
     n = sc.n
+    shape = {"d": circ.d, "n_a": circ.n_a, "n_b": circ.n_b, "n_in": sc.n_in, "n_aux": sc.n_aux,
+             "num_vars": sc.num_vars}
     vk, ic = pk.verifying_key()
     pub_inputs = zhost.array[32:32 * sc.n_in].tobytes()
     log(rank, f"setup: synth {t_synth:.1f}s circuit load {t_load:.1f}s srs {'load' if args.params else 'gen'} "
@@ -381,6 +423,18 @@ def main():
         except Exception as e:  # reported, never fatal to the GPU measurement
             cpu = {"value": None, "unit": "constraints/s", "cores": None, "kind": "port", "sample": f"failed: {e}"}
 
+    config4 = None
+    if rank == 0 and world == 1 and args.config4_log_rows:
+        import gc
+
+        del pk, circ, zhost, sc
+        gc.collect()
+        ctx.synchronize()
+        try:
+            config4 = config4_leg(args, fg, synth_mod, ctx)
+        except Exception as e:  # reported, never fatal to the config-3 measurement
+            config4 = {"value": None, "error": str(e)}
+
     if rank != 0:
         if dist:
             dist.destroy_process_group()
@@ -434,8 +488,8 @@ def main():
         "data": "synthetic R1CS + satisfying witness (csrc/synth.hip) in page-locked host memory, proving key "
                 + ("loaded from " + args.params if args.params else "generated on device from fixed toxic waste"),
         "config": {"workload": workload_name(args.log_rows, P, world),
-                   "constraints": n, "domain": circ.d, "num_inputs": sc.n_in, "num_aux": sc.n_aux,
-                   "a_query": circ.n_a, "b_query": circ.n_b, "proofs_per_step": P if P else world,
+                   "constraints": n, "domain": shape["d"], "num_inputs": shape["n_in"], "num_aux": shape["n_aux"],
+                   "a_query": shape["n_a"], "b_query": shape["n_b"], "proofs_per_step": P if P else world,
                    "partitions_per_rank": per_step,
                    "parallelism": f"partition-sharded x{world}"},
         "verified": verified,
@@ -443,7 +497,7 @@ def main():
         "verify_s": t_ver,
         "witness": "host (pinned), H2D of partition k + 1 overlapped with proof k",
         "h2d": {"ms_per_proof": h2d["ms"] / max(h2d["launches"], 1),
-                "gb_per_s": h2d["units"] / max(h2d["ms"], 1e-9) / 1e6, "bytes_per_proof": 32 * sc.num_vars},
+                "gb_per_s": h2d["units"] / max(h2d["ms"], 1e-9) / 1e6, "bytes_per_proof": 32 * shape["num_vars"]},
         "device_resident": resident,
         "msm_g1_mpoints_per_s": msm_n / msm_dt / 1e6,
         "msm_g1_points": msm_n,
@@ -478,6 +532,7 @@ def main():
         },
         "cpu_baseline": cpu,
         "tree_c": tree,
+        "config4": config4,
         "timers_ms": {k: round(v["ms"], 3) for k, v in stats.items()},
         "setup_s": {"synth": t_synth, "circuit_load": t_load, "srs": t_srs},
         "multiproof_bytes": 192 * len(proofs),

@@ -42,10 +42,130 @@ __global__ void __launch_bounds__(256) k_poseidon(const fr_t *__restrict__ in, u
     if (i >= n) return;
     const fr29_t r2 = k.img[k.off_tag + 1];
     fr29_t s[T];
-    s[0] = k.img[k.off_tag];
+    MI_UNROLL for (int l = 0; l < 9; l++) s[0].v[l] = k.img[k.off_tag].v[l];
     const fr_t *p = in + i * stride_hash;
     sfor<T - 1>([&](auto j) { s[j + 1] = fr29_mul(fr29_from_fr(p[(uint64_t)j * stride_elem]), r2); });
     out[i] = fr_from_fr29(fr29_from_mont(poseidon_permute<T>(s, k)));
+}
+
+// Wave-pair form (default): a 128-thread workgroup hashes 64 inputs; wave 0 holds state elements
+// [0, H0) and wave 1 elements [H0, t) of the same 64 hashes (H0 = ceil(t / 2)), and the halves are
+// exchanged through LDS around every matrix step.  Each wave's role is uniform, so round constants and
+// matrix rows stay scalar loads, and a lane holds half a state plus the partner half and the new half
+// (3 x ceil(t/2) x 9 registers: 162 at t = 12) -- two waves per SIMD instead of one for k_poseidon<12>
+// (353 registers), which is what hides the dependent product-scanning chains.  Partial rounds exchange
+// one element each way: the S-boxed s0 (wave 0 -> 1) and wave 1's half of the sparse row (1 -> 0).
+// Every barrier sits in code both waves execute.
+template <int T>
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) k_poseidon_pair(const fr_t *__restrict__ in, uint64_t n, uint64_t stride_hash,
+                                                       uint64_t stride_elem, PosK k, fr_t *__restrict__ out) {
+    constexpr int H0 = (T + 1) / 2, H1 = T / 2;
+    __shared__ uint32_t xb[2][H0][9][64];
+    const unsigned lane = threadIdx.x & 63, role = threadIdx.x >> 6;
+    const uint64_t i = (uint64_t)blockIdx.x * 64 + lane;
+    const bool live = i < n;
+    const fr29_t *img = k.img;
+    const fr29_t zero = {{0, 0, 0, 0, 0, 0, 0, 0, 0}};
+    fr29_t s[H0], p[H0];
+    {
+        const fr29_t r2 = img[k.off_tag + 1];
+        const fr_t *src = in + (live ? i : 0) * stride_hash;
+        if (role == 0) {
+            MI_UNROLL for (int l = 0; l < 9; l++) s[0].v[l] = img[k.off_tag].v[l];  // limb-wise: a struct memcpy into s kept it in scratch
+            sfor<H0 - 1>([&](auto j) {
+                s[j + 1] = live ? fr29_mul(fr29_from_fr(src[(uint64_t)j * stride_elem]), r2) : zero;
+            });
+        } else {
+            sfor<H0>([&](auto j) { s[j] = zero; });
+            sfor<H1>([&](auto j) {
+                s[j] = live ? fr29_mul(fr29_from_fr(src[(uint64_t)(H0 - 1 + j) * stride_elem]), r2) : zero;
+            });
+        }
+    }
+    const int own = role ? H1 : H0, partner = role ? H0 : H1;
+    auto put = [&](int cnt) __attribute__((always_inline)) {
+        __syncthreads();  // the partner has read the previous exchange
+        sfor<H0>([&](auto j) {
+            if (j < cnt) MI_UNROLL for (int l = 0; l < 9; l++) xb[role][j][l][lane] = s[j].v[l];
+        });
+        __syncthreads();
+    };
+    auto get = [&](int cnt) __attribute__((always_inline)) {
+        sfor<H0>([&](auto j) {
+            if (j < cnt) MI_UNROLL for (int l = 0; l < 9; l++) p[j].v[l] = xb[role ^ 1][j][l][lane];
+        });
+    };
+    // s <- M s for a t x t matrix (full rounds, dense last partial round)
+    auto mat = [&](const fr29_t *__restrict__ m) __attribute__((always_inline)) {
+        put(own);
+        get(partner);
+        if (role == 0) {
+            fr29_t nn[H0];
+            sfor<H0>([&](auto r) {
+                __builtin_amdgcn_sched_barrier(0);  // one row at a time (register pressure)
+                nn[r] = fr29_add(fr29_row<H0>(m + r * T, s), fr29_row<H1>(m + r * T + H0, p));
+            });
+            __builtin_amdgcn_sched_barrier(0);
+            sfor<H0>([&](auto r) { s[r] = nn[r]; });
+        } else {
+            fr29_t nn[H1];
+            sfor<H1>([&](auto r) {
+                __builtin_amdgcn_sched_barrier(0);
+                nn[r] = fr29_add(fr29_row<H1>(m + (H0 + r) * T + H0, s), fr29_row<H0>(m + (H0 + r) * T, p));
+            });
+            __builtin_amdgcn_sched_barrier(0);
+            sfor<H1>([&](auto r) { s[r] = nn[r]; });
+        }
+    };
+    auto full = [&](const fr29_t *__restrict__ rc) __attribute__((always_inline)) {
+        if (role == 0)
+            sfor<H0>([&](auto j) {
+                __builtin_amdgcn_sched_barrier(0);
+                s[j] = fr29_sbox(fr29_add(s[j], rc[j]));
+            });
+        else
+            sfor<H1>([&](auto j) {
+                __builtin_amdgcn_sched_barrier(0);
+                s[j] = fr29_sbox(fr29_add(s[j], rc[H0 + j]));
+            });
+        __builtin_amdgcn_sched_barrier(0);
+        mat(img + k.off_mds);
+    };
+#pragma unroll 1
+    for (int r = 0; r < k.rf / 2; r++) full(img + k.off_rc_first + r * T);
+    const fr29_t *sp = img + k.off_sparse;
+#pragma unroll 1
+    for (int q = 0; q < k.rp - 1; q++, sp += 2 * T - 1) {
+        fr29_t d;
+        if (role == 0) {
+            s[0] = fr29_sbox(fr29_add(s[0], img[k.off_rc_part + q]));
+            d = fr29_row<H0>(sp, s);
+        } else {
+            d = fr29_row<H1>(sp + H0, s);
+        }
+        __syncthreads();
+        MI_UNROLL for (int l = 0; l < 9; l++) xb[role][0][l][lane] = role ? d.v[l] : s[0].v[l];
+        __syncthreads();
+        fr29_t recv;
+        MI_UNROLL for (int l = 0; l < 9; l++) recv.v[l] = xb[role ^ 1][0][l][lane];
+        if (role == 0) {  // recv = wave 1's half of the row
+            sfor<H0 - 1>([&](auto j) {
+                __builtin_amdgcn_sched_barrier(0);
+                s[j + 1] = fr29_sub_if_ge(fr29_add(s[j + 1], fr29_mul(sp[T + j], s[0])), R2X29);
+            });
+            s[0] = fr29_add(d, recv);
+        } else {  // recv = S-boxed s0
+            sfor<H1>([&](auto j) {
+                __builtin_amdgcn_sched_barrier(0);
+                s[j] = fr29_sub_if_ge(fr29_add(s[j], fr29_mul(sp[T + H0 - 1 + j], recv)), R2X29);
+            });
+        }
+    }
+    if (role == 0) s[0] = fr29_sbox(fr29_add(s[0], img[k.off_rc_part + k.rp - 1]));
+    mat(img + k.off_dense);
+#pragma unroll 1
+    for (int r = 0; r < k.rf / 2; r++) full(img + k.off_rc_last + r * T);
+    if (role == 0 && live) out[i] = fr_from_fr29(fr29_from_mont(s[1]));
 }
 
 // replica = label + data (mod r), written back over data: the tree R-last leaves (porep encode)
@@ -102,11 +222,28 @@ void poseidon_hash_dev(Ctx &c, unsigned arity, const fr_t *in, uint64_t n, uint6
     PosK k;
     poseidon_tables(c, arity, &k);
     ScopedTimer tm(c, &c.stats.poseidon, n);
+    // MI_POSEIDON_PAIR (read per call, for A/B): 1 wave-pair kernel, 0 one thread per hash; unset = the
+    // measured choice, pairs for the wide states (arity 8, 11) and one thread per hash for arity 2, 4
+    const char *pe = getenv("MI_POSEIDON_PAIR");
+    const bool pair = pe ? atoi(pe) != 0 : arity >= 8;
+    const unsigned gp = (unsigned)((n + 63) / 64);
     switch (arity) {
-        case 2: k_poseidon<3><<<grid256(n), 256, 0, c.stream>>>(in, n, stride_hash, stride_elem, k, out); break;
-        case 4: k_poseidon<5><<<grid256(n), 256, 0, c.stream>>>(in, n, stride_hash, stride_elem, k, out); break;
-        case 8: k_poseidon<9><<<grid256(n), 256, 0, c.stream>>>(in, n, stride_hash, stride_elem, k, out); break;
-        case 11: k_poseidon<12><<<grid256(n), 256, 0, c.stream>>>(in, n, stride_hash, stride_elem, k, out); break;
+        case 2:
+            if (pair) k_poseidon_pair<3><<<gp, 128, 0, c.stream>>>(in, n, stride_hash, stride_elem, k, out);
+            else k_poseidon<3><<<grid256(n), 256, 0, c.stream>>>(in, n, stride_hash, stride_elem, k, out);
+            break;
+        case 4:
+            if (pair) k_poseidon_pair<5><<<gp, 128, 0, c.stream>>>(in, n, stride_hash, stride_elem, k, out);
+            else k_poseidon<5><<<grid256(n), 256, 0, c.stream>>>(in, n, stride_hash, stride_elem, k, out);
+            break;
+        case 8:
+            if (pair) k_poseidon_pair<9><<<gp, 128, 0, c.stream>>>(in, n, stride_hash, stride_elem, k, out);
+            else k_poseidon<9><<<grid256(n), 256, 0, c.stream>>>(in, n, stride_hash, stride_elem, k, out);
+            break;
+        case 11:
+            if (pair) k_poseidon_pair<12><<<gp, 128, 0, c.stream>>>(in, n, stride_hash, stride_elem, k, out);
+            else k_poseidon<12><<<grid256(n), 256, 0, c.stream>>>(in, n, stride_hash, stride_elem, k, out);
+            break;
         default: throw std::invalid_argument("poseidon: arity must be 2, 4, 8 or 11");
     }
     MI_LAUNCHED(c, "k_poseidon");
