@@ -15,7 +15,12 @@
 // Every twiddle is omega_{2^32}^e = LO[e & 0xffff] * HI[e >> 16] from two 2 MiB tables, so
 // one pair of tables serves all domain sizes up to 2^32; in-tile twiddles need HI only.
 // Each pass moves the vector through HBM once (read + write): 3 passes at 2^26.
+// Inside a pass elements live in 9 x 29-bit limbs (fr29.h, same Montgomery radix as fr_t) in registers
+// and in the LDS tile: products need no limb conversion and no final subtraction, butterfly sums and
+// differences are lazy and each radix-4 output is brought back below 2r by at most two conditional
+// subtractions; HBM keeps the canonical 8 x 32-bit image (< r).
 #include "ctx.h"
+#include "fr29.h"
 
 namespace mi {
 
@@ -32,6 +37,14 @@ __device__ __forceinline__ fr_t tw_full(const fr_t *__restrict__ lo, const fr_t 
     return lo[l] * hi[h];
 }
 
+// the same twiddle in 9 x 29-bit limbs (< 2r)
+__device__ __forceinline__ fr29_t tw29(const fr_t *__restrict__ lo, const fr_t *__restrict__ hi, uint32_t e) {
+    uint32_t l = e & 0xffffu, h = e >> 16;
+    if (l == 0) return fr29_from_fr(hi[h]);
+    if (h == 0) return fr29_from_fr(lo[l]);
+    return fr29_mul(fr29_from_fr(lo[l]), fr29_from_fr(hi[h]));
+}
+
 __device__ __forceinline__ uint32_t brev(uint32_t x, unsigned bits) {
     return bits ? (__builtin_bitreverse32(x) >> (32 - bits)) : 0;
 }
@@ -40,23 +53,35 @@ __device__ __forceinline__ uint32_t brev(uint32_t x, unsigned bits) {
 // 32-lane groups; positions are XOR-swizzled inside 32-word rows (worst case 2-way bank conflicts
 // for every radix-4 access pattern and conflict-free for the contiguous load/store phases).
 struct LdsTile {
-    uint64_t p[4][TILE];
+    uint64_t p[4][TILE];  // limbs (0,1) (2,3) (4,5) (6,7)
+    uint32_t q[TILE];     // limb 8
 };
 __device__ __forceinline__ unsigned swz(unsigned p) { return p ^ (((p >> 5) * 5u) & 31u); }
-__device__ __forceinline__ void lds_put(LdsTile &s, unsigned p, const fr_t &x) {
+__device__ __forceinline__ void lds_put(LdsTile &s, unsigned p, const fr29_t &x) {
     const unsigned q = swz(p);
     MI_UNROLL for (int k = 0; k < 4; k++) s.p[k][q] = (uint64_t)x.v[2 * k] | ((uint64_t)x.v[2 * k + 1] << 32);
+    s.q[q] = x.v[8];
 }
-__device__ __forceinline__ fr_t lds_get(const LdsTile &s, unsigned p) {
+__device__ __forceinline__ fr29_t lds_get(const LdsTile &s, unsigned p) {
     const unsigned q = swz(p);
-    fr_t x;
+    fr29_t x;
     MI_UNROLL for (int k = 0; k < 4; k++) {
         uint64_t w = s.p[k][q];
         x.v[2 * k] = (uint32_t)w;
         x.v[2 * k + 1] = (uint32_t)(w >> 32);
     }
+    x.v[8] = s.q[q];
     return x;
 }
+// 4r in 29-bit limbs (2r is R2X29, r is FrDesc::MOD29)
+constexpr uint32_t R4X29[9] = {0x00000004u, 0x1fffffe0u, 0x1e5bfeffu, 0x0d2017ffu, 0x160154efu,
+                               0x10101343u, 0x1483339du, 0x0994cebeu, 0x01cfb69du};
+// v < 8r -> v < 2r
+__device__ __forceinline__ fr29_t red8(const fr29_t &v) { return fr29_sub_if_ge(fr29_sub_if_ge(v, R4X29), R2X29); }
+__device__ __forceinline__ fr29_t red4(const fr29_t &v) { return fr29_sub_if_ge(v, R2X29); }  // v < 4r -> < 2r
+__device__ __forceinline__ fr29_t f29(const fr_t &x) { return fr29_from_fr(x); }
+// value < 2r -> canonical 8 x 32-bit image (< r)
+__device__ __forceinline__ fr_t to_fr(const fr29_t &x) { return fr_from_fr29(fr29_sub_if_ge(x, FrDesc::MOD29)); }
 // insert zero bits at positions p0 < p1 (p1 = p0 + 1 here) / at position p
 __device__ __forceinline__ unsigned ins2(unsigned q, unsigned p0) {
     return (q & ((1u << p0) - 1)) | ((q >> p0) << (p0 + 2));
@@ -97,36 +122,40 @@ __device__ __forceinline__ void ntt_rounds(LdsTile &sh, unsigned b, unsigned Tlo
                 const unsigned j0 = (i1 & (h - 1)) << s;        // stage s, pair (x0, x2)
                 const unsigned j1 = j0 + (1u << (b - 2));       // stage s, pair (x1, x3)
                 const unsigned jq = (i1 & ((h >> 1) - 1)) << (s + 1);  // stage s + 1, both pairs
-                fr_t x0 = lds_get(sh, base), x1 = lds_get(sh, base + o1);
-                fr_t x2 = lds_get(sh, base + o2), x3 = lds_get(sh, base + o2 + o1);
+                // LDS values < 2r; sums / differences lazy (< 8r), products < 1.1r, outputs back below 2r
+                fr29_t x0 = lds_get(sh, base), x1 = lds_get(sh, base + o1);
+                fr29_t x2 = lds_get(sh, base + o2), x3 = lds_get(sh, base + o2 + o1);
                 if (DIF) {
-                    fr_t a = x0 + x2, c = x0 - x2;
-                    fr_t bb = x1 + x3, dd = x1 - x3;
-                    if (j0) c = c * tw_b(tw10, j0, tsh);
-                    dd = dd * tw_b(tw10, j1, tsh);
-                    x0 = a + bb;
-                    x1 = a - bb;
-                    x2 = c + dd;
-                    x3 = c - dd;
+                    fr29_t a = fr29_add(x0, x2), c = fr29_sub_lazy(x0, x2, R2X29);
+                    fr29_t bb = fr29_add(x1, x3), dd = fr29_sub_lazy(x1, x3, R2X29);
+                    if (j0) c = fr29_mul(c, f29(tw_b(tw10, j0, tsh)));
+                    dd = fr29_mul(dd, f29(tw_b(tw10, j1, tsh)));
+                    x0 = red8(fr29_add(a, bb));
+                    x1 = fr29_sub_lazy(a, bb, R4X29);
+                    x2 = red8(fr29_add(c, dd));
+                    x3 = fr29_sub_lazy(c, dd, R2X29);
                     if (jq) {
-                        fr_t w = tw_b(tw10, jq, tsh);
-                        x1 = x1 * w;
-                        x3 = x3 * w;
+                        const fr29_t w = f29(tw_b(tw10, jq, tsh));
+                        x1 = fr29_mul(x1, w);
+                        x3 = fr29_mul(x3, w);
+                    } else {
+                        x1 = red8(x1);
+                        x3 = red8(x3);
                     }
                 } else {
                     if (jq) {
-                        fr_t w = tw_b(tw10, jq, tsh);
-                        x1 = x1 * w;
-                        x3 = x3 * w;
+                        const fr29_t w = f29(tw_b(tw10, jq, tsh));
+                        x1 = fr29_mul(x1, w);
+                        x3 = fr29_mul(x3, w);
                     }
-                    fr_t a = x0 + x1, bb = x0 - x1;
-                    fr_t c = x2 + x3, dd = x2 - x3;
-                    if (j0) c = c * tw_b(tw10, j0, tsh);
-                    dd = dd * tw_b(tw10, j1, tsh);
-                    x0 = a + c;
-                    x2 = a - c;
-                    x1 = bb + dd;
-                    x3 = bb - dd;
+                    fr29_t a = fr29_add(x0, x1), bb = fr29_sub_lazy(x0, x1, R2X29);
+                    fr29_t c = fr29_add(x2, x3), dd = fr29_sub_lazy(x2, x3, R2X29);
+                    if (j0) c = fr29_mul(c, f29(tw_b(tw10, j0, tsh)));
+                    dd = fr29_mul(dd, f29(tw_b(tw10, j1, tsh)));
+                    x0 = red8(fr29_add(a, c));
+                    x2 = red8(fr29_sub_lazy(a, c, R4X29));
+                    x1 = red8(fr29_add(bb, dd));
+                    x3 = red8(fr29_sub_lazy(bb, dd, R2X29));
                 }
                 lds_put(sh, base, x0);
                 lds_put(sh, base + o1, x1);
@@ -136,9 +165,9 @@ __device__ __forceinline__ void ntt_rounds(LdsTile &sh, unsigned b, unsigned Tlo
         } else {  // radix-2 round: DIF stage b - 1 (pairs at i1 bit 0, twiddle exponent 0)
             for (unsigned u = q; u < (tile >> 1); u += NTT_THREADS) {
                 const unsigned base = ins1(u, Tlog);
-                fr_t x0 = lds_get(sh, base), x1 = lds_get(sh, base + T);
-                lds_put(sh, base, x0 + x1);
-                lds_put(sh, base + T, x0 - x1);
+                const fr29_t x0 = lds_get(sh, base), x1 = lds_get(sh, base + T);
+                lds_put(sh, base, red4(fr29_add(x0, x1)));
+                lds_put(sh, base + T, red4(fr29_sub_lazy(x0, x1, R2X29)));
             }
         }
         __syncthreads();
@@ -180,6 +209,7 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(fr_t *__restrict__ d, 
     const fr_t *twA = tw10, *twB = tw10b;
     const unsigned tsh = TILE_LOG - b;
 #endif
+    const fr29_t sc29 = fr29_from_fr(scale);
     const unsigned T = 1u << Tlog;
     const unsigned Slog = M - b;
     const uint64_t S = 1ull << Slog;
@@ -199,11 +229,11 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(fr_t *__restrict__ d, 
     for (unsigned e = threadIdx.x; e < tile; e += NTT_THREADS) {
         unsigned t = e & (T - 1), i1 = (e >> Tlog) & bmask, g = e >> (Tlog + b);
         uint64_t gi = ((sub0 + g) << M) + ((uint64_t)i1 << Slog) + i20 + t;
-        fr_t x = d[gi];
+        fr29_t x = f29(d[gi]);
         if (!DIF && twiddle) {
             uint32_t k1 = brev(i1, b);
             uint32_t ex = (uint32_t)(((uint64_t)(i20 + t) * k1) << (32 - M));
-            if (ex) x = x * tw_full(lo, hi, ex);
+            if (ex) x = fr29_mul(x, tw29(lo, hi, ex));
         }
         lds_put(sh, e, x);
     }
@@ -213,10 +243,10 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(fr_t *__restrict__ d, 
         for (unsigned e = threadIdx.x; e < tile; e += NTT_THREADS) {
             unsigned t = e & (T - 1), i1 = (e >> Tlog) & bmask, g = e >> (Tlog + b);
             uint64_t gi = ((sub0 + g) << M) + ((uint64_t)i1 << Slog) + i20 + t;
-            fr_t x = lds_get(sh, e);
+            fr29_t x = lds_get(sh, e);
             uint32_t ex = brev((uint32_t)gi, L);
-            if (ex) x = x * tw_full(glo, ghi, ex);
-            lds_put(sh, e, x * scale);
+            if (ex) x = fr29_mul(x, tw29(glo, ghi, ex));
+            lds_put(sh, e, fr29_mul(x, sc29));
         }
         __syncthreads();
         ntt_rounds<false>(sh, b, Tlog, tile, twB, tsh);
@@ -225,19 +255,22 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(fr_t *__restrict__ d, 
     for (unsigned e = threadIdx.x; e < tile; e += NTT_THREADS) {
         unsigned t = e & (T - 1), i1 = (e >> Tlog) & bmask, g = e >> (Tlog + b);
         uint64_t gi = ((sub0 + g) << M) + ((uint64_t)i1 << Slog) + i20 + t;
-        fr_t x = lds_get(sh, e);
+        fr29_t x = lds_get(sh, e);
         if (DIF && !FUSED && twiddle) {
             uint32_t k1 = brev(i1, b);
             uint32_t ex = (uint32_t)(((uint64_t)(i20 + t) * k1) << (32 - M));
-            if (ex) x = x * tw_full(lo, hi, ex);
+            if (ex) x = fr29_mul(x, tw29(lo, hi, ex));
         }
         if (DIF && !FUSED && epi) {
             uint32_t ex = brev((uint32_t)gi, L);
-            if (ex) x = x * tw_full(glo, ghi, ex);
-            x = x * scale;
-            if (epi == 2) x = from_mont(x);
+            if (ex) x = fr29_mul(x, tw29(glo, ghi, ex));
+            x = fr29_mul(x, sc29);
+            if (epi == 2) {
+                d[gi] = fr_from_fr29(fr29_from_mont(x));
+                continue;
+            }
         }
-        d[gi] = x;
+        d[gi] = to_fr(x);
     }
 }
 

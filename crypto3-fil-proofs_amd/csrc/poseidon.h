@@ -3,13 +3,9 @@
 #include <vector>
 
 #include "ctx.h"
+#include "fr29.h"
 
 namespace mi {
-
-// Fr in 9 x 29-bit limbs, Montgomery radix R = 2^261 (the radix of fr_t): the Poseidon state
-struct alignas(8) fr29_t {  // 40 bytes: 8-byte aligned so vectorised copies never straddle two elements
-    uint32_t v[9];
-};
 
 // Device view of one arity's constant image (9 x 29-bit Montgomery limbs per element):
 //   [off_tag] domain tag 2^arity - 1, [off_tag + 1] R^2 mod r, [off_rc_first] R_F/2 x t full-round

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "field.h"
+#include "fr29.h"
 #include "poseidon.h"
 
 namespace mi {
@@ -16,101 +17,6 @@ namespace mi {
 // ---------------------------------------------------------------------------------------------
 // Fr over 9 x 29-bit limbs
 // ---------------------------------------------------------------------------------------------
-constexpr uint32_t M29 = (1u << 29) - 1;
-// 2r in 29-bit limbs (conditional subtraction), r itself is FrDesc::MOD29
-constexpr uint32_t R2X29[9] = {0x00000002u, 0x1ffffff0u, 0x1f2dff7fu, 0x16900bffu, 0x1b00aa77u,
-                               0x180809a1u, 0x0a4199ceu, 0x14ca675fu, 0x00e7db4eu};
-
-MI_HD fr29_t fr29_from_fr(const fr_t &a) {
-    fr29_t r;
-    MI_UNROLL for (int i = 0; i < 9; i++) {
-        const int bit = 29 * i, w = bit >> 5, s = bit & 31;
-        uint64_t x = a.v[w];
-        if (w + 1 < 8) x |= (uint64_t)a.v[w + 1] << 32;
-        r.v[i] = (uint32_t)(x >> s) & M29;
-    }
-    return r;
-}
-// value < 2^256 (canonical here)
-MI_HD fr_t fr_from_fr29(const fr29_t &t) {
-    fr_t r;
-    MI_UNROLL for (int j = 0; j < 8; j++) r.v[j] = 0;
-    MI_UNROLL for (int i = 0; i < 9; i++) {
-        const int bit = 29 * i, w = bit >> 5, s = bit & 31;
-        r.v[w] |= t.v[i] << s;
-        if (s > 3 && w + 1 < 8) r.v[w + 1] |= t.v[i] >> (32 - s);
-    }
-    return r;
-}
-
-// sum_k a[k] b[k] R^-1 with one Montgomery reduction, K <= 6 (column sums <= 63 products < 2^58 plus a
-// carry < 2^35 stay below 2^64).  Result < sum a_k b_k / R + r.
-template <int K>
-MI_HD fr29_t fr29_dot(const fr29_t *a, const fr29_t *b) {
-    static_assert(K >= 1 && K <= 6, "fr29_dot: at most 6 products per reduction");
-    constexpr int L = 9;
-    uint32_t m[L];
-    fr29_t r;
-    uint64_t acc = 0;
-    MI_UNROLL for (int k = 0; k < L; k++) {
-        MI_UNROLL for (int i = 0; i < k; i++) {
-            MI_UNROLL for (int q = 0; q < K; q++) acc += (uint64_t)a[q].v[i] * b[q].v[k - i];
-            acc += (uint64_t)m[i] * FrDesc::MOD29[k - i];
-        }
-        MI_UNROLL for (int q = 0; q < K; q++) acc += (uint64_t)a[q].v[k] * b[q].v[0];
-        m[k] = ((uint32_t)acc * FrDesc::INV29) & M29;
-        acc += (uint64_t)m[k] * FrDesc::MOD29[0];
-        acc >>= 29;
-    }
-    MI_UNROLL for (int k = L; k < 2 * L - 1; k++) {
-        MI_UNROLL for (int i = k - L + 1; i < L; i++) {
-            MI_UNROLL for (int q = 0; q < K; q++) acc += (uint64_t)a[q].v[i] * b[q].v[k - i];
-            acc += (uint64_t)m[i] * FrDesc::MOD29[k - i];
-        }
-        r.v[k - L] = (uint32_t)acc & M29;
-        acc >>= 29;
-    }
-    r.v[L - 1] = (uint32_t)acc;
-    return r;
-}
-MI_HD fr29_t fr29_mul(const fr29_t &a, const fr29_t &b) { return fr29_dot<1>(&a, &b); }
-
-// a + b, carry-normalised, not reduced
-MI_HD fr29_t fr29_add(const fr29_t &a, const fr29_t &b) {
-    fr29_t r;
-    uint32_t c = 0;
-    MI_UNROLL for (int i = 0; i < 8; i++) {
-        uint32_t t = a.v[i] + b.v[i] + c;
-        r.v[i] = t & M29;
-        c = t >> 29;
-    }
-    r.v[8] = a.v[8] + b.v[8] + c;
-    return r;
-}
-// a - m if a >= m, for m = r or 2r given in 29-bit limbs
-MI_HD fr29_t fr29_sub_if_ge(const fr29_t &a, const uint32_t *m) {
-    fr29_t d;
-    int32_t bw = 0;
-    MI_UNROLL for (int i = 0; i < 8; i++) {
-        int32_t t = (int32_t)a.v[i] - (int32_t)m[i] + bw;
-        d.v[i] = (uint32_t)t & M29;
-        bw = t >> 29;
-    }
-    const int32_t top = (int32_t)a.v[8] - (int32_t)m[8] + bw;
-    d.v[8] = (uint32_t)top;
-    return top < 0 ? a : d;
-}
-MI_HD fr29_t fr29_sbox(const fr29_t &x) {  // x^5
-    const fr29_t x2 = fr29_mul(x, x);
-    const fr29_t x4 = fr29_mul(x2, x2);
-    return fr29_mul(x4, x);
-}
-// Montgomery value < 4r -> canonical integer < r
-MI_HD fr29_t fr29_from_mont(const fr29_t &a) {
-    fr29_t one = {{1, 0, 0, 0, 0, 0, 0, 0, 0}};
-    return fr29_sub_if_ge(fr29_mul(a, one), FrDesc::MOD29);  // REDC(a) < a / R + r <= r
-}
-
 // row . s over T terms: chunks of <= 6 products per reduction, sums lazily added (each chunk < 1.5r
 // for rows < r and s < 5r, so T <= 12 gives < 3r)
 template <int T>
