@@ -166,3 +166,38 @@ def test_large_tree_sampled_parents(ctx):
             kids = [int.from_bytes(rows[level - 1][32 * (8 * j + q):32 * (8 * j + q + 1)].tobytes(), "little")
                     for q in range(8)]
             assert int.from_bytes(rows[level][32 * j:32 * (j + 1)].tobytes(), "little") == h.hash(kids), (level, j)
+
+
+def test_large_tree_c_sampled_columns_and_parents(ctx):
+    """BASELINE-scale property check: tree C over 2^24 columns x 11 layers (one 512 MiB-per-layer sub-tree,
+    5.6 GB of labels in HBM); 256 random column hashes and every level's sampled parents are recomputed by
+    the C oracle (or_poseidon_hash)."""
+    import oracle_py
+
+    n, L = 8 ** 8, 11
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    labels = torch.randint(0, 2 ** 62, (L * n, 4), dtype=torch.int64, device="cuda", generator=g)
+    labels[:, 3] &= 0x0FFFFFFFFFFFFFFF
+    base = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    tsz = fg.tree.get_merkle_tree_cache_size(n, 8, 0)
+    tree = torch.zeros((tsz, 4), dtype=torch.int64, device="cuda")
+    fg.tree.ColumnTreeBuilder(ctx, L, 8).add_final_columns_dev(labels.data_ptr(), n, base.data_ptr(), tree.data_ptr())
+    ctx.synchronize()
+    pr = random.Random(2)
+    cols = sorted(pr.randrange(n) for _ in range(256))
+    idx = torch.tensor(cols, device="cuda")
+    lab = labels.view(L, n, 4)[:, idx].permute(1, 0, 2).contiguous().cpu().numpy().view(np.uint8).tobytes()
+    want = oracle_py.poseidon_hash(11, lab)
+    got = base[idx].cpu().numpy().view(np.uint8).tobytes()
+    assert got == want
+    t = tree.cpu().numpy().view(np.uint8).reshape(-1, 32)
+    rows, off, cnt = [base.cpu().numpy().view(np.uint8).reshape(-1, 32)], 0, n // 8
+    while cnt >= 1:
+        rows.append(t[off:off + cnt])
+        off += cnt
+        cnt //= 8
+    for level in range(1, len(rows)):
+        js = [pr.randrange(len(rows[level])) for _ in range(16)]
+        kids = b"".join(rows[level - 1][8 * j:8 * j + 8].tobytes() for j in js)
+        assert oracle_py.poseidon_hash(8, kids) == b"".join(rows[level][j].tobytes() for j in js), level
