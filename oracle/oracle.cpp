@@ -988,6 +988,74 @@ int or_poseidon_hash(unsigned arity, const uint8_t *rc32, const uint8_t *mds32, 
     return bad ? -1 : 0;
 }
 
+/* The same hash in the optimised (sparse) form -- constants from poseidon_ref.sparse_form, derived there
+ * independently of the GPU library -- for a CPU baseline with the operation count Filecoin's CPU
+ * implementation has: folded partial-round constants, 2t - 1 products per partial round.
+ * first / last: (rf / 2) * t, part: rp, mds / dense: t * t, rows: (rp - 1) * (t + t - 1). */
+int or_poseidon_hash_sparse(unsigned arity, unsigned rf, unsigned rp, const uint8_t *first32, const uint8_t *part32,
+                            const uint8_t *last32, const uint8_t *mds32, const uint8_t *rows32, const uint8_t *dense32,
+                            const uint8_t *in32, uint64_t n, uint8_t *out32) {
+    const unsigned t = arity + 1, half = rf / 2;
+    if (t > 17) return -1;
+    auto vec = [](const uint8_t *b, size_t cnt) {
+        std::vector<fr> v(cnt);
+        for (size_t i = 0; i < cnt; i++) v[i] = fr_from_le(b + 32 * i);
+        return v;
+    };
+    const std::vector<fr> cf = vec(first32, (size_t)half * t), cp = vec(part32, rp), cl = vec(last32, (size_t)half * t),
+                          m = vec(mds32, (size_t)t * t), rows = vec(rows32, (size_t)(rp - 1) * (2 * t - 1)),
+                          dn = vec(dense32, (size_t)t * t);
+    uint8_t tagb[32] = {0};
+    const uint64_t tag = (1ull << arity) - 1;
+    memcpy(tagb, &tag, 8);
+    const fr ftag = fr_from_le(tagb);
+    int bad = 0;
+    const int nt = nthreads();
+#pragma omp parallel for num_threads(nt) schedule(static) reduction(| : bad) if (n >= 64)
+    for (int64_t i = 0; i < (int64_t)n; i++) {
+        fr s[17], nx[17];
+        s[0] = ftag;
+        for (unsigned j = 0; j < arity; j++) {
+            uint64_t raw[4];
+            memcpy(raw, in32 + 32 * ((uint64_t)i * arity + j), 32);
+            if (!FR::is_canonical(raw)) bad |= 1;
+            s[j + 1] = FR::from_raw(raw);
+        }
+        auto sbox = [](const fr &x) {
+            fr x2 = FR::mul(x, x);
+            return FR::mul(FR::mul(x2, x2), x);
+        };
+        auto matv = [&](const std::vector<fr> &a) {
+            for (unsigned r = 0; r < t; r++) {
+                fr acc = FR::zero();
+                for (unsigned q = 0; q < t; q++) acc = FR::add(acc, FR::mul(a[(size_t)r * t + q], s[q]));
+                nx[r] = acc;
+            }
+            for (unsigned r = 0; r < t; r++) s[r] = nx[r];
+        };
+        for (unsigned r = 0; r < half; r++) {
+            for (unsigned j = 0; j < t; j++) s[j] = sbox(FR::add(s[j], cf[(size_t)r * t + j]));
+            matv(m);
+        }
+        for (unsigned k = 0; k + 1 < rp; k++) {
+            const fr *row = &rows[(size_t)k * (2 * t - 1)];
+            s[0] = sbox(FR::add(s[0], cp[k]));
+            fr n0 = FR::zero();
+            for (unsigned q = 0; q < t; q++) n0 = FR::add(n0, FR::mul(row[q], s[q]));
+            for (unsigned j = 1; j < t; j++) s[j] = FR::add(s[j], FR::mul(row[t + j - 1], s[0]));
+            s[0] = n0;
+        }
+        s[0] = sbox(FR::add(s[0], cp[rp - 1]));
+        matv(dn);
+        for (unsigned r = 0; r < half; r++) {
+            for (unsigned j = 0; j < t; j++) s[j] = sbox(FR::add(s[j], cl[(size_t)r * t + j]));
+            matv(m);
+        }
+        fr_to_le(s[1], out32 + 32 * (uint64_t)i);
+    }
+    return bad ? -1 : 0;
+}
+
 void or_set_threads(int n) { g_threads = n; }
 int or_get_threads(void) { return nthreads(); }
 

@@ -112,6 +112,10 @@ int or_groth16_verify(const uint8_t vk864[864], const uint8_t *ic96, uint64_t nu
 /* Poseidon, literal form (constants from oracle/poseidon_ref.py); out[i] = hash of in[i*arity ..] */
 int or_poseidon_hash(unsigned arity, const uint8_t *rc32, const uint8_t *mds32, unsigned rf, unsigned rp,
                      const uint8_t *in32, uint64_t n, uint8_t *out32);
+/* the same in the sparse form (constants from poseidon_ref.sparse_form) */
+int or_poseidon_hash_sparse(unsigned arity, unsigned rf, unsigned rp, const uint8_t *first32, const uint8_t *part32,
+                            const uint8_t *last32, const uint8_t *mds32, const uint8_t *rows32, const uint8_t *dense32,
+                            const uint8_t *in32, uint64_t n, uint8_t *out32);
 void or_set_threads(int n);
 int or_get_threads(void);
 

@@ -186,6 +186,32 @@ def poseidon_hash(arity: int, preimages: bytes) -> bytes:
     return out.raw[:32 * n]
 
 
+_SPARSE = {}
+
+
+def poseidon_hash_sparse(arity: int, preimages: bytes) -> bytes:
+    """The same digests through the C oracle's sparse (optimised) form, constants from
+    poseidon_ref.sparse_form: the CPU baseline of the tree builders."""
+    import poseidon_ref as P
+
+    if arity not in _SPARSE:
+        first, part, last, rows, dense = P.sparse_form(arity)
+        h = P.poseidon(arity)
+        enc = lambda xs: b"".join(P.fr_to_bytes(x) for x in xs)
+        _SPARSE[arity] = (h.r_f, h.r_p, enc([x for r in first for x in r]), enc(part), enc([x for r in last for x in r]),
+                          enc([x for row in h.m for x in row]), enc([x for row, w in rows for x in row + w]),
+                          enc([x for row in dense for x in row]))
+    rf, rp, first, part, last, mds, rows, dense = _SPARSE[arity]
+    n = len(preimages) // (32 * arity)
+    out = _buf(32 * max(n, 1))
+    L = lib()
+    L.or_poseidon_hash_sparse.argtypes = [ctypes.c_uint, ctypes.c_uint, ctypes.c_uint] + [ctypes.c_char_p] * 7 + [
+        ctypes.c_uint64, ctypes.c_void_p]
+    if L.or_poseidon_hash_sparse(arity, rf, rp, first, part, last, mds, rows, dense, bytes(preimages), n, out) != 0:
+        raise ValueError("non-canonical Poseidon input")
+    return out.raw[:32 * n]
+
+
 # ------------------------------------------------------------------ R1CS / Groth16
 class R1CS(ctypes.Structure):
     _fields_ = [

@@ -118,6 +118,84 @@ class Poseidon:
         return self.permute([self.tag] + list(xs))[1]
 
 
+def _mat_inv(a):
+    """Gauss-Jordan inverse over Fr (plain ints)."""
+    n = len(a)
+    m = [list(row) + [1 if i == j else 0 for j in range(n)] for i, row in enumerate(a)]
+    for c in range(n):
+        p = next(r for r in range(c, n) if m[r][c] % R)
+        m[c], m[p] = m[p], m[c]
+        iv = pow(m[c][c], R - 2, R)
+        m[c] = [x * iv % R for x in m[c]]
+        for r in range(n):
+            if r != c and m[r][c]:
+                f = m[r][c]
+                m[r] = [(x - f * y) % R for x, y in zip(m[r], m[c])]
+    return [row[n:] for row in m]
+
+
+def _mat_mul(a, b):
+    return [[sum(a[i][k] * b[k][j] for k in range(len(b))) % R for j in range(len(b[0]))] for i in range(len(a))]
+
+
+def sparse_form(arity):
+    """The optimised evaluation (Poseidon paper, appendix B; neptune's "optimized static" constants), derived
+    here independently of the library's C++: round constants of elements 1.. of every partial round folded
+    into the next round; M A_{k-1} = A_k B_k with A_k = diag(1, M^^k), B_k = [[m00, v^T M^^{k-1}],
+    [M^^-k w, I]]; the last partial round uses the dense M A_{R_P - 1}.  Returns (rc_first, rc_part, rc_last,
+    sparse rows [(row, w_hat)], dense)."""
+    h = poseidon(arity)
+    t, rf, rp, m = h.t, h.r_f, h.r_p, h.m
+    rc = [h.rc[r * t:(r + 1) * t] for r in range(rf + rp)]
+    half = rf // 2
+    for r in range(half, half + rp):
+        tail = [0] + rc[r][1:]
+        add = [sum(m[i][j] * tail[j] for j in range(t)) % R for i in range(t)]
+        rc[r + 1] = [(x + y) % R for x, y in zip(rc[r + 1], add)]
+        rc[r] = [rc[r][0]] + [0] * (t - 1)
+    mh = [row[1:] for row in m[1:]]
+    v, w = m[0][1:], [m[i][0] for i in range(1, t)]
+    mh_inv = _mat_inv(mh)
+    ah = [[1 if i == j else 0 for j in range(t - 1)] for i in range(t - 1)]
+    w_k = w
+    rows = []
+    for _ in range(1, rp):
+        row = [m[0][0]] + [sum(v[q] * ah[q][j] for q in range(t - 1)) % R for j in range(t - 1)]
+        ah = _mat_mul(mh, ah)
+        w_k = [sum(mh_inv[i][q] * w_k[q] for q in range(t - 1)) % R for i in range(t - 1)]
+        rows.append((row, list(w_k)))
+    a = [[1 if (i == 0 and j == 0) else 0 for j in range(t)] for i in range(t)]
+    for i in range(t - 1):
+        for j in range(t - 1):
+            a[i + 1][j + 1] = ah[i][j]
+    dense = _mat_mul(m, a)
+    return rc[:half], [rc[r][0] for r in range(half, half + rp)], rc[half + rp:], rows, dense
+
+
+def permute_sparse(arity, state):
+    """The permutation evaluated in the sparse form (must equal Poseidon.permute)."""
+    h = poseidon(arity)
+    t = h.t
+    first, part, last, rows, dense = sparse_form(arity)
+    s = [x % R for x in state]
+
+    def full(s, c):
+        s = [pow((x + y) % R, 5, R) for x, y in zip(s, c)]
+        return [sum(h.m[i][j] * s[j] for j in range(t)) % R for i in range(t)]
+
+    for c in first:
+        s = full(s, c)
+    for k, (row, wh) in enumerate(rows):
+        s[0] = pow((s[0] + part[k]) % R, 5, R)
+        n0 = sum(a * b for a, b in zip(row, s)) % R
+        s = [n0] + [(s[j + 1] + wh[j] * s[0]) % R for j in range(t - 1)]
+    s[0] = pow((s[0] + part[-1]) % R, 5, R)
+    s = [sum(dense[i][j] * s[j] for j in range(t)) % R for i in range(t)]
+    for c in last:
+        s = full(s, c)
+    return s
+
+
 _CACHE = {}
 
 

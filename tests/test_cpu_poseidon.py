@@ -86,3 +86,20 @@ def test_tree_cache_size_semantics():
     leaves = list(range(64))
     assert len(P.tree_data(leaves, 8, 0)) == fg.tree.get_merkle_tree_cache_size(64, 8, 0)
     assert len(P.tree_data(leaves, 8, 1)) == fg.tree.get_merkle_tree_cache_size(64, 8, 1)
+
+
+def test_sparse_form_restatements_agree():
+    """The oracle's own sparse-form derivation (poseidon_ref.sparse_form, independent of the library's C++)
+    evaluates to the literal permutation, in Python and in the C oracle used as the CPU baseline."""
+    import oracle_py
+
+    rng = random.Random(9)
+    for a in (2, 4, 8, 11):
+        for _ in range(2):
+            st = [P.poseidon(a).tag] + [rng.randrange(P.R) for _ in range(a)]
+            assert P.permute_sparse(a, st) == P.poseidon(a).permute(st)
+        xs = [rng.randrange(P.R) for _ in range(8 * a)]
+        b = b"".join(P.fr_to_bytes(x) for x in xs)
+        assert oracle_py.poseidon_hash_sparse(a, b) == oracle_py.poseidon_hash(a, b)
+        assert fg.tree.to_ints(oracle_py.poseidon_hash(a, b)) == [P.poseidon(a).hash(xs[i * a:(i + 1) * a])
+                                                                   for i in range(8)]
