@@ -240,8 +240,8 @@ def config4_leg(args, fg, synth_mod, ctx):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--log-rows", type=int, default=26, help="log2 of the evaluation domain (config 3: 26)")
     ap.add_argument("--n-in", type=int, default=4)
     ap.add_argument("--seed", type=int, default=1)

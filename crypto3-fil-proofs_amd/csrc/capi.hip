@@ -577,33 +577,63 @@ int mi_groth16_prove_batch(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *cir
         uint64_t nv = circ->p->n_in + circ->p->n_aux;
         // partition k + 1's upload (and, for pageable witnesses, its host staging on a helper thread)
         // runs while partition k is proven; witness_ready(k) then finds it finished
-        mi::fr_t *zd[2] = {witness_upload(ctx, 0, z[0], nv), nullptr};
+        // the blinding scalars are checked before any GPU work
+        std::vector<mi::fr_t> rr(count), ss(count);
         for (uint64_t k = 0; k < count; k++) {
-            const int slot = (int)(k & 1);
-            witness_ready(ctx, slot, nv);
-            std::thread next;
-            std::exception_ptr up_err;
-            if (k + 1 < count) {
-                const int ns = slot ^ 1;
-                const uint8_t *zn = z[k + 1];
-                next = std::thread([&, ns, zn] {
+            rr[k] = fr_checked(rs + 64 * k);
+            ss[k] = fr_checked(rs + 64 * k + 32);
+        }
+        const mi::AssemblyKey key = mi::assembly_key(*srs->p);
+        // proof k's host assembly (blinding scalar multiplications, affine conversion, compression: ~10 ms
+        // of CPU) runs on a helper thread while proof k + 1's MSMs run on the GPU
+        std::thread assembler;
+        std::exception_ptr asm_err;
+        auto join_assembler = [&] {
+            if (assembler.joinable()) assembler.join();
+            if (asm_err) std::rethrow_exception(asm_err);
+        };
+        mi::fr_t *zd[2] = {witness_upload(ctx, 0, z[0], nv), nullptr};
+        try {
+            for (uint64_t k = 0; k < count; k++) {
+                const int slot = (int)(k & 1);
+                witness_ready(ctx, slot, nv);
+                std::thread next;
+                std::exception_ptr up_err;
+                if (k + 1 < count) {
+                    const int ns = slot ^ 1;
+                    const uint8_t *zn = z[k + 1];
+                    next = std::thread([&, ns, zn] {
+                        try {
+                            MI_HIP(hipSetDevice(ctx->c.device));
+                            zd[ns] = witness_upload(ctx, ns, zn, nv);
+                        } catch (...) {
+                            up_err = std::current_exception();
+                        }
+                    });
+                }
+                mi::ProofSums sums;
+                try {
+                    sums = mi::groth16_sums(ctx->c, *srs->p, *circ->p, zd[slot]);
+                } catch (...) {
+                    if (next.joinable()) next.join();
+                    throw;
+                }
+                if (next.joinable()) next.join();
+                if (up_err) std::rethrow_exception(up_err);
+                join_assembler();
+                assembler = std::thread([&, sums, k] {
                     try {
-                        MI_HIP(hipSetDevice(ctx->c.device));
-                        zd[ns] = witness_upload(ctx, ns, zn, nv);
+                        proof_bytes(mi::groth16_assemble(key, sums, rr[k], ss[k]), proofs_out + 192 * k, nullptr);
                     } catch (...) {
-                        up_err = std::current_exception();
+                        asm_err = std::current_exception();
                     }
                 });
             }
-            try {
-                prove_impl(ctx, srs, circ, zd[slot], rs + 64 * k, rs + 64 * k + 32, proofs_out + 192 * k, nullptr);
-            } catch (...) {
-                if (next.joinable()) next.join();
-                throw;
-            }
-            if (next.joinable()) next.join();
-            if (up_err) std::rethrow_exception(up_err);
+        } catch (...) {
+            if (assembler.joinable()) assembler.join();
+            throw;
         }
+        join_assembler();
     });
 }
 
