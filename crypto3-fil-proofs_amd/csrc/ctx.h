@@ -14,6 +14,7 @@
 
 #include "curve.h"
 #include "field.h"
+#include "fr29.h"
 
 namespace mi {
 
@@ -63,7 +64,9 @@ struct NttTables {
     fr_t *iv_lo = nullptr, *iv_hi = nullptr;  // powers of omega_{2^32}^-1
     fr_t *g_lo = nullptr, *g_hi = nullptr;    // powers of the coset generator 7
     fr_t *gi_lo = nullptr, *gi_hi = nullptr;  // powers of 7^-1
-    fr_t *fw_1024 = nullptr, *iv_1024 = nullptr;  // omega_1024^j, j < 512 (in-tile twiddles)
+    fr29_t *fw_1024 = nullptr, *iv_1024 = nullptr;  // omega_1024^j, j < 512 (in-tile twiddles, 29-bit limbs)
+    fr29_t *lo29[4] = {nullptr, nullptr, nullptr, nullptr};  // fw, iv, g, gi LO / HI tables in 29-bit limbs
+    fr29_t *hi29[4] = {nullptr, nullptr, nullptr, nullptr};  // (the NTT passes)
 };
 
 // Per-kernel-class device time from HIP events recorded on the launching stream.  Event pairs are

@@ -38,11 +38,11 @@ __device__ __forceinline__ fr_t tw_full(const fr_t *__restrict__ lo, const fr_t 
 }
 
 // the same twiddle in 9 x 29-bit limbs (< 2r)
-__device__ __forceinline__ fr29_t tw29(const fr_t *__restrict__ lo, const fr_t *__restrict__ hi, uint32_t e) {
+__device__ __forceinline__ fr29_t tw29(const fr29_t *__restrict__ lo, const fr29_t *__restrict__ hi, uint32_t e) {
     uint32_t l = e & 0xffffu, h = e >> 16;
-    if (l == 0) return fr29_from_fr(hi[h]);
-    if (h == 0) return fr29_from_fr(lo[l]);
-    return fr29_mul(fr29_from_fr(lo[l]), fr29_from_fr(hi[h]));
+    if (l == 0) return hi[h];
+    if (h == 0) return lo[l];
+    return fr29_mul(lo[l], hi[h]);
 }
 
 __device__ __forceinline__ uint32_t brev(uint32_t x, unsigned bits) {
@@ -89,18 +89,16 @@ __device__ __forceinline__ unsigned ins2(unsigned q, unsigned p0) {
 __device__ __forceinline__ unsigned ins1(unsigned q, unsigned p) {
     return (q & ((1u << p) - 1)) | ((q >> p) << (p + 1));
 }
-// In-tile twiddle omega_{2^b}^j = tw[j << sh]: sh = TILE_LOG - b on the 512-entry omega_1024 table,
-// 0 on the per-pass copy in LDS (MI_NTT_TWLDS).
-__device__ __forceinline__ fr_t tw_b(const fr_t *__restrict__ tw, unsigned j, unsigned sh) { return tw[j << sh]; }
-#ifndef MI_NTT_TWLDS
-#define MI_NTT_TWLDS 0  // same-box A/B: 11.7 (global, L1-resident) vs 11.8 ms (LDS copy) per 2^26 transform
-#endif
+// In-tile twiddle omega_{2^b}^j = tw[j << sh], sh = TILE_LOG - b, from the 512-entry omega_1024 table kept
+// in 29-bit limbs (no conversion in the rounds).  (An LDS copy of the table measured 11.8 vs 11.7 ms per
+// 2^26 transform in round 1 and was dropped.)
+__device__ __forceinline__ fr29_t tw_b(const fr29_t *__restrict__ tw, unsigned j, unsigned sh) { return tw[j << sh]; }
 
 // The b stages of one tile: radix-4 register rounds (two stages per LDS round trip) plus one
 // radix-2 round when b is odd.  DIF runs rounds in order, DIT the transpose in reverse order.
 template <bool DIF>
 __device__ __forceinline__ void ntt_rounds(LdsTile &sh, unsigned b, unsigned Tlog, unsigned tile,
-                                           const fr_t *__restrict__ tw10, unsigned tsh) {
+                                           const fr29_t *__restrict__ tw10, unsigned tsh) {
     const unsigned T = 1u << Tlog;
     const unsigned nquad = tile >> 2;
     const unsigned nr4 = b >> 1;  // radix-4 rounds: DIF stage pairs (0,1), (2,3), ...
@@ -128,14 +126,14 @@ __device__ __forceinline__ void ntt_rounds(LdsTile &sh, unsigned b, unsigned Tlo
                 if (DIF) {
                     fr29_t a = fr29_add(x0, x2), c = fr29_sub_lazy(x0, x2, R2X29);
                     fr29_t bb = fr29_add(x1, x3), dd = fr29_sub_lazy(x1, x3, R2X29);
-                    if (j0) c = fr29_mul(c, f29(tw_b(tw10, j0, tsh)));
-                    dd = fr29_mul(dd, f29(tw_b(tw10, j1, tsh)));
+                    if (j0) c = fr29_mul(c, tw_b(tw10, j0, tsh));
+                    dd = fr29_mul(dd, tw_b(tw10, j1, tsh));
                     x0 = red8(fr29_add(a, bb));
                     x1 = fr29_sub_lazy(a, bb, R4X29);
                     x2 = red8(fr29_add(c, dd));
                     x3 = fr29_sub_lazy(c, dd, R2X29);
                     if (jq) {
-                        const fr29_t w = f29(tw_b(tw10, jq, tsh));
+                        const fr29_t w = tw_b(tw10, jq, tsh);
                         x1 = fr29_mul(x1, w);
                         x3 = fr29_mul(x3, w);
                     } else {
@@ -144,14 +142,14 @@ __device__ __forceinline__ void ntt_rounds(LdsTile &sh, unsigned b, unsigned Tlo
                     }
                 } else {
                     if (jq) {
-                        const fr29_t w = f29(tw_b(tw10, jq, tsh));
+                        const fr29_t w = tw_b(tw10, jq, tsh);
                         x1 = fr29_mul(x1, w);
                         x3 = fr29_mul(x3, w);
                     }
                     fr29_t a = fr29_add(x0, x1), bb = fr29_sub_lazy(x0, x1, R2X29);
                     fr29_t c = fr29_add(x2, x3), dd = fr29_sub_lazy(x2, x3, R2X29);
-                    if (j0) c = fr29_mul(c, f29(tw_b(tw10, j0, tsh)));
-                    dd = fr29_mul(dd, f29(tw_b(tw10, j1, tsh)));
+                    if (j0) c = fr29_mul(c, tw_b(tw10, j0, tsh));
+                    dd = fr29_mul(dd, tw_b(tw10, j1, tsh));
                     x0 = red8(fr29_add(a, c));
                     x2 = red8(fr29_sub_lazy(a, c, R4X29));
                     x1 = red8(fr29_add(bb, dd));
@@ -185,30 +183,15 @@ __device__ __forceinline__ void ntt_rounds(LdsTile &sh, unsigned b, unsigned Tlo
 template <bool DIF, bool FUSED = false>
 __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(fr_t *__restrict__ d, unsigned L, unsigned M, unsigned b,
                                                           unsigned Tlog, unsigned Glog, int twiddle,
-                                                          const fr_t *__restrict__ lo,
-                                                          const fr_t *__restrict__ hi,
-                                                          const fr_t *__restrict__ tw10, int epi,
-                                                          const fr_t *__restrict__ glo,
-                                                          const fr_t *__restrict__ ghi, fr_t scale,
-                                                          const fr_t *__restrict__ tw10b = nullptr) {
+                                                          const fr29_t *__restrict__ lo,
+                                                          const fr29_t *__restrict__ hi,
+                                                          const fr29_t *__restrict__ tw10, int epi,
+                                                          const fr29_t *__restrict__ glo,
+                                                          const fr29_t *__restrict__ ghi, fr_t scale,
+                                                          const fr29_t *__restrict__ tw10b = nullptr) {
     __shared__ LdsTile sh;
-#if MI_NTT_TWLDS
-    // this pass's in-tile twiddles omega_{2^b}^j, j < 2^(b-1), copied to LDS once per workgroup
-    // (and the forward table behind them for the fused pass): no global-load latency in the rounds
-    extern __shared__ fr_t twl[];
-    {
-        const unsigned half = b ? 1u << (b - 1) : 0, shft = TILE_LOG - b;
-        for (unsigned j = threadIdx.x; j < half; j += NTT_THREADS) {
-            twl[j] = tw10[j << shft];
-            if (FUSED) twl[half + j] = tw10b[j << shft];
-        }
-    }
-    const fr_t *twA = twl, *twB = twl + (b ? 1u << (b - 1) : 0);
-    const unsigned tsh = 0;
-#else
-    const fr_t *twA = tw10, *twB = tw10b;
+    const fr29_t *twA = tw10, *twB = tw10b;
     const unsigned tsh = TILE_LOG - b;
-#endif
     const fr29_t sc29 = fr29_from_fr(scale);
     const unsigned T = 1u << Tlog;
     const unsigned Slog = M - b;
@@ -274,9 +257,6 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(fr_t *__restrict__ d, 
     }
 }
 
-inline size_t twl_bytes(unsigned b, bool fused) {
-    return MI_NTT_TWLDS && b ? (sizeof(fr_t) << (b - 1)) * (fused ? 2 : 1) : 0;
-}
 
 struct PassPlan {
     unsigned M, b, Tlog, Glog;
@@ -401,21 +381,34 @@ void ntt_init_tables(Ctx &c) {
         MI_HIP(hipMalloc(dst[k][1], sizeof(fr_t) * 65536));
         MI_HIP(hipMemcpy(*dst[k][0], lo.data(), sizeof(fr_t) * 65536, hipMemcpyHostToDevice));
         MI_HIP(hipMemcpy(*dst[k][1], hi.data(), sizeof(fr_t) * 65536, hipMemcpyHostToDevice));
-        if (k < 2) {  // omega_1024^j = HI[j * 64] (HI[h] = omega_{2^16}^h), j < 512
-            std::vector<fr_t> t10(TILE / 2);
-            for (unsigned j = 0; j < TILE / 2; j++) t10[j] = hi[j << (16 - TILE_LOG)];
-            fr_t **p10 = k == 0 ? &c.tw.fw_1024 : &c.tw.iv_1024;
-            MI_HIP(hipMalloc(p10, sizeof(fr_t) * (TILE / 2)));
-            MI_HIP(hipMemcpy(*p10, t10.data(), sizeof(fr_t) * (TILE / 2), hipMemcpyHostToDevice));
+        {  // the same tables in 29-bit limbs for the NTT passes
+            std::vector<fr29_t> l29(65536), h29(65536);
+            for (int i = 0; i < 65536; i++) l29[i] = fr29_from_fr(lo[i]), h29[i] = fr29_from_fr(hi[i]);
+            MI_HIP(hipMalloc(&c.tw.lo29[k], sizeof(fr29_t) * 65536));
+            MI_HIP(hipMalloc(&c.tw.hi29[k], sizeof(fr29_t) * 65536));
+            MI_HIP(hipMemcpy(c.tw.lo29[k], l29.data(), sizeof(fr29_t) * 65536, hipMemcpyHostToDevice));
+            MI_HIP(hipMemcpy(c.tw.hi29[k], h29.data(), sizeof(fr29_t) * 65536, hipMemcpyHostToDevice));
+        }
+        if (k < 2) {  // omega_1024^j = HI[j * 64] (HI[h] = omega_{2^16}^h), j < 512, in 29-bit limbs
+            std::vector<fr29_t> t10(TILE / 2);
+            for (unsigned j = 0; j < TILE / 2; j++) t10[j] = fr29_from_fr(hi[j << (16 - TILE_LOG)]);
+            fr29_t **p10 = k == 0 ? &c.tw.fw_1024 : &c.tw.iv_1024;
+            MI_HIP(hipMalloc(p10, sizeof(fr29_t) * (TILE / 2)));
+            MI_HIP(hipMemcpy(*p10, t10.data(), sizeof(fr29_t) * (TILE / 2), hipMemcpyHostToDevice));
         }
     }
 }
 
 void ntt_free_tables(Ctx &c) {
-    fr_t *ps[10] = {c.tw.fw_lo, c.tw.fw_hi, c.tw.iv_lo, c.tw.iv_hi, c.tw.g_lo,   c.tw.g_hi,
-                    c.tw.gi_lo, c.tw.gi_hi, c.tw.fw_1024, c.tw.iv_1024};
+    fr_t *ps[8] = {c.tw.fw_lo, c.tw.fw_hi, c.tw.iv_lo, c.tw.iv_hi, c.tw.g_lo, c.tw.g_hi, c.tw.gi_lo, c.tw.gi_hi};
     for (auto p : ps)
         if (p) hipFree(p);
+    for (int k = 0; k < 4; k++) {
+        if (c.tw.lo29[k]) hipFree(c.tw.lo29[k]);
+        if (c.tw.hi29[k]) hipFree(c.tw.hi29[k]);
+    }
+    if (c.tw.fw_1024) hipFree(c.tw.fw_1024);
+    if (c.tw.iv_1024) hipFree(c.tw.iv_1024);
     c.tw = NttTables();
 }
 
@@ -431,24 +424,22 @@ static void ntt_run(Ctx &c, fr_t *d, unsigned L, bool inverse, bool dif, int epi
         return;
     }
     ScopedTimer tm(c, &c.stats.ntt, 1ull << L);
-    const fr_t *lo = inverse ? c.tw.iv_lo : c.tw.fw_lo;
-    const fr_t *hi = inverse ? c.tw.iv_hi : c.tw.fw_hi;
-    const fr_t *glo = inv_gen ? c.tw.gi_lo : c.tw.g_lo;
-    const fr_t *ghi = inv_gen ? c.tw.gi_hi : c.tw.g_hi;
-    const fr_t *tw10 = inverse ? c.tw.iv_1024 : c.tw.fw_1024;
+    const fr29_t *lo = c.tw.lo29[inverse ? 1 : 0], *hi = c.tw.hi29[inverse ? 1 : 0];
+    const fr29_t *glo = c.tw.lo29[inv_gen ? 3 : 2], *ghi = c.tw.hi29[inv_gen ? 3 : 2];
+    const fr29_t *tw10 = inverse ? c.tw.iv_1024 : c.tw.fw_1024;
     auto plan = plan_passes(L);
     if (dif) {
         for (size_t i = 0; i < plan.size(); i++) {
             auto &p = plan[i];
             int e = (i + 1 == plan.size()) ? epi : 0;
-            k_ntt_pass<true><<<(unsigned)p.blocks, NTT_THREADS, twl_bytes(p.b, false), c.stream>>>(d, L, p.M, p.b, p.Tlog, p.Glog,
+            k_ntt_pass<true><<<(unsigned)p.blocks, NTT_THREADS, 0, c.stream>>>(d, L, p.M, p.b, p.Tlog, p.Glog,
                                                                                  p.twiddle, lo, hi, tw10, e, glo,
                                                                                  ghi, scale);
         }
     } else {
         for (int i = (int)plan.size() - 1; i >= 0; i--) {
             auto &p = plan[i];
-            k_ntt_pass<false><<<(unsigned)p.blocks, NTT_THREADS, twl_bytes(p.b, false), c.stream>>>(d, L, p.M, p.b, p.Tlog, p.Glog,
+            k_ntt_pass<false><<<(unsigned)p.blocks, NTT_THREADS, 0, c.stream>>>(d, L, p.M, p.b, p.Tlog, p.Glog,
                                                                                   p.twiddle, lo, hi, tw10, 0, glo,
                                                                                   ghi, scale);
         }
@@ -471,21 +462,21 @@ void ntt_coset_roundtrip(Ctx &c, fr_t *d, unsigned L, const fr_t &scale) {
     const size_t last = plan.size() - 1;
     for (size_t i = 0; i < last; i++) {
         auto &p = plan[i];
-        k_ntt_pass<true><<<(unsigned)p.blocks, NTT_THREADS, twl_bytes(p.b, false), c.stream>>>(d, L, p.M, p.b, p.Tlog, p.Glog, p.twiddle,
-                                                                             c.tw.iv_lo, c.tw.iv_hi, c.tw.iv_1024, 0,
-                                                                             c.tw.g_lo, c.tw.g_hi, scale);
+        k_ntt_pass<true><<<(unsigned)p.blocks, NTT_THREADS, 0, c.stream>>>(d, L, p.M, p.b, p.Tlog, p.Glog, p.twiddle,
+                                                                             c.tw.lo29[1], c.tw.hi29[1], c.tw.iv_1024, 0,
+                                                                             c.tw.lo29[2], c.tw.hi29[2], scale);
     }
     {
         auto &p = plan[last];
-        k_ntt_pass<true, true><<<(unsigned)p.blocks, NTT_THREADS, twl_bytes(p.b, true), c.stream>>>(
-            d, L, p.M, p.b, p.Tlog, p.Glog, 0, c.tw.iv_lo, c.tw.iv_hi, c.tw.iv_1024, 1, c.tw.g_lo, c.tw.g_hi, scale,
-            c.tw.fw_1024);
+        k_ntt_pass<true, true><<<(unsigned)p.blocks, NTT_THREADS, 0, c.stream>>>(
+            d, L, p.M, p.b, p.Tlog, p.Glog, 0, c.tw.lo29[1], c.tw.hi29[1], c.tw.iv_1024, 1, c.tw.lo29[2], c.tw.hi29[2],
+            scale, c.tw.fw_1024);
     }
     for (int i = (int)last - 1; i >= 0; i--) {
         auto &p = plan[i];
-        k_ntt_pass<false><<<(unsigned)p.blocks, NTT_THREADS, twl_bytes(p.b, false), c.stream>>>(d, L, p.M, p.b, p.Tlog, p.Glog, p.twiddle,
-                                                                              c.tw.fw_lo, c.tw.fw_hi, c.tw.fw_1024, 0,
-                                                                              c.tw.g_lo, c.tw.g_hi, scale);
+        k_ntt_pass<false><<<(unsigned)p.blocks, NTT_THREADS, 0, c.stream>>>(d, L, p.M, p.b, p.Tlog, p.Glog, p.twiddle,
+                                                                              c.tw.lo29[0], c.tw.hi29[0], c.tw.fw_1024, 0,
+                                                                              c.tw.lo29[2], c.tw.hi29[2], scale);
     }
     MI_HIP(hipGetLastError());
 }

@@ -788,12 +788,18 @@ ProofSums groth16_sums(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *
     {
         // L, B_G1 and B_G2 do not depend on the QAP: they run on the auxiliary lane (second stream,
         // second host thread) while this stream runs the witness map, the NTT chain, H and A.
-        Ctx &x = ctx_aux(c);
+        // MI_PROVE_LANES=1 runs the auxiliary work after the main lane on the same stream (measurement
+        // only: every phase's device time without the other lane's kernels beside it)
+        static const bool one_lane = [] {
+            const char *e = getenv("MI_PROVE_LANES");
+            return e && atoi(e) == 1;
+        }();
+        Ctx &x = one_lane ? c : ctx_aux(c);
         hipEvent_t ready = x.timer.get(), done = x.timer.get();
         MI_HIP(hipEventRecord(ready, st));  // z_dev and everything queued before this prove
         MI_HIP(hipStreamWaitEvent(x.stream, ready, 0));
         std::exception_ptr err;
-        std::thread lane([&] {
+        auto aux_work = [&] {
             try {
                 MI_HIP(hipSetDevice(c.device));
                 // B_G1 and B_G2 share the scalars (z over the B-density): sort them once
@@ -819,7 +825,9 @@ ProofSums groth16_sums(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *
             } catch (...) {
                 err = std::current_exception();
             }
-        });
+        };
+        std::thread lane;
+        if (!one_lane) lane = std::thread(aux_work);
         std::exception_ptr err_main;
         try {
             fr_t *zm = c.scratch[20].as<fr_t>(nv + 3 * d);
@@ -847,15 +855,21 @@ ProofSums groth16_sums(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *
         } catch (...) {
             err_main = std::current_exception();
         }
-        lane.join();
+        if (one_lane) {
+            if (!err_main) aux_work();
+        } else {
+            lane.join();
+        }
         if (err_main) std::rethrow_exception(err_main);
         if (err) std::rethrow_exception(err);
         MI_HIP(hipStreamWaitEvent(st, done, 0));  // the prove timer ends after both lanes
         x.timer.pool.push_back(ready);
         x.timer.pool.push_back(done);
-        x.timer.resolve();
-        c.stats.merge(x.stats);
-        x.stats = Stats();
+        if (!one_lane) {
+            x.timer.resolve();
+            c.stats.merge(x.stats);
+            x.stats = Stats();
+        }
     }
     }
     MI_HIP(hipStreamSynchronize(st));
