@@ -9,6 +9,9 @@
 //   * multi_proof  ~ multi_proof{circuit_proofs, verifying_key} (core/proof/multi_proof.hpp:38-58),
 //                    written as P x 192 bytes (api/seal.hpp:306-308)
 //   * partition_count ~ core/partitions.hpp:36-38
+//   * column_tree_builder / tree_builder / generate_tree_r_last / hash_single_column ~ the tree C / tree
+//                    R-last builders and the column hash of porep/stacked/vanilla/proof.hpp:383-810 and
+//                    porep/stacked/vanilla/hash.hpp:37-47
 // Errors are thrown as mi355x::error, like the reference's BOOST_ASSERT_MSG / throw style
 // (compound_proof.hpp:94).
 #pragma once
@@ -180,6 +183,67 @@ inline multi_proof circuit_proofs(context &ctx, const proving_key &pk, const cir
     mp.verifying_key = pk.verifying_key();
     mp.ic = pk.ic();
     return mp;
+}
+
+// ---- stacked-PoRep Poseidon trees ----------------------------------------------
+// Fr values are 32-byte little-endian canonical (< r); trees are returned row by row, bottom-up, without
+// the base row (and without the rows_to_discard lowest rows above it).
+inline std::uint64_t merkle_tree_cache_size(std::uint64_t leafs, unsigned arity, unsigned rows_to_discard) {
+    std::uint64_t n = 0;
+    check(mi_tree_cache_size(leafs, arity, rows_to_discard, &n));  // get_merkle_tree_cache_size
+    return n;
+}
+
+// hash_single_column (porep/stacked/vanilla/hash.hpp:37-47): Poseidon over 2 or 11 labels
+inline fr32 hash_single_column(context &ctx, const std::vector<fr32> &column) {
+    if (column.size() != 2 && column.size() != 11) throw error(MI_ERR_ARG, "unsupported column size");
+    fr32 out{};
+    check(mi_poseidon_hash(ctx.get(), (unsigned)column.size(), column.front().data(), 1, out.data()));
+    return out;
+}
+
+// ColumnTreeBuilder<ColumnArity, TreeArity>::add_final_columns -> (base_data, tree_data)
+class column_tree_builder {
+public:
+    column_tree_builder(context &ctx, unsigned column_arity = 11, unsigned tree_arity = 8)
+        : ctx_(ctx), column_arity_(column_arity), tree_arity_(tree_arity) {}
+    // layers[l] points at the nodes labels of layer l + 1 for this sub-tree (32 B each)
+    std::pair<std::vector<uint8_t>, std::vector<uint8_t>> add_final_columns(const std::vector<const uint8_t *> &layers,
+                                                                            std::uint64_t nodes) const {
+        if (layers.size() != column_arity_) throw error(MI_ERR_ARG, "one label vector per column layer");
+        std::vector<uint8_t> base(32 * nodes), tree(32 * merkle_tree_cache_size(nodes, tree_arity_, 0));
+        check(mi_tree_c_build(ctx_.get(), column_arity_, nodes, layers.data(), tree_arity_, base.data(), tree.data()));
+        return {std::move(base), std::move(tree)};
+    }
+
+private:
+    context &ctx_;
+    unsigned column_arity_, tree_arity_;
+};
+
+// TreeBuilder<Arity>::add_final_leaves -> tree_data
+class tree_builder {
+public:
+    tree_builder(context &ctx, unsigned arity = 8, unsigned rows_to_discard = 0)
+        : ctx_(ctx), arity_(arity), rows_to_discard_(rows_to_discard) {}
+    std::vector<uint8_t> add_final_leaves(const uint8_t *leaves, std::uint64_t n) const {
+        std::vector<uint8_t> tree(32 * merkle_tree_cache_size(n, arity_, rows_to_discard_));
+        check(mi_tree_build(ctx_.get(), arity_, leaves, n, rows_to_discard_, tree.data()));
+        return tree;
+    }
+
+private:
+    context &ctx_;
+    unsigned arity_, rows_to_discard_;
+};
+
+// generate_tree_r_last, GPU branch: data (the sector's nodes) becomes the replica in place
+// (encode: label + data), then the tree over it
+inline std::vector<uint8_t> generate_tree_r_last(context &ctx, std::uint64_t nodes, const uint8_t *last_layer_labels,
+                                                 uint8_t *data, unsigned arity = 8, unsigned rows_to_discard = 0) {
+    std::vector<uint8_t> tree(32 * merkle_tree_cache_size(nodes, arity, rows_to_discard));
+    check(mi_tree_r_last_build(ctx.get(), nodes, last_layer_labels, data, arity, rows_to_discard, tree.data()));
+    return tree;
 }
 
 }  // namespace mi355x

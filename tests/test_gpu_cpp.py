@@ -28,3 +28,48 @@ def test_cpp_circuit_proofs_match_python(ctx):
     pk = fg.generate_random_parameters(ctx, gc, [11, 12, 13, 14, 15])
     py = [fg.prove(ctx, pk, gc, sc.z_bytes(), 100 + k, 200 + k) for k in range(3)]
     assert cpp == py
+
+
+def test_cpp_tree_builders_match_python(ctx):
+    """examples/tree_c.cpp (C++ host layer: column_tree_builder, generate_tree_r_last) against the Python
+    binding and the oracle on the same SplitMix64 labels."""
+    import numpy as np
+    import poseidon_ref as P
+
+    pkg = os.path.join(ROOT, "crypto3-fil-proofs_amd")
+    exe = os.path.join(pkg, "build", "tree_c")
+    if not os.path.exists(exe):
+        subprocess.check_call(["g++", "-std=c++17", "-O2", "-I" + os.path.join(ROOT, "include"),
+                               os.path.join(pkg, "examples", "tree_c.cpp"), "-L" + os.path.join(pkg, "build"),
+                               "-lfilgpu", "-Wl,-rpath,$ORIGIN", "-o", exe], timeout=120)
+    out = subprocess.run([exe, "3"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    root_c, root_r, rep0 = [int(x, 16) for x in out.stdout.split()]
+
+    state = [42]
+
+    def splitmix():
+        state[0] = (state[0] + 0x9E3779B97F4A7C15) & (2 ** 64 - 1)
+        z = state[0]
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & (2 ** 64 - 1)
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & (2 ** 64 - 1)
+        return z ^ (z >> 31)
+
+    def labels(n):
+        out = []
+        for _ in range(n):
+            w = [splitmix() for _ in range(4)]
+            w[3] &= 0x0FFFFFFFFFFFFFFF
+            out.append(sum(x << (64 * i) for i, x in enumerate(w)))
+        return out
+
+    nodes = 512
+    layers = [labels(nodes) for _ in range(11)]
+    data = labels(nodes)
+    base = P.hash_columns(layers)
+    assert root_c == P.merkle_rows(base, 8)[-1][0]
+    replica = [P.encode(k, d) for k, d in zip(layers[10], data)]
+    assert rep0 == replica[0]
+    assert root_r == P.merkle_rows(replica, 8)[-1][0]
+    _, tree = fg.tree.ColumnTreeBuilder(ctx, 11, 8).add_final_columns(layers)
+    assert fg.tree.to_ints(tree)[-1] == root_c
