@@ -961,8 +961,18 @@ bool g2_second_level(Ctx &c, const MsmPlan &pl, XYZZ<F> *P0, std::vector<XYZZ<F>
         // 1. bucket sums -> affine
         Affine<F> *Baff = c.scratch[18].as<Affine<F>>(nb);
         F *pre = c.scratch[19].as<F>(nb);
-        k_bucket_affine<F, 32><<<grid_for(((uint64_t)nb + 31) / 32, 256), 256, 0, st>>>(pl.coff, pl.cnt, P0, nb,
-                                                                                       pre, Baff);
+        // MI_G2_AFF_K buckets per inversion (Montgomery's trick; read per call for A/B)
+        const char *ek = getenv("MI_G2_AFF_K");
+        const int kaff = ek ? atoi(ek) : 64;  // same-box: 538.2 (32) vs 535.8 (64) vs 536.1 (128) ms per proof
+        if (kaff == 128)
+            k_bucket_affine<F, 128><<<grid_for(((uint64_t)nb + 127) / 128, 256), 256, 0, st>>>(pl.coff, pl.cnt, P0, nb,
+                                                                                             pre, Baff);
+        else if (kaff == 64)
+            k_bucket_affine<F, 64><<<grid_for(((uint64_t)nb + 63) / 64, 256), 256, 0, st>>>(pl.coff, pl.cnt, P0, nb,
+                                                                                           pre, Baff);
+        else
+            k_bucket_affine<F, 32><<<grid_for(((uint64_t)nb + 31) / 32, 256), 256, 0, st>>>(pl.coff, pl.cnt, P0, nb,
+                                                                                           pre, Baff);
         MI_LAUNCHED(c, "k_bucket_affine");
         // 2. two digit entries per non-empty bucket, one sort over all of them
         const uint32_t np2 = 2 * nb;
