@@ -292,6 +292,8 @@ def main():
         pk = fg.generate_random_parameters(ctx, circ, splitmix_frs(TOXIC_SEED, 5))
     ctx.synchronize()
     t_srs = time.perf_counter() - t_setup - t_synth - t_load
+    free_b, total_b = torch.cuda.mem_get_info(local_rank)
+    dev_used_gb = (total_b - free_b) / 1e9  # circuit + proving key (+ split tables unless MI_MSM_GLV=1)
     # the witness in page-locked host memory, where a synthesiser would write it (mi_host_alloc)
     zhost = fg.HostBuffer(32 * sc.num_vars)
     np.copyto(zhost.array, sc.z_array())
@@ -537,6 +539,9 @@ def main():
         "config4": config4,
         "timers_ms": {k: round(v["ms"], 3) for k, v in stats.items()},
         "setup_s": {"synth": t_synth, "circuit_load": t_load, "srs": t_srs},
+        "device_gb_after_setup": round(dev_used_gb, 2),
+        "msm_split": {"1": "glv", "0": "2^128 tables"}.get(os.environ.get("MI_MSM_GLV", ""),
+                                                          "auto: 2^128 tables when they fit in HBM, else glv"),
         "multiproof_bytes": 192 * len(proofs),
         "msm_reps": args.msm_reps,
     }

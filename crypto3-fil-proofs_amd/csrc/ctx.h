@@ -234,6 +234,7 @@ struct MsmPlan {
     unsigned cb = 0, nwin = 0;
     uint32_t nbk = 0, nb = 0, L0 = 0, maxcnt = 0, total = 0;
     uint64_t entries = 0;  // non-zero digits over all windows
+    bool glv = false;      // split through the GLV endomorphism: nbk / nb count sub-buckets (2 per bucket)
     const uint32_t *vals_s = nullptr, *off = nullptr, *cnt = nullptr, *coff = nullptr, *ccnt = nullptr,
                    *chunk_bucket = nullptr, *order = nullptr;
 };
@@ -252,6 +253,11 @@ void msm_g1(Ctx &c, const g1_affine_t *bases, const fr_t *scalars, const uint32_
             g1_xyzz_t *result_host, const g1_affine_t *bases_hi = nullptr);
 // whether msm_g1 with a bases_hi table takes the split path for n points
 bool msm_use_split(uint64_t n);
+// G1 split mode through the GLV endomorphism (glv.h) instead of the 2^128 tables: MI_MSM_GLV unset -> 2
+// (auto: GLV for bases without a table, e.g. caller-uploaded ones, and when the tables would not fit in
+// HBM at key load), 0 -> never, 1 -> always (key load builds no tables).  Same-box 2^26 proof: tables 525-526
+// ms and 88.9 GB after setup, GLV 532-533 ms and 68.9 GB.
+int msm_glv_mode();
 // bases_hi table: out[i] = 2^128 in[i] (128 doublings, batch-normalised to affine); scratch slots 10, 11
 void g1_shift128(Ctx &c, const g1_affine_t *in, uint64_t n, g1_affine_t *out);
 void msm_g2(Ctx &c, const g2_affine_t *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,
@@ -259,7 +265,7 @@ void msm_g2(Ctx &c, const g2_affine_t *bases, const fr_t *scalars, const uint32_
 // host-side window-size heuristic (exposed for tests)
 unsigned msm_window_bits(uint64_t n);
 // same for `n` points with scalars of `sbits` bits including the signed-digit carry (256 plain, 129 split)
-unsigned msm_window_bits_for(uint64_t n, unsigned sbits);
+unsigned msm_window_bits_for(uint64_t n, unsigned sbits, bool glv = false);
 
 // ---- encodings (encode.hip) ----
 // zcash uncompressed big-endian -> device Montgomery affine (zcash from_uncompressed flag rules).

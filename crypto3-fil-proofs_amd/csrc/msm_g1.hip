@@ -7,7 +7,7 @@ namespace mi {
 
 unsigned msm_window_bits(uint64_t n) { return msm_window_bits_for(n, 256); }
 
-unsigned msm_window_bits_for(uint64_t n, unsigned sbits) {
+unsigned msm_window_bits_for(uint64_t n, unsigned sbits, bool glv) {
     // minimise (mixed adds) + 1.4 x (bucket-reduction full adds) over c; split plans (129-bit scalars)
     // keep c >= 9 so their ceil(129 / c) windows fit the split digit kernel (MAXW_S = 16)
     const unsigned cmin = sbits < 256 ? 9 : 4;
@@ -21,7 +21,9 @@ unsigned msm_window_bits_for(uint64_t n, unsigned sbits) {
     double best_cost = 1e300;
     for (unsigned c = cmin; c <= 22; c++) {
         unsigned nwin = (sbits + c - 1) / c;
-        double cost = (double)n * nwin + 1.4 * 2.0 * nwin * (double)(1u << (c - 1)) + 64.0 * nwin * c;
+        // GLV plans add one full addition (+ one multiplication) per bucket in k_glv_merge
+        const double per_bucket = glv ? 3.0 : 2.0;
+        double cost = (double)n * nwin + 1.4 * per_bucket * nwin * (double)(1u << (c - 1)) + 64.0 * nwin * c;
         if (cost < best_cost) {
             best_cost = cost;
             best = c;
@@ -35,6 +37,13 @@ bool msm_use_split(uint64_t n) {
     const char *e = getenv("MI_MSM_SPLIT");
     const int mode = e ? atoi(e) : 1;
     return mode == 2 || (mode == 1 && n >= (1u << 16));
+}
+
+int msm_glv_mode() {
+    // MI_MSM_GLV (read per call): unset = auto (the 2^128 table where the key has one, GLV otherwise),
+    // 0 = never GLV, 1 = always GLV (and key load builds no tables)
+    const char *e = getenv("MI_MSM_GLV");
+    return e && *e ? (atoi(e) != 0 ? 1 : 0) : 2;
 }
 
 void msm_g1(Ctx &c, const g1_affine_t *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,

@@ -27,6 +27,7 @@
 
 #include "ctx.h"
 #include "g2pair.h"
+#include "glv.h"
 
 namespace mi {
 
@@ -207,6 +208,10 @@ MI_HD void digits128(const uint32_t *v, unsigned c, unsigned nwin, uint32_t *dg)
         }
     }
 }
+// GLV (glv.h): the halves are k1 = k mod lambda (over P_i) and k2 = k div lambda (over phi(P_i)), and the
+// key carries the half as its low bit -- sub-bucket 2 (digit - 1) + half -- so the entries over P and over
+// phi(P) of one bucket are accumulated apart and phi is applied once per bucket sum (k_glv_merge).
+template <bool GLV>
 __global__ void __launch_bounds__(256) k_digits_split(const fr_t *__restrict__ scalars,
                                                       const uint32_t *__restrict__ idx, uint32_t nreal, unsigned c,
                                                       unsigned nwin, uint32_t *__restrict__ wcount,
@@ -218,8 +223,15 @@ __global__ void __launch_bounds__(256) k_digits_split(const fr_t *__restrict__ s
     fr_t s = fr_t::zero();
     if (i < nreal) s = scalars[idx ? idx[i] : i];
     uint32_t dlo[MAXW_S], dhi[MAXW_S];
-    digits128(s.v, c, nwin, dlo);
-    digits128(s.v + 4, c, nwin, dhi);
+    if constexpr (GLV) {
+        uint32_t k1[4], k2[4];
+        glv_split(s.v, k1, k2);
+        digits128(k1, c, nwin, dlo);
+        digits128(k2, c, nwin, dhi);
+    } else {
+        digits128(s.v, c, nwin, dlo);
+        digits128(s.v + 4, c, nwin, dhi);
+    }
     const uint64_t below = (1ull << lane) - 1;
     uint32_t rlo[MAXW_S], rhi[MAXW_S];
     MI_UNROLL for (unsigned w = 0; w < MAXW_S; w++) {
@@ -247,11 +259,11 @@ __global__ void __launch_bounds__(256) k_digits_split(const fr_t *__restrict__ s
         if (w < nwin) {
             const uint64_t o = (uint64_t)w * n + wc[wave][w];
             if (dlo[w]) {
-                keys[o + rlo[w]] = (dlo[w] & 0x7fffffffu) - 1;
+                keys[o + rlo[w]] = ((dlo[w] & 0x7fffffffu) - 1) << (GLV ? 1 : 0);
                 vals[o + rlo[w]] = i | (dlo[w] & 0x80000000u);
             }
             if (dhi[w]) {
-                keys[o + rhi[w]] = (dhi[w] & 0x7fffffffu) - 1;
+                keys[o + rhi[w]] = GLV ? (((dhi[w] & 0x7fffffffu) - 1) << 1) | 1u : (dhi[w] & 0x7fffffffu) - 1;
                 vals[o + rhi[w]] = (i + nreal) | (dhi[w] & 0x80000000u);
             }
         }
@@ -524,6 +536,32 @@ __global__ void __launch_bounds__(256) MI_WAVES_RED k_seg_fold(const XYZZ<F> *__
     LP::st(out + t, acc);
 }
 
+// GLV plans (G1): bucket g's entries over P_i sit in sub-bucket 2g and those over phi(P_i) -- gathered as
+// P_i -- in 2g + 1.  B_g = S_2g + phi(S_2g+1) with phi(X, Y, ZZ, ZZZ) = (beta X, Y, ZZ, ZZZ): one Fq
+// multiplication and at most one full addition per bucket instead of a beta multiplication per gathered
+// point (or a 2^128 table).  Writes the dense bucket sums Bm, live[g] = non-empty and iota[g] = g, the
+// off / cnt view reduce_windows reads.
+template <class F>
+__global__ void __launch_bounds__(256) MI_WAVES_RED k_glv_merge(const uint32_t *__restrict__ coff,
+                                                   const uint32_t *__restrict__ cnt,
+                                                   const XYZZ<F> *__restrict__ P0, uint32_t nb, F beta,
+                                                   XYZZ<F> *__restrict__ Bm, uint32_t *__restrict__ live,
+                                                   uint32_t *__restrict__ iota) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= nb) return;
+    const uint32_t c0 = cnt[2 * g], c1 = cnt[2 * g + 1];
+    XYZZ<F> a = XYZZ<F>::inf();
+    if (c0) a = P0[coff[2 * g]];
+    if (c1) {
+        XYZZ<F> b = P0[coff[2 * g + 1]];
+        b.X = b.X * beta;
+        a = c0 ? xyzz_add_inl(a, b) : b;
+    }
+    Bm[g] = a;
+    live[g] = (c0 | c1) ? 1u : 0u;
+    iota[g] = g;
+}
+
 // out[w * (n / G) + g] = sum of in[w * n + g * G ... + G)   (n % G == 0)
 template <class F>
 __global__ void __launch_bounds__(256) MI_WAVES_RED k_sum_groups(const XYZZ<F> *__restrict__ in, uint32_t total_out,
@@ -689,18 +727,21 @@ inline bool plan_chunks(Ctx &c, MsmPlan &pl, uint32_t *offA, uint32_t *cntA, uin
 // The plan's arrays live in scratch slots 3, 5-8, 16, 17 and stay valid until the next prepare on
 // this ctx; the accumulation phase only uses the other slots.
 inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, uint64_t nscal, MsmPlan &pl,
-                             bool split = false) {
+                             bool split = false, bool glv = false) {
     pl = MsmPlan();
     if (nscal == 0) return false;
+    split = split || glv;
+    pl.glv = glv;
     // split mode: 2 nscal points with 128-bit scalars (+1 carry bit), always on the compacted path
     const uint64_t n = split ? 2 * nscal : nscal;
     const unsigned sbits = split ? 129 : 256;
     pl.n = n;
     pl.nreal = split ? nscal : 0;
     hipStream_t st = c.stream;
-    const unsigned cb = msm_window_bits_for(n, sbits);
+    const unsigned cb = msm_window_bits_for(n, sbits, glv);
     const unsigned nwin = (sbits + cb - 1) / cb;
-    const uint32_t nbk = 1u << (cb - 1);
+    // plan buckets per window: 2^(c-1), or twice that for GLV (sub-buckets over P and over phi(P))
+    const uint32_t nbk = (glv ? 2u : 1u) << (cb - 1);
     const uint64_t nb64 = (uint64_t)nwin * nbk;
     const uint64_t np64 = (uint64_t)nwin * n;
     if (np64 >= 0xffffffffull || nb64 >= 0x7fffffffull || n >= 0x80000000ull)
@@ -708,6 +749,10 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
     const uint32_t nb = (uint32_t)nb64, np = (uint32_t)np64, invalid = nbk;  // window-local keys
     unsigned key_bits = 1;
     while ((1ull << key_bits) <= invalid) key_bits++;  // cb bits: one fewer onesweep pass than global keys
+    if (glv) {  // compacted GLV keys stay below nbk (no zero-digit sentinel): cb bits, as the 2^128 split
+        key_bits = 1;
+        while ((1ull << key_bits) < nbk) key_bits++;
+    }
     // Small MSMs sort every window in ONE call over keys w * (nbk + 1) + local when that still takes
     // two 11-bit onesweep places (2^20: 2 launches instead of 32); large ones sort window by window.
     unsigned all_bits = 1;
@@ -744,8 +789,12 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
             MI_HIP(hipMemsetAsync(wcount, 0, sizeof(uint32_t) * nwin, st));
             if (split) {
                 if (nwin > MAXW_S) throw std::logic_error("msm: split plan with more than MAXW_S windows");
-                k_digits_split<<<grid_for(nscal, 256), 256, 0, st>>>(scalars, idx, (uint32_t)nscal, cb, nwin, wcount,
-                                                                      keys, vals);
+                if (glv)
+                    k_digits_split<true><<<grid_for(nscal, 256), 256, 0, st>>>(scalars, idx, (uint32_t)nscal, cb, nwin,
+                                                                                wcount, keys, vals);
+                else
+                    k_digits_split<false><<<grid_for(nscal, 256), 256, 0, st>>>(scalars, idx, (uint32_t)nscal, cb, nwin,
+                                                                                 wcount, keys, vals);
                 MI_LAUNCHED(c, "k_digits_split");
             } else {
                 k_digits_c<<<grid_for(n, 256), 256, 0, st>>>(scalars, idx, (uint32_t)n, cb, nwin, 0u, wcount, keys,
@@ -1033,9 +1082,29 @@ bool g2_second_level(Ctx &c, const MsmPlan &pl, XYZZ<F> *P0, std::vector<XYZZ<F>
 template <class F>
 void msm_accumulate_impl(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, XYZZ<F> *result,
                          const Affine<F> *bases_hi = nullptr) {
-    XYZZ<F> *P0 = accumulate_chunks<F>(c, pl, bases, bases_hi);
+    // GLV plans gather the phi(P_i) half as P_i itself (bases doubles as the "hi" table)
+    XYZZ<F> *P0 = accumulate_chunks<F>(c, pl, bases, pl.glv ? bases : bases_hi);
     std::vector<XYZZ<F>> W;
-    if (!g2_second_level<F>(c, pl, P0, W)) reduce_windows<F>(c, pl, P0, W);
+    if constexpr (sizeof(F) == sizeof(fq_t)) {
+        if (pl.glv) {  // sub-bucket pairs -> bucket sums (k_glv_merge), then the plain reduction over them
+            MsmPlan p2 = pl;
+            p2.nbk = pl.nbk / 2;
+            p2.nb = pl.nb / 2;
+            XYZZ<F> *Bm = c.scratch[18].as<XYZZ<F>>(p2.nb);
+            uint32_t *live = c.scratch[19].as<uint32_t>(2 * (uint64_t)p2.nb), *iota = live + p2.nb;
+            static const fq_t beta = glv_beta();
+            k_glv_merge<F><<<grid_for(p2.nb, 256), 256, 0, c.stream>>>(pl.coff, pl.cnt, P0, p2.nb, beta, Bm, live,
+                                                                       iota);
+            MI_LAUNCHED(c, "k_glv_merge");
+            p2.coff = iota;
+            p2.cnt = live;
+            reduce_windows<F>(c, p2, Bm, W);
+        } else {
+            reduce_windows<F>(c, pl, P0, W);
+        }
+    } else {
+        if (!g2_second_level<F>(c, pl, P0, W)) reduce_windows<F>(c, pl, P0, W);
+    }
     const unsigned nwin = pl.nwin, cb = pl.cb;
     XYZZ<F> acc = W[nwin - 1];
     for (int w = (int)nwin - 2; w >= 0; w--) {
@@ -1051,8 +1120,11 @@ void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const uint32_t
              XYZZ<F> *result, const Affine<F> *bases_hi = nullptr) {
     ScopedTimer whole(c, sizeof(F) == sizeof(fq_t) ? &c.stats.msm_g1 : &c.stats.msm_g2, n);
     MsmPlan pl;
-    const bool split = bases_hi && msm_use_split(n);
-    if (!msm_prepare_impl(c, scalars, idx, n, pl, split)) {
+    // G1 split mode: the GLV endomorphism (no table) when MI_MSM_GLV selects it, else the 2^128 table
+    const int glv_mode = msm_glv_mode();
+    const bool glv = sizeof(F) == sizeof(fq_t) && msm_use_split(n) && (glv_mode == 1 || (glv_mode == 2 && !bases_hi));
+    const bool split = !glv && bases_hi && msm_use_split(n);
+    if (!msm_prepare_impl(c, scalars, idx, n, pl, split, glv)) {
         *result = XYZZ<F>::inf();
         return;
     }

@@ -589,11 +589,19 @@ namespace {
 // split-mode tables of the three G1 queries whose MSMs run alone (B_G1 shares B_G2's plan, which has
 // no table on the G2 side, so b_g1 gets none)
 void build_hi_tables(Ctx &c, Srs &S) {
+    if (msm_glv_mode() == 1) return;  // GLV split mode needs no table (glv.h)
     struct Q {
         const g1_affine_t *src;
         uint64_t n;
         g1_affine_t **dst;
     } qs[] = {{S.h_perm, S.n_h, &S.h_hi}, {S.l, S.n_l, &S.l_hi}, {S.a, S.n_a, &S.a_hi}};
+    if (msm_glv_mode() == 2) {  // auto: tables only while they leave half of the free HBM to the prover
+        uint64_t need = 0;
+        for (auto &q : qs) need += q.src ? q.n * sizeof(g1_affine_t) : 0;
+        size_t free_b = 0, total_b = 0;
+        MI_HIP(hipMemGetInfo(&free_b, &total_b));
+        if (need > free_b / 2) return;  // the MSMs take the GLV split instead
+    }
     for (auto &q : qs) {
         if (!q.src || !q.n) continue;
         *q.dst = dalloc<g1_affine_t>(q.n);

@@ -7,13 +7,15 @@
 // (doubling), P + (-P) (infinity), infinity operands, non-canonical representatives v + p of every
 // coordinate -- and compares each result with the oracle's affine group law.  It also checks the lazy
 // field forms against the reduced operators on random and extreme (near 2p) values.
-// Build/run: tests/test_cpu_grouplaw.py (hipcc host-only, -fsanitize=address,undefined).
+// Build/run: tests/test_cpu_grouplaw.py (hipcc host-only, ASan + UBSan, host code only).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <vector>
 
 #include "curve.h"
+#include "glv.h"
 #include "oracle.h"
 
 using namespace mi;
@@ -249,10 +251,97 @@ static void check_g2() {
     }
 }
 
+// GLV (glv.h): k = k1 + lambda k2 for random / edge / non-canonical scalars, and phi(P) = lambda P
+static void words_of(const uint8_t *b, uint32_t *w, int n) {
+    for (int i = 0; i < n; i++) std::memcpy(&w[i], b + 4 * i, 4);
+}
+static void check_glv() {
+    static const uint32_t R[8] = {0x00000001u, 0xffffffffu, 0xfffe5bfeu, 0x53bda402u,
+                                  0x09a1d805u, 0x3339d808u, 0x299d7d48u, 0x73eda753u};
+    std::vector<std::vector<uint32_t>> ks;
+    auto add = [&](std::initializer_list<uint32_t> w) {
+        std::vector<uint32_t> v(w);
+        v.resize(8, 0);
+        ks.push_back(v);
+    };
+    add({0});
+    add({1});
+    add({GLV_LAMBDA[0] - 1, GLV_LAMBDA[1], GLV_LAMBDA[2], GLV_LAMBDA[3]});  // lambda - 1
+    add({GLV_LAMBDA[0], GLV_LAMBDA[1], GLV_LAMBDA[2], GLV_LAMBDA[3]});      // lambda
+    add({0, 0, 0, 0, 1});                                                   // 2^128
+    add({R[0] - 1, R[1], R[2], R[3], R[4], R[5], R[6], R[7]});              // r - 1 = lambda^2 + lambda
+    add({R[0], R[1], R[2], R[3], R[4], R[5], R[6], R[7]});                  // r (non-canonical: 0)
+    add({R[0] + 5, R[1], R[2], R[3], R[4], R[5], R[6], R[7]});              // r + 5
+    add({~0u, ~0u, ~0u, ~0u, ~0u, ~0u, ~0u, ~0u});                          // 2^256 - 1
+    for (int i = 0; i < 2000; i++) {
+        std::vector<uint32_t> v(8);
+        for (auto &x : v) x = (uint32_t)rng();
+        v[7] &= (i & 1) ? 0x7fffffffu : 0x3fffffffu;
+        ks.push_back(v);
+    }
+    for (size_t t = 0; t < ks.size(); t++) {
+        uint32_t k[8], k1[4], k2[4];
+        for (int i = 0; i < 8; i++) k[i] = ks[t][i];
+        glv_split(k, k1, k2);
+        // expected: k mod r (at most two subtractions: 2^256 < 3 r)
+        uint32_t km[8];
+        std::memcpy(km, k, sizeof(km));
+        for (int j = 0; j < 2; j++)
+            if (glv_geq(km, R, 8)) glv_sub(km, R, 8);
+        // k1 + lambda k2 over 9 words
+        uint32_t sum[9] = {0};
+        for (int i = 0; i < 4; i++) {
+            uint64_t carry = 0;
+            for (int j = 0; j < 4; j++) {
+                uint64_t cur = (uint64_t)sum[i + j] + (uint64_t)k2[i] * GLV_LAMBDA[j] + carry;
+                sum[i + j] = (uint32_t)cur;
+                carry = cur >> 32;
+            }
+            for (int j = i + 4; carry && j < 9; j++) {
+                uint64_t cur = (uint64_t)sum[j] + carry;
+                sum[j] = (uint32_t)cur;
+                carry = cur >> 32;
+            }
+        }
+        uint64_t carry = 0;
+        for (int i = 0; i < 9; i++) {
+            uint64_t cur = (uint64_t)sum[i] + (i < 4 ? k1[i] : 0) + carry;
+            sum[i] = (uint32_t)cur;
+            carry = cur >> 32;
+        }
+        bool eq = sum[8] == 0;
+        for (int i = 0; i < 8; i++) eq = eq && sum[i] == km[i];
+        CHECK(eq, "glv_split recombination t=%zu", t);
+        CHECK(!glv_geq(k1, GLV_LAMBDA, 4), "glv_split k1 >= lambda t=%zu", t);
+    }
+    // phi(P) = lambda P on multiples of the generator (beta in the device's Montgomery form)
+    uint8_t gen[96], lam[32] = {0};
+    or_g1_generator(gen);
+    std::memcpy(lam, GLV_LAMBDA, 16);
+    const fq_t beta = glv_beta();
+    for (int it = 0; it < 20; it++) {
+        uint8_t s[32], pt[96], want[96], got[96];
+        rand_scalar(s);
+        or_g1_mul(gen, s, pt);
+        or_g1_mul(pt, lam, want);
+        g1_affine_t p = g1_from_bytes(pt);
+        p.x = fq_canon(p.x * beta);
+        g1_to_bytes(p, got);
+        CHECK(std::memcmp(got, want, 96) == 0, "phi != lambda it=%d", it);
+        // and on an XYZZ sum: phi(X, Y, ZZ, ZZZ) = (beta X, Y, ZZ, ZZZ)
+        g1_xyzz_t acc = xyzz_dbl_inl(xyzz_add_affine_inl(g1_xyzz_t::inf(), g1_from_bytes(pt)));
+        acc.X = acc.X * beta;
+        uint8_t twice[96];
+        or_g1_add(want, want, twice);
+        CHECK(same_point(acc, twice), "phi on XYZZ it=%d", it);
+    }
+}
+
 int main() {
     check_fields();
     check_g1_sequences();
     check_g2();
+    check_glv();
     if (failures) {
         std::printf("%d failures\n", failures);
         return 1;

@@ -25,8 +25,8 @@ def grouplaw_bin(oracle):
     exe = os.path.join(out_dir, "grouplaw_check")
     lib_dir = os.path.join(ROOT, "oracle", "build")  # liboracle.so (built by the oracle fixture)
     # -O0: the fully unrolled limb code takes minutes to instrument at -O1 and the checks do not need it
-    cmd = [HIPCC, "-x", "hip", "--offload-host-only", "-std=c++17", "-O0", "-fsanitize=address,undefined",
-           "-fno-sanitize-recover=undefined", "-fno-gpu-sanitize", "-I", os.path.join(ROOT, "crypto3-fil-proofs_amd", "csrc"),
+    cmd = [HIPCC, "-x", "hip", "--offload-host-only", "-std=c++17", "-O0",
+           "-fno-gpu-sanitize", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-I", os.path.join(ROOT, "crypto3-fil-proofs_amd", "csrc"),
            "-I", os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests", "host", "grouplaw_check.cpp"),
            "-L", lib_dir, "-loracle", "-Wl,-rpath," + lib_dir, "-o", exe]
     subprocess.run(cmd, check=True, capture_output=True, timeout=600)

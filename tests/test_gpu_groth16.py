@@ -112,11 +112,13 @@ def test_groth16_windowed_sort_vs_oracle(ctx, oracle, monkeypatch):
     assert proof == oproof and raw == oraw
 
 
-@pytest.mark.parametrize("split", ["0", "2"])
+@pytest.mark.parametrize("split", ["0", "2", "glv"])
 def test_groth16_split_msm_vs_oracle(ctx, oracle, monkeypatch, split):
     """H, L and A through the split-mode MSM (2^128 base tables, two 128-bit half scalars per point)
-    forced at a size the oracle proves in seconds; "0" is the plain path at the same size."""
-    monkeypatch.setenv("MI_MSM_SPLIT", split)
+    forced at a size the oracle proves in seconds; "0" is the plain path at the same size, "glv" the
+    split through the GLV endomorphism (no tables built at key generation)."""
+    monkeypatch.setenv("MI_MSM_SPLIT", "2" if split == "glv" else split)
+    monkeypatch.setenv("MI_MSM_GLV", "1" if split == "glv" else "0")
     n_in, n_aux, rws, z = circuits.random_circuit(35, 5000, n_in=6, n_free=32)
     oc, gc = _load(ctx, oracle, n_in, n_aux, rws, z)
     tox = circuits.toxic(35)

@@ -213,13 +213,15 @@ def _split_scalars(n, seed):
     return w.tobytes()
 
 
-@pytest.mark.parametrize("split", ["0", "2"])
+@pytest.mark.parametrize("split", ["0", "2", "glv"])
 def test_msm_split_tables_vs_oracle(ctx, oracle, monkeypatch, split):
     """Split mode (MI_MSM_SPLIT=2 forces it at any size): the l and a queries' MSMs over their 2^128
-    tables, against the oracle's MSM over the same points."""
+    tables, against the oracle's MSM over the same points; "glv": keys generated and MSMs run with
+    MI_MSM_GLV=1 (no tables)."""
     import torch
 
-    monkeypatch.setenv("MI_MSM_SPLIT", split)
+    monkeypatch.setenv("MI_MSM_SPLIT", "2" if split == "glv" else split)
+    monkeypatch.setenv("MI_MSM_GLV", "1" if split == "glv" else "0")
     n_in, n_aux, rws, z = circuits.random_circuit(91, 3000, n_in=6, n_free=32)
     gc = fg.Circuit(ctx, len(rws), n_in, n_aux, circuits.to_csr(rws))
     pk = fg.generate_random_parameters(ctx, gc, circuits.toxic())
@@ -248,3 +250,95 @@ def test_msm_split_default_2_17(ctx, oracle):
     sb = _split_scalars(n, 5)
     sd = torch.from_numpy(np.frombuffer(sb, dtype=np.uint8).copy()).cuda()
     assert pts.msm_dev(sd.data_ptr(), n) == oracle.msm_g1(q, sb)
+
+
+GLV_LAMBDA = 0xAC45A4010001A40200000000FFFFFFFF  # csrc/glv.h: phi(P) = lambda P, lambda^2 + lambda + 1 = r
+
+
+def _glv_scalars(n, seed):
+    """random, zero, one and the decomposition's edges: lambda - 1, lambda, lambda + 1, 2^128 +- 1,
+    r - 1 = lambda^2 + lambda, lambda^2, r - lambda"""
+    rng = random.Random(seed)
+    edges = [0, 1, GLV_LAMBDA - 1, GLV_LAMBDA, GLV_LAMBDA + 1, 2**128 - 1, 2**128, 2**128 + 1, R - 1,
+             GLV_LAMBDA**2 % R, R - GLV_LAMBDA, 2]
+    sc = [edges[i] if i < len(edges) else rng.choice([rng.randrange(R), rng.randrange(2**128), 0, 1,
+                                                       rng.choice(edges)]) for i in range(n)]
+    return b"".join(x.to_bytes(32, "little") for x in sc)
+
+
+@pytest.mark.parametrize("n,c", [(1, ""), (13, ""), (5000, ""), (5000, "12"), (5000, "22")])
+def test_msm_glv_vs_oracle(ctx, oracle, monkeypatch, n, c):
+    """G1 split mode through the GLV endomorphism (MI_MSM_GLV=1; MI_MSM_SPLIT=2 forces split at any size)
+    over caller-uploaded bases, which have no 2^128 table: edge scalars of the k = k1 + lambda k2
+    decomposition, at the default window, c = 12 and the production c = 22 (2^22 sub-buckets per window)."""
+    monkeypatch.setenv("MI_MSM_GLV", "1")
+    monkeypatch.setenv("MI_MSM_SPLIT", "2")
+    if c:
+        monkeypatch.setenv("MI_MSM_C", c)
+    bases = _bases_g1(oracle, n, 555 + n)
+    sb = _glv_scalars(n, 7 + n)
+    assert ctx.msm_g1(bases, sb) == oracle.msm_g1(bases, sb)
+
+
+def test_msm_glv_repeated_base_and_negation(ctx, oracle, monkeypatch):
+    """GLV sub-bucket merge branches: one base repeated (P and phi(P) sums in the same bucket), P with -P
+    (a sub-bucket sum at infinity), and scalars lambda / 1 on the same base (phi(P) + ... hits the doubling
+    of the merge when k2 = 1, k1 = 0 meets k1 = 1)."""
+    monkeypatch.setenv("MI_MSM_GLV", "1")
+    monkeypatch.setenv("MI_MSM_SPLIT", "2")
+    g = oracle.g1_generator()
+    neg = oracle.g1_mul(g, R - 1)
+    pts = (g + neg) * 20 + g * 24
+    rng = random.Random(3)
+    sc = [GLV_LAMBDA, 1, 1, GLV_LAMBDA] * 16
+    sc = [rng.choice(sc + [rng.randrange(R)]) for _ in range(len(pts) // 96)]
+    sb = b"".join(x.to_bytes(32, "little") for x in sc)
+    assert ctx.msm_g1(pts, sb) == oracle.msm_g1(pts, sb)
+    lam_pts = g * 8
+    lam_sc = b"".join(x.to_bytes(32, "little") for x in [GLV_LAMBDA, 1, GLV_LAMBDA + 1, 0, GLV_LAMBDA, 1, 2, 3])
+    assert ctx.msm_g1(lam_pts, lam_sc) == oracle.msm_g1(lam_pts, lam_sc)
+
+
+def test_msm_glv_boolean_heavy_2_20(ctx, oracle, monkeypatch):
+    """GLV at the 2^20 config-2 size with Filecoin-like boolean-heavy scalars, against the table-free
+    plain path's result (the plain path is pinned against the oracle by the linearity tests)."""
+    monkeypatch.setenv("MI_MSM_SPLIT", "2")
+    n = 1 << 20
+    rng = np.random.default_rng(11)
+    small = _bases_g1(oracle, 64, 91)
+    bases = small * (n // 64)
+    kind = rng.integers(0, 10, size=n)
+    w = np.zeros((n, 4), dtype=np.uint64)
+    w[kind < 6, 0] = 1
+    w[kind == 6, 0] = rng.integers(2, 2**20, size=int((kind == 6).sum()), dtype=np.uint64)
+    full = kind >= 8
+    w[full] = rng.integers(0, 2**64, size=(int(full.sum()), 4), dtype=np.uint64)
+    w[full, 3] &= np.uint64(0x3FFFFFFFFFFFFFFF)
+    sb = w.tobytes()
+    monkeypatch.setenv("MI_MSM_GLV", "0")
+    monkeypatch.setenv("MI_MSM_SPLIT", "0")
+    plain = ctx.msm_g1(bases, sb)
+    monkeypatch.setenv("MI_MSM_GLV", "1")
+    monkeypatch.setenv("MI_MSM_SPLIT", "2")
+    assert ctx.msm_g1(bases, sb) == plain
+    # and the oracle on the 64 distinct bases: sum over i of s_i P_(i mod 64) = sum_j (sum_{i = j mod 64} s_i) P_j
+    agg = [0] * 64
+    ints = [int.from_bytes(sb[32 * i:32 * i + 32], "little") for i in range(n)]
+    for i, v in enumerate(ints):
+        agg[i % 64] = (agg[i % 64] + v) % R
+    ab = b"".join(x.to_bytes(32, "little") for x in agg)
+    assert plain == oracle.msm_g1(small, ab)
+
+
+def test_msm_glv_auto_uploaded_bases(ctx, oracle, monkeypatch):
+    """Default policy (MI_MSM_GLV unset): caller-uploaded bases have no 2^128 table, so a split-size G1 MSM
+    takes the GLV split; the same MSM with MI_MSM_GLV=0 runs the plain 256-bit path."""
+    monkeypatch.delenv("MI_MSM_GLV", raising=False)
+    monkeypatch.setenv("MI_MSM_SPLIT", "2")
+    n = 3001
+    bases = _bases_g1(oracle, n, 4242)
+    sb = _glv_scalars(n, 99)
+    want = oracle.msm_g1(bases, sb)
+    assert ctx.msm_g1(bases, sb) == want
+    monkeypatch.setenv("MI_MSM_GLV", "0")
+    assert ctx.msm_g1(bases, sb) == want
