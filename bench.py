@@ -267,13 +267,17 @@ def main():
     import numpy as np
     import torch
 
+    # Multi-rank rehearsal on a one-GPU box (the driver's N > 1 runs use neither): MI_BENCH_BACKEND=gloo
+    # keeps the collectives on host tensors and MI_BENCH_SHARED_DEVICE=1 puts every rank on device 0.
+    backend = os.environ.get("MI_BENCH_BACKEND", "nccl")
+    dev_index = 0 if os.environ.get("MI_BENCH_SHARED_DEVICE") == "1" else local_rank
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
-    device = torch.device("cuda", local_rank)
+        torch.cuda.set_device(dev_index)
+        dist.init_process_group(backend)
+    device = torch.device("cuda", dev_index)
 
     import fil_groth16 as fg
     from fil_groth16 import synth as synth_mod
@@ -281,7 +285,7 @@ def main():
     from fil_groth16.distributed import gather_multiproof, prove_partitions
 
     t_setup = time.perf_counter()
-    ctx = fg.Context(local_rank)
+    ctx = fg.Context(dev_index)
     sc = synth_mod.SynthCircuit(args.log_rows, args.n_in, args.seed)
     t_synth = time.perf_counter() - t_setup
     circ = sc.load(ctx)
@@ -292,7 +296,7 @@ def main():
         pk = fg.generate_random_parameters(ctx, circ, splitmix_frs(TOXIC_SEED, 5))
     ctx.synchronize()
     t_srs = time.perf_counter() - t_setup - t_synth - t_load
-    free_b, total_b = torch.cuda.mem_get_info(local_rank)
+    free_b, total_b = torch.cuda.mem_get_info(dev_index)
     dev_used_gb = (total_b - free_b) / 1e9  # circuit + proving key (+ split tables unless MI_MSM_GLV=1)
     # the witness in page-locked host memory, where a synthesiser would write it (mi_host_alloc)
     zhost = fg.HostBuffer(32 * sc.num_vars)
@@ -323,7 +327,7 @@ def main():
     torch.cuda.synchronize()
     ctx.reset_stats()
 
-    gdev = device if dist else "cpu"
+    gdev = device if dist and backend == "nccl" else "cpu"
     t0 = time.perf_counter()
     if P:
         multiproofs = []
@@ -346,7 +350,7 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if dist:
-        tt = torch.tensor([dt], dtype=torch.float64, device=device)
+        tt = torch.tensor([dt], dtype=torch.float64, device=gdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     stats = ctx.stats()
