@@ -29,6 +29,16 @@ namespace {
 constexpr unsigned TILE_LOG = 10;  // 1024 elements = 32 KiB of LDS per workgroup
 constexpr unsigned TILE = 1u << TILE_LOG;
 constexpr unsigned NTT_THREADS = 256;
+// Occupancy target of the pass kernel (waves per SIMD).  LDS (36 KB per 1024-element tile) allows 4
+// workgroups = 4 waves per SIMD; the register count decides whether they fit (<= 128 VGPRs).
+#ifndef MI_NTT_WAVES
+#define MI_NTT_WAVES 0
+#endif
+#if MI_NTT_WAVES
+#define MI_NTT_OCC __attribute__((amdgpu_waves_per_eu(MI_NTT_WAVES)))
+#else
+#define MI_NTT_OCC
+#endif
 
 __device__ __forceinline__ fr_t tw_full(const fr_t *__restrict__ lo, const fr_t *__restrict__ hi, uint32_t e) {
     uint32_t l = e & 0xffffu, h = e >> 16;
@@ -181,7 +191,7 @@ __device__ __forceinline__ void ntt_rounds(LdsTile &sh, unsigned b, unsigned Tlo
 // G^bitrev_L(pos) * scale (coset shift of the bit-reversed coefficients, fused 1/d); epi = 2 also
 // converts to canonical form (icoset: H for the MSM).
 template <bool DIF, bool FUSED = false>
-__global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(fr_t *__restrict__ d, unsigned L, unsigned M, unsigned b,
+__global__ void __launch_bounds__(NTT_THREADS) MI_NTT_OCC k_ntt_pass(fr_t *__restrict__ d, unsigned L, unsigned M, unsigned b,
                                                           unsigned Tlog, unsigned Glog, int twiddle,
                                                           const fr29_t *__restrict__ lo,
                                                           const fr29_t *__restrict__ hi,
