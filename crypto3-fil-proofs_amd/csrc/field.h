@@ -485,7 +485,36 @@ MI_HD fq_t operator*(const fq_t &a, const fq_t &b) {
     r.v[L - 1] = (uint32_t)acc;
     return r;
 }
-MI_HD fq_t sqr(const fq_t &a) { return a * a; }
+// Squaring: the same product scanning over the symmetric products only -- column k takes
+// (2 a_i) a_(k-i) for i < k - i and a_(k/2)^2 -- so the product half costs 105 MADs instead of 196
+// (301 instead of 392 in all).  2 a_i < 2^30 for the normalised limbs 0..12 and for a top limb below
+// 2^16 (operands < 2^12 p), so each column stays within operator*'s bound (pair products < 2^59, at most
+// 7 of them, plus 14 reduction products < 2^58).
+MI_HD fq_t sqr(const fq_t &a) {
+    constexpr int L = 14;
+    uint32_t a2[L];
+    MI_UNROLL for (int i = 0; i < L; i++) a2[i] = a.v[i] << 1;
+    uint32_t m[L];
+    fq_t r;
+    uint64_t acc = 0;
+    MI_UNROLL for (int k = 0; k < L; k++) {
+        MI_UNROLL for (int i = 0; i < k - i; i++) acc += (uint64_t)a2[i] * a.v[k - i];
+        if ((k & 1) == 0) acc += (uint64_t)a.v[k >> 1] * a.v[k >> 1];
+        MI_UNROLL for (int i = 0; i < k; i++) acc += (uint64_t)m[i] * Fq29::P[k - i];
+        m[k] = ((uint32_t)acc * Fq29::INV) & Fq29::M;
+        acc += (uint64_t)m[k] * Fq29::P[0];
+        acc >>= 29;
+    }
+    MI_UNROLL for (int k = L; k < 2 * L - 1; k++) {
+        MI_UNROLL for (int i = k - L + 1; i < k - i; i++) acc += (uint64_t)a2[i] * a.v[k - i];
+        if ((k & 1) == 0) acc += (uint64_t)a.v[k >> 1] * a.v[k >> 1];
+        MI_UNROLL for (int i = k - L + 1; i < L; i++) acc += (uint64_t)m[i] * Fq29::P[k - i];
+        r.v[k - L] = (uint32_t)acc & Fq29::M;
+        acc >>= 29;
+    }
+    r.v[L - 1] = (uint32_t)acc;
+    return r;
+}
 
 // a*b + c*d with ONE Montgomery reduction (the group law's "X * Y - Z * W" with c = -Z in lazy
 // form): 392 + 196 MADs instead of 2 x 392 plus a subtraction.  Column sums stay below 2^64:

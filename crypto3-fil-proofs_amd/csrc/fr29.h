@@ -97,9 +97,36 @@ MI_HD fr29_t fr29_sub_if_ge(const fr29_t &a, const uint32_t *m) {
     d.v[8] = (uint32_t)top;
     return top < 0 ? a : d;
 }
+// x^2 over the symmetric products only ((2 a_i) a_(k-i), i < k - i, and a_(k/2)^2): 45 + 81 MADs instead
+// of 81 + 81.  2 a_i fits 32 bits for operands below 2^31 r, and the column sums stay within fr29_dot<1>'s.
+MI_HD fr29_t fr29_sqr(const fr29_t &a) {
+    constexpr int L = 9;
+    uint32_t a2[L];
+    MI_UNROLL for (int i = 0; i < L; i++) a2[i] = a.v[i] << 1;
+    uint32_t m[L];
+    fr29_t r;
+    uint64_t acc = 0;
+    MI_UNROLL for (int k = 0; k < L; k++) {
+        MI_UNROLL for (int i = 0; i < k - i; i++) acc += (uint64_t)a2[i] * a.v[k - i];
+        if ((k & 1) == 0) acc += (uint64_t)a.v[k >> 1] * a.v[k >> 1];
+        MI_UNROLL for (int i = 0; i < k; i++) acc += (uint64_t)m[i] * FrDesc::MOD29[k - i];
+        m[k] = ((uint32_t)acc * FrDesc::INV29) & M29;
+        acc += (uint64_t)m[k] * FrDesc::MOD29[0];
+        acc >>= 29;
+    }
+    MI_UNROLL for (int k = L; k < 2 * L - 1; k++) {
+        MI_UNROLL for (int i = k - L + 1; i < k - i; i++) acc += (uint64_t)a2[i] * a.v[k - i];
+        if ((k & 1) == 0) acc += (uint64_t)a.v[k >> 1] * a.v[k >> 1];
+        MI_UNROLL for (int i = k - L + 1; i < L; i++) acc += (uint64_t)m[i] * FrDesc::MOD29[k - i];
+        r.v[k - L] = (uint32_t)acc & M29;
+        acc >>= 29;
+    }
+    r.v[L - 1] = (uint32_t)acc;
+    return r;
+}
 MI_HD fr29_t fr29_sbox(const fr29_t &x) {  // x^5
-    const fr29_t x2 = fr29_mul(x, x);
-    const fr29_t x4 = fr29_mul(x2, x2);
+    const fr29_t x2 = fr29_sqr(x);
+    const fr29_t x4 = fr29_sqr(x2);
     return fr29_mul(x4, x);
 }
 // Montgomery value < 4r -> canonical integer < r

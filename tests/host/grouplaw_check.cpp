@@ -121,6 +121,10 @@ static void check_fields() {
         CHECK(fq_canon(fq_neg_lazy(a) * c) == fq_canon((-a) * c), "neg_lazy it=%d", it);
         CHECK(fq_canon(mul_add(a, fq_sub_lazy(b, c), fq_neg_lazy(d), a)) ==
                   fq_canon(a * (b - c) - d * a), "mul_add lazy it=%d", it);
+        // symmetric-product squaring equals the general product, also on lazy operands in [0, 4p)
+        CHECK(fq_canon(sqr(a)) == fq_canon(a * a), "sqr it=%d", it);
+        const fq_t lz = fq_sub_lazy(a, b);
+        CHECK(fq_canon(sqr(lz)) == fq_canon(lz * lz), "sqr lazy it=%d", it);
         // one-pass X3 equals the three reduced operations, and stays in [0, 2p)
         fq_t x3 = fq_x3(a, b, c);
         CHECK(x3 == a - b - dbl(c), "x3 it=%d", it);

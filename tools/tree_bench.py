@@ -5,8 +5,8 @@ Workload: one sub-tree of a 32 GiB sector at 2^log_nodes nodes (2^27 for 32 GiB'
 2^24 so a run takes seconds): 11 layers of labels -> column hashes (Poseidon, arity 11) -> arity-8 tree
 (tree C); last-layer labels + data -> replica -> arity-8 tree with rows_to_discard = 2 (tree R-last).
 Prints one JSON line: columns/s, leaves/s, per-arity hashes/s, and the VALU roofline of k_poseidon
-(v_mad_u64_u32 issue: one Fr product = 162 MADs over 9 x 29-bit limbs; an MDS row of K <= 6 terms =
-81 K + 81 MADs).
+(v_mad_u64_u32 issue: one Fr product = 162 MADs over 9 x 29-bit limbs, a square 126 (symmetric
+products); an MDS row of K <= 6 terms = 81 K + 81 MADs).
     python tools/tree_bench.py [--log-nodes 24] [--reps 3]
 """
 import argparse
@@ -27,6 +27,7 @@ ROUNDS = {2: 55, 4: 56, 8: 57, 11: 57}
 def mads_per_hash(arity):
     t, rp, rf = arity + 1, ROUNDS[arity], 8
     mul = 162
+    sbox = 2 * 126 + mul  # x^2, x^4 as symmetric squares (fr29_sqr), x^5
 
     def row(k):  # t-term row in chunks of <= 6 products per reduction
         if k <= 6:
@@ -34,9 +35,9 @@ def mads_per_hash(arity):
         a = (k + 1) // 2
         return row(a) + row(k - a)
 
-    full = rf * (3 * t * mul + t * row(t))
-    sparse = (rp - 1) * (3 * mul + row(t) + (t - 1) * mul)
-    last = 3 * mul + t * row(t)
+    full = rf * (t * sbox + t * row(t))
+    sparse = (rp - 1) * (sbox + row(t) + (t - 1) * mul)
+    last = sbox + t * row(t)
     io = (t - 1) * mul + mul
     return full + sparse + last + io
 
