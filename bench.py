@@ -200,6 +200,78 @@ def tree_c_leg(args, fg, ctx, device, world):
     return out
 
 
+# SHA-256 compression cost model for the SDR label kernel (VALU lane-ops, gfx950 3-input forms): per round
+# Sigma0/Sigma1 3 v_alignbit + 1 v_bitop3 (xor3) each, Ch and Maj 1 v_bitop3 each, T1 2 v_add3, e 1 add,
+# a 1 v_add3 = 14; per schedule word sigma0/sigma1 2 v_alignbit + 1 shift + 1 xor3 each, v_add3 + add = 10;
+# 8 feed-forward adds.  The compiled block loop issues 1,410 VALU per compression (this + the byte swaps).
+SHA256_OPS_PER_COMPRESSION = 64 * 14 + 48 * 10 + 8
+VALU_LANE_OPS = 1024 * 64 / 4 * 2.4e9  # 1024 SIMDs x 16 lanes per clock x 2.4 GHz (same issue model as MAD_RATE)
+
+
+def sdr_leg(args, fg, ctx, device, world):
+    """labelling-proof labels of 2^N challenges gathered from 11 device-resident layers of 2^20
+    nodes (6 base + 8 expander parents each, repeated to 37: 20 SHA-256 compressions per label), with the
+    VALU roofline of k_sdr_labels_gather and the oracle's CPU rate on a sample."""
+    import numpy as np
+    import torch
+
+    n_layers, nodes, count = 11, 1 << 20, 1 << args.sdr_log_labels
+    g = torch.Generator(device=device)
+    g.manual_seed(21)
+    labels = torch.randint(0, 256, (n_layers * nodes * 32,), dtype=torch.uint8, device=device, generator=g)
+    layers = torch.randint(1, n_layers + 1, (count,), dtype=torch.int32, device=device, generator=g)
+    chal = torch.randint(1, nodes, (count,), dtype=torch.int64, device=device, generator=g)
+    pidx = torch.randint(0, nodes, (count * 14,), dtype=torch.int32, device=device, generator=g)
+    out = torch.empty(count * 32, dtype=torch.uint8, device=device)
+    rid = bytes(range(32))
+    torch.cuda.synchronize()
+
+    def run():
+        fg.sdr.labeling_proofs_dev(ctx, rid, n_layers, nodes, labels.data_ptr(), count, layers.data_ptr(),
+                                   chal.data_ptr(), pidx.data_ptr(), out.data_ptr())
+
+    run()
+    ctx.synchronize()
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+    ctx.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    compressions = count * 20
+    ops = compressions * SHA256_OPS_PER_COMPRESSION
+    res = {"workload": f"SDR labelling-proof labels: 2^{args.sdr_log_labels} challenges x 37 parents (6 base + 8 "
+                       f"expander, repeated) gathered from 11 device-resident layers of 2^20 nodes; SHA-256 over "
+                       f"1248 B each",
+           "labels_per_s": count / dt, "ms_per_batch": dt * 1e3,
+           "note": "wall time per call includes the device-side index range check (k_sdr_check) and one host "
+                   "synchronisation; rocprofv3 gives the kernel alone",
+           "valu_roofline": {"kernel": "k_sdr_labels_gather", "bound": "valu (32-bit integer issue)",
+                             "ops_per_compression": SHA256_OPS_PER_COMPRESSION, "compressions_per_label": 20,
+                             "achieved_ops_per_s": ops / dt, "peak_ops_per_s": VALU_LANE_OPS,
+                             "frac": ops / dt / VALU_LANE_OPS},
+           "hbm_algorithmic_GBps": count * (14 * 32 + 4 + 8 + 56 + 32) / dt / 1e9}
+    if world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle_py
+
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+        oracle_py.set_threads(threads)
+        m = 1 << 19
+        par = np.random.default_rng(1).integers(0, 256, 32 * 14 * m, dtype=np.uint8).tobytes()
+        lay = np.random.default_rng(2).integers(2, 12, m, dtype=np.uint32)
+        nod = np.random.default_rng(3).integers(1, 1 << 20, m, dtype=np.uint64)
+        t0 = time.perf_counter()
+        oracle_py.sdr_labels(rid, lay, nod, par, 14)
+        dtc = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": m / dtc, "unit": "labels/s", "cores": threads, "kind": "port",
+                               "sample": f"{m} labels (14 parents repeated to 37) by the oracle's scalar C SHA-256, "
+                                         f"OpenMP, on {cpu_model()}"}
+        res["gpu_over_cpu"] = res["labels_per_s"] / res["cpu_baseline"]["value"]
+    del labels, layers, chal, pidx, out
+    return res
+
+
 def config4_leg(args, fg, synth_mod, ctx):
     """BASELINE config 4 (the north-star target: a 32 GiB Seal-PoRep-sized circuit, ~1.3e8 constraints,
     d = 2^27) on the same GPU after the config-3 objects are freed: host (pinned) witness, one warm-up and
@@ -259,6 +331,8 @@ def main():
     ap.add_argument("--config4-steps", type=int, default=2)
     ap.add_argument("--tree-log-nodes", type=int, default=21,
                     help="secondary: tree C over 2^N columns x 11 layers (N a multiple of 3; 0 skips)")
+    ap.add_argument("--sdr-log-labels", type=int, default=24,
+                    help="secondary: SDR labelling-proof labels of 2^N challenges (0 skips)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -424,6 +498,14 @@ def main():
     if args.tree_log_nodes and rank == 0:
         tree = tree_c_leg(args, fg, ctx, device, world)
 
+    # SDR labelling-witness labels (SHA-256 over gathered parents)
+    sdr = None
+    if args.sdr_log_labels and rank == 0:
+        try:
+            sdr = sdr_leg(args, fg, ctx, device, world)
+        except Exception as e:  # reported, never fatal to the main measurement
+            sdr = {"error": str(e)}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
@@ -540,6 +622,7 @@ def main():
         },
         "cpu_baseline": cpu,
         "tree_c": tree,
+        "sdr_labels": sdr,
         "config4": config4,
         "timers_ms": {k: round(v["ms"], 3) for k, v in stats.items()},
         "setup_s": {"synth": t_synth, "circuit_load": t_load, "srs": t_srs},

@@ -14,6 +14,7 @@
 #include "../../include/mi355x_groth16.h"
 #include "poseidon_math.h"
 #include "prover.h"
+#include "sdr.h"
 
 // Witness uploads (host z -> HBM) run on their own stream into one of two device slots, so the copy
 // of partition k + 1 overlaps the proof of partition k (mi_groth16_prove_batch).  Pinned witnesses
@@ -1306,3 +1307,81 @@ int mi_tree_r_last_build(mi_ctx *ctx, uint64_t nodes, const uint8_t *last_layer_
 }
 
 }  // extern "C"
+
+// ---- SDR labelling witness (sdr.hip) -------------------------------------------------
+namespace {
+__global__ void k_sdr_check(const uint32_t *layers, const uint32_t *parent_idx, uint64_t n, uint32_t per,
+                            uint32_t n_layers, uint64_t nodes_per_layer, int *bad) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    bool ok = layers[i] >= 1 && layers[i] <= n_layers;
+    for (uint32_t k = 0; k < per; k++) ok &= parent_idx[i * per + k] < nodes_per_layer;
+    if (!ok) atomicOr(bad, 1);
+}
+}  // namespace
+
+int mi_sdr_labels_dev(mi_ctx *ctx, const uint8_t replica_id[32], uint64_t count, const void *layers_dev,
+                      const void *nodes_dev, const void *parents_dev, unsigned n_parents, void *labels_dev) {
+    return guard([&] {
+        need(ctx && replica_id && (count == 0 || (layers_dev && nodes_dev && labels_dev)), "null argument");
+        need(n_parents <= 37, "n_parents must be <= 37");
+        need(count == 0 || n_parents == 0 || parents_dev, "null parents");
+        CtxLock l(ctx);
+        mi::sdr_labels_dev(ctx->c, mi::sdr_replica(replica_id), (const uint32_t *)layers_dev,
+                           (const uint64_t *)nodes_dev, parents_dev, n_parents, count, labels_dev);
+    });
+}
+
+int mi_sdr_labels(mi_ctx *ctx, const uint8_t replica_id[32], uint64_t count, const uint32_t *layers,
+                  const uint64_t *nodes, const uint8_t *parents, unsigned n_parents, uint8_t *labels) {
+    return guard([&] {
+        need(ctx && replica_id && (count == 0 || (layers && nodes && labels)), "null argument");
+        need(n_parents <= 37, "n_parents must be <= 37");
+        need(count == 0 || n_parents == 0 || parents, "null parents");
+        CtxLock l(ctx);
+        if (!count) return;
+        mi::Ctx &c = ctx->c;
+        uint8_t *idx = c.scratch[21].as<uint8_t>(count * 12);  // nodes (u64) then layers (u32)
+        uint8_t *par = n_parents ? c.scratch[20].as<uint8_t>(count * n_parents * 32) : nullptr;
+        uint8_t *out = c.scratch[22].as<uint8_t>(count * 32);
+        MI_HIP(hipMemcpyAsync(idx, nodes, 8 * count, hipMemcpyHostToDevice, c.stream));
+        MI_HIP(hipMemcpyAsync(idx + 8 * count, layers, 4 * count, hipMemcpyHostToDevice, c.stream));
+        if (par) MI_HIP(hipMemcpyAsync(par, parents, 32ull * n_parents * count, hipMemcpyHostToDevice, c.stream));
+        mi::sdr_labels_dev(c, mi::sdr_replica(replica_id), (const uint32_t *)(idx + 8 * count),
+                           (const uint64_t *)idx, par, n_parents, count, out);
+        MI_HIP(hipMemcpyAsync(labels, out, 32 * count, hipMemcpyDeviceToHost, c.stream));
+        MI_HIP(hipStreamSynchronize(c.stream));
+    });
+}
+
+int mi_sdr_labeling_proofs_dev(mi_ctx *ctx, const uint8_t replica_id[32], unsigned n_layers,
+                               uint64_t nodes_per_layer, const void *layer_labels_dev, uint64_t count,
+                               const void *layers_dev, const void *challenges_dev, const void *parent_idx_dev,
+                               unsigned n_base, unsigned n_exp, void *labels_dev, void *parents_out_dev) {
+    return guard([&] {
+        need(ctx && replica_id && (count == 0 || (layer_labels_dev && layers_dev && challenges_dev &&
+                                                  parent_idx_dev && labels_dev)),
+             "null argument");
+        need(n_base >= 1 && n_base + n_exp <= 37, "need 1 <= n_base and n_base + n_exp <= 37");
+        need(n_layers >= 1 && nodes_per_layer >= 1, "need at least one layer and one node");
+        need(nodes_per_layer <= (1ull << 32), "nodes_per_layer must fit the u32 parent indices");
+        CtxLock l(ctx);
+        if (!count) return;
+        mi::Ctx &c = ctx->c;
+        // every layer and parent index is checked on the device before the gather reads through them
+        int *bad = c.scratch[23].as<int>(1);
+        MI_HIP(hipMemsetAsync(bad, 0, sizeof(int), c.stream));
+        k_sdr_check<<<(unsigned)((count + 255) / 256), 256, 0, c.stream>>>(
+            (const uint32_t *)layers_dev, (const uint32_t *)parent_idx_dev, count, n_base + n_exp, n_layers,
+            nodes_per_layer, bad);
+        MI_LAUNCHED(c, "k_sdr_check");
+        int h = 0;
+        MI_HIP(hipMemcpyAsync(&h, bad, sizeof(int), hipMemcpyDeviceToHost, c.stream));
+        MI_HIP(hipStreamSynchronize(c.stream));
+        need(h == 0, "sdr: a layer is outside [1, n_layers] or a parent index is >= nodes_per_layer");
+        mi::sdr_labels_gather_dev(c, mi::sdr_replica(replica_id), layer_labels_dev, nodes_per_layer,
+                                  (const uint32_t *)layers_dev, (const uint64_t *)challenges_dev,
+                                  (const uint32_t *)parent_idx_dev, n_base, n_exp, count, labels_dev,
+                                  parents_out_dev);
+    });
+}

@@ -296,6 +296,29 @@ int mi_tree_r_last_build(mi_ctx *ctx, uint64_t nodes, const uint8_t *last_layer_
 int mi_tree_r_last_build_dev(mi_ctx *ctx, uint64_t nodes, const void *labels_dev, void *data_dev, unsigned tree_arity,
                              unsigned rows_to_discard, void *tree_dev);
 
+/* ---- SDR labelling witness: SHA-256 labels of challenged nodes ------------------
+ * label = SHA256(replica_id || u32_be(layer) || u64_be(node) || 0^20 || parent_0 .. parent_36) with byte 31
+ * &= 0x3f, the parents repeated cyclically to 37; no parents (node 0): the 64-byte prefix alone.  Replaces:
+ *   mi_sdr_labels / _dev        <- LabelingProof create_label (porep/stacked/vanilla/detail/processing/naive/
+ *                                  labelling_proof.hpp:46-60) and EncodingProof::create_key
+ *                                  (vanilla/encoding_proof.hpp:42-53) over parents_data_full; n_parents
+ *                                  labels per entry are repeated to 37 as vanilla/proof.hpp:233-237 does
+ *   mi_sdr_labeling_proofs_dev  <- the per-challenge labelling-proof loop of prove_layers
+ *                                  (vanilla/proof.hpp:190-255): base parents read from the challenged layer,
+ *                                  expander parents from the layer below (layer 1: base parents only),
+ *                                  parents_data_full optionally written out (37 x 32 B per challenge)
+ * Device layouts: layers u32[count], nodes / challenges u64[count], parents 32 B x n_parents per entry,
+ * parent_idx u32[count x (n_base + n_exp)], layer labels layer-major (layer l at entry (l-1) x nodes_per_layer).
+ * Out-of-range layers or parent indices are refused with MI_ERR_ARG before any gather. */
+int mi_sdr_labels(mi_ctx *ctx, const uint8_t replica_id[32], uint64_t count, const uint32_t *layers,
+                  const uint64_t *nodes, const uint8_t *parents, unsigned n_parents, uint8_t *labels);
+int mi_sdr_labels_dev(mi_ctx *ctx, const uint8_t replica_id[32], uint64_t count, const void *layers_dev,
+                      const void *nodes_dev, const void *parents_dev, unsigned n_parents, void *labels_dev);
+int mi_sdr_labeling_proofs_dev(mi_ctx *ctx, const uint8_t replica_id[32], unsigned n_layers,
+                               uint64_t nodes_per_layer, const void *layer_labels_dev, uint64_t count,
+                               const void *layers_dev, const void *challenges_dev, const void *parent_idx_dev,
+                               unsigned n_base, unsigned n_exp, void *labels_dev, void *parents_out_dev);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1494,3 +1494,102 @@ int or_groth16_verify(const uint8_t vk[864], const uint8_t *ic96, uint64_t num_i
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------------------------------
+// SDR labelling witness: SHA-256 (FIPS 180-4, restated) and the stacked-DRG label
+//   label = SHA256(replica_id || u32_be(layer) || u64_be(node) || 0^20 || parents[0..P_full)) with the
+//   top two bits of byte 31 cleared.  Follows LabelingProof create_label
+//   (libs/storage/include/nil/filecoin/storage/proofs/porep/stacked/vanilla/detail/processing/naive/
+//   labelling_proof.hpp:46-60), create_label (vanilla/create_label.hpp:43-78: the 32-byte prefix block
+//   whose 12-byte truncation the reference shows, then the parents, "strip last two bits") and the cyclic
+//   parent repetition to TOTAL_PARENTS = 37 (vanilla/proof.hpp:49, 233-237).  n_parents = 0 is node 0's
+//   label (no parents: create_label.hpp:67-69).
+namespace {
+const uint32_t kSha256K[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+inline uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+
+void sha256_block(uint32_t h[8], const uint8_t *blk) {
+    uint32_t w[64];
+    for (int t = 0; t < 16; t++)
+        w[t] = (uint32_t)blk[4 * t] << 24 | (uint32_t)blk[4 * t + 1] << 16 | (uint32_t)blk[4 * t + 2] << 8 | blk[4 * t + 3];
+    for (int t = 16; t < 64; t++) {
+        const uint32_t s0 = rotr32(w[t - 15], 7) ^ rotr32(w[t - 15], 18) ^ (w[t - 15] >> 3);
+        const uint32_t s1 = rotr32(w[t - 2], 17) ^ rotr32(w[t - 2], 19) ^ (w[t - 2] >> 10);
+        w[t] = w[t - 16] + s0 + w[t - 7] + s1;
+    }
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], k = h[7];
+    for (int t = 0; t < 64; t++) {
+        const uint32_t t1 = k + (rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25)) + ((e & f) ^ (~e & g)) + kSha256K[t] + w[t];
+        const uint32_t t2 = (rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+        k = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += k;
+}
+
+// streaming SHA-256 over a message given as pieces
+struct Sha256 {
+    uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+    uint8_t buf[64];
+    size_t fill = 0;
+    uint64_t len = 0;
+    void update(const uint8_t *p, size_t n) {
+        len += n;
+        while (n) {
+            const size_t take = std::min(n, 64 - fill);
+            memcpy(buf + fill, p, take);
+            fill += take; p += take; n -= take;
+            if (fill == 64) { sha256_block(h, buf); fill = 0; }
+        }
+    }
+    void finish(uint8_t out[32]) {
+        const uint64_t bits = len * 8;
+        const uint8_t pad = 0x80, zero = 0;
+        update(&pad, 1);
+        while (fill != 56) update(&zero, 1);
+        uint8_t l[8];
+        for (int i = 0; i < 8; i++) l[i] = (uint8_t)(bits >> (56 - 8 * i));
+        update(l, 8);
+        for (int i = 0; i < 8; i++)
+            for (int j = 0; j < 4; j++) out[4 * i + j] = (uint8_t)(h[i] >> (24 - 8 * j));
+    }
+};
+}  // namespace
+
+extern "C" {
+void or_sha256(const uint8_t *msg, uint64_t len, uint8_t out[32]) {
+    Sha256 s;
+    s.update(msg, len);
+    s.finish(out);
+}
+
+int or_sdr_labels(const uint8_t replica_id[32], uint64_t count, const uint32_t *layers, const uint64_t *nodes,
+                  const uint8_t *parents, unsigned n_parents, uint8_t *labels) {
+    if (n_parents > 37) return -1;
+    const int nt = nthreads();
+#pragma omp parallel for num_threads(nt) schedule(static) if (count >= 256)
+    for (int64_t i = 0; i < (int64_t)count; i++) {
+        uint8_t pre[64] = {0};
+        memcpy(pre, replica_id, 32);
+        for (int j = 0; j < 4; j++) pre[32 + j] = (uint8_t)(layers[i] >> (24 - 8 * j));
+        for (int j = 0; j < 8; j++) pre[36 + j] = (uint8_t)(nodes[i] >> (56 - 8 * j));
+        Sha256 s;
+        s.update(pre, 64);
+        const uint8_t *p = parents + (uint64_t)i * n_parents * 32;
+        if (n_parents)
+            for (unsigned k = 0; k < 37; k++) s.update(p + 32 * (k % n_parents), 32);
+        uint8_t *o = labels + 32 * (uint64_t)i;
+        s.finish(o);
+        o[31] &= 0x3f;
+    }
+    return 0;
+}
+}  // extern "C"

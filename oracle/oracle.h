@@ -119,6 +119,13 @@ int or_poseidon_hash_sparse(unsigned arity, unsigned rf, unsigned rp, const uint
 void or_set_threads(int n);
 int or_get_threads(void);
 
+/* SHA-256 (FIPS 180-4) and the SDR labelling witness: labels[i] = SHA256(replica_id || u32_be(layers[i]) ||
+ * u64_be(nodes[i]) || 0^20 || 37 parents repeated cyclically from parents[i * n_parents ..]), byte 31 &= 0x3f;
+ * n_parents = 0: the prefix alone (node 0) */
+void or_sha256(const uint8_t *msg, uint64_t len, uint8_t out[32]);
+int or_sdr_labels(const uint8_t replica_id[32], uint64_t count, const uint32_t *layers, const uint64_t *nodes,
+                  const uint8_t *parents, unsigned n_parents, uint8_t *labels);
+
 #ifdef __cplusplus
 }
 #endif

@@ -186,6 +186,33 @@ def poseidon_hash(arity: int, preimages: bytes) -> bytes:
     return out.raw[:32 * n]
 
 
+def sha256(msg: bytes) -> bytes:
+    """The oracle's FIPS 180-4 SHA-256 restatement (pinned against hashlib in the CPU tests)."""
+    L = lib()
+    L.or_sha256.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p]
+    out = _buf(32)
+    L.or_sha256(bytes(msg), len(msg), out)
+    return out.raw
+
+
+def sdr_labels(replica_id: bytes, layers, nodes, parents: bytes, n_parents: int) -> bytes:
+    """SDR labelling witness (oracle.cpp or_sdr_labels): one 32-byte label per (layer, node), parents given
+    as n_parents labels per entry and repeated cyclically to 37 (vanilla/proof.hpp:233-237)."""
+    import numpy as _np
+
+    lay = _np.ascontiguousarray(layers, dtype=_np.uint32)
+    nod = _np.ascontiguousarray(nodes, dtype=_np.uint64)
+    n = len(lay)
+    assert len(nod) == n and len(replica_id) == 32 and len(parents) == 32 * n_parents * n
+    L = lib()
+    L.or_sdr_labels.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_char_p,
+                                ctypes.c_uint, ctypes.c_void_p]
+    out = _buf(32 * max(n, 1))
+    if L.or_sdr_labels(bytes(replica_id), n, lay.ctypes.data, nod.ctypes.data, bytes(parents), n_parents, out) != 0:
+        raise ValueError("n_parents must be <= 37")
+    return out.raw[:32 * n]
+
+
 _SPARSE = {}
 
 
