@@ -1385,3 +1385,41 @@ int mi_sdr_labeling_proofs_dev(mi_ctx *ctx, const uint8_t replica_id[32], unsign
                                   parents_out_dev);
     });
 }
+
+// ---- Merkle inclusion paths over device-resident Poseidon trees (poseidon.hip) --------------------------
+namespace {
+__global__ void k_chal_check(const uint64_t *chal, uint64_t count, uint64_t n, int *bad) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count && chal[i] >= n) atomicOr(bad, 1);
+}
+}  // namespace
+
+int mi_tree_inclusion_paths_dev(mi_ctx *ctx, unsigned arity, const void *leaves_dev, uint64_t leaf_count,
+                                unsigned rows_to_discard, const void *tree_dev, uint64_t count,
+                                const void *challenges_dev, void *leaf_out_dev, void *siblings_out_dev) {
+    return guard([&] {
+        need(ctx && leaves_dev && tree_dev && (count == 0 || (challenges_dev && leaf_out_dev && siblings_out_dev)),
+             "null argument");
+        need_tree_arity(arity);
+        CtxLock l(ctx);
+        mi::tree_rows_size(leaf_count, arity, rows_to_discard);
+        if (!count) return;
+        mi::Ctx &c = ctx->c;
+        int *bad = c.scratch[23].as<int>(1);
+        MI_HIP(hipMemsetAsync(bad, 0, sizeof(int), c.stream));
+        k_chal_check<<<(unsigned)((count + 255) / 256), 256, 0, c.stream>>>((const uint64_t *)challenges_dev, count,
+                                                                            leaf_count, bad);
+        MI_LAUNCHED(c, "k_chal_check");
+        int h = 0;
+        MI_HIP(hipMemcpyAsync(&h, bad, sizeof(int), hipMemcpyDeviceToHost, c.stream));
+        MI_HIP(hipStreamSynchronize(c.stream));
+        need(h == 0, "tree: a challenge is >= the leaf count");
+        uint64_t B = 1;
+        for (unsigned r = 0; r <= rows_to_discard; r++) B *= arity;
+        mi::fr_t *rec = rows_to_discard ? c.scratch[22].as<mi::fr_t>(2 * count * B) : nullptr;
+        mi::tree_paths_dev(c, arity, (const mi::fr_t *)leaves_dev, leaf_count, rows_to_discard,
+                           (const mi::fr_t *)tree_dev, (const uint64_t *)challenges_dev, count, rec,
+                           (mi::fr_t *)leaf_out_dev, (mi::fr_t *)siblings_out_dev);
+        MI_HIP(hipStreamSynchronize(c.stream));
+    });
+}

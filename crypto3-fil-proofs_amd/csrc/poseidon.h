@@ -40,6 +40,14 @@ void encode_dev(Ctx &c, const fr_t *key, fr_t *data, uint64_t n);
 // entries of the cached tree rows above the base (rows_to_discard lowest ones dropped)
 uint64_t tree_rows_size(uint64_t leaves, unsigned arity, unsigned rows_to_discard);
 // rows: tree_rows_size entries, bottom-up; discard_tmp: >= 2 * (n / arity) entries
+unsigned tree_height(uint64_t n, unsigned arity);
+// inclusion paths of count challenges: leaf_out[i] = base[c_i]; sib_out[(i * H + j) * (arity - 1) ..] = the
+// siblings in row j (0 = base) in position order skipping the path's own slot, H = tree height.  stored:
+// the cached rows (tree_rows_size layout); discarded rows are rebuilt per challenge block in rec_tmp
+// (>= count * arity^(rtd+1) * 2 entries when rows_to_discard > 0)
+void tree_paths_dev(Ctx &c, unsigned arity, const fr_t *base, uint64_t n, unsigned rows_to_discard,
+                    const fr_t *stored, const uint64_t *chal, uint64_t count, fr_t *rec_tmp, fr_t *leaf_out,
+                    fr_t *sib_out);
 void tree_build_dev(Ctx &c, unsigned arity, const fr_t *leaves, uint64_t n, unsigned rows_to_discard, fr_t *rows,
                     fr_t *discard_tmp);
 

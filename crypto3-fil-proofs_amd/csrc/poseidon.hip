@@ -297,4 +297,108 @@ void tree_build_dev(Ctx &c, unsigned arity, const fr_t *leaves, uint64_t n, unsi
     }
 }
 
+// ---- inclusion proofs (MerkleTree_gen_proof / gen_cached_proof, vanilla/proof.hpp:139-140,183-186) ----
+namespace {
+struct RowOffsets {
+    uint64_t off[48];  // entry offset in the stored rows of row j (j > rows_to_discard)
+};
+
+// blocks[i * B + k] = base[(c_i / B) * B + k]: the aligned arity^(rtd+1)-leaf block holding challenge i
+__global__ void __launch_bounds__(256) k_path_blocks(const fr_t *__restrict__ base, const uint64_t *__restrict__ chal,
+                                                     uint64_t count, uint64_t B, fr_t *__restrict__ blocks) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= count * B) return;
+    const uint64_t i = t / B, k = t % B;
+    blocks[t] = base[(chal[i] / B) * B + k];
+}
+
+// one thread per (challenge, row): the arity - 1 siblings of the challenge's ancestor in row j, in position
+// order skipping its own slot; row 0 also writes the leaf
+__global__ void __launch_bounds__(256) k_path_siblings(const fr_t *__restrict__ base, const fr_t *__restrict__ stored,
+                                                       const fr_t *__restrict__ rec, const uint64_t *__restrict__ chal,
+                                                       uint64_t count, uint32_t A, uint32_t H, uint32_t rtd, uint64_t B,
+                                                       RowOffsets ro, fr_t *__restrict__ leaf_out,
+                                                       fr_t *__restrict__ sib_out) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= count * H) return;
+    const uint64_t i = t / H;
+    const uint32_t j = (uint32_t)(t % H);
+    const uint64_t c = chal[i];
+    uint64_t pw = 1;
+    for (uint32_t r = 0; r < j; r++) pw *= A;
+    const fr_t *row;
+    uint64_t idx;
+    if (j == 0) {
+        row = base;
+        idx = c;
+        leaf_out[i] = base[c];
+    } else if (j <= rtd) {
+        // recomputed row j of challenge i's block: rows of all blocks are contiguous, block i's part at i * B / A^j
+        uint64_t roff = 0, rows = count * B;
+        for (uint32_t r = 1; r < j; r++) {
+            rows /= A;
+            roff += rows;
+        }
+        row = rec + roff + i * (B / pw);
+        idx = (c % B) / pw;
+    } else {
+        row = stored + ro.off[j];
+        idx = c / pw;
+    }
+    const uint64_t g = idx - idx % A;
+    const uint32_t own = (uint32_t)(idx % A);
+    fr_t *o = sib_out + t * (A - 1);
+    for (uint32_t s = 0, k = 0; s < A; s++)
+        if (s != own) o[k++] = row[g + s];
+}
+inline unsigned grid_of(uint64_t n) { return (unsigned)((n + 255) / 256); }
+}  // namespace
+
+unsigned tree_height(uint64_t n, unsigned arity) {
+    unsigned h = 0;
+    while (n > 1) {
+        n /= arity;
+        h++;
+    }
+    return h;
+}
+
+void tree_paths_dev(Ctx &c, unsigned arity, const fr_t *base, uint64_t n, unsigned rows_to_discard,
+                    const fr_t *stored, const uint64_t *chal, uint64_t count, fr_t *rec_tmp, fr_t *leaf_out,
+                    fr_t *sib_out) {
+    tree_rows_size(n, arity, rows_to_discard);  // validates the shape
+    if (!count) return;
+    const unsigned H = tree_height(n, arity);
+    if (H >= 48) throw std::invalid_argument("tree: too many rows");
+    RowOffsets ro{};
+    uint64_t off = 0, row = n;
+    for (unsigned j = 1; j <= H; j++) {
+        row /= arity;
+        if (j > rows_to_discard) {
+            ro.off[j] = off;
+            off += row;
+        }
+    }
+    uint64_t B = 1;
+    for (unsigned r = 0; r <= rows_to_discard; r++) B *= arity;
+    if (rows_to_discard) {
+        // rebuild the discarded rows of each challenge's aligned block (cached-proof regeneration)
+        fr_t *blocks = rec_tmp;
+        fr_t *dst = rec_tmp + count * B;
+        k_path_blocks<<<grid_of(count * B), 256, 0, c.stream>>>(base, chal, count, B, blocks);
+        MI_LAUNCHED(c, "k_path_blocks");
+        const fr_t *cur = blocks;
+        uint64_t m = count * B;
+        for (unsigned r = 1; r <= rows_to_discard; r++) {
+            m /= arity;
+            poseidon_hash_dev(c, arity, cur, m, arity, 1, dst);
+            cur = dst;
+            dst += m;
+        }
+    }
+    k_path_siblings<<<grid_of(count * H), 256, 0, c.stream>>>(base, stored, rows_to_discard ? rec_tmp + count * B : nullptr, chal, count, arity,
+                                                               H, rows_to_discard, B, ro, leaf_out, sib_out);
+    MI_LAUNCHED(c, "k_path_siblings");
+}
+
 }  // namespace mi

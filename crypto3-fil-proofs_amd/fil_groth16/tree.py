@@ -157,3 +157,23 @@ def generate_tree_r_last_dev(ctx, nodes: int, labels_ptr: int, data_ptr: int, tr
 
 def encode(key: int, value: int) -> int:
     return (key + value) % FR_MODULUS
+
+
+def tree_height(leafs: int, arity: int) -> int:
+    h = 0
+    while leafs > 1:
+        leafs //= arity
+        h += 1
+    return h
+
+
+def gen_proofs_dev(ctx, arity: int, leaves_ptr: int, leafs: int, rows_to_discard: int, tree_ptr: int, count: int,
+                   challenges_ptr: int, leaf_out_ptr: int, siblings_out_ptr: int) -> None:
+    """Inclusion proofs of `count` challenges (u64 leaf indices) in a device-resident tree (MerkleTree_gen_proof /
+    MerkleTree_gen_cached_proof, porep/stacked/vanilla/proof.hpp:139-140,183-186): the leaf, then per row
+    j = 0 .. height-1 the arity - 1 siblings in position order skipping the path's own slot (digit j of the
+    challenge in base arity).  tree_ptr holds the cached rows built with the same rows_to_discard."""
+    vp = ctypes.c_void_p
+    check(lib().mi_tree_inclusion_paths_dev(ctx.h, arity, vp(leaves_ptr), leafs, rows_to_discard, vp(tree_ptr), count,
+                                            vp(challenges_ptr), vp(leaf_out_ptr), vp(siblings_out_ptr)))
+

@@ -295,6 +295,17 @@ int mi_tree_r_last_build(mi_ctx *ctx, uint64_t nodes, const uint8_t *last_layer_
                          unsigned tree_arity, unsigned rows_to_discard, uint8_t *tree_out);
 int mi_tree_r_last_build_dev(mi_ctx *ctx, uint64_t nodes, const void *labels_dev, void *data_dev, unsigned tree_arity,
                              unsigned rows_to_discard, void *tree_dev);
+/* inclusion proofs of count challenges (u64 leaf indices) in a device-resident tree: leaf_out[i] = leaves[c_i];
+ * siblings_out[(i * H + j) * (arity - 1) ..] = the arity - 1 siblings of c_i's ancestor in row j (0 = leaves,
+ * H = log_arity(leaf_count) rows), in position order skipping its own slot (that slot is digit j of c_i in
+ * base arity).  tree_dev is the cached rows of mi_tree_build_dev / mi_tree_c_build_dev / mi_tree_r_last_build_dev
+ * with the same rows_to_discard; discarded rows are rebuilt per challenge from the leaves.  Replaces
+ * MerkleTree_gen_proof (tree D / tree C openings, porep/stacked/vanilla/proof.hpp:139-140, column_proof.hpp
+ * make_proof) and MerkleTree_gen_cached_proof (tree R-last, proof.hpp:183-186).  A challenge >= leaf_count is
+ * refused with MI_ERR_ARG before any read. */
+int mi_tree_inclusion_paths_dev(mi_ctx *ctx, unsigned arity, const void *leaves_dev, uint64_t leaf_count,
+                                unsigned rows_to_discard, const void *tree_dev, uint64_t count,
+                                const void *challenges_dev, void *leaf_out_dev, void *siblings_out_dev);
 
 /* ---- SDR labelling witness: SHA-256 labels of challenged nodes ------------------
  * label = SHA256(replica_id || u32_be(layer) || u64_be(node) || 0^20 || parent_0 .. parent_36) with byte 31
