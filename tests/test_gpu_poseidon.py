@@ -201,3 +201,65 @@ def test_large_tree_c_sampled_columns_and_parents(ctx):
         js = [pr.randrange(len(rows[level])) for _ in range(16)]
         kids = b"".join(rows[level - 1][8 * j:8 * j + 8].tobytes() for j in js)
         assert oracle_py.poseidon_hash(8, kids) == b"".join(rows[level][j].tobytes() for j in js), level
+
+
+def _proof_root(leaf, sibs, c, arity):
+    """MerkleProof root from a leaf and its per-row siblings (position order, own slot = digit of c)."""
+    h = P.poseidon(arity)
+    cur = leaf
+    for row in sibs:
+        own = c % arity
+        cur = h.hash(row[:own] + [cur] + row[own:])
+        c //= arity
+    return cur
+
+
+@pytest.mark.parametrize("arity,n,discard", [(8, 512, 0), (8, 512, 1), (8, 4096, 2), (2, 256, 3), (4, 1024, 0)])
+def test_inclusion_paths_vs_oracle(ctx, arity, n, discard):
+    # gen_proof / gen_cached_proof (vanilla/proof.hpp:139-140,183-186): siblings equal the oracle tree's, and
+    # every proof hashes back to the root; challenges cover both ends and repeats
+    leaves = seeded(1000 + n + discard, n)
+    rows = P.merkle_rows(leaves, arity)
+    tree = fg.tree.TreeBuilder(ctx, arity, discard).add_final_leaves(leaves)
+    d_leaves = torch.from_numpy(fg.tree._fr_array(leaves)).cuda()
+    d_tree = torch.from_numpy(np.frombuffer(tree, dtype=np.uint8).copy()).cuda()
+    chal = np.array([0, n - 1, 1, arity, n // 2, 5, 5] + list(np.random.default_rng(n).integers(0, n, 57)),
+                    dtype=np.uint64)
+    H = fg.tree.tree_height(n, arity)
+    d_chal = torch.from_numpy(chal.view(np.int64)).cuda()
+    d_leaf = torch.zeros(32 * len(chal), dtype=torch.uint8, device="cuda")
+    d_sib = torch.zeros(32 * len(chal) * H * (arity - 1), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    fg.tree.gen_proofs_dev(ctx, arity, d_leaves.data_ptr(), n, discard, d_tree.data_ptr(), len(chal),
+                           d_chal.data_ptr(), d_leaf.data_ptr(), d_sib.data_ptr())
+    ctx.synchronize()
+    got_leaf = ints(d_leaf.cpu().numpy())
+    got_sib = ints(d_sib.cpu().numpy())
+    root = rows[-1][0]
+    for i, c in enumerate(int(x) for x in chal):
+        assert got_leaf[i] == leaves[c]
+        sibs = []
+        for j in range(H):
+            idx = c // arity ** j
+            g = idx - idx % arity
+            exp = [rows[j][g + s] for s in range(arity) if s != idx % arity]
+            row = got_sib[(i * H + j) * (arity - 1):(i * H + j + 1) * (arity - 1)]
+            assert row == exp, (c, j)
+            sibs.append(row)
+        assert _proof_root(got_leaf[i], sibs, c, arity) == root
+
+
+def test_inclusion_paths_refuse_out_of_range(ctx):
+    n = 64
+    leaves = seeded(77, n)
+    tree = fg.tree.TreeBuilder(ctx, 8, 0).add_final_leaves(leaves)
+    d_leaves = torch.from_numpy(fg.tree._fr_array(leaves)).cuda()
+    d_tree = torch.from_numpy(np.frombuffer(tree, dtype=np.uint8).copy()).cuda()
+    d_chal = torch.tensor([3, n], dtype=torch.int64, device="cuda")
+    d_leaf = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    d_sib = torch.zeros(32 * 2 * 2 * 7, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    with pytest.raises(fg.FilGpuError):
+        fg.tree.gen_proofs_dev(ctx, 8, d_leaves.data_ptr(), n, 0, d_tree.data_ptr(), 2, d_chal.data_ptr(),
+                               d_leaf.data_ptr(), d_sib.data_ptr())
+    assert int(d_sib.sum()) == 0
