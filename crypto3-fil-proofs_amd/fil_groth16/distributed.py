@@ -79,3 +79,53 @@ def prove_split(ctx, pk, circuit, z, r, s, rank: int, world: int, device="cpu", 
     vk, _ = pk.verifying_key()
     shares = gather_shares(prove_share(ctx, pk, circuit, z, rank, world), world, device)
     return assemble(vk, shares, r, s, want_raw=want_raw)
+
+
+SRS_PARTS = ("vk", "ic", "h", "l", "a", "b_g1", "b_g2")
+
+
+def broadcast_srs_parts(parts, rank: int, world: int, src: int = 0, device="cpu", chunk_bytes: int = 1 << 30):
+    """Broadcast a proving key in the bellman wire layout (dict of SRS_PARTS -> bytes, held by ``src``) to
+    every rank: one size vector, then each part in chunks of at most ``chunk_bytes`` (large transfers over
+    xGMI with backend "nccl" on device tensors, bounded staging memory).  The reference loads the same
+    params file in every process (get_groth_params, core/parameter_cache.hpp:185-200); here one rank reads
+    the file and the others receive it.  Returns the dict on every rank."""
+    import torch
+    import torch.distributed as dist
+
+    if world == 1:
+        return dict(parts)
+    sizes = torch.zeros(len(SRS_PARTS), dtype=torch.int64)
+    if rank == src:
+        sizes = torch.tensor([len(parts[k]) for k in SRS_PARTS], dtype=torch.int64)
+    sizes = sizes.to(device)
+    dist.broadcast(sizes, src)
+    out = {}
+    for k, n in zip(SRS_PARTS, sizes.cpu().tolist()):
+        host = np.empty(n, dtype=np.uint8)
+        src_view = np.frombuffer(parts[k], dtype=np.uint8) if rank == src else None
+        for off in range(0, n, chunk_bytes):
+            m = min(chunk_bytes, n - off)
+            t = (torch.from_numpy(src_view[off:off + m].copy()) if rank == src
+                 else torch.empty(m, dtype=torch.uint8)).to(device)
+            dist.broadcast(t, src)
+            host[off:off + m] = t.cpu().numpy()
+        out[k] = host.tobytes()
+    return out
+
+
+def broadcast_proving_key(ctx, pk, circuit, rank: int, world: int, src: int = 0, device="cpu", checked=False,
+                          chunk_bytes: int = 1 << 30):
+    """Rank ``src`` holds ``pk`` (e.g. ProvingKey.load_params from a v28 file); every other rank receives
+    the key over the process group and uploads it to its own GPU.  Returns this rank's ProvingKey."""
+    from .core import ProvingKey
+
+    parts = None
+    if rank == src:
+        vk, ic = pk.verifying_key()
+        parts = dict(vk=vk, ic=ic, h=pk.query(0), l=pk.query(1), a=pk.query(2), b_g1=pk.query(3),
+                     b_g2=pk.query(4))
+    parts = broadcast_srs_parts(parts, rank, world, src, device, chunk_bytes)
+    if rank == src:
+        return pk
+    return ProvingKey.load(ctx, circuit, *(parts[k] for k in SRS_PARTS), checked=checked)

@@ -159,3 +159,51 @@ def test_gloo_partition_runner(tmp_path, oracle, world, num_partitions):
     zb = circuits.z_bytes(z)
     serial = b"".join(P.prove(zb, 300 + p, 400 + p)[0] for p in range(num_partitions))
     assert all(o == serial for o in outs)
+
+
+def _srs_worker(rank, world, port, outdir):
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "crypto3-fil-proofs_amd"), os.path.join(root, "oracle"),
+              os.path.join(root, "tests", "golden")):
+        sys.path.insert(0, p)
+    import hashlib
+
+    import torch.distributed as dist
+
+    import circuits
+    import oracle_py
+    from fil_groth16.distributed import SRS_PARTS, broadcast_srs_parts
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    parts = None
+    if rank == 1:  # a non-zero source rank, and chunks far smaller than the parts
+        n_in, n_aux, rows, z = circuits.random_circuit(63, 40)
+        oc = oracle_py.OracleCircuit(len(rows), n_in, n_aux, circuits.to_csr(rows))
+        parts = oracle_py.OracleParams(oc, circuits.toxic()).export()
+    got = broadcast_srs_parts(parts, rank, world, src=1, chunk_bytes=1000)
+    with open(os.path.join(outdir, f"s{rank}.txt"), "w") as f:
+        f.write(",".join(hashlib.sha256(got[k]).hexdigest() for k in SRS_PARTS))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_srs_broadcast(tmp_path):
+    """One rank holds the proving key (bellman wire layout); every rank ends with identical bytes."""
+    import hashlib
+
+    import circuits
+    import oracle_py
+    from fil_groth16.distributed import SRS_PARTS
+
+    world = 3
+    mp.spawn(_srs_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    outs = [open(tmp_path / f"s{r}.txt").read() for r in range(world)]
+    n_in, n_aux, rows, z = circuits.random_circuit(63, 40)
+    oc = oracle_py.OracleCircuit(len(rows), n_in, n_aux, circuits.to_csr(rows))
+    ex = oracle_py.OracleParams(oc, circuits.toxic()).export()
+    assert all(len(ex[k]) > 1000 or k == "vk" for k in ("h", "l", "a", "b_g2"))
+    exp = ",".join(hashlib.sha256(bytes(ex[k])).hexdigest() for k in SRS_PARTS)
+    assert outs == [exp] * world

@@ -336,3 +336,50 @@ def test_prove_split_two_processes(oracle, tmp_path):
     n_in, n_aux, rws, z = circuits.random_circuit(84, 3000, n_in=6, n_free=32)
     op = oracle.OracleParams(oracle.OracleCircuit(len(rws), n_in, n_aux, circuits.to_csr(rws)), circuits.toxic())
     assert outs[0] == outs[1] == op.prove(circuits.z_bytes(z), 21, 22)[0]
+
+
+def _srs_bcast_gpu_worker(rank, world, port, outdir):
+    import os
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "crypto3-fil-proofs_amd"), os.path.join(root, "tests", "golden")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+
+    import circuits
+    import fil_groth16 as fg
+    from fil_groth16.distributed import broadcast_proving_key
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    c = fg.Context(0)
+    n_in, n_aux, rws, z = circuits.random_circuit(85, 2000, n_in=4, n_free=16)
+    gc = fg.Circuit(c, len(rws), n_in, n_aux, circuits.to_csr(rws))
+    pk = fg.generate_random_parameters(c, gc, circuits.toxic()) if rank == 0 else None
+    pk = broadcast_proving_key(c, pk, gc, rank, world, src=0, checked=True, chunk_bytes=1 << 16)
+    proof = fg.prove(c, pk, gc, circuits.z_bytes(z), 31, 32)
+    with open(os.path.join(outdir, f"b{rank}.bin"), "wb") as f:
+        f.write(proof)
+    dist.barrier()
+    dist.destroy_process_group()
+    del pk, gc
+    c.close()
+
+
+def test_srs_broadcast_two_processes(oracle, tmp_path):
+    """fil_groth16.distributed.broadcast_proving_key: rank 0 holds the key, rank 1 receives it over the
+    process group (checked load: subgroup checks on every point) and proves; both equal the oracle proof."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    mp.spawn(_srs_bcast_gpu_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    outs = [open(tmp_path / f"b{k}.bin", "rb").read() for k in range(2)]
+    n_in, n_aux, rws, z = circuits.random_circuit(85, 2000, n_in=4, n_free=16)
+    op = oracle.OracleParams(oracle.OracleCircuit(len(rws), n_in, n_aux, circuits.to_csr(rws)), circuits.toxic())
+    assert outs[0] == outs[1] == op.prove(circuits.z_bytes(z), 31, 32)[0]
