@@ -22,7 +22,29 @@ def main():
 
     args = argparse.Namespace(sdr_log_labels=a.log_labels, no_cpu_baseline=a.no_cpu_baseline)
     ctx = fg.Context(0)
-    res = bench.sdr_leg(args, fg, ctx, torch.device("cuda:0"), 1)
+    dev = torch.device("cuda:0")
+    res = bench.sdr_leg(args, fg, ctx, dev, 1)
+    # the per-entry form (k_sdr_labels): 14 parents per label given contiguously, the same hash work with
+    # streaming reads instead of random gathers -- separates the VALU bound from the gather traffic
+    import time
+
+    n = 1 << a.log_labels
+    par = torch.randint(0, 256, (n * 14 * 32,), dtype=torch.uint8, device=dev)
+    lay = torch.randint(2, 12, (n,), dtype=torch.int32, device=dev)
+    nod = torch.randint(1, 1 << 30, (n,), dtype=torch.int64, device=dev)
+    out = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    run = lambda: fg.sdr.create_labels_dev(ctx, bytes(32), n, lay.data_ptr(), nod.data_ptr(), par.data_ptr(), 14,
+                                           out.data_ptr())
+    run()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        run()
+    ctx.synchronize()
+    dt = (time.perf_counter() - t0) / 5
+    res["per_entry_form"] = {"kernel": "k_sdr_labels", "labels_per_s": n / dt, "ms_per_batch": dt * 1e3,
+                             "valu_frac": n * 20 * bench.SHA256_OPS_PER_COMPRESSION / dt / bench.VALU_LANE_OPS}
     print(json.dumps(res), flush=True)
     ctx.close()
 
