@@ -246,4 +246,33 @@ inline std::vector<uint8_t> generate_tree_r_last(context &ctx, std::uint64_t nod
     return tree;
 }
 
+// ---- SDR labelling witness ----
+// labels[i] = create_label(replica_id, layers[i], nodes[i], n_parents parents of entry i repeated to 37)
+inline std::vector<fr32> create_labels(context &ctx, const fr32 &replica_id, const std::vector<std::uint32_t> &layers,
+                                       const std::vector<std::uint64_t> &nodes, const std::vector<fr32> &parents,
+                                       unsigned n_parents) {
+    if (layers.size() != nodes.size() || parents.size() != (size_t)n_parents * layers.size())
+        throw error(MI_ERR_ARG, "create_labels: layers, nodes and parents disagree");
+    std::vector<fr32> out(layers.size());
+    if (!layers.empty())
+        check(mi_sdr_labels(ctx.get(), replica_id.data(), layers.size(), layers.data(), nodes.data(),
+                            n_parents ? parents.front().data() : nullptr, n_parents, out.front().data()));
+    return out;
+}
+
+// LabelingProof (porep/stacked/vanilla/labelling_proof.hpp:40-48) with create_label / verify as in
+// vanilla/detail/processing/naive/labelling_proof.hpp:46-70; EncodingProof::create_key is the same hash
+struct labeling_proof {
+    std::vector<fr32> parents;  // parents_data_full (37), or the distinct parents (repeated to 37)
+    std::uint32_t layer_index = 0;
+    std::uint64_t node = 0;
+
+    fr32 create_label(context &ctx, const fr32 &replica_id) const {
+        return create_labels(ctx, replica_id, {layer_index}, {node}, parents, (unsigned)parents.size()).front();
+    }
+    bool verify(context &ctx, const fr32 &replica_id, const fr32 &expected_label) const {
+        return create_label(ctx, replica_id) == expected_label;
+    }
+};
+
 }  // namespace mi355x

@@ -73,3 +73,40 @@ def test_cpp_tree_builders_match_python(ctx):
     assert root_r == P.merkle_rows(replica, 8)[-1][0]
     _, tree = fg.tree.ColumnTreeBuilder(ctx, 11, 8).add_final_columns(layers)
     assert fg.tree.to_ints(tree)[-1] == root_c
+
+
+def test_cpp_sdr_labels_match_oracle(oracle):
+    """examples/sdr_labels.cpp (C++ host layer: create_labels, labeling_proof) against the oracle on the same
+    SplitMix64 inputs."""
+    import numpy as np
+
+    pkg = os.path.join(ROOT, "crypto3-fil-proofs_amd")
+    exe = os.path.join(pkg, "build", "sdr_labels")
+    if not os.path.exists(exe):
+        subprocess.check_call(["g++", "-std=c++17", "-O2", "-I" + os.path.join(ROOT, "include"),
+                               os.path.join(pkg, "examples", "sdr_labels.cpp"), "-L" + os.path.join(pkg, "build"),
+                               "-lfilgpu", "-Wl,-rpath,$ORIGIN", "-o", exe], timeout=120)
+    count = 40
+    out = subprocess.run([exe, str(count)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    lines = out.stdout.split()
+    assert lines[-1] == "ok" and lines[-2] == "verify"
+
+    state = [7]
+
+    def splitmix():
+        state[0] = (state[0] + 0x9E3779B97F4A7C15) & (2 ** 64 - 1)
+        z = state[0]
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & (2 ** 64 - 1)
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & (2 ** 64 - 1)
+        return z ^ (z >> 31)
+
+    def fr():
+        return b"".join(splitmix().to_bytes(8, "little") for _ in range(4))
+
+    rid = fr()
+    layers = [2 + i % 10 for i in range(count)]
+    nodes = [1 + splitmix() % (1 << 30) for _ in range(count)]
+    parents = b"".join(fr() for _ in range(14 * count))
+    exp = oracle.sdr_labels(rid, np.array(layers, np.uint32), np.array(nodes, np.uint64), parents, 14)
+    assert [bytes.fromhex(x) for x in lines[:count]] == [exp[32 * i:32 * i + 32] for i in range(count)]
