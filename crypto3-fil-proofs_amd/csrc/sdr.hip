@@ -20,6 +20,8 @@
 //   * k_sdr_labels_gather: parents gathered from the device-resident layer labels by node index
 //     (base parents from the challenged layer, expander parents from the layer below), optionally writing
 //     the 37 repeated parent labels out as the proof's parents_data_full.
+#include <cstdlib>
+
 #include "ctx.h"
 #include "sdr.h"
 
@@ -141,6 +143,75 @@ __device__ __forceinline__ void label_one(const SdrReplica &rid, uint32_t layer,
                         __builtin_bswap32(st[7]));
 }
 
+__device__ __forceinline__ void unpack_parent(const uint4 *raw, uint32_t *w) {
+    const uint4 lo = raw[0], hi = raw[1];
+    w[0] = __builtin_bswap32(lo.x);
+    w[1] = __builtin_bswap32(lo.y);
+    w[2] = __builtin_bswap32(lo.z);
+    w[3] = __builtin_bswap32(lo.w);
+    w[4] = __builtin_bswap32(hi.x);
+    w[5] = __builtin_bswap32(hi.y);
+    w[6] = __builtin_bswap32(hi.z);
+    w[7] = __builtin_bswap32(hi.w);
+}
+
+// software-pipelined form of label_one: the next block's two parents are loaded (raw, 4 x 16 B) before the
+// current block is compressed, so a wave's own gather latency overlaps its hashing.  fetch_raw(k, raw2)
+// issues the loads of parent k; sink(k, raw2) sees parent k when it is consumed (parents_data_full stores).
+template <class FetchRaw, class Sink>
+__device__ __forceinline__ void label_one_pf(const SdrReplica &rid, uint32_t layer, uint64_t node, bool has_parents,
+                                             FetchRaw &&fetch_raw, Sink &&sink, uint4 *__restrict__ out) {
+    uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+    uint32_t w[16];
+#pragma unroll
+    for (int j = 0; j < 8; j++) w[j] = rid.w[j];
+    w[8] = layer;
+    w[9] = (uint32_t)(node >> 32);
+    w[10] = (uint32_t)node;
+#pragma unroll
+    for (int j = 11; j < 16; j++) w[j] = 0;
+    uint4 nx[4];
+    if (has_parents) {
+        fetch_raw(0, nx);
+        fetch_raw(1, nx + 2);
+    }
+    compress(st, w);  // the prefix block overlaps the first gathers
+    uint32_t bits = 512;
+    if (has_parents) {
+#pragma unroll 1
+        for (uint32_t k = 0; k < kTotalParents - 1; k += 2) {
+            sink(k, nx);
+            sink(k + 1, nx + 2);
+            unpack_parent(nx, w);
+            unpack_parent(nx + 2, w + 8);
+            if (k + 2 < kTotalParents - 1) {
+                fetch_raw(k + 2, nx);
+                fetch_raw(k + 3, nx + 2);
+            } else {
+                fetch_raw(kTotalParents - 1, nx);
+            }
+            compress(st, w);
+        }
+        sink(kTotalParents - 1, nx);
+        unpack_parent(nx, w);
+        bits = kMsgBits;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; j++) w[j] = 0;
+    }
+#pragma unroll
+    for (int j = 8; j < 16; j++) w[j] = 0;
+    if (has_parents) w[8] = 0x80000000u;
+    else w[0] = 0x80000000u;
+    w[15] = bits;
+    compress(st, w);
+    st[7] &= 0xffffff3fu;
+    out[0] = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]), __builtin_bswap32(st[2]),
+                        __builtin_bswap32(st[3]));
+    out[1] = make_uint4(__builtin_bswap32(st[4]), __builtin_bswap32(st[5]), __builtin_bswap32(st[6]),
+                        __builtin_bswap32(st[7]));
+}
+
 __global__ void __launch_bounds__(256) k_sdr_labels(SdrReplica rid, const uint32_t *__restrict__ layers,
                                                     const uint64_t *__restrict__ nodes,
                                                     const uint4 *__restrict__ parents, uint32_t np, uint64_t n,
@@ -161,6 +232,7 @@ __global__ void __launch_bounds__(256) k_sdr_labels(SdrReplica rid, const uint32
 // the n_base base parents take part (proof.hpp:196-209), at layer >= 2 base parents read layer l and
 // expander parents layer l - 1 (proof.hpp:210-231).  full_out (optional) receives the 37 repeated parent
 // labels per challenge (LabelingProof::parents).
+template <bool PF>
 __global__ void __launch_bounds__(256) k_sdr_labels_gather(SdrReplica rid, const uint4 *__restrict__ labels,
                                                            uint64_t nodes_per_layer,
                                                            const uint32_t *__restrict__ layers,
@@ -187,7 +259,26 @@ __global__ void __launch_bounds__(256) k_sdr_labels_gather(SdrReplica rid, const
         load_parent(src, w);
         cur = cur + 1 == np ? 0 : cur + 1;
     };
-    label_one(rid, layer, challenges[i], np != 0 && challenges[i] != 0, fetch, out + 2 * i);
+    const bool has = np != 0 && challenges[i] != 0;
+    if constexpr (PF) {
+        uint32_t nxt = 0;
+        auto fetch_raw = [&](uint32_t, uint4 *raw) __attribute__((always_inline)) {
+            const uint32_t node = pi[nxt];
+            const uint4 *src = (nxt < n_base ? cur_layer : prev_layer) + (uint64_t)node * 2;
+            raw[0] = src[0];
+            raw[1] = src[1];
+            nxt = nxt + 1 == np ? 0 : nxt + 1;
+        };
+        auto sink = [&](uint32_t k, const uint4 *raw) __attribute__((always_inline)) {
+            if (fo) {
+                fo[2 * k] = raw[0];
+                fo[2 * k + 1] = raw[1];
+            }
+        };
+        label_one_pf(rid, layer, challenges[i], has, fetch_raw, sink, out + 2 * i);
+    } else {
+        label_one(rid, layer, challenges[i], has, fetch, out + 2 * i);
+    }
 }
 
 inline unsigned grid256(uint64_t n) { return (unsigned)((n + 255) / 256); }
@@ -217,9 +308,19 @@ void sdr_labels_gather_dev(Ctx &c, const SdrReplica &rid, const void *layer_labe
     if (!n) return;
     if (n_base + n_exp > kTotalParents || n_base == 0)
         throw std::invalid_argument("sdr: 1 <= n_base and n_base + n_exp <= 37");
-    k_sdr_labels_gather<<<grid256(n), 256, 0, c.stream>>>(rid, (const uint4 *)layer_labels, nodes_per_layer,
-                                                          layers, challenges, parent_idx, n_base, n_exp, n,
-                                                          (uint4 *)labels_out, (uint4 *)parents_out);
+    // MI_SDR_PREFETCH (read per call, for A/B): 1 = software-pipelined parent gathers, 0 = load at use
+    const char *pe = getenv("MI_SDR_PREFETCH");
+    const bool pf = pe ? atoi(pe) != 0 : false;
+    if (pf)
+        k_sdr_labels_gather<true><<<grid256(n), 256, 0, c.stream>>>(rid, (const uint4 *)layer_labels,
+                                                                    nodes_per_layer, layers, challenges, parent_idx,
+                                                                    n_base, n_exp, n, (uint4 *)labels_out,
+                                                                    (uint4 *)parents_out);
+    else
+        k_sdr_labels_gather<false><<<grid256(n), 256, 0, c.stream>>>(rid, (const uint4 *)layer_labels,
+                                                                     nodes_per_layer, layers, challenges, parent_idx,
+                                                                     n_base, n_exp, n, (uint4 *)labels_out,
+                                                                     (uint4 *)parents_out);
     MI_LAUNCHED(c, "k_sdr_labels_gather");
 }
 
