@@ -250,7 +250,9 @@ def sdr_leg(args, fg, ctx, device, world):
                              "ops_per_compression": SHA256_OPS_PER_COMPRESSION, "compressions_per_label": 20,
                              "achieved_ops_per_s": ops / dt, "peak_ops_per_s": VALU_LANE_OPS,
                              "frac": ops / dt / VALU_LANE_OPS},
-           "hbm_algorithmic_GBps": count * (14 * 32 + 4 + 8 + 56 + 32) / dt / 1e9}
+           "hbm_algorithmic_GBps": count * (14 * 32 + 4 + 8 + 56 + 32) / dt / 1e9,
+           "traffic_source": "profiles/r02_sdr_summary.json (FETCH_SIZE 2,644 B per label raw vs 548 B "
+                             "algorithmic: line-granular random 32-B parent gathers; WRITE_SIZE 32 B per label)"}
     if world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle_py
