@@ -1423,3 +1423,13 @@ int mi_tree_inclusion_paths_dev(mi_ctx *ctx, unsigned arity, const void *leaves_
         MI_HIP(hipStreamSynchronize(c.stream));
     });
 }
+
+int mi_tree_d_build_dev(mi_ctx *ctx, const void *leaves_dev, uint64_t leaf_count, void *tree_dev) {
+    return guard([&] {
+        need(ctx && leaves_dev && tree_dev, "null argument");
+        need(leaf_count >= 2 && (leaf_count & (leaf_count - 1)) == 0, "tree D: leaf count must be a power of two >= 2");
+        CtxLock l(ctx);
+        mi::tree_d_build_dev(ctx->c, leaves_dev, leaf_count, tree_dev);
+        MI_HIP(hipStreamSynchronize(ctx->c.stream));
+    });
+}

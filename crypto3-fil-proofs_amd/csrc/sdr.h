@@ -21,4 +21,7 @@ void sdr_labels_dev(Ctx &c, const SdrReplica &rid, const uint32_t *layers, const
 void sdr_labels_gather_dev(Ctx &c, const SdrReplica &rid, const void *layer_labels, uint64_t nodes_per_layer,
                            const uint32_t *layers, const uint64_t *challenges, const uint32_t *parent_idx,
                            uint32_t n_base, uint32_t n_exp, uint64_t n, void *labels_out, void *parents_out);
+// tree D: every row above the leaves of the binary SHA-256 tree (node = SHA256(left || right), byte 31 &=
+// 0x3f), bottom-up, n - 1 entries of 32 B; n a power of two
+void tree_d_build_dev(Ctx &c, const void *leaves, uint64_t n, void *rows);
 }  // namespace mi

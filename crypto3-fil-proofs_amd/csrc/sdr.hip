@@ -281,6 +281,30 @@ __global__ void __launch_bounds__(256) k_sdr_labels_gather(SdrReplica rid, const
     }
 }
 
+// tree D (the SHA-256 binary tree over the sector's data, comm_d; openings at vanilla/proof.hpp:139-140):
+// out[i] = SHA256(in[2i] || in[2i + 1]) with byte 31 &= 0x3f (Sha256Hasher's node hash, truncated into Fr).
+// Two compressions per node: the 64-byte message block, then the constant padding block (length 512).
+__global__ void __launch_bounds__(256) k_sha256_pairs(const uint4 *__restrict__ in, uint64_t n_out,
+                                                      uint4 *__restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_out) return;
+    uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+    uint32_t w[16];
+    load_parent(in + 4 * i, w);
+    load_parent(in + 4 * i + 2, w + 8);
+    compress(st, w);
+    w[0] = 0x80000000u;
+#pragma unroll
+    for (int j = 1; j < 15; j++) w[j] = 0;
+    w[15] = 512;
+    compress(st, w);
+    st[7] &= 0xffffff3fu;
+    out[2 * i] = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]), __builtin_bswap32(st[2]),
+                            __builtin_bswap32(st[3]));
+    out[2 * i + 1] = make_uint4(__builtin_bswap32(st[4]), __builtin_bswap32(st[5]), __builtin_bswap32(st[6]),
+                                __builtin_bswap32(st[7]));
+}
+
 inline unsigned grid256(uint64_t n) { return (unsigned)((n + 255) / 256); }
 
 }  // namespace
@@ -322,6 +346,18 @@ void sdr_labels_gather_dev(Ctx &c, const SdrReplica &rid, const void *layer_labe
                                                                      n_base, n_exp, n, (uint4 *)labels_out,
                                                                      (uint4 *)parents_out);
     MI_LAUNCHED(c, "k_sdr_labels_gather");
+}
+
+void tree_d_build_dev(Ctx &c, const void *leaves, uint64_t n, void *rows) {
+    if (n < 2 || (n & (n - 1))) throw std::invalid_argument("tree D: the leaf count must be a power of two >= 2");
+    const uint4 *cur = (const uint4 *)leaves;
+    uint4 *dst = (uint4 *)rows;
+    for (uint64_t m = n / 2; m >= 1; m /= 2) {
+        k_sha256_pairs<<<grid256(m), 256, 0, c.stream>>>(cur, m, dst);
+        MI_LAUNCHED(c, "k_sha256_pairs");
+        cur = dst;
+        dst += 2 * m;
+    }
 }
 
 }  // namespace mi

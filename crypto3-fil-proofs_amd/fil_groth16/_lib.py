@@ -28,6 +28,7 @@ EXPORTS = [
     "mi_tree_build", "mi_tree_build_dev", "mi_tree_c_build", "mi_tree_c_build_dev",
     "mi_tree_r_last_build", "mi_tree_r_last_build_dev",
     "mi_sdr_labels", "mi_sdr_labels_dev", "mi_sdr_labeling_proofs_dev", "mi_tree_inclusion_paths_dev",
+    "mi_tree_d_build_dev",
 ]
 
 _lib = None
@@ -127,6 +128,7 @@ def lib():
         "mi_tree_r_last_build": ([vp, u64, vp, vp, ctypes.c_uint, ctypes.c_uint, vp], c_int),
         "mi_tree_r_last_build_dev": ([vp, u64, vp, vp, ctypes.c_uint, ctypes.c_uint, vp], c_int),
         "mi_tree_inclusion_paths_dev": ([vp, ctypes.c_uint, vp, u64, ctypes.c_uint, vp, u64, vp, vp, vp], c_int),
+        "mi_tree_d_build_dev": ([vp, vp, u64, vp], c_int),
         "mi_sdr_labels": ([vp, vp, u64, vp, vp, vp, ctypes.c_uint, vp], c_int),
         "mi_sdr_labels_dev": ([vp, vp, u64, vp, vp, vp, ctypes.c_uint, vp], c_int),
         "mi_sdr_labeling_proofs_dev": ([vp, vp, ctypes.c_uint, u64, vp, u64, vp, vp, vp, ctypes.c_uint,

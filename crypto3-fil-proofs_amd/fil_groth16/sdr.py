@@ -111,3 +111,9 @@ class EncodingProof:
 
     def verify(self, ctx, replica_id: bytes, exp_encoded_node: bytes, decoded_node: bytes) -> bool:
         return encode(self.create_key(ctx, replica_id), decoded_node) == bytes(exp_encoded_node)
+
+
+def build_tree_d_dev(ctx, leaves_ptr: int, leafs: int, tree_ptr: int) -> None:
+    """tree D over 32-byte data nodes on the device (node = SHA256(left || right), byte 31 &= 0x3f): every row
+    above the leaves, bottom-up, leafs - 1 entries.  Openings: tree.gen_proofs_dev(arity=2, rows_to_discard=0)."""
+    check(lib().mi_tree_d_build_dev(ctx.h, ctypes.c_void_p(leaves_ptr), leafs, ctypes.c_void_p(tree_ptr)))

@@ -325,6 +325,12 @@ int mi_sdr_labels(mi_ctx *ctx, const uint8_t replica_id[32], uint64_t count, con
                   const uint64_t *nodes, const uint8_t *parents, unsigned n_parents, uint8_t *labels);
 int mi_sdr_labels_dev(mi_ctx *ctx, const uint8_t replica_id[32], uint64_t count, const void *layers_dev,
                       const void *nodes_dev, const void *parents_dev, unsigned n_parents, void *labels_dev);
+/* tree D (comm_d): the binary SHA-256 tree over the sector's 32-byte data nodes, node = SHA256(left || right)
+ * with byte 31 &= 0x3f (Sha256Hasher, truncated into Fr); tree_dev receives every row above the leaves,
+ * bottom-up, leaf_count - 1 entries (mi_tree_cache_size(leaf_count, 2, 0)).  leaf_count a power of two.
+ * Openings: mi_tree_inclusion_paths_dev(arity 2, rows_to_discard 0).  Replaces the tree D build of
+ * transform_and_replicate_layers / MerkleTree_gen_proof(tree_d) (porep/stacked/vanilla/proof.hpp:139-140). */
+int mi_tree_d_build_dev(mi_ctx *ctx, const void *leaves_dev, uint64_t leaf_count, void *tree_dev);
 int mi_sdr_labeling_proofs_dev(mi_ctx *ctx, const uint8_t replica_id[32], unsigned n_layers,
                                uint64_t nodes_per_layer, const void *layer_labels_dev, uint64_t count,
                                const void *layers_dev, const void *challenges_dev, const void *parent_idx_dev,

@@ -45,6 +45,18 @@ def main():
     dt = (time.perf_counter() - t0) / 5
     res["per_entry_form"] = {"kernel": "k_sdr_labels", "labels_per_s": n / dt, "ms_per_batch": dt * 1e3,
                              "valu_frac": n * 20 * bench.SHA256_OPS_PER_COMPRESSION / dt / bench.VALU_LANE_OPS}
+    # tree D (binary SHA-256 tree over the data, comm_d): 2^log_labels leaves, 2 compressions per node
+    leaves = torch.randint(0, 256, (n * 32,), dtype=torch.uint8, device=dev)
+    tree = torch.empty((n - 1) * 32, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    fg.sdr.build_tree_d_dev(ctx, leaves.data_ptr(), n, tree.data_ptr())
+    t0 = time.perf_counter()
+    for _ in range(5):
+        fg.sdr.build_tree_d_dev(ctx, leaves.data_ptr(), n, tree.data_ptr())
+    dt = (time.perf_counter() - t0) / 5
+    res["tree_d"] = {"kernel": "k_sha256_pairs (one launch per level)", "leaves": n, "ms_per_tree": dt * 1e3,
+                     "leaves_per_s": n / dt, "GB_per_s_of_data": n * 32 / dt / 1e9,
+                     "valu_frac": (n - 1) * 2 * bench.SHA256_OPS_PER_COMPRESSION / dt / bench.VALU_LANE_OPS}
     print(json.dumps(res), flush=True)
     ctx.close()
 
