@@ -205,7 +205,13 @@ def tree_c_leg(args, fg, ctx, device, world):
 # a 1 v_add3 = 14; per schedule word sigma0/sigma1 2 v_alignbit + 1 shift + 1 xor3 each, v_add3 + add = 10;
 # 8 feed-forward adds.  The compiled block loop issues 1,410 VALU per compression (this + the byte swaps).
 SHA256_OPS_PER_COMPRESSION = 64 * 14 + 48 * 10 + 8
-VALU_LANE_OPS = 1024 * 64 / 4 * 2.4e9  # 1024 SIMDs x 16 lanes per clock x 2.4 GHz (same issue model as MAD_RATE)
+# Peak: the measured chip-wide issue rates of the model's instructions (crypto3-fil-proofs_amd/microbench/
+# intrate.hip, profiles/r02_intrate_microbench.jsonl): v_alignbit_b32 and v_add3_u32 3.54e13 lane-ops/s,
+# v_bitop3_b32 / v_add_u32 / shifts 5.31e13.  Per compression the model holds 816 of the former (6 + 4
+# rotations per round / schedule word, 3 + 1 add3) and 568 of the latter.
+SHA256_SLOW_OPS, SHA256_FAST_OPS = 64 * 6 + 48 * 4 + 64 * 3 + 48, 64 * 14 + 48 * 10 + 8 - (64 * 9 + 48 * 5)
+SHA256_PEAK_COMPRESSIONS = 1.0 / (SHA256_SLOW_OPS / 3.54e13 + SHA256_FAST_OPS / 5.31e13)
+VALU_LANE_OPS = SHA256_PEAK_COMPRESSIONS * SHA256_OPS_PER_COMPRESSION  # model lane-ops/s at that peak
 
 
 def sdr_leg(args, fg, ctx, device, world):
@@ -249,6 +255,8 @@ def sdr_leg(args, fg, ctx, device, world):
            "valu_roofline": {"kernel": "k_sdr_labels_gather", "bound": "valu (32-bit integer issue)",
                              "ops_per_compression": SHA256_OPS_PER_COMPRESSION, "compressions_per_label": 20,
                              "achieved_ops_per_s": ops / dt, "peak_ops_per_s": VALU_LANE_OPS,
+                             "peak_source": "measured issue rates of the model's instructions "
+                                            "(microbench/intrate.hip, profiles/r02_intrate_microbench.jsonl)",
                              "frac": ops / dt / VALU_LANE_OPS},
            "hbm_algorithmic_GBps": count * (14 * 32 + 4 + 8 + 56 + 32) / dt / 1e9,
            "traffic_source": "profiles/r02_sdr_summary.json (FETCH_SIZE 2,644 B per label raw vs 548 B "
