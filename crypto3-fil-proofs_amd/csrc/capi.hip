@@ -66,6 +66,7 @@ struct mi_points {
     int is_g2;
     int owns;
     const void *hi = nullptr;  // 2^128 multiples (split-mode MSM table), proving-key queries h, l, a only
+    int subgroup = 0;          // every point known to be in the prime-order subgroup (GLV split allowed)
 };
 
 namespace {
@@ -486,6 +487,15 @@ int mi_srs_info(const mi_srs *srs, uint64_t out[6]) {
     });
 }
 
+int mi_srs_msm_info(const mi_srs *srs, uint64_t out[2]) {
+    return guard([&] {
+        need(srs && out, "null argument");
+        const mi::Srs &s = *srs->p;
+        out[0] = (s.h_hi || s.l_hi || s.a_hi) ? 1 : 0;
+        out[1] = s.in_subgroup ? 1 : 0;
+    });
+}
+
 int mi_srs_export_query(mi_ctx *ctx, const mi_srs *srs, int which, uint8_t *out, uint64_t cap) {
     return guard([&] {
         need(ctx && srs && out, "null argument");
@@ -738,13 +748,42 @@ int mi_points_from_srs(mi_ctx *ctx, const mi_srs *srs, int which, mi_points **ou
         need(ctx && srs && out, "null argument");
         const mi::Srs &s = *srs->p;
         switch (which) {
-            case 0: *out = new mi_points{s.h_perm, s.n_h, 0, 0, s.h_hi}; break;
-            case 1: *out = new mi_points{s.l, s.n_l, 0, 0, s.l_hi}; break;
-            case 2: *out = new mi_points{s.a, s.n_a, 0, 0, s.a_hi}; break;
-            case 3: *out = new mi_points{s.b_g1, s.n_b, 0, 0}; break;
-            case 4: *out = new mi_points{s.b_g2, s.n_b, 1, 0}; break;
+            case 0: *out = new mi_points{s.h_perm, s.n_h, 0, 0, s.h_hi, s.in_subgroup}; break;
+            case 1: *out = new mi_points{s.l, s.n_l, 0, 0, s.l_hi, s.in_subgroup}; break;
+            case 2: *out = new mi_points{s.a, s.n_a, 0, 0, s.a_hi, s.in_subgroup}; break;
+            case 3: *out = new mi_points{s.b_g1, s.n_b, 0, 0, nullptr, s.in_subgroup}; break;
+            case 4: *out = new mi_points{s.b_g2, s.n_b, 1, 0, nullptr, s.in_subgroup}; break;
             default: throw std::invalid_argument("which must be 0..4");
         }
+    });
+}
+int mi_points_check_subgroup(mi_ctx *ctx, mi_points *p) {
+    return guard([&] {
+        need(ctx && p, "null argument");
+        CtxLock l(ctx);
+        mi::Ctx &c = ctx->c;
+        int *bad = c.scratch[9].as<int>(4);
+        MI_HIP(hipMemsetAsync(bad, 0, 3 * sizeof(int), c.stream));
+        if (p->is_g2)
+            mi::g2_subgroup_check(c, (const mi::g2_affine_t *)p->dev, p->n, bad);
+        else
+            mi::g1_subgroup_check(c, (const mi::g1_affine_t *)p->dev, p->n, bad);
+        int nbad[3] = {0, 0, 0};
+        MI_HIP(hipMemcpyAsync(nbad, bad, sizeof(nbad), hipMemcpyDeviceToHost, c.stream));
+        MI_HIP(hipStreamSynchronize(c.stream));
+        if (nbad[2]) {
+            p->subgroup = 0;
+            throw std::invalid_argument(std::to_string(nbad[2]) + " point(s) outside the prime-order subgroup");
+        }
+        p->subgroup = 1;
+    });
+}
+int mi_points_info(const mi_points *p, uint64_t out[3]) {
+    return guard([&] {
+        need(p && out, "null argument");
+        out[0] = p->n;
+        out[1] = p->hi ? 1 : 0;
+        out[2] = p->subgroup ? 1 : 0;
     });
 }
 void mi_points_free(mi_points *p) {
@@ -762,7 +801,7 @@ int mi_msm_g1_dev(mi_ctx *ctx, const mi_points *bases, const void *scalars_dev, 
         CtxLock l(ctx);
         mi::g1_xyzz_t r;
         mi::msm_g1(ctx->c, (const mi::g1_affine_t *)bases->dev, (const mi::fr_t *)scalars_dev, nullptr, n, &r,
-                   (const mi::g1_affine_t *)bases->hi);
+                   (const mi::g1_affine_t *)bases->hi, bases->subgroup != 0);
         mi::g1_encode(mi::xyzz_to_affine(r), out96);
     });
 }

@@ -249,13 +249,16 @@ void msm_g2_planned(Ctx &c, const MsmPlan &plan, const g2_affine_t *bases, g2_xy
 // k_i = lo_i + 2^128 hi_i becomes two 128-bit scalars over bases[i] and bases_hi[i], which halves the
 // windows (and the bucket reduction) for the same number of mixed additions (MI_MSM_SPLIT: 0 off,
 // 1 default from 2^16 points, 2 always).
+// subgroup: every base is known to lie in the prime-order subgroup (a generated key, a checked load, or
+// bases that passed mi_points_check_subgroup); only then may auto mode take the GLV split (glv.h).
 void msm_g1(Ctx &c, const g1_affine_t *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,
-            g1_xyzz_t *result_host, const g1_affine_t *bases_hi = nullptr);
+            g1_xyzz_t *result_host, const g1_affine_t *bases_hi = nullptr, bool subgroup = false);
 // whether msm_g1 with a bases_hi table takes the split path for n points
 bool msm_use_split(uint64_t n);
 // G1 split mode through the GLV endomorphism (glv.h) instead of the 2^128 tables: MI_MSM_GLV unset -> 2
-// (auto: GLV for bases without a table, e.g. caller-uploaded ones, and when the tables would not fit in
-// HBM at key load), 0 -> never, 1 -> always (key load builds no tables).  Same-box 2^26 proof: tables 525-526
+// (auto: GLV for subgroup-known bases without a table, e.g. a generated or checked key whose tables would
+// not fit in HBM at key load), 0 -> never, 1 -> always (key load builds no tables; the caller asserts
+// that every base is in the subgroup).  Same-box 2^26 proof: tables 525-526
 // ms and 88.9 GB after setup, GLV 532-533 ms and 68.9 GB.
 int msm_glv_mode();
 // bases_hi table: out[i] = 2^128 in[i] (128 doublings, batch-normalised to affine); scratch slots 10, 11

@@ -47,8 +47,8 @@ int msm_glv_mode() {
 }
 
 void msm_g1(Ctx &c, const g1_affine_t *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,
-            g1_xyzz_t *result_host, const g1_affine_t *bases_hi) {
-    msm_run<fq_t>(c, bases, scalars, idx, n, result_host, bases_hi);
+            g1_xyzz_t *result_host, const g1_affine_t *bases_hi, bool subgroup) {
+    msm_run<fq_t>(c, bases, scalars, idx, n, result_host, bases_hi, subgroup);
 }
 
 bool msm_prepare(Ctx &c, const fr_t *scalars, const uint32_t *idx, uint64_t n, MsmPlan &plan, bool split) {

@@ -1117,12 +1117,16 @@ void msm_accumulate_impl(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, XYZZ
 
 template <class F>
 void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,
-             XYZZ<F> *result, const Affine<F> *bases_hi = nullptr) {
+             XYZZ<F> *result, const Affine<F> *bases_hi = nullptr, bool subgroup = false) {
     ScopedTimer whole(c, sizeof(F) == sizeof(fq_t) ? &c.stats.msm_g1 : &c.stats.msm_g2, n);
     MsmPlan pl;
-    // G1 split mode: the GLV endomorphism (no table) when MI_MSM_GLV selects it, else the 2^128 table
+    // G1 split mode: the GLV endomorphism (no table) when MI_MSM_GLV selects it, else the 2^128 table.
+    // phi(P) = lambda P holds only on the r-torsion, so auto mode takes GLV only for bases known to be in
+    // the prime-order subgroup (generated / checked keys, mi_points_check_subgroup); other on-curve bases
+    // run the plain path, which computes sum k_i P_i exactly like bellman's multiexp.
     const int glv_mode = msm_glv_mode();
-    const bool glv = sizeof(F) == sizeof(fq_t) && msm_use_split(n) && (glv_mode == 1 || (glv_mode == 2 && !bases_hi));
+    const bool glv = sizeof(F) == sizeof(fq_t) && msm_use_split(n) &&
+                     (glv_mode == 1 || (glv_mode == 2 && !bases_hi && subgroup));
     const bool split = !glv && bases_hi && msm_use_split(n);
     if (!msm_prepare_impl(c, scalars, idx, n, pl, split, glv)) {
         *result = XYZZ<F>::inf();

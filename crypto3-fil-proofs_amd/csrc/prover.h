@@ -41,6 +41,9 @@ struct Srs {
     fr_t *at = nullptr, *bt = nullptr, *ct = nullptr;
     fr_t toxic[5];
     bool has_trapdoor = false;
+    // every query point is known to lie in the prime-order subgroup (generated from toxic waste, or
+    // loaded with checked = 1): the condition for the GLV split in auto mode (msm_g1 `subgroup`)
+    bool in_subgroup = false;
     ~Srs();
 };
 

@@ -547,6 +547,7 @@ Srs *srs_load(Ctx &c, const Circuit *circ, const SrsHost &h, bool checked) {
             if (S->ic[i].is_inf()) throw std::invalid_argument("ic point at infinity");
             if (!g1_ok(S->ic[i])) throw std::invalid_argument("ic point not on the curve / outside the subgroup");
         }
+        S->in_subgroup = checked;
         build_hi_tables(c, *S);
     } catch (...) {
         delete S;
@@ -623,6 +624,7 @@ Srs *srs_generate(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5]) {
              delta = to_mont(toxic_canonical[4]);
         for (int i = 0; i < 5; i++) S->toxic[i] = toxic_canonical[i];
         S->has_trapdoor = true;
+        S->in_subgroup = true;  // k G for known k: every point is in the prime-order subgroup
         // powers of tau via two 65536-entry tables
         std::vector<fr_t> lo(65536), hi(65536);
         lo[0] = fr_t::one();
@@ -827,7 +829,7 @@ ProofSums groth16_sums(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *
                 if (b_first) run_b();
                 uint64_t l_lo, l_cnt = slice(circ.n_aux, l_lo);
                 msm_g1(x, srs.l + l_lo, z_dev + circ.n_in + l_lo, nullptr, l_cnt, &Lq,
-                       srs.l_hi ? srs.l_hi + l_lo : nullptr);
+                       srs.l_hi ? srs.l_hi + l_lo : nullptr, srs.in_subgroup);
                 if (!b_first) run_b();
                 MI_HIP(hipEventRecord(done, x.stream));
             } catch (...) {
@@ -858,8 +860,10 @@ ProofSums groth16_sums(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *
             k_qap_divide<<<grid1(d), 256, 0, st>>>(a, b, cc, d, zinv);
             ntt_dif_coset_epilogue(c, a, L, true, true, dinv, true);  // icoset, canonical H (bit-reversed order)
             uint64_t h_lo, h_cnt = slice(d - 1, h_lo), a_lo, a_cnt = slice(circ.n_a, a_lo);
-            msm_g1(c, srs.h_perm + h_lo, a + h_lo, nullptr, h_cnt, &H, srs.h_hi ? srs.h_hi + h_lo : nullptr);
-            msm_g1(c, srs.a + a_lo, z_dev, circ.idx_a + a_lo, a_cnt, &As, srs.a_hi ? srs.a_hi + a_lo : nullptr);
+            msm_g1(c, srs.h_perm + h_lo, a + h_lo, nullptr, h_cnt, &H, srs.h_hi ? srs.h_hi + h_lo : nullptr,
+                   srs.in_subgroup);
+            msm_g1(c, srs.a + a_lo, z_dev, circ.idx_a + a_lo, a_cnt, &As, srs.a_hi ? srs.a_hi + a_lo : nullptr,
+                   srs.in_subgroup);
         } catch (...) {
             err_main = std::current_exception();
         }

@@ -28,7 +28,7 @@ EXPORTS = [
     "mi_tree_build", "mi_tree_build_dev", "mi_tree_c_build", "mi_tree_c_build_dev",
     "mi_tree_r_last_build", "mi_tree_r_last_build_dev",
     "mi_sdr_labels", "mi_sdr_labels_dev", "mi_sdr_labeling_proofs_dev", "mi_tree_inclusion_paths_dev",
-    "mi_tree_d_build_dev",
+    "mi_tree_d_build_dev", "mi_srs_msm_info", "mi_points_check_subgroup", "mi_points_info",
 ]
 
 _lib = None
@@ -81,6 +81,9 @@ def lib():
         "mi_srs_export_query": ([vp, vp, c_int, vp, u64], c_int),
         "mi_srs_info": ([vp, vp], c_int),
         "mi_srs_free": ([vp], None),
+        "mi_srs_msm_info": ([vp, vp], c_int),
+        "mi_points_check_subgroup": ([vp, vp], c_int),
+        "mi_points_info": ([vp, vp], c_int),
         "mi_groth16_prove": ([vp, vp, vp, u8p, u8p, u8p, c_int, vp, vp], c_int),
         "mi_groth16_prove_dev": ([vp, vp, vp, vp, u8p, u8p, c_int, vp, vp], c_int),
         "mi_groth16_prove_batch": ([vp, vp, vp, u64, vp, u8p, c_int, vp], c_int),

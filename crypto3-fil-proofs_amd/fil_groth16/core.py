@@ -133,6 +133,17 @@ class Points:
             check(f(ctx.h, bytes(data), n, ctypes.byref(self.h)))
         self.n = lib().mi_points_count(self.h)
 
+    def check_subgroup(self):
+        """r P == O for every base (raises FilGpuError otherwise); marks the bases subgroup-known, which
+        lets large G1 MSMs over them take the GLV split."""
+        check(lib().mi_points_check_subgroup(self.ctx.h, self.h))
+
+    def info(self):
+        """{"count", "split_table", "subgroup"}"""
+        out = (ctypes.c_uint64 * 3)()
+        check(lib().mi_points_info(self.h, out))
+        return {"count": out[0], "split_table": bool(out[1]), "subgroup": bool(out[2])}
+
     def msm_dev(self, scalars_ptr: int, n: int) -> bytes:
         out = ctypes.create_string_buffer(192 if self.g2 else 96)
         f = lib().mi_msm_g2_dev if self.g2 else lib().mi_msm_g1_dev
@@ -241,6 +252,13 @@ class ProvingKey:
     def write_vk(self, path: str):
         """bellman VerifyingKey::write (write_cached_verifying_key, core/parameter_cache.hpp:136-144)."""
         check(lib().mi_vk_write(self.h, os.fsencode(path)))
+
+    def msm_info(self):
+        """{"split_tables": 2^128 tables of h, l, a resident, "subgroup": every point subgroup-known}.
+        A subgroup-known key without tables runs its split-size G1 MSMs through GLV."""
+        out = (ctypes.c_uint64 * 2)()
+        check(lib().mi_srs_msm_info(self.h, out))
+        return {"split_tables": bool(out[0]), "subgroup": bool(out[1])}
 
     def verifying_key(self):
         vk = ctypes.create_string_buffer(VK_BYTES)

@@ -127,6 +127,11 @@ int mi_srs_export_vk(const mi_srs *srs, uint8_t *vk_out, uint8_t *ic_out);
 int mi_srs_export_query(mi_ctx *ctx, const mi_srs *srs, int which, uint8_t *out, uint64_t cap_points);
 /* sizes: d, |h|, |l|, |a|, |b|, |ic| */
 int mi_srs_info(const mi_srs *srs, uint64_t out[6]);
+/* G1 MSM mode of a key: out[0] = 1 when the 2^128 split tables of h, l, a are resident (built at load
+ * unless MI_MSM_GLV=1 or they would take more than half of the free HBM), out[1] = 1 when every point is
+ * known to be in the prime-order subgroup (generated key or checked load).  Without tables, the G1
+ * MSMs of a subgroup-known key take the GLV split; otherwise they run the plain 256-bit path. */
+int mi_srs_msm_info(const mi_srs *srs, uint64_t out[2]);
 void mi_srs_free(mi_srs *srs);
 
 /* ---- verification (host CPU; no device needed) ----
@@ -219,6 +224,12 @@ int mi_points_upload_g2(mi_ctx *ctx, const uint8_t *bases192, uint64_t n, mi_poi
 /* device copies of a generated key's queries (for MSM benchmarking on real SRS points) */
 int mi_points_from_srs(mi_ctx *ctx, const mi_srs *srs, int which, mi_points **out);
 void mi_points_free(mi_points *p);
+/* r P == O for every point (the checked-load test); on success the bases are marked subgroup-known so that
+ * large G1 MSMs over them may take the GLV split (phi(P) = lambda P holds only on the r-torsion).  A point
+ * outside the subgroup: MI_ERR_ARG, and the bases stay on the exact plain path. */
+int mi_points_check_subgroup(mi_ctx *ctx, mi_points *p);
+/* out: count, has a 2^128 split table, subgroup-known */
+int mi_points_info(const mi_points *p, uint64_t out[3]);
 uint64_t mi_points_count(const mi_points *p);
 int mi_msm_g1_dev(mi_ctx *ctx, const mi_points *bases, const void *scalars_dev, uint64_t n, uint8_t out96[96]);
 int mi_msm_g2_dev(mi_ctx *ctx, const mi_points *bases, const void *scalars_dev, uint64_t n, uint8_t out192[192]);

@@ -73,3 +73,25 @@ def test_repeat_parents_and_encode():
     assert fg.sdr.encode((r - 1).to_bytes(32, "little"), (5).to_bytes(32, "little")) == (4).to_bytes(32, "little")
     with pytest.raises(ValueError):
         fg.sdr.encode(r.to_bytes(32, "little"), bytes(32))
+
+
+# Reference-held tree D vectors: compute_comm_d of an empty 2048-byte and 128-byte sector
+# (libs/filecoin/test/pieces.cpp:86-95): 64 / 4 zero leaves, SHA-256 node hash, byte 31 &= 0x3f.
+COMM_D_EMPTY = {
+    64: bytes([252, 126, 146, 130, 150, 229, 22, 250, 173, 233, 134, 178, 143, 146, 212, 74,
+               79, 36, 185, 53, 72, 82, 35, 55, 106, 121, 144, 39, 188, 24, 248, 51]),
+    4: bytes.fromhex("3731bb99ac689f66eef5973e4a94da188f4ddcae580724fc6f3fd60dfd488333"),
+}
+
+
+@pytest.mark.parametrize("leaves", sorted(COMM_D_EMPTY))
+def test_oracle_tree_d_root_matches_reference_comm_d(oracle, leaves):
+    row = [bytes(32)] * leaves
+    while len(row) > 1:
+        nxt = []
+        for i in range(0, len(row), 2):
+            d = bytearray(oracle.sha256(row[i] + row[i + 1]))
+            d[31] &= 0x3F
+            nxt.append(bytes(d))
+        row = nxt
+    assert row[0] == COMM_D_EMPTY[leaves]

@@ -119,3 +119,71 @@ def test_groth16_2_26_default_settings_verified(ctx, oracle):
     assert oracle.groth16_verify(vk, ic, sc.z_array()[:32 * sc.n_in].tobytes(), raw)
     del z, pk, gc
     torch.cuda.synchronize()
+
+
+def test_groth16_2_27_config4_default_settings_verified(ctx, oracle, monkeypatch):
+    """BASELINE config 4 shape (2^27 domain, ~1.3e8 constraints: the 32 GiB PoRep partition size) with
+    default settings, as bench.py's config4 leg times it.  The trapdoor discrete logs and both pairing
+    verifiers check the proof.  Then the G1 split mode the auto policy did NOT pick is forced on the same
+    key (MI_MSM_GLV=1 over resident 2^128 tables, or MI_MSM_GLV=0 = the plain 256-bit path when the
+    tables were skipped for HBM), and the proof bytes must be identical."""
+    import torch
+
+    from fil_groth16 import synth
+
+    monkeypatch.delenv("MI_MSM_GLV", raising=False)
+    sc = synth.SynthCircuit(log_rows=27, n_in=4, seed=3)
+    gc = sc.load(ctx)
+    assert gc.d == 1 << 27
+    pk = fg.generate_random_parameters(ctx, gc, circuits.toxic())
+    mode = pk.msm_info()
+    assert mode["subgroup"]  # generated from toxic waste: every query point is k G
+    free_b, total_b = torch.cuda.mem_get_info()
+    print("config4: split tables resident = %s, free HBM after key setup %.1f GB of %.1f"
+          % (mode["split_tables"], free_b / 1e9, total_b / 1e9))
+    z = torch.from_numpy(sc.z_array().copy()).cuda()
+    r, s = circuits.blinding(27)
+    proof, raw = fg.prove(ctx, pk, gc, z.data_ptr(), r, s, want_raw=True)
+    a, b, c = fg.trapdoor_dlogs(ctx, pk, gc, z.data_ptr(), r, s)
+    g1, g2 = oracle.g1_generator(), oracle.g2_generator()
+    assert raw[:96] == oracle.g1_mul(g1, a)
+    assert raw[96:288] == oracle.g2_mul(g2, b)
+    assert raw[288:] == oracle.g1_mul(g1, c)
+    vk, ic = pk.verifying_key()
+    assert fg.verify(vk, ic, sc.z_array()[32:32 * sc.n_in].tobytes(), proof)
+    assert oracle.groth16_verify(vk, ic, sc.z_array()[:32 * sc.n_in].tobytes(), raw)
+    monkeypatch.setenv("MI_MSM_GLV", "1" if mode["split_tables"] else "0")
+    assert fg.prove(ctx, pk, gc, z.data_ptr(), r, s) == proof
+    del z, pk, gc
+    torch.cuda.synchronize()
+
+
+def test_msm_g1_non_subgroup_base_stays_exact(ctx, oracle, key17, monkeypatch):
+    """the GLV split assumes phi(P) = lambda P, true only on the r-torsion.  Caller bases are
+    checked for the curve equation only, so a 2^16-point MSM (split size) over bases holding on-curve
+    points outside the subgroup must still equal sum k_i P_i: auto mode takes the exact plain path for
+    them, and mi_points_check_subgroup refuses them.  Clean bases that pass the check take GLV."""
+    import badpoints
+
+    monkeypatch.delenv("MI_MSM_GLV", raising=False)
+    n = 1 << 16
+    q = key17["l"][:96 * n]
+    assert key17["pk"].msm_info()["subgroup"]
+    base = bytearray(q)
+    _, bad = badpoints.g1_non_subgroup()
+    for i in (0, 777, n - 1):
+        base[96 * i:96 * i + 96] = bad
+    base = bytes(base)
+    sb = _scalars(n, 99)
+    want = oracle.msm_g1(base, sb)
+    assert ctx.msm_g1(base, sb) == want
+    pts = fg.Points(ctx, base)
+    assert pts.info() == {"count": n, "split_table": False, "subgroup": False}
+    with pytest.raises(fg.FilGpuError, match="subgroup"):
+        pts.check_subgroup()
+    sd = _dev(sb)
+    assert pts.msm_dev(sd.data_ptr(), n) == want
+    clean = fg.Points(ctx, q)
+    clean.check_subgroup()
+    assert clean.info()["subgroup"]
+    assert clean.msm_dev(sd.data_ptr(), n) == oracle.msm_g1(q, sb)

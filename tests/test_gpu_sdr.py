@@ -199,3 +199,19 @@ def test_tree_d_vs_hashlib_and_openings(ctx, n):
 def test_tree_d_refuses_bad_shape(ctx):
     with pytest.raises(fg.FilGpuError):
         fg.sdr.build_tree_d_dev(ctx, 1, 3, 1)  # not a power of two: refused before any launch
+
+
+@pytest.mark.parametrize("leaves", [4, 64])
+def test_tree_d_root_matches_reference_comm_d(ctx, leaves):
+    """mi_tree_d_build_dev over an empty 128-byte / 2048-byte sector: the root must equal the reference's
+    compute_comm_d vectors (libs/filecoin/test/pieces.cpp:86-95). This pins the SHA-256 node hash and
+    the byte-31 truncation that the label kernel shares."""
+    from test_cpu_sdr import COMM_D_EMPTY
+
+    dev = torch.device("cuda:0")
+    d_leaves = torch.zeros(leaves * 32, dtype=torch.uint8, device=dev)
+    d_tree = torch.zeros((leaves - 1) * 32, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    fg.sdr.build_tree_d_dev(ctx, d_leaves.data_ptr(), leaves, d_tree.data_ptr())
+    ctx.synchronize()
+    assert d_tree.cpu().numpy().tobytes()[-32:] == COMM_D_EMPTY[leaves]
