@@ -38,7 +38,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # gap to it is the non-MAD instructions (carries, subtractions, selects).
 MAD_RATE = 1024 * 64 / 4 * 2.4e9
 FQ_MUL_MADS = 392
-FQ_MUL_PER_MIXED_ADD = {"G1": 10, "G2": 28}  # madd-2008-s: 8M + 2S over Fq / Fq2 (Karatsuba 3M, 2M per sqr)
+FQ_MUL_PER_MIXED_ADD = {"G1": 10, "G2": 28}
+# The chip's spec VALU issue rate (MI355X_MICROARCH.md "Wave scheduling": a wave64 VALU instruction issues
+# over 2 cycles, 32 lanes/cycle per SIMD): 1024 SIMDs x 32 x 2.4 GHz lane-instructions/s.  Reported next to
+# the measured-rate peaks so that a fraction of a measured instruction rate is not read as "done".
+SPEC_VALU_LANE_INSTR = 1024 * 32 * 2.4e9
+# ISA VALU instructions per G1 mixed addition in k_accum_level0 (3,546 v_mad_u64_u32 +
+# ~1,550 other after the lazy reduction)
+G1_MADD_VALU_INSTR = 3546 + 1550  # madd-2008-s: 8M + 2S over Fq / Fq2 (Karatsuba 3M, 2M per sqr)
 TOXIC_SEED = 0x5EED
 
 
@@ -91,8 +98,8 @@ def cpu_baseline(args, fg, synth_mod, ctx):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py
 
-    affinity = len(os.sched_getaffinity(0))
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or affinity
+    lease = cpu_lease()
+    threads = lease["threads"]
     oracle_py.set_threads(threads)
     samples = []
     for lr in sorted(int(x) for x in str(args.cpu_log_rows).split(",")):
@@ -123,24 +130,56 @@ def cpu_baseline(args, fg, synth_mod, ctx):
                   f"{all(x['gpu_proof_bytes_identical'] for x in samples)}",
         "cpu_model": cpu_model(),
         "host_cpus": os.cpu_count(),
-        "affinity_cpus": affinity,
+        "lease": lease,
         "samples": samples,
     }
-    if len(samples) >= 2:
-        a, b = samples[-2], samples[-1]
-        alpha = math.log(b["seconds"] / a["seconds"]) / math.log(b["constraints"] / a["constraints"])
+    if len(samples) >= 3:
+        # least-squares fit of log t = alpha log n + c over every sample (>= 3 points), evaluated at the target
+        xs = [math.log(x["constraints"]) for x in samples]
+        ys = [math.log(x["seconds"]) for x in samples]
+        mx, my = sum(xs) / len(xs), sum(ys) / len(ys)
+        alpha = sum((x - mx) * (y - my) for x, y in zip(xs, ys)) / sum((x - mx) ** 2 for x in xs)
+        c0 = my - alpha * mx
+        resid = max(abs(y - (alpha * x + c0)) for x, y in zip(xs, ys))
         n_t = (1 << args.log_rows) - args.n_in
-        t_t = b["seconds"] * (n_t / b["constraints"]) ** alpha
+        t_t = math.exp(alpha * math.log(n_t) + c0)
         out["extrapolated"] = {
             "label": "extrapolated",
             "log_rows": args.log_rows,
             "constraints": n_t,
             "seconds": t_t,
             "constraints_per_s": n_t / t_t,
-            "model": f"t(n) = t(2^{b['log_rows']}) (n / n_{b['log_rows']})^alpha, alpha = {alpha:.3f} fitted on "
-                     f"the 2^{a['log_rows']} and 2^{b['log_rows']} samples, {threads} threads",
+            "model": f"least-squares log t = alpha log n + c over the {len(samples)} samples 2^"
+                     f"{'/2^'.join(str(x['log_rows']) for x in samples)}, alpha = {alpha:.3f}, max |log residual| "
+                     f"{resid:.3f}, {threads} threads",
         }
     return out
+
+
+def cpu_lease():
+    """The CPUs this process may really use, side by side: the affinity mask, the cgroup v2 cpu.max quota
+    (quota / period CPUs, if any), and OMP_NUM_THREADS (the pool sets it to the lease's per-GPU share).
+    threads = the quota when one is set, else OMP_NUM_THREADS, else the affinity mask; never more than the
+    affinity mask."""
+    affinity = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None
+    if quota:
+        threads, basis = max(1, int(quota)), "cgroup cpu.max quota"
+    elif omp:
+        threads, basis = omp, "OMP_NUM_THREADS (the pool's per-GPU CPU share)"
+    else:
+        threads, basis = affinity, "affinity mask"
+    threads = min(threads, affinity)
+    return {"threads": threads, "basis": basis, "affinity_cpus": affinity, "cgroup_cpu_max_cpus": quota,
+            "omp_num_threads": omp, "host_cpus": os.cpu_count()}
 
 
 def tree_c_leg(args, fg, ctx, device, world):
@@ -178,13 +217,18 @@ def tree_c_leg(args, fg, ctx, device, world):
            "columns_per_s": n / dt, "ms_per_tree": dt * 1e3, "kernel_ms_per_tree": kern_s * 1e3,
            "valu_roofline": {"kernel": "k_poseidon<12> + k_poseidon<9>", "bound": "valu (v_mad_u64_u32 issue)",
                              "mads_per_tree": mads, "achieved_mads_per_s": mads / kern_s,
-                             "peak_mads_per_s": TREE_MAD_RATE, "frac": mads / kern_s / TREE_MAD_RATE},
+                             "peak_mads_per_s": TREE_MAD_RATE, "frac": mads / kern_s / TREE_MAD_RATE,
+                             "spec_issue": {"peak_lane_instr_per_s": SPEC_VALU_LANE_INSTR,
+                                            "frac_mads_only": mads / kern_s / SPEC_VALU_LANE_INSTR,
+                                            "note": "v_mad_u64_u32 lane-instructions alone against the spec "
+                                                    "VALU issue rate (a lower bound on issue use: the other "
+                                                    "VALU instructions are not counted)"}},
            "hbm_algorithmic_GBps": (n * (32 * L + 32) + node_hashes * 9 * 32) / kern_s / 1e9}
     if world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle_py
 
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+        threads = cpu_lease()["threads"]
         oracle_py.set_threads(threads)
         m = 4096
         sample = labels.view(L, n, 4)[:, :m].permute(1, 0, 2).contiguous().cpu().numpy().view(np.uint8).tobytes()
@@ -257,7 +301,11 @@ def sdr_leg(args, fg, ctx, device, world):
                              "achieved_ops_per_s": ops / dt, "peak_ops_per_s": VALU_LANE_OPS,
                              "peak_source": "measured issue rates of the model's instructions "
                                             "(microbench/intrate.hip, profiles/r02_intrate_microbench.jsonl)",
-                             "frac": ops / dt / VALU_LANE_OPS},
+                             "frac": ops / dt / VALU_LANE_OPS,
+                             "spec_issue": {"peak_lane_instr_per_s": SPEC_VALU_LANE_INSTR,
+                                            "frac": ops / dt / SPEC_VALU_LANE_INSTR,
+                                            "note": "the model's lane-ops against the spec VALU issue rate "
+                                                    "(32 lanes/cycle/SIMD, 2.4 GHz)"}},
            "hbm_algorithmic_GBps": count * (14 * 32 + 4 + 8 + 56 + 32) / dt / 1e9,
            "traffic_source": "profiles/r02_sdr_summary.json (FETCH_SIZE 2,644 B per label raw vs 548 B "
                              "algorithmic: line-granular random 32-B parent gathers; WRITE_SIZE 32 B per label)"}
@@ -265,7 +313,7 @@ def sdr_leg(args, fg, ctx, device, world):
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle_py
 
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+        threads = cpu_lease()["threads"]
         oracle_py.set_threads(threads)
         m = 1 << 19
         par = np.random.default_rng(1).integers(0, 256, 32 * 14 * m, dtype=np.uint8).tobytes()
@@ -319,6 +367,90 @@ def config4_leg(args, fg, synth_mod, ctx):
     return out
 
 
+def config5_leg(args, fg, synth_mod, ctx, rank, world, gdev, dist, partitions=10):
+    """BASELINE config 5 on the driver's N-GPU run: a Window-PoSt batch of 10 partitions of 32 GiB-sector
+    size (2^27-domain synthetic circuit) proven round-robin over the ranks (10 over 8 GPUs: two rounds on
+    ranks 0 and 1; post.cpp:37-46, constants.hpp:88), the 10 x 192-byte multi-proof all-gathered over
+    RCCL.  Every rank builds its own circuit and key (independent partitions over one SRS); the makespan is
+    the max over ranks; rank 0 pairing-verifies every gathered proof.  Host memory per rank is bounded by
+    one synthetic circuit (freed after upload) plus the pinned witness; below that the leg falls back to
+    2^26 and says so."""
+    import gc
+
+    import numpy as np
+    import torch
+
+    from fil_groth16.compound import shard_partitions
+    from fil_groth16.distributed import prove_partitions
+
+    lr = args.config5_log_rows
+    need_gb = 30.0 * 2.0 ** (lr - 27)  # host CSR + witness of one synthetic circuit, plus the pinned copy
+    try:
+        avail_gb = int(next(l for l in open("/proc/meminfo") if l.startswith("MemAvailable")).split()[1]) / 1e6
+    except (OSError, StopIteration):
+        avail_gb = None
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    fallback = None
+    if avail_gb is not None and lr > 26 and avail_gb < local_world * need_gb:
+        fallback = f"MemAvailable {avail_gb:.0f} GB < {local_world} ranks x {need_gb:.0f} GB: 2^26"
+        lr = 26
+    t0 = time.perf_counter()
+    sc = synth_mod.SynthCircuit(lr, args.n_in, args.seed)
+    circ = sc.load(ctx)
+    pk = fg.generate_random_parameters(ctx, circ, splitmix_frs(TOXIC_SEED, 5))
+    z = fg.HostBuffer(32 * sc.num_vars)
+    np.copyto(z.array, sc.z_array())
+    n, n_in = sc.n, sc.n_in
+    del sc
+    gc.collect()
+    ctx.synchronize()
+    t_setup = time.perf_counter() - t0
+    mine = shard_partitions(partitions, rank, world)
+    blind = splitmix_frs(9000 + rank, 2 * (len(mine) * (args.config5_steps + 1) + 1))
+    fg.prove_batch(ctx, pk, circ, [z], [(blind[0], blind[1])])  # warm-up
+    ctx.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    multi = []
+    for k in range(args.config5_steps):
+        off = 2 + 2 * k * len(mine)
+        multi.append(prove_partitions(
+            lambda ids: fg.prove_batch(ctx, pk, circ, [z] * len(ids),
+                                       [(blind[off + 2 * i], blind[off + 2 * i + 1]) for i in range(len(ids))]),
+            partitions, rank, world, gdev))
+    ctx.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t1
+    mine_dt = dt
+    if dist:
+        tt = torch.tensor([dt], dtype=torch.float64, device=gdev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    counts = [len(shard_partitions(partitions, r, world)) for r in range(world)]
+    out = None
+    if rank == 0:
+        vk, ic = pk.verifying_key()
+        pub = z.array[32:32 * n_in].tobytes()
+        proofs = [m[192 * i:192 * (i + 1)] for m in multi for i in range(partitions)]
+        verified = bool(fg.verify_batch(vk, ic, [pub] * len(proofs), proofs))
+        makespan = dt / args.config5_steps
+        out = {"workload": f"BASELINE config 5: Window-PoSt batch of {partitions} partitions x synthetic "
+                           f"2^{lr}-domain R1CS ({n} constraints each, 32 GiB-sector partition size), round-robin "
+                           f"over {world} GPU(s), 10 x 192-byte multi-proof all-gathered",
+               "partitions": partitions, "n_gpus": world, "per_rank_partitions": counts,
+               "steps": args.config5_steps, "makespan_s": makespan, "proofs_per_s": partitions / makespan,
+               "constraints_per_s": partitions * n / makespan, "rank0_busy_s": mine_dt / args.config5_steps,
+               "verified": verified, "verified_proofs": len(proofs), "setup_s": t_setup,
+               "host_mem_available_gb": avail_gb, "fallback": fallback}
+    del pk, circ, z
+    gc.collect()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -332,13 +464,17 @@ def main():
     ap.add_argument("--params", default=None,
                     help="load the proving key from a bellman/filecoin params file (mmap) instead of generating it")
     ap.add_argument("--msm-reps", type=int, default=3, help="reps of the standalone 2^log-rows G1 MSM")
-    ap.add_argument("--cpu-log-rows", default="21,22", help="oracle sample sizes (comma-separated log2 rows)")
+    ap.add_argument("--cpu-log-rows", default="21,22,23,24",
+                    help="oracle sample sizes (comma-separated log2 rows; >= 3 for the fitted extrapolation)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-device-resident", action="store_true", help="skip the secondary HBM-resident run")
     ap.add_argument("--stats-json", default=None, help="write per-kernel timers here")
     ap.add_argument("--config4-log-rows", type=int, default=27,
                     help="secondary: BASELINE config 4 (2^N domain) after the main run on one GPU (0 skips)")
     ap.add_argument("--config4-steps", type=int, default=2)
+    ap.add_argument("--config5-log-rows", type=int, default=27,
+                    help="multi-GPU runs: the 10-partition config-5 leg at this domain (0 skips)")
+    ap.add_argument("--config5-steps", type=int, default=2)
     ap.add_argument("--tree-log-nodes", type=int, default=21,
                     help="secondary: tree C over 2^N columns x 11 layers (N a multiple of 3; 0 skips)")
     ap.add_argument("--sdr-log-labels", type=int, default=24,
@@ -523,6 +659,18 @@ def main():
         except Exception as e:  # reported, never fatal to the GPU measurement
             cpu = {"value": None, "unit": "constraints/s", "cores": None, "kind": "port", "sample": f"failed: {e}"}
 
+    config5 = None
+    if world > 1 and not P and args.config5_log_rows:
+        import gc
+
+        del pk, circ, zhost, sc
+        gc.collect()
+        ctx.synchronize()
+        try:
+            config5 = config5_leg(args, fg, synth_mod, ctx, rank, world, gdev, dist)
+        except Exception as e:  # reported, never fatal to the main measurement
+            config5 = {"error": str(e)}
+
     config4 = None
     if rank == 0 and world == 1 and args.config4_log_rows:
         import gc
@@ -626,6 +774,13 @@ def main():
             "unit": "Fq-mul/s",
             "frac": valu_ach / valu_peak if valu_ach else None,
             "madds_per_launch": madds_per_launch,
+            "spec_issue": {"peak_lane_instr_per_s": SPEC_VALU_LANE_INSTR,
+                           "instr_per_mixed_add": G1_MADD_VALU_INSTR if grp == "G1" else None,
+                           "frac": (madds_per_launch * G1_MADD_VALU_INSTR / (avg_ms * 1e-3) / SPEC_VALU_LANE_INSTR)
+                           if grp == "G1" and avg_ms > 0 and madds_per_launch else None,
+                           "note": "ISA VALU instructions per mixed add x mixed adds issued / launch time, against "
+                                   "the spec issue rate (MI355X_MICROARCH.md: 32 lanes/cycle/SIMD); the gap to "
+                                   "1 is v_mad_u64_u32's 4-cycle issue (measured, DESIGN.md §5) and DVFS"},
             "model": f"{FQ_MUL_PER_MIXED_ADD[grp]} Fq-mul per mixed add x mixed adds issued (non-zero signed digits "
                      f"counted by the library; split-mode MSMs: 2n half-scalar points over 6 windows); "
                      f"peak = v_mad_u64_u32 issue rate / {FQ_MUL_MADS} MADs",
@@ -634,6 +789,7 @@ def main():
         "tree_c": tree,
         "sdr_labels": sdr,
         "config4": config4,
+        "config5": config5,
         "timers_ms": {k: round(v["ms"], 3) for k, v in stats.items()},
         "setup_s": {"synth": t_synth, "circuit_load": t_load, "srs": t_srs},
         "device_gb_after_setup": round(dev_used_gb, 2),

@@ -2,8 +2,10 @@
 // wire formats, owns object lifetimes, serialises each context and turns C++ exceptions into
 // status codes + mi_last_error().  No CPU fallback exists: every compute entry point runs the
 // HIP kernels of this library or fails.
+#include <errno.h>
 #include <fcntl.h>
 #include <string.h>
+#include <sys/random.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -59,6 +61,10 @@ struct mi_circuit {
 struct mi_srs {
     mi::Srs *p;
     int device;
+};
+struct mi_srs_stream {
+    mi::SrsStream *p;
+    mi_ctx *ctx;
 };
 struct mi_points {
     void *dev;
@@ -194,6 +200,26 @@ mi::fr_t fr_checked(const uint8_t *b) {
     mi::fr_t x = mi::fr_from_le(b);
     need(!mi::geq_raw(x, mi::fr_t::modulus_raw()), "scalar is not canonical (>= r)");
     return x;
+}
+
+// bellman create_random_proof draws r, s = E::Fr::random(&mut OsRng): uniform canonical Fr.  Here: 255-bit
+// candidates from getrandom() with rejection (P(reject) = 1 - r / 2^255 ~ 0.09); out = count x (r | s).
+void random_blinding(uint64_t count, uint8_t *out) {
+    for (uint64_t k = 0; k < 2 * count; k++) {
+        uint8_t *dst = out + 32 * k;
+        for (;;) {
+            for (size_t o = 0; o < 32;) {
+                ssize_t got = getrandom(dst + o, 32 - o, 0);
+                if (got < 0) {
+                    if (errno == EINTR) continue;
+                    throw std::runtime_error("getrandom failed");
+                }
+                o += (size_t)got;
+            }
+            dst[31] &= 0x7f;
+            if (!mi::geq_raw(mi::fr_from_le(dst), mi::fr_t::modulus_raw())) break;
+        }
+    }
 }
 
 // upload z (host) to a device scratch buffer and reduce it mod r (building blocks: MSM scalars, NTT data)
@@ -449,6 +475,51 @@ int mi_srs_load(mi_ctx *ctx, const mi_circuit *circ, const mi_srs_host *h, int c
     });
 }
 
+int mi_srs_stream_begin(mi_ctx *ctx, const mi_circuit *circ, const uint8_t *vk, const uint8_t *ic, uint64_t n_ic,
+                        const uint64_t counts[5], int checked, mi_srs_stream **out) {
+    return guard([&] {
+        need(ctx && vk && (n_ic == 0 || ic) && counts && out, "null argument");
+        CtxLock l(ctx);
+        mi::SrsHost sh{};
+        sh.vk = vk;
+        sh.ic = ic;
+        sh.n_ic = n_ic;
+        sh.n_h = counts[0];
+        sh.n_l = counts[1];
+        sh.n_a = counts[2];
+        sh.n_b_g1 = counts[3];
+        sh.n_b_g2 = counts[4];
+        mi::SrsStream *st = mi::srs_stream_begin(ctx->c, circ ? circ->p : nullptr, sh, checked != 0);
+        *out = new mi_srs_stream{st, ctx};
+    });
+}
+int mi_srs_stream_part(mi_srs_stream *st, int which, uint64_t first, const void *bytes, uint64_t n_points,
+                       int on_device) {
+    return guard([&] {
+        need(st && st->p && (bytes || !n_points), "null argument");
+        CtxLock l(st->ctx);
+        mi::srs_stream_part(st->ctx->c, *st->p, which, first, (const uint8_t *)bytes, n_points, on_device != 0);
+    });
+}
+int mi_srs_stream_end(mi_srs_stream *st, mi_srs **out) {
+    if (!st) return guard([&] { need(false, "null argument"); });
+    mi_ctx *ctx = st->ctx;
+    mi::SrsStream *p = st->p;
+    delete st;  // consumed whatever happens
+    return guard([&] {
+        need(out && p, "null argument");
+        CtxLock l(ctx);
+        mi::Srs *S = mi::srs_stream_end(ctx->c, p);
+        *out = new mi_srs{S, ctx->c.device};
+    });
+}
+void mi_srs_stream_abort(mi_srs_stream *st) {
+    if (!st) return;
+    hipSetDevice(st->ctx->c.device);
+    mi::srs_stream_abort(st->p);
+    delete st;
+}
+
 int mi_srs_generate(mi_ctx *ctx, const mi_circuit *circ, const uint8_t toxic[160], mi_srs **out) {
     return guard([&] {
         need(ctx && circ && toxic && out, "null argument");
@@ -493,6 +564,33 @@ int mi_srs_msm_info(const mi_srs *srs, uint64_t out[2]) {
         const mi::Srs &s = *srs->p;
         out[0] = (s.h_hi || s.l_hi || s.a_hi) ? 1 : 0;
         out[1] = s.in_subgroup ? 1 : 0;
+    });
+}
+
+int mi_srs_export_query_dev(mi_ctx *ctx, const mi_srs *srs, int which, uint64_t first, uint64_t n, void *dev_out) {
+    return guard([&] {
+        need(ctx && srs && (dev_out || !n), "null argument");
+        CtxLock l(ctx);
+        const mi::Srs &s = *srs->p;
+        uint64_t total = 0;
+        switch (which) {
+            case 0: total = s.n_h; break;
+            case 1: total = s.n_l; break;
+            case 2: total = s.n_a; break;
+            case 3: case 4: total = s.n_b; break;
+            default: throw std::invalid_argument("which must be 0..4");
+        }
+        need(first <= total && n <= total - first, "range past the end of the query");
+        if (!n) return;
+        uint8_t *o = (uint8_t *)dev_out;
+        switch (which) {
+            case 0: mi::g1_encode_uncompressed(ctx->c, s.h_perm, o, n, s.log_d, first); break;
+            case 1: mi::g1_encode_uncompressed(ctx->c, s.l, o, n, 0, first); break;
+            case 2: mi::g1_encode_uncompressed(ctx->c, s.a, o, n, 0, first); break;
+            case 3: mi::g1_encode_uncompressed(ctx->c, s.b_g1, o, n, 0, first); break;
+            case 4: mi::g2_encode_uncompressed(ctx->c, s.b_g2 + first, o, n); break;
+        }
+        MI_HIP(hipStreamSynchronize(ctx->c.stream));
     });
 }
 
@@ -646,6 +744,34 @@ int mi_groth16_prove_batch(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *cir
         }
         join_assembler();
     });
+}
+
+int mi_groth16_prove_random(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circ, const uint8_t *z, int priority,
+                            uint8_t *proof) {
+    uint8_t rs[64];
+    int rc = guard([&] { random_blinding(1, rs); });
+    if (rc != MI_OK) return rc;
+    rc = mi_groth16_prove(ctx, srs, circ, z, rs, rs + 32, priority, proof, nullptr);
+    memset(rs, 0, sizeof rs);
+    return rc;
+}
+int mi_groth16_prove_dev_random(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circ, const void *z_dev,
+                                int priority, uint8_t *proof) {
+    uint8_t rs[64];
+    int rc = guard([&] { random_blinding(1, rs); });
+    if (rc != MI_OK) return rc;
+    rc = mi_groth16_prove_dev(ctx, srs, circ, z_dev, rs, rs + 32, priority, proof, nullptr);
+    memset(rs, 0, sizeof rs);
+    return rc;
+}
+int mi_groth16_prove_batch_random(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circ, uint64_t count,
+                                  const uint8_t *const *z, int priority, uint8_t *proofs_out) {
+    std::vector<uint8_t> rs(64 * (count ? count : 1));
+    int rc = guard([&] { random_blinding(count, rs.data()); });
+    if (rc != MI_OK) return rc;
+    rc = mi_groth16_prove_batch(ctx, srs, circ, count, z, rs.data(), priority, proofs_out);
+    memset(rs.data(), 0, rs.size());
+    return rc;
 }
 
 static void share_impl(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circ, const mi::fr_t *z_dev, uint32_t rank,

@@ -283,7 +283,8 @@ void g2_subgroup_check(Ctx &c, const g2_affine_t *pts, uint64_t n, int *bad_dev)
 // *bad_dev += entries >= r (witness validation: an Fr32 must represent a valid Fr, core/fr32.hpp:36-40)
 void fr_count_noncanonical(Ctx &c, const fr_t *d, uint64_t n, int *bad_dev, hipStream_t st);
 // device affine -> zcash uncompressed bytes (device buffer); perm_log != 0 un-bit-reverses the source
-void g1_encode_uncompressed(Ctx &c, const g1_affine_t *in, uint8_t *dev_out, uint64_t n, unsigned perm_log);
+void g1_encode_uncompressed(Ctx &c, const g1_affine_t *in, uint8_t *dev_out, uint64_t n, unsigned perm_log,
+                            uint64_t first = 0);
 void g2_encode_uncompressed(Ctx &c, const g2_affine_t *in, uint8_t *dev_out, uint64_t n);
 // canonical LE Fr bytes (already on device, 32B each) -> canonical, reduced mod r (in place)
 void fr_canonicalize(Ctx &c, fr_t *d, uint64_t n);

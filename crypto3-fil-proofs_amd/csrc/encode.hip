@@ -114,10 +114,11 @@ __device__ __forceinline__ void fq_to_be48_dev(const fq_t &a, uint8_t *out) {
 }
 // device affine -> zcash uncompressed; src index = perm_log ? bitrev(i) : i (h is stored bit-reversed)
 __global__ void k_g1_encode(const g1_affine_t *__restrict__ in, uint8_t *__restrict__ out, uint64_t n,
-                            unsigned perm_log) {
+                            unsigned perm_log, uint64_t first) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    uint64_t src = perm_log ? (__builtin_bitreverse64(i) >> (64 - perm_log)) : i;
+    // natural index first + i; with perm_log the source is stored bit-reversed (the h query)
+    uint64_t src = perm_log ? (__builtin_bitreverse64(first + i) >> (64 - perm_log)) : first + i;
     uint8_t *p = out + 96 * i;
     const g1_affine_t a = in[src];
     if (a.is_inf()) {
@@ -202,9 +203,10 @@ void fr_count_noncanonical(Ctx &c, const fr_t *d, uint64_t n, int *bad_dev, hipS
     k_fr_check<<<grid1(n), 256, 0, st>>>(d, n, bad_dev);
     MI_HIP(hipGetLastError());
 }
-void g1_encode_uncompressed(Ctx &c, const g1_affine_t *in, uint8_t *dev_out, uint64_t n, unsigned perm_log) {
+void g1_encode_uncompressed(Ctx &c, const g1_affine_t *in, uint8_t *dev_out, uint64_t n, unsigned perm_log,
+                            uint64_t first) {
     if (!n) return;
-    k_g1_encode<<<grid1(n), 256, 0, c.stream>>>(in, dev_out, n, perm_log);
+    k_g1_encode<<<grid1(n), 256, 0, c.stream>>>(in, dev_out, n, perm_log, first);
     MI_HIP(hipGetLastError());
 }
 void g2_encode_uncompressed(Ctx &c, const g2_affine_t *in, uint8_t *dev_out, uint64_t n) {

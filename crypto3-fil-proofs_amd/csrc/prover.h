@@ -64,6 +64,22 @@ struct SrsHost {
     uint64_t n_h, n_l, n_a, n_b_g1, n_b_g2;
 };
 Srs *srs_load(Ctx &c, const Circuit *circ, const SrsHost &h, bool checked);
+// Streaming form of srs_load (chunked broadcast receivers): begin takes vk, ic and the query sizes (the
+// query pointers of `h` are ignored), part decodes points [first, first + n) of query `which`
+// (0 h natural order, 1 l, 2 a, 3 b_g1, 4 b_g2) from host or device memory, end validates and returns the
+// key.  abort releases a stream that will not be ended (end and a throwing begin release it themselves).
+struct SrsStream {
+    Srs *S = nullptr;
+    bool checked = false;
+    g1_affine_t *hnat = nullptr;  // h in natural order until end permutes it
+    void *dst[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    uint64_t n[5] = {0, 0, 0, 0, 0}, filled[5] = {0, 0, 0, 0, 0};
+    int *bad = nullptr;  // 5 queries x {malformed, infinity, outside subgroup}
+};
+SrsStream *srs_stream_begin(Ctx &c, const Circuit *circ, const SrsHost &h, bool checked);
+void srs_stream_part(Ctx &c, SrsStream &st, int which, uint64_t first, const uint8_t *bytes, uint64_t n, bool on_device);
+Srs *srs_stream_end(Ctx &c, SrsStream *st);
+void srs_stream_abort(SrsStream *st);
 Srs *srs_generate(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5]);
 
 struct ProofPoints {

@@ -456,52 +456,22 @@ Circuit *circuit_load(Ctx &c, const R1csHost &cs) {
     return C;
 }
 
-// One proving-key query, streamed through a bounded staging buffer and decoded on the device with
-// bellman's Parameters::read rules: canonical coordinates, on the curve, the identity refused in every
-// query ("point at infinity"), and with checked = true also r P = O (from_uncompressed vs _unchecked).
-template <class A>
-static A *upload_points(Ctx &c, const uint8_t *bytes, uint64_t n, bool is_g2, bool checked, const char *name) {
-    if (!n) return nullptr;
-    const size_t esz = is_g2 ? 192 : 96;
-    A *out = dalloc<A>(n);
-    int *bad = c.scratch[9].as<int>(4);
-    MI_HIP(hipMemsetAsync(bad, 0, 3 * sizeof(int), c.stream));
-    const uint64_t chunk = 1ull << 22;
-    uint8_t *stage = c.scratch[0].as<uint8_t>(esz * (n < chunk ? n : chunk));
-    for (uint64_t o = 0; o < n; o += chunk) {
-        uint64_t m = n - o < chunk ? n - o : chunk;
-        MI_HIP(hipMemcpyAsync(stage, bytes + esz * o, esz * m, hipMemcpyHostToDevice, c.stream));
-        if (is_g2)
-            g2_decode_uncompressed(c, stage, (g2_affine_t *)out + o, m, bad, true);
-        else
-            g1_decode_uncompressed(c, stage, (g1_affine_t *)out + o, m, bad, true);
-    }
-    if (checked) {
-        if (is_g2)
-            g2_subgroup_check(c, (const g2_affine_t *)out, n, bad);
-        else
-            g1_subgroup_check(c, (const g1_affine_t *)out, n, bad);
-    }
-    int nbad[3] = {0, 0, 0};
-    MI_HIP(hipMemcpyAsync(nbad, bad, sizeof(nbad), hipMemcpyDeviceToHost, c.stream));
-    MI_HIP(hipStreamSynchronize(c.stream));
-    if (nbad[0] || nbad[1] || nbad[2]) {
-        hipFree(out);
-        std::string q = std::string("SRS ") + name + " query: ";
-        if (nbad[0]) throw std::invalid_argument(q + std::to_string(nbad[0]) + " malformed or off-curve point(s)");
-        if (nbad[1]) throw std::invalid_argument(q + std::to_string(nbad[1]) + " point(s) at infinity");
-        throw std::invalid_argument(q + std::to_string(nbad[2]) + " point(s) outside the prime-order subgroup");
-    }
-    return out;
-}
-
+// Proving-key upload as a stream of chunks (mi_srs_stream_*; srs_load is begin + whole queries + end).
+// Each chunk is decoded on the device with bellman's Parameters::read rules: canonical coordinates, on
+// the curve, the identity refused in every query ("point at infinity"), and with checked = true also
+// r P = O (from_uncompressed vs _unchecked) once the query is complete.  Chunks come from host memory
+// (staged through a bounded buffer) or from device memory (a received RCCL broadcast buffer: decoded in
+// place, no host copy).  Per query the chunks must arrive in order.
 namespace {
 void build_hi_tables(Ctx &c, Srs &S);
+const char *kQueryName[5] = {"h", "l", "a", "b_g1", "b_g2"};
 }
 
-Srs *srs_load(Ctx &c, const Circuit *circ, const SrsHost &h, bool checked) {
-    Srs *S = new Srs();
+SrsStream *srs_stream_begin(Ctx &c, const Circuit *circ, const SrsHost &h, bool checked) {
+    SrsStream *st = new SrsStream();
+    Srs *S = st->S = new Srs();
     try {
+        st->checked = checked;
         if (h.n_h < 1) throw std::invalid_argument("empty h query");
         uint64_t d = h.n_h + 1;
         if (d & (d - 1)) throw std::invalid_argument("|h| + 1 must be a power of two");
@@ -515,20 +485,11 @@ Srs *srs_load(Ctx &c, const Circuit *circ, const SrsHost &h, bool checked) {
                 throw std::invalid_argument("|b_g1| / |b_g2| != B-density of the circuit");
             if (h.n_ic != circ->n_in) throw std::invalid_argument("|ic| != number of inputs");
         }
+        if (h.n_b_g1 != h.n_b_g2) throw std::invalid_argument("|b_g1| != |b_g2|");
         S->n_h = h.n_h;
         S->n_l = h.n_l;
         S->n_a = h.n_a;
         S->n_b = h.n_b_g1;
-        if (h.n_b_g1 != h.n_b_g2) throw std::invalid_argument("|b_g1| != |b_g2|");
-        g1_affine_t *hnat = upload_points<g1_affine_t>(c, h.h, h.n_h, false, checked, "h");
-        S->h_perm = dalloc<g1_affine_t>(h.n_h);
-        k_permute_h<<<grid1(h.n_h), 256, 0, c.stream>>>(hnat, S->h_perm, S->log_d, h.n_h);
-        MI_HIP(hipStreamSynchronize(c.stream));
-        hipFree(hnat);
-        S->l = upload_points<g1_affine_t>(c, h.l, h.n_l, false, checked, "l");
-        S->a = upload_points<g1_affine_t>(c, h.a, h.n_a, false, checked, "a");
-        S->b_g1 = upload_points<g1_affine_t>(c, h.b_g1, h.n_b_g1, false, checked, "b_g1");
-        S->b_g2 = upload_points<g2_affine_t>(c, h.b_g2, h.n_b_g2, true, checked, "b_g2");
         // verifying key and ic on the host: curve equation always, subgroup when checked; ic points are
         // refused at infinity like the queries (bellman VerifyingKey::read)
         auto g1_ok = [&](const g1_affine_t &p) { return p.is_inf() || (g1_on_curve(p) && (!checked || in_prime_subgroup(p))); };
@@ -547,13 +508,109 @@ Srs *srs_load(Ctx &c, const Circuit *circ, const SrsHost &h, bool checked) {
             if (S->ic[i].is_inf()) throw std::invalid_argument("ic point at infinity");
             if (!g1_ok(S->ic[i])) throw std::invalid_argument("ic point not on the curve / outside the subgroup");
         }
-        S->in_subgroup = checked;
-        build_hi_tables(c, *S);
+        st->n[0] = S->n_h;
+        st->n[1] = S->n_l;
+        st->n[2] = S->n_a;
+        st->n[3] = S->n_b;
+        st->n[4] = S->n_b;
+        st->dst[0] = st->hnat = dalloc<g1_affine_t>(S->n_h);
+        st->dst[1] = S->l = S->n_l ? dalloc<g1_affine_t>(S->n_l) : nullptr;
+        st->dst[2] = S->a = S->n_a ? dalloc<g1_affine_t>(S->n_a) : nullptr;
+        st->dst[3] = S->b_g1 = S->n_b ? dalloc<g1_affine_t>(S->n_b) : nullptr;
+        st->dst[4] = S->b_g2 = S->n_b ? dalloc<g2_affine_t>(S->n_b) : nullptr;
+        st->bad = dalloc<int>(15);
+        MI_HIP(hipMemsetAsync(st->bad, 0, 15 * sizeof(int), c.stream));
     } catch (...) {
-        delete S;
+        srs_stream_abort(st);
         throw;
     }
+    return st;
+}
+
+void srs_stream_part(Ctx &c, SrsStream &st, int which, uint64_t first, const uint8_t *bytes, uint64_t n,
+                     bool on_device) {
+    if (which < 0 || which > 4) throw std::invalid_argument("which must be 0..4");
+    if (first != st.filled[which]) throw std::invalid_argument("SRS stream chunks must arrive in order per query");
+    if (n > st.n[which] - first) throw std::invalid_argument("SRS stream chunk runs past the end of the query");
+    if (!n) return;
+    const bool g2 = which == 4;
+    const size_t esz = g2 ? 192 : 96;
+    int *bad = st.bad + 3 * which;
+    const uint64_t chunk = 1ull << 22;
+    uint8_t *stage = on_device ? nullptr : c.scratch[0].as<uint8_t>(esz * (n < chunk ? n : chunk));
+    for (uint64_t o = 0; o < n; o += chunk) {
+        uint64_t m = n - o < chunk ? n - o : chunk;
+        const uint8_t *src = bytes + esz * o;
+        if (!on_device) {
+            MI_HIP(hipMemcpyAsync(stage, src, esz * m, hipMemcpyHostToDevice, c.stream));
+            src = stage;
+        }
+        if (g2)
+            g2_decode_uncompressed(c, src, (g2_affine_t *)st.dst[which] + first + o, m, bad, true);
+        else
+            g1_decode_uncompressed(c, src, (g1_affine_t *)st.dst[which] + first + o, m, bad, true);
+    }
+    // the staging buffer (and a caller's device chunk) may be reused as soon as this returns
+    MI_HIP(hipStreamSynchronize(c.stream));
+    st.filled[which] += n;
+}
+
+Srs *srs_stream_end(Ctx &c, SrsStream *st) {
+    Srs *S = st->S;
+    try {
+        for (int q = 0; q < 5; q++)
+            if (st->filled[q] != st->n[q])
+                throw std::invalid_argument(std::string("SRS ") + kQueryName[q] + " query incomplete: " +
+                                            std::to_string(st->filled[q]) + " of " + std::to_string(st->n[q]) +
+                                            " points received");
+        if (st->checked) {
+            for (int q = 0; q < 4; q++) g1_subgroup_check(c, (const g1_affine_t *)st->dst[q], st->n[q], st->bad + 3 * q);
+            g2_subgroup_check(c, (const g2_affine_t *)st->dst[4], st->n[4], st->bad + 12);
+        }
+        int nbad[15];
+        MI_HIP(hipMemcpyAsync(nbad, st->bad, sizeof(nbad), hipMemcpyDeviceToHost, c.stream));
+        MI_HIP(hipStreamSynchronize(c.stream));
+        for (int q = 0; q < 5; q++) {
+            const int *b = nbad + 3 * q;
+            std::string m = std::string("SRS ") + kQueryName[q] + " query: ";
+            if (b[0]) throw std::invalid_argument(m + std::to_string(b[0]) + " malformed or off-curve point(s)");
+            if (b[1]) throw std::invalid_argument(m + std::to_string(b[1]) + " point(s) at infinity");
+            if (b[2]) throw std::invalid_argument(m + std::to_string(b[2]) + " point(s) outside the prime-order subgroup");
+        }
+        S->h_perm = dalloc<g1_affine_t>(S->n_h);
+        k_permute_h<<<grid1(S->n_h), 256, 0, c.stream>>>(st->hnat, S->h_perm, S->log_d, S->n_h);
+        MI_HIP(hipStreamSynchronize(c.stream));
+        hipFree(st->hnat);
+        st->hnat = nullptr;
+        S->in_subgroup = st->checked;
+        build_hi_tables(c, *S);
+    } catch (...) {
+        srs_stream_abort(st);
+        throw;
+    }
+    st->S = nullptr;
+    srs_stream_abort(st);
     return S;
+}
+
+void srs_stream_abort(SrsStream *st) {
+    if (!st) return;
+    if (st->hnat) hipFree(st->hnat);
+    if (st->bad) hipFree(st->bad);
+    delete st->S;  // ~Srs frees the queries allocated so far
+    delete st;
+}
+
+Srs *srs_load(Ctx &c, const Circuit *circ, const SrsHost &h, bool checked) {
+    SrsStream *st = srs_stream_begin(c, circ, h, checked);
+    const uint8_t *q[5] = {h.h, h.l, h.a, h.b_g1, h.b_g2};
+    try {
+        for (int k = 0; k < 5; k++) srs_stream_part(c, *st, k, 0, q[k], st->n[k], false);
+    } catch (...) {
+        srs_stream_abort(st);
+        throw;
+    }
+    return srs_stream_end(c, st);
 }
 
 // ------------------------------------------------------------------------------ fixed-base helper

@@ -46,6 +46,12 @@ int main(int argc, char **argv) {
             fprintf(stderr, "post-seal verification sanity check failed\n");
             return 2;
         }
+        // the production form: blinding drawn inside the library (internal randomness)
+        mi355x::multi_proof mr = mi355x::circuit_proofs(ctx, pk, circ, assignments);
+        if (!mr.verify(inputs) || (parts > 1 && mr.circuit_proofs[0] == mr.circuit_proofs[1])) {
+            fprintf(stderr, "random-blinding proofs failed verification or repeated\n");
+            return 2;
+        }
         for (auto &p : mp.circuit_proofs) {
             for (uint8_t b : p) printf("%02x", b);
             printf("\n");

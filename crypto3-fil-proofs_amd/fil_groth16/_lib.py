@@ -29,6 +29,8 @@ EXPORTS = [
     "mi_tree_r_last_build", "mi_tree_r_last_build_dev",
     "mi_sdr_labels", "mi_sdr_labels_dev", "mi_sdr_labeling_proofs_dev", "mi_tree_inclusion_paths_dev",
     "mi_tree_d_build_dev", "mi_srs_msm_info", "mi_points_check_subgroup", "mi_points_info",
+    "mi_groth16_prove_random", "mi_groth16_prove_dev_random", "mi_groth16_prove_batch_random",
+    "mi_srs_stream_begin", "mi_srs_stream_part", "mi_srs_stream_end", "mi_srs_stream_abort", "mi_srs_export_query_dev",
 ]
 
 _lib = None
@@ -82,6 +84,14 @@ def lib():
         "mi_srs_info": ([vp, vp], c_int),
         "mi_srs_free": ([vp], None),
         "mi_srs_msm_info": ([vp, vp], c_int),
+        "mi_srs_stream_begin": ([vp, vp, u8p, u8p, u64, vp, c_int, pp], c_int),
+        "mi_srs_stream_part": ([vp, c_int, u64, vp, u64, c_int], c_int),
+        "mi_srs_stream_end": ([vp, pp], c_int),
+        "mi_srs_stream_abort": ([vp], None),
+        "mi_srs_export_query_dev": ([vp, vp, c_int, u64, u64, vp], c_int),
+        "mi_groth16_prove_random": ([vp, vp, vp, u8p, c_int, vp], c_int),
+        "mi_groth16_prove_dev_random": ([vp, vp, vp, vp, c_int, vp], c_int),
+        "mi_groth16_prove_batch_random": ([vp, vp, vp, u64, vp, c_int, vp], c_int),
         "mi_points_check_subgroup": ([vp, vp], c_int),
         "mi_points_info": ([vp, vp], c_int),
         "mi_groth16_prove": ([vp, vp, vp, u8p, u8p, u8p, c_int, vp, vp], c_int),

@@ -14,7 +14,7 @@
   generate_winning_post_proof     generate_winning_post (api/post.hpp:178-230): one partition
   shard_partitions                one process per GPU: partition k goes to rank k % world
 """
-from .core import PROOF_BYTES, prove, verify_batch
+from .core import PROOF_BYTES, prove_batch, verify_batch
 
 
 def partition_count(partitions: int) -> int:
@@ -65,19 +65,25 @@ class MultiProof:
         return cls([buf[i:i + PROOF_BYTES] for i in range(0, len(buf), PROOF_BYTES)], verifying_key)
 
 
-def circuit_proofs(ctx, pk, circuit, witnesses, blindings, priority=False):
-    """One proof per partition, in partition order (compound_proof.hpp:127-137)."""
+def circuit_proofs(ctx, pk, circuit, witnesses, blindings=None, priority=False):
+    """One proof per partition, in partition order (compound_proof.hpp:127-137), through the batch entry
+    the bench times (mi_groth16_prove_batch: partition k + 1's witness upload and proof k's host assembly
+    overlap proof k's GPU work).  blindings = None is the production call: r, s drawn inside the library
+    (crypto3 prove's internal randomness); explicit (r, s) pairs are the parity/test entry."""
     if not witnesses:
         raise ValueError("Cannot create a circuit proof over missing vanilla proofs")
-    if len(witnesses) != len(blindings):
+    if blindings is not None and len(witnesses) != len(blindings):
         raise ValueError("one (r, s) pair per partition is required")
-    return [prove(ctx, pk, circuit, z, r, s, priority=priority) for z, (r, s) in zip(witnesses, blindings)]
+    return prove_batch(ctx, pk, circuit, list(witnesses), blindings, priority=priority)
 
 
-def seal_commit_phase2_proofs(ctx, pk, circuit, witnesses, blindings, num_inputs, priority=False) -> bytes:
+def seal_commit_phase2_proofs(ctx, pk, circuit, witnesses, blindings=None, num_inputs=None,
+                              priority=False) -> bytes:
     """api/seal.hpp:296-313: prove every partition, pack the MultiProof buffer and refuse to return
     one that does not verify.  ``witnesses`` are full assignments (ONE first); the public inputs of
     partition k are its witness entries 1 .. num_inputs - 1."""
+    if num_inputs is None:
+        num_inputs = circuit.num_inputs
     proofs = circuit_proofs(ctx, pk, circuit, witnesses, blindings, priority=priority)
     mp = MultiProof(proofs, pk.verifying_key())
     inputs = [bytes(z[32:32 * num_inputs]) for z in witnesses]
@@ -98,7 +104,7 @@ def _post_partitions(num_sectors: int, sector_count: int) -> int:
     return partition_count(-1 if p is None else p)
 
 
-def generate_window_post_proofs(ctx, pk, circuit, num_sectors: int, sector_count: int, witnesses, blindings,
+def generate_window_post_proofs(ctx, pk, circuit, num_sectors: int, sector_count: int, witnesses, blindings=None,
                                 priority: bool = True) -> bytes:
     """api/post.hpp:305-348: the Window-PoSt SNARK.  ``witnesses`` holds one synthesised assignment per
     partition (circuit synthesis is upstream of the boundary); their number must equal the partition
@@ -112,10 +118,11 @@ def generate_window_post_proofs(ctx, pk, circuit, num_sectors: int, sector_count
     return MultiProof(circuit_proofs(ctx, pk, circuit, witnesses, blindings, priority=priority)).to_bytes()
 
 
-def generate_winning_post_proof(ctx, pk, circuit, num_replicas: int, sector_count: int, witness, blinding,
+def generate_winning_post_proof(ctx, pk, circuit, num_replicas: int, sector_count: int, witness, blinding=None,
                                 priority: bool = False) -> bytes:
     """api/post.hpp:178-230: the Winning-PoSt SNARK -- exactly ``sector_count`` replicas ("invalid amount
     of replicas"), partitions unset (one partition), one 192-byte proof."""
     if num_replicas != sector_count:
         raise ValueError("invalid amount of replicas")
-    return MultiProof(circuit_proofs(ctx, pk, circuit, [witness], [blinding], priority=priority)).to_bytes()
+    return MultiProof(circuit_proofs(ctx, pk, circuit, [witness], None if blinding is None else [blinding],
+                                     priority=priority)).to_bytes()

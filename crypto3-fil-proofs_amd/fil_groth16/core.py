@@ -206,6 +206,34 @@ class _SrsHost(ctypes.Structure):
                 ("n_b_g1", ctypes.c_uint64), ("b_g2", ctypes.c_void_p), ("n_b_g2", ctypes.c_uint64)]
 
 
+class SrsStream:
+    """A proving key arriving in chunks (ProvingKey.stream_begin)."""
+
+    def __init__(self, ctx, handle):
+        self.ctx, self.h = ctx, handle
+
+    def part(self, which: int, first: int, data, n: int, on_device=False):
+        if on_device:
+            ptr, keep = ctypes.c_void_p(int(data)), None
+        else:
+            buf = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray)
+                                       else data)
+            ptr, keep = ctypes.c_void_p(buf.ctypes.data), buf
+        check(lib().mi_srs_stream_part(self.h, which, first, ptr, n, int(on_device)))
+        del keep
+
+    def end(self):
+        h, self.h = self.h, None
+        hd = ctypes.c_void_p()
+        check(lib().mi_srs_stream_end(h, ctypes.byref(hd)))
+        return ProvingKey(self.ctx, hd)
+
+    def abort(self):
+        if self.h is not None:
+            lib().mi_srs_stream_abort(self.h)
+            self.h = None
+
+
 class ProvingKey:
     """Device-resident Groth16 proving key (bellman layout)."""
 
@@ -252,6 +280,21 @@ class ProvingKey:
     def write_vk(self, path: str):
         """bellman VerifyingKey::write (write_cached_verifying_key, core/parameter_cache.hpp:136-144)."""
         check(lib().mi_vk_write(self.h, os.fsencode(path)))
+
+    @classmethod
+    def stream_begin(cls, ctx: Context, circuit, vk: bytes, ic: bytes, counts, checked=False):
+        """Streaming key load (mi_srs_stream_*): counts = |h|, |l|, |a|, |b_g1|, |b_g2|; feed every query in
+        order with .part(which, first, data, n, on_device) and finish with .end() -> ProvingKey."""
+        hd = ctypes.c_void_p()
+        arr = (ctypes.c_uint64 * 5)(*counts)
+        check(lib().mi_srs_stream_begin(ctx.h, circuit.h if circuit is not None else None, bytes(vk), bytes(ic),
+                                        len(ic) // 96, arr, int(checked), ctypes.byref(hd)))
+        return SrsStream(ctx, hd)
+
+    def export_query_dev(self, which: int, first: int, n: int, dev_ptr: int):
+        """points [first, first + n) of one query (0 h natural order, 1 l, 2 a, 3 b_g1, 4 b_g2) in the wire
+        format, written to device memory"""
+        check(lib().mi_srs_export_query_dev(self.ctx.h, self.h, which, first, n, ctypes.c_void_p(dev_ptr)))
 
     def msm_info(self):
         """{"split_tables": 2^128 tables of h, l, a resident, "subgroup": every point subgroup-known}.
@@ -336,9 +379,23 @@ def generate_random_parameters(ctx: Context, circuit: Circuit, toxic) -> Proving
     return ProvingKey(ctx, hd)
 
 
-def prove(ctx: Context, pk: ProvingKey, circuit: Circuit, z, r: int, s: int, priority=False, want_raw=False):
-    """One Groth16 proof. z: bytes (num_vars x 32 LE) or a device pointer (int) to the same layout."""
+def prove(ctx: Context, pk: ProvingKey, circuit: Circuit, z, r: int = None, s: int = None, priority=False,
+          want_raw=False):
+    """One Groth16 proof. z: bytes (num_vars x 32 LE) or a device pointer (int) to the same layout.
+    r = s = None: the production entry, blinding drawn inside the library from getrandom() (crypto3 prove /
+    bellman create_random_proof); explicit r, s are the parity/test entry."""
     proof = ctypes.create_string_buffer(PROOF_BYTES)
+    if r is None and s is None:
+        if want_raw:
+            raise ValueError("want_raw needs injected r, s")
+        if isinstance(z, int):
+            check(lib().mi_groth16_prove_dev_random(ctx.h, pk.h, circuit.h, ctypes.c_void_p(z), int(priority), proof))
+        else:
+            assert len(z) == 32 * circuit.num_vars, "witness length must be (num_inputs + num_aux) * 32"
+            check(lib().mi_groth16_prove_random(ctx.h, pk.h, circuit.h, bytes(z), int(priority), proof))
+        return proof.raw
+    if r is None or s is None:
+        raise ValueError("give both r and s, or neither")
     raw = ctypes.create_string_buffer(384) if want_raw else None
     if isinstance(z, int):
         check(lib().mi_groth16_prove_dev(ctx.h, pk.h, circuit.h, ctypes.c_void_p(z), fr_bytes(r), fr_bytes(s),
@@ -350,22 +407,33 @@ def prove(ctx: Context, pk: ProvingKey, circuit: Circuit, z, r: int, s: int, pri
     return (proof.raw, raw.raw) if want_raw else proof.raw
 
 
-class HostBuffer:
-    """Page-locked host memory from mi_host_alloc: a witness written here goes to the GPU at full DMA
-    rate (and prove_batch overlaps the next partition's copy with the current proof)."""
+class _PinnedAlloc:
+    """Owner of one mi_host_alloc block; freed when the last view of it is gone."""
 
     def __init__(self, nbytes: int):
         p = ctypes.c_void_p()
         check(lib().mi_host_alloc(nbytes, ctypes.byref(p)))
-        self.ptr, self.nbytes = p.value, nbytes
-        self.array = np.frombuffer((ctypes.c_uint8 * nbytes).from_address(self.ptr), dtype=np.uint8)
+        self.ptr = p.value
 
     def __del__(self):
         try:
-            self.array = None
             lib().mi_host_free(ctypes.c_void_p(self.ptr))
         except Exception:
             pass
+
+
+class HostBuffer:
+    """Page-locked host memory from mi_host_alloc: a witness written here goes to the GPU at full DMA
+    rate (and prove_batch overlaps the next partition's copy with the current proof).  ``array`` owns the
+    allocation through its base (a ctypes array holding the _PinnedAlloc), so a view that outlives the
+    HostBuffer object keeps the pages alive instead of dangling."""
+
+    def __init__(self, nbytes: int):
+        owner = _PinnedAlloc(nbytes)
+        self.ptr, self.nbytes = owner.ptr, nbytes
+        cbuf = (ctypes.c_uint8 * nbytes).from_address(self.ptr)
+        cbuf._owner = owner  # the numpy view -> cbuf -> owner chain keeps the allocation alive
+        self.array = np.frombuffer(cbuf, dtype=np.uint8)
 
 
 def _host_ptr(z, nbytes):
@@ -382,16 +450,21 @@ def _host_ptr(z, nbytes):
     return arr.ctypes.data, arr
 
 
-def prove_batch(ctx: Context, pk: ProvingKey, circuit: Circuit, zs, rs, priority=False):
+def prove_batch(ctx: Context, pk: ProvingKey, circuit: Circuit, zs, rs=None, priority=False):
     """count independent partition proofs -> list of 192-byte proofs.  Witnesses stay in host memory
     (HostBuffer, numpy arrays or bytes; never copied here): the library uploads partition k + 1 while
-    it proves partition k."""
+    it proves partition k.  rs = None: blinding drawn inside the library (mi_groth16_prove_batch_random)."""
     count = len(zs)
     nbytes = 32 * circuit.num_vars
     keep = [_host_ptr(z, nbytes) for z in zs]
     arr = (ctypes.c_void_p * count)(*[p for p, _ in keep])
-    rsb = b"".join(fr_bytes(r) + fr_bytes(s) for r, s in rs)
     out = ctypes.create_string_buffer(PROOF_BYTES * count)
+    if rs is None:
+        check(lib().mi_groth16_prove_batch_random(ctx.h, pk.h, circuit.h, count, arr, int(priority), out))
+        return [out.raw[i * PROOF_BYTES:(i + 1) * PROOF_BYTES] for i in range(count)]
+    if len(rs) != count:
+        raise ValueError("one (r, s) pair per partition is required")
+    rsb = b"".join(fr_bytes(r) + fr_bytes(s) for r, s in rs)
     check(lib().mi_groth16_prove_batch(ctx.h, pk.h, circuit.h, count, arr, rsb, int(priority), out))
     return [out.raw[i * PROOF_BYTES:(i + 1) * PROOF_BYTES] for i in range(count)]
 

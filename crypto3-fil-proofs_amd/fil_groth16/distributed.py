@@ -82,50 +82,122 @@ def prove_split(ctx, pk, circuit, z, r, s, rank: int, world: int, device="cpu", 
 
 
 SRS_PARTS = ("vk", "ic", "h", "l", "a", "b_g1", "b_g2")
+_POINT_BYTES = {"vk": 1, "ic": 96, "h": 96, "l": 96, "a": 96, "b_g1": 96, "b_g2": 192}
+
+
+def _broadcast_chunks(sizes, rank, src, device, chunk_bytes, source, sink):
+    """Broadcast every part of ``sizes`` (name -> bytes) from ``src`` in chunks of whole points of at most
+    ``chunk_bytes``: ``source(name, offset, nbytes) -> uint8 tensor on device`` on the source rank,
+    ``sink(name, offset, tensor)`` on the others.  Only one chunk is in flight per rank."""
+    import torch
+    import torch.distributed as dist
+
+    for k, n in sizes:
+        esz = _POINT_BYTES[k]
+        step = max(esz, chunk_bytes // esz * esz)
+        for off in range(0, n, step):
+            m = min(step, n - off)
+            t = source(k, off, m) if rank == src else torch.empty(m, dtype=torch.uint8, device=device)
+            dist.broadcast(t, src)
+            if rank != src:
+                sink(k, off, t)
+
+
+def _broadcast_sizes(sizes, rank, src, device):
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor(sizes if rank == src else [0] * len(SRS_PARTS), dtype=torch.int64).to(device)
+    dist.broadcast(t, src)
+    return [int(x) for x in t.cpu().tolist()]
 
 
 def broadcast_srs_parts(parts, rank: int, world: int, src: int = 0, device="cpu", chunk_bytes: int = 1 << 30):
     """Broadcast a proving key in the bellman wire layout (dict of SRS_PARTS -> bytes, held by ``src``) to
-    every rank: one size vector, then each part in chunks of at most ``chunk_bytes`` (large transfers over
-    xGMI with backend "nccl" on device tensors, bounded staging memory).  The reference loads the same
-    params file in every process (get_groth_params, core/parameter_cache.hpp:185-200); here one rank reads
-    the file and the others receive it.  Returns the dict on every rank."""
-    import torch
-    import torch.distributed as dist
-
+    every rank: one size vector, then each part in chunks of whole points (bounded staging memory).  The
+    source returns its own dict untouched; a receiver assembles each part in ONE preallocated bytearray
+    (no second copy).  For a device-resident key use broadcast_proving_key, which streams the chunks
+    device to device and never materialises the key in host memory."""
     if world == 1:
         return dict(parts)
-    sizes = torch.zeros(len(SRS_PARTS), dtype=torch.int64)
+    sizes = _broadcast_sizes([len(parts[k]) for k in SRS_PARTS] if rank == src else None, rank, src, device)
     if rank == src:
-        sizes = torch.tensor([len(parts[k]) for k in SRS_PARTS], dtype=torch.int64)
-    sizes = sizes.to(device)
-    dist.broadcast(sizes, src)
-    out = {}
-    for k, n in zip(SRS_PARTS, sizes.cpu().tolist()):
-        host = np.empty(n, dtype=np.uint8)
-        src_view = np.frombuffer(parts[k], dtype=np.uint8) if rank == src else None
-        for off in range(0, n, chunk_bytes):
-            m = min(chunk_bytes, n - off)
-            t = (torch.from_numpy(src_view[off:off + m].copy()) if rank == src
-                 else torch.empty(m, dtype=torch.uint8)).to(device)
-            dist.broadcast(t, src)
-            host[off:off + m] = t.cpu().numpy()
-        out[k] = host.tobytes()
+        import torch
+
+        views = {k: memoryview(parts[k]) for k in SRS_PARTS}
+        source = (lambda k, off, m: torch.frombuffer(bytearray(views[k][off:off + m]), dtype=torch.uint8)
+                  .to(device))
+        _broadcast_chunks(list(zip(SRS_PARTS, sizes)), rank, src, device, chunk_bytes, source, None)
+        return parts
+    out = {k: bytearray(n) for k, n in zip(SRS_PARTS, sizes)}
+
+    def sink(k, off, t):
+        out[k][off:off + t.numel()] = memoryview(t.cpu().numpy())
+
+    _broadcast_chunks(list(zip(SRS_PARTS, sizes)), rank, src, device, chunk_bytes, None, sink)
     return out
 
 
 def broadcast_proving_key(ctx, pk, circuit, rank: int, world: int, src: int = 0, device="cpu", checked=False,
                           chunk_bytes: int = 1 << 30):
-    """Rank ``src`` holds ``pk`` (e.g. ProvingKey.load_params from a v28 file); every other rank receives
-    the key over the process group and uploads it to its own GPU.  Returns this rank's ProvingKey."""
+    """Rank ``src`` holds ``pk`` (e.g. ProvingKey.load_params from a v28 file); every other rank receives the
+    key over the process group and loads it into its own GPU through the streaming loader
+    (mi_srs_stream_*), chunk by chunk with the same rules as mi_srs_load (``checked``: subgroup checks).
+    The reference reads the params file in every process (get_groth_params,
+    core/parameter_cache.hpp:185-200); here one rank reads it and the others receive it.
+
+    With backend "nccl" (``device`` a CUDA device) the source encodes each chunk on its GPU
+    (mi_srs_export_query_dev), RCCL moves it over xGMI, and the receiver decodes it in place from device
+    memory: no rank holds the key in host memory.  With gloo the chunks travel through host tensors, one
+    chunk at a time.  Memory per rank beyond the key itself: one chunk.  Returns this rank's ProvingKey."""
+    import torch
+
     from .core import ProvingKey
 
-    parts = None
+    if world == 1:
+        return pk
+    on_gpu = torch.device(device).type == "cuda"
+    sizes = None
     if rank == src:
         vk, ic = pk.verifying_key()
-        parts = dict(vk=vk, ic=ic, h=pk.query(0), l=pk.query(1), a=pk.query(2), b_g1=pk.query(3),
-                     b_g2=pk.query(4))
-    parts = broadcast_srs_parts(parts, rank, world, src, device, chunk_bytes)
+        sizes = [len(vk), len(ic), 96 * pk.n_h, 96 * pk.n_l, 96 * pk.n_a, 96 * pk.n_b, 192 * pk.n_b]
+    sizes = _broadcast_sizes(sizes, rank, src, device)
+    small = {"vk": None, "ic": None}
     if rank == src:
+        small = {"vk": vk, "ic": ic}
+        source_small = lambda k, off, m: torch.frombuffer(bytearray(small[k][off:off + m]), dtype=torch.uint8).to(device)
+    else:
+        small = {"vk": bytearray(sizes[0]), "ic": bytearray(sizes[1])}
+        source_small = None
+
+    def sink_small(k, off, t):
+        small[k][off:off + t.numel()] = memoryview(t.cpu().numpy())
+
+    _broadcast_chunks([("vk", sizes[0]), ("ic", sizes[1])], rank, src, device, chunk_bytes, source_small, sink_small)
+    queries = list(zip(SRS_PARTS[2:], sizes[2:]))
+    which = {k: i for i, k in enumerate(SRS_PARTS[2:])}
+    gpu = torch.device("cuda", ctx.device) if hasattr(ctx, "device") else torch.device("cuda")
+    if rank == src:
+        def source(k, off, m):
+            t = torch.empty(m, dtype=torch.uint8, device=gpu)
+            pk.export_query_dev(which[k], off // _POINT_BYTES[k], m // _POINT_BYTES[k], t.data_ptr())
+            return t if on_gpu else t.cpu()
+
+        _broadcast_chunks(queries, rank, src, device, chunk_bytes, source, None)
         return pk
-    return ProvingKey.load(ctx, circuit, *(parts[k] for k in SRS_PARTS), checked=checked)
+    counts = [n // _POINT_BYTES[k] for k, n in queries]
+    stream = ProvingKey.stream_begin(ctx, circuit, bytes(small["vk"]), bytes(small["ic"]), counts, checked)
+
+    def sink(k, off, t):
+        if t.is_cuda:
+            torch.cuda.current_stream(t.device).synchronize()  # the broadcast landed before the decode reads it
+            stream.part(which[k], off // _POINT_BYTES[k], t.data_ptr(), t.numel() // _POINT_BYTES[k], on_device=True)
+        else:
+            stream.part(which[k], off // _POINT_BYTES[k], t.numpy(), t.numel() // _POINT_BYTES[k], on_device=False)
+
+    try:
+        _broadcast_chunks(queries, rank, src, device, chunk_bytes, None, sink)
+    except BaseException:
+        stream.abort()
+        raise
+    return stream.end()

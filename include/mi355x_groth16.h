@@ -119,12 +119,27 @@ void mi_circuit_free(mi_circuit *c);
  * additionally verifies r * P == O for every point (prime-order subgroup).  Failures: MI_ERR_ARG. */
 int mi_srs_load(mi_ctx *ctx, const mi_circuit *circuit_or_null, const mi_srs_host *host, int checked,
                 mi_srs **out);
+/* Streaming key load (a key broadcast over RCCL arrives in chunks; no rank holds it whole in host memory):
+ * begin with vk, ic and counts = |h|, |l|, |a|, |b_g1|, |b_g2|; then every query in order as chunks of
+ * wire-format points [first, first + n_points) (query `which` 0 h natural order, 1 l, 2 a, 3 b_g1, 4 b_g2),
+ * read from host memory or, with on_device != 0, from device memory on this context's GPU (a received
+ * broadcast buffer, decoded in place); the chunk may be reused when the call returns.  end applies the
+ * same rules as mi_srs_load and consumes the stream (also on failure); abort discards one. */
+typedef struct mi_srs_stream mi_srs_stream;
+int mi_srs_stream_begin(mi_ctx *ctx, const mi_circuit *circuit_or_null, const uint8_t *vk, const uint8_t *ic,
+                        uint64_t n_ic, const uint64_t counts[5], int checked, mi_srs_stream **out);
+int mi_srs_stream_part(mi_srs_stream *st, int which, uint64_t first, const void *bytes, uint64_t n_points,
+                       int on_device);
+int mi_srs_stream_end(mi_srs_stream *st, mi_srs **out);
+void mi_srs_stream_abort(mi_srs_stream *st);
 /* toxic waste tau, alpha, beta, gamma, delta: 5 x 32 B LE canonical; generators = standard G1/G2 */
 int mi_srs_generate(mi_ctx *ctx, const mi_circuit *circuit, const uint8_t toxic[160], mi_srs **out);
 /* vk (MI_VK_BYTES) and ic (num_inputs x 96 B) of a loaded / generated key */
 int mi_srs_export_vk(const mi_srs *srs, uint8_t *vk_out, uint8_t *ic_out);
 /* download one query in the wire format: which = 0 h (natural order), 1 l, 2 a, 3 b_g1, 4 b_g2 */
 int mi_srs_export_query(mi_ctx *ctx, const mi_srs *srs, int which, uint8_t *out, uint64_t cap_points);
+/* points [first, first + n) of one query in the wire format, written to device memory (the broadcast source) */
+int mi_srs_export_query_dev(mi_ctx *ctx, const mi_srs *srs, int which, uint64_t first, uint64_t n, void *dev_out);
 /* sizes: d, |h|, |l|, |a|, |b|, |ic| */
 int mi_srs_info(const mi_srs *srs, uint64_t out[6]);
 /* G1 MSM mode of a key: out[0] = 1 when the 2^128 split tables of h, l, a are resident (built at load
@@ -192,6 +207,16 @@ int mi_groth16_prove_dev(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circu
 int mi_groth16_prove_batch(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circuit, uint64_t count,
                            const uint8_t *const *z, const uint8_t *rs /* count x 64 B: r | s */, int priority,
                            uint8_t *proofs_out);
+/* Production entries with internal randomness (crypto3 prove / bellman create_random_proof: r, s drawn by
+ * the prover, never supplied by the caller): r, s uniform in [0, r) from getrandom(), wiped after use.
+ * These are what compound_proof::circuit_proofs binds; the injected-(r, s) entries
+ * above are the parity/test entries (they accept r = s = 0, which drops zero-knowledge). */
+int mi_groth16_prove_random(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circuit, const uint8_t *z,
+                            int priority, uint8_t proof_out[MI_PROOF_BYTES]);
+int mi_groth16_prove_dev_random(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circuit, const void *z_dev,
+                                int priority, uint8_t proof_out[MI_PROOF_BYTES]);
+int mi_groth16_prove_batch_random(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circuit, uint64_t count,
+                                  const uint8_t *const *z, int priority, uint8_t *proofs_out);
 /* Single-proof latency mode (one proof split over `world` GPUs).  Rank `rank` runs the
  * witness map and NTT chain in full and the MSMs over its contiguous slice of each query (h in the
  * bit-reversed coefficient order the device keeps it in; l, a, b_g1/b_g2 in key order), writing the five partial sums, zcash-uncompressed, to share_out.  The callers exchange

@@ -15,6 +15,7 @@
 // Errors are thrown as mi355x::error, like the reference's BOOST_ASSERT_MSG / throw style
 // (compound_proof.hpp:94).
 #pragma once
+#include <algorithm>
 #include <array>
 #include <cstdint>
 #include <stdexcept>
@@ -127,6 +128,16 @@ inline proof_bytes prove(context &ctx, const proving_key &pk, const circuit &c, 
     return out;
 }
 
+// The production call: r, s drawn inside the library from getrandom() (crypto3 prove / bellman
+// create_random_proof); the overload above with injected r, s is the parity/test entry.
+inline proof_bytes prove(context &ctx, const proving_key &pk, const circuit &c, const std::vector<fr32> &z,
+                         bool priority = false) {
+    if (z.size() != c.num_variables()) throw error(MI_ERR_ARG, "assignment length != number of variables");
+    proof_bytes out;
+    check(mi_groth16_prove_random(ctx.get(), pk.get(), c.get(), z.front().data(), priority ? 1 : 0, out.data()));
+    return out;
+}
+
 // bellman verify_proof on the host; inputs = public inputs without ONE (generate_public_inputs order)
 inline bool verify(const std::vector<uint8_t> &vk, const std::vector<uint8_t> &ic, const std::vector<fr32> &inputs,
                    const proof_bytes &proof) {
@@ -169,20 +180,56 @@ struct multi_proof {
     }
 };
 
-// compound_proof::circuit_proofs: one Groth16 proof per partition, in partition order.
-inline multi_proof circuit_proofs(context &ctx, const proving_key &pk, const circuit &c,
-                                  const std::vector<std::vector<fr32>> &partition_assignments,
-                                  const std::vector<std::pair<fr32, fr32>> &blindings, bool priority = false) {
+namespace detail {
+inline multi_proof circuit_proofs_impl(context &ctx, const proving_key &pk, const circuit &c,
+                                       const std::vector<std::vector<fr32>> &partition_assignments,
+                                       const std::vector<std::pair<fr32, fr32>> *blindings, bool priority) {
     if (partition_assignments.empty())
         throw error(MI_ERR_ARG, "Cannot create a circuit proof over missing vanilla proofs");
-    if (blindings.size() != partition_assignments.size()) throw error(MI_ERR_ARG, "one (r, s) per partition");
+    if (blindings && blindings->size() != partition_assignments.size())
+        throw error(MI_ERR_ARG, "one (r, s) per partition");
+    std::vector<const uint8_t *> zs;
+    for (auto &z : partition_assignments) {
+        if (z.size() != c.num_variables()) throw error(MI_ERR_ARG, "assignment length != number of variables");
+        zs.push_back(z.front().data());
+    }
+    std::vector<uint8_t> out(MI_PROOF_BYTES * zs.size());
+    if (blindings) {
+        std::vector<uint8_t> rs;
+        for (auto &b : *blindings) {
+            rs.insert(rs.end(), b.first.begin(), b.first.end());
+            rs.insert(rs.end(), b.second.begin(), b.second.end());
+        }
+        check(mi_groth16_prove_batch(ctx.get(), pk.get(), c.get(), zs.size(), zs.data(), rs.data(), priority ? 1 : 0,
+                                     out.data()));
+    } else {
+        check(mi_groth16_prove_batch_random(ctx.get(), pk.get(), c.get(), zs.size(), zs.data(), priority ? 1 : 0,
+                                            out.data()));
+    }
     multi_proof mp;
-    for (size_t k = 0; k < partition_assignments.size(); k++)
-        mp.circuit_proofs.push_back(
-            prove(ctx, pk, c, partition_assignments[k], blindings[k].first, blindings[k].second, priority));
+    for (size_t k = 0; k < zs.size(); k++) {
+        proof_bytes p;
+        std::copy(out.begin() + MI_PROOF_BYTES * k, out.begin() + MI_PROOF_BYTES * (k + 1), p.begin());
+        mp.circuit_proofs.push_back(p);
+    }
     mp.verifying_key = pk.verifying_key();
     mp.ic = pk.ic();
     return mp;
+}
+}  // namespace detail
+
+// compound_proof::circuit_proofs (compound_proof.hpp:127-137): one Groth16 proof per partition, in partition
+// order, through mi_groth16_prove_batch (partition k + 1's witness upload and proof k's host assembly overlap
+// proof k's GPU work).  Production form: r, s drawn inside the library for every partition.
+inline multi_proof circuit_proofs(context &ctx, const proving_key &pk, const circuit &c,
+                                  const std::vector<std::vector<fr32>> &partition_assignments, bool priority = false) {
+    return detail::circuit_proofs_impl(ctx, pk, c, partition_assignments, nullptr, priority);
+}
+// parity/test form with injected (r, s) per partition
+inline multi_proof circuit_proofs(context &ctx, const proving_key &pk, const circuit &c,
+                                  const std::vector<std::vector<fr32>> &partition_assignments,
+                                  const std::vector<std::pair<fr32, fr32>> &blindings, bool priority = false) {
+    return detail::circuit_proofs_impl(ctx, pk, c, partition_assignments, &blindings, priority);
 }
 
 // ---- stacked-PoRep Poseidon trees ----------------------------------------------

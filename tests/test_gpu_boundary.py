@@ -154,3 +154,49 @@ def test_msm_bases_flag_rules(ctx, oracle):
     assert ctx.msm_g1(INF_G1 + b[96:], sc) == oracle.msm_g1(INF_G1 + b[96:], sc)
     with pytest.raises(fg.FilGpuError):
         ctx.msm_g1(bytes([b[0] | 0x80]) + b[1:], sc)
+
+
+def test_srs_stream_load_chunks_host_and_device(ctx, oracle):
+    """mi_srs_stream_*: the key arrives in chunks (the receiving side of broadcast_proving_key), from host
+    memory and from device memory, and proves the oracle's bytes; a chunk out of order, a missing tail and a
+    non-subgroup point under checked are refused.  Source chunks come from mi_srs_export_query_dev."""
+    import torch
+
+    n_in, n_aux, rows, z, mats, ex = _export(oracle)
+    gc = fg.Circuit(ctx, len(rows), n_in, n_aux, mats)
+    pk0 = fg.generate_random_parameters(ctx, gc, circuits.toxic())
+    counts = [pk0.n_h, pk0.n_l, pk0.n_a, pk0.n_b, pk0.n_b]
+    vk, ic = pk0.verifying_key()
+    r, s = circuits.blinding()
+    want = oracle.OracleParams(oracle.OracleCircuit(len(rows), n_in, n_aux, mats), circuits.toxic()).prove(
+        circuits.z_bytes(z), r, s)[0]
+    for on_device in (False, True):
+        st = fg.ProvingKey.stream_begin(ctx, gc, vk, ic, counts, checked=True)
+        for q in range(5):
+            esz = 192 if q == 4 else 96
+            for first in range(0, counts[q], 7):
+                m = min(7, counts[q] - first)
+                t = torch.empty(esz * m, dtype=torch.uint8, device="cuda")
+                pk0.export_query_dev(q, first, m, t.data_ptr())
+                assert t.cpu().numpy().tobytes() == pk0.query(q)[esz * first:esz * (first + m)]
+                if on_device:
+                    st.part(q, first, t.data_ptr(), m, on_device=True)
+                else:
+                    st.part(q, first, t.cpu().numpy(), m)
+        pk = st.end()
+        assert fg.prove(ctx, pk, gc, circuits.z_bytes(z), r, s) == want
+    st = fg.ProvingKey.stream_begin(ctx, gc, vk, ic, counts)
+    with pytest.raises(fg.FilGpuError, match="order"):
+        st.part(0, 1, ex["h"][96:192], 1)
+    st.part(0, 0, ex["h"][:96], 1)
+    with pytest.raises(fg.FilGpuError, match="incomplete"):
+        st.end()
+    _, bad = badpoints.g1_non_subgroup()
+    st = fg.ProvingKey.stream_begin(ctx, gc, vk, ic, counts, checked=True)
+    for q, name in enumerate(("h", "l", "a", "b_g1", "b_g2")):
+        data = bytearray(pk0.query(q))
+        if name == "l":
+            data[:96] = bad
+        st.part(q, 0, bytes(data), counts[q])
+    with pytest.raises(fg.FilGpuError, match="subgroup"):
+        st.end()

@@ -383,3 +383,29 @@ def test_srs_broadcast_two_processes(oracle, tmp_path):
     n_in, n_aux, rws, z = circuits.random_circuit(85, 2000, n_in=4, n_free=16)
     op = oracle.OracleParams(oracle.OracleCircuit(len(rws), n_in, n_aux, circuits.to_csr(rws)), circuits.toxic())
     assert outs[0] == outs[1] == op.prove(circuits.z_bytes(z), 31, 32)[0]
+
+
+def test_production_random_blinding_entries(ctx, oracle):
+    """crypto3 prove / bellman create_random_proof: r, s drawn inside the library (getrandom).  The proofs
+    verify, differ between calls on the same witness, and the batch-routed compound.circuit_proofs with
+    injected (r, s) still equals the oracle proof for proof."""
+    n_in, n_aux, rows, z = circuits.random_circuit(65, 300, n_in=4)
+    oc, gc = _load(ctx, oracle, n_in, n_aux, rows, z)
+    tox = circuits.toxic()
+    pk = fg.generate_random_parameters(ctx, gc, tox)
+    op = oracle.OracleParams(oc, tox)
+    zb = circuits.z_bytes(z)
+    vk, ic = pk.verifying_key()
+    p1, p2 = fg.prove(ctx, pk, gc, zb), fg.prove(ctx, pk, gc, zb)
+    assert p1 != p2
+    assert fg.verify(vk, ic, zb[32:32 * n_in], p1) and fg.verify(vk, ic, zb[32:32 * n_in], p2)
+    import torch
+
+    zd = torch.from_numpy(np.frombuffer(zb, dtype=np.uint8).copy()).cuda()
+    assert fg.verify(vk, ic, zb[32:32 * n_in], fg.prove(ctx, pk, gc, zd.data_ptr()))
+    rand = fg.circuit_proofs(ctx, pk, gc, [zb] * 3)
+    assert len(set(rand)) == 3 and all(fg.verify(vk, ic, zb[32:32 * n_in], p) for p in rand)
+    blind = [(7 + k, 9 + k) for k in range(3)]
+    assert fg.circuit_proofs(ctx, pk, gc, [zb] * 3, blind) == [op.prove(zb, r, s)[0] for r, s in blind]
+    buf = fg.seal_commit_phase2_proofs(ctx, pk, gc, [zb] * 2)
+    assert all(fg.verify(vk, ic, zb[32:32 * n_in], buf[192 * k:192 * k + 192]) for k in range(2))
