@@ -438,9 +438,10 @@ def config5_leg(args, fg, synth_mod, ctx, rank, world, gdev, dist, partitions=10
         proofs = [m[192 * i:192 * (i + 1)] for m in multi for i in range(partitions)]
         verified = bool(fg.verify_batch(vk, ic, [pub] * len(proofs), proofs))
         makespan = dt / args.config5_steps
+        size = "32 GiB-sector partition size" if lr >= 27 else "REDUCED size, not the config-5 shape"
         out = {"workload": f"BASELINE config 5: Window-PoSt batch of {partitions} partitions x synthetic "
-                           f"2^{lr}-domain R1CS ({n} constraints each, 32 GiB-sector partition size), round-robin "
-                           f"over {world} GPU(s), 10 x 192-byte multi-proof all-gathered",
+                           f"2^{lr}-domain R1CS ({n} constraints each, {size}), round-robin "
+                           f"over {world} GPU(s), {partitions} x 192-byte multi-proof all-gathered",
                "partitions": partitions, "n_gpus": world, "per_rank_partitions": counts,
                "steps": args.config5_steps, "makespan_s": makespan, "proofs_per_s": partitions / makespan,
                "constraints_per_s": partitions * n / makespan, "rank0_busy_s": mine_dt / args.config5_steps,
