@@ -17,6 +17,7 @@
 #include "poseidon_math.h"
 #include "prover.h"
 #include "sdr.h"
+#include "stacked.h"
 
 // Witness uploads (host z -> HBM) run on their own stream into one of two device slots, so the copy
 // of partition k + 1 overlaps the proof of partition k (mi_groth16_prove_batch).  Pinned witnesses
@@ -62,6 +63,9 @@ struct mi_srs {
     mi::Srs *p;
     int device;
 };
+struct mi_stacked {
+    mi::stacked::Built *b;
+};
 struct mi_srs_stream {
     mi::SrsStream *p;
     mi_ctx *ctx;
@@ -105,6 +109,9 @@ int guard(Fn &&f) {
     }
 }
 
+void need(bool cond, const std::string &msg) {
+    if (!cond) throw std::invalid_argument(msg);
+}
 void need(bool cond, const char *msg) {
     if (!cond) throw std::invalid_argument(msg);
 }
@@ -1021,7 +1028,114 @@ int mi_ntt_fr(mi_ctx *ctx, uint8_t *data32, unsigned log_n, int inverse, int cos
 }
 
 // ------------------------------------------------------------------------------------------
-int mi_ctx_get_stats(mi_ctx *ctx, double out[30]) {
+// ------------------------------------------------------------------------------------------ stacked circuit
+int mi_stacked_build(const mi_stacked_shape *sh, int with_r1cs, mi_stacked **out) {
+    return guard([&] {
+        need(sh && out, "null argument");
+        mi::stacked::Shape s;
+        s.layers = sh->layers;
+        s.challenges = sh->challenges;
+        s.nodes = sh->nodes;
+        s.base = sh->base_arity;
+        s.sub = sh->sub_arity;
+        s.top = sh->top_arity;
+        *out = new mi_stacked{mi::stacked::build(s, with_r1cs != 0)};
+    });
+}
+int mi_stacked_info(const mi_stacked *s, uint64_t out[12]) {
+    return guard([&] {
+        need(s && out, "null argument");
+        const mi::stacked::Built &b = *s->b;
+        uint64_t v[12] = {b.n_constraints, b.n_in, b.n_aux, b.lay.slots, b.lay.stride, b.lay.depth_d, b.lay.path_c,
+                          b.ops.size(), b.level_off.empty() ? 0 : b.level_off.size() - 1, b.blocks.size(),
+                          b.poseidon_ops.size(), b.col[0].size() + b.col[1].size() + b.col[2].size()};
+        memcpy(out, v, sizeof v);
+    });
+}
+int mi_stacked_r1cs(const mi_stacked *s, mi_r1cs *out) {
+    return guard([&] {
+        need(s && out, "null argument");
+        const mi::stacked::Built &b = *s->b;
+        need(b.rp[0].size() == b.n_constraints + 1, "circuit was built without its R1CS (with_r1cs = 0)");
+        out->num_constraints = b.n_constraints;
+        out->num_inputs = b.n_in;
+        out->num_aux = b.n_aux;
+        for (int m = 0; m < 3; m++) {
+            out->row_ptr[m] = b.rp[m].data();
+            out->col[m] = b.col[m].data();
+            out->coeff[m] = (const uint8_t *)b.coeff[m].data();
+        }
+    });
+}
+static void stacked_check_slots(const mi::stacked::Built &b, const uint8_t *slots) {
+    const mi::stacked::Layout &L = b.lay;
+    for (uint64_t q = 0; q < L.slots; q++)
+        need(!mi::geq_raw(mi::fr_from_le(slots + 32 * q), mi::fr_t::modulus_raw()),
+             "instance slot " + std::to_string(q) + " is not a canonical Fr element");
+    for (unsigned c = 0; c < b.shape.challenges; c++) {
+        std::vector<uint64_t> idx{L.ch_base(c)};
+        for (unsigned p = 0; p < 14; p++) idx.push_back(L.ch_base(c) + L.off_parent(p, b.shape.layers));
+        for (uint64_t q : idx) {
+            uint64_t v;
+            memcpy(&v, slots + 32 * q, 8);
+            bool high = false;
+            for (int k = 8; k < 32; k++) high |= slots[32 * q + k] != 0;
+            need(!high && v < b.shape.nodes, "challenge / parent index in slot " + std::to_string(q) +
+                                                 " is not a node index (< nodes)");
+        }
+    }
+}
+int mi_stacked_public_inputs(const mi_stacked *s, const uint8_t *slots, uint8_t *out) {
+    return guard([&] {
+        need(s && slots && out, "null argument");
+        stacked_check_slots(*s->b, slots);
+        std::vector<mi::fr_t> in;
+        mi::stacked::public_inputs(*s->b, slots, in);
+        for (size_t i = 0; i < in.size(); i++) memcpy(out + 32 * i, in[i].v, 32);
+    });
+}
+int mi_stacked_witness_dev(mi_ctx *ctx, mi_stacked *s, const void *slots_dev, void *z_dev) {
+    return guard([&] {
+        need(ctx && s && slots_dev && z_dev, "null argument");
+        CtxLock l(ctx);
+        std::vector<uint8_t> host(32 * s->b->lay.slots);
+        MI_HIP(hipMemcpyAsync(host.data(), slots_dev, host.size(), hipMemcpyDeviceToHost, ctx->c.stream));
+        MI_HIP(hipStreamSynchronize(ctx->c.stream));
+        stacked_check_slots(*s->b, host.data());
+        mi::stacked::witness_dev(ctx->c, *s->b, (const uint8_t *)slots_dev, (mi::fr_t *)z_dev);
+    });
+}
+int mi_stacked_witness(mi_ctx *ctx, mi_stacked *s, const uint8_t *slots, uint8_t *z_out) {
+    return guard([&] {
+        need(ctx && s && slots && z_out, "null argument");
+        CtxLock l(ctx);
+        const mi::stacked::Built &b = *s->b;
+        stacked_check_slots(b, slots);
+        const uint64_t nv = b.n_in + b.n_aux;
+        mi::fr_t *z = ctx->c.scratch[2].as<mi::fr_t>(nv);
+        uint8_t *sd = ctx->c.scratch[3].as<uint8_t>(32 * b.lay.slots);
+        MI_HIP(hipMemcpyAsync(sd, slots, 32 * b.lay.slots, hipMemcpyHostToDevice, ctx->c.stream));
+        mi::stacked::witness_dev(ctx->c, *s->b, sd, z);
+        MI_HIP(hipMemcpyAsync(z_out, z, 32 * nv, hipMemcpyDeviceToHost, ctx->c.stream));
+        MI_HIP(hipStreamSynchronize(ctx->c.stream));
+    });
+}
+void mi_stacked_free(mi_stacked *s) {
+    if (!s) return;
+    delete s->b;
+    delete s;
+}
+int mi_circuit_check_dev(mi_ctx *ctx, const mi_circuit *circ, const void *z_dev, uint64_t out[2]) {
+    return guard([&] {
+        need(ctx && circ && z_dev && out, "null argument");
+        CtxLock l(ctx);
+        uint64_t first = ~0ull;
+        out[0] = mi::circuit_check(ctx->c, *circ->p, (const mi::fr_t *)z_dev, &first);
+        out[1] = first;
+    });
+}
+
+int mi_ctx_get_stats(mi_ctx *ctx, double out[39]) {
     return guard([&] {
         need(ctx && out, "null argument");
         CtxLock l(ctx);
@@ -1030,7 +1144,8 @@ int mi_ctx_get_stats(mi_ctx *ctx, double out[30]) {
         ctx->c.timer.resolve();
         const mi::Stats &s = ctx->c.stats;
         const mi::KStat *ks[mi::Stats::NK] = {&s.accum_g1, &s.accum_g2, &s.msm_g1, &s.msm_g2, &s.sort,
-                                              &s.ntt,      &s.prove,    &s.h2d,    &s.poseidon, &s.tree_h2d};
+                                              &s.ntt,      &s.prove,    &s.h2d,    &s.poseidon, &s.tree_h2d,
+                                              &s.wit_a,    &s.wit_sha,  &s.wit_pos};
         for (int i = 0; i < mi::Stats::NK; i++) {
             out[3 * i] = ks[i]->ms;
             out[3 * i + 1] = (double)ks[i]->launches;

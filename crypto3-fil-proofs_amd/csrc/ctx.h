@@ -86,14 +86,18 @@ struct Stats {
     KStat h2d;                 // witness upload + canonical check on the copy stream (units = bytes)
     KStat poseidon;            // k_poseidon launches (units = hashes)
     KStat tree_h2d;            // tree builders' label / data uploads (units = bytes)
+    KStat wit_a;               // stacked witness phase A (levelled light ops + native hashes; units = ops)
+    KStat wit_sha;             // stacked witness phase B, SHA-256 gadget blocks (units = blocks)
+    KStat wit_pos;             // stacked witness phase B, Poseidon gadgets (units = hashes)
     uint64_t madds_g1 = 0, madds_g2 = 0;  // mixed additions issued by k_accum_level0 (non-zero digits)
-    static constexpr int NK = 10;
+    static constexpr int NK = 13;
     void merge(const Stats &o) {
         madds_g1 += o.madds_g1;
         madds_g2 += o.madds_g2;
-        KStat *d[] = {&accum_g1, &accum_g2, &msm_g1, &msm_g2, &sort, &ntt, &prove, &h2d, &poseidon, &tree_h2d};
+        KStat *d[] = {&accum_g1, &accum_g2, &msm_g1, &msm_g2, &sort, &ntt, &prove, &h2d, &poseidon, &tree_h2d,
+                      &wit_a, &wit_sha, &wit_pos};
         const KStat *x[] = {&o.accum_g1, &o.accum_g2, &o.msm_g1, &o.msm_g2, &o.sort, &o.ntt, &o.prove, &o.h2d,
-                            &o.poseidon, &o.tree_h2d};
+                            &o.poseidon, &o.tree_h2d, &o.wit_a, &o.wit_sha, &o.wit_pos};
         for (int i = 0; i < NK; i++) {
             d[i]->ms += x[i]->ms;
             d[i]->launches += x[i]->launches;

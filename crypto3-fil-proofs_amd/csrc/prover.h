@@ -55,6 +55,8 @@ struct R1csHost {
 };
 
 Circuit *circuit_load(Ctx &c, const R1csHost &cs);
+// rows j < n with (A z)_j (B z)_j != (C z)_j (z canonical, device); *first_bad = the first such row or ~0
+uint64_t circuit_check(Ctx &c, const Circuit &C, const fr_t *z_dev, uint64_t *first_bad);
 
 struct SrsHost {
     const uint8_t *vk;  // 864 bytes

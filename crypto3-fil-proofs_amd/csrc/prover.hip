@@ -56,6 +56,25 @@ __global__ void k_eval_rows(const uint64_t *__restrict__ rp0, const uint32_t *__
     c[j] = vc;
 }
 
+// R1CS satisfaction: rows j with (A z)_j (B z)_j != (C z)_j counted, the first one kept
+__global__ void k_check_rows(const uint64_t *__restrict__ rp0, const uint32_t *__restrict__ c0,
+                             const fr_t *__restrict__ k0, const uint64_t *__restrict__ rp1,
+                             const uint32_t *__restrict__ c1, const fr_t *__restrict__ k1,
+                             const uint64_t *__restrict__ rp2, const uint32_t *__restrict__ c2,
+                             const fr_t *__restrict__ k2, const fr_t *__restrict__ zm, uint64_t n,
+                             unsigned long long *__restrict__ out) {
+    uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    fr_t va = fr_t::zero(), vb = fr_t::zero(), vc = fr_t::zero();
+    for (uint64_t e = rp0[j]; e < rp0[j + 1]; e++) va = va + k0[e] * zm[c0[e]];
+    for (uint64_t e = rp1[j]; e < rp1[j + 1]; e++) vb = vb + k1[e] * zm[c1[e]];
+    for (uint64_t e = rp2[j]; e < rp2[j + 1]; e++) vc = vc + k2[e] * zm[c2[e]];
+    if (!(va * vb == vc)) {
+        atomicAdd(&out[0], 1ull);
+        atomicMin(&out[1], (unsigned long long)j);
+    }
+}
+
 __global__ void k_qap_divide(fr_t *__restrict__ a, const fr_t *__restrict__ b, const fr_t *__restrict__ c,
                              uint64_t d, fr_t zinv) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -611,6 +630,24 @@ Srs *srs_load(Ctx &c, const Circuit *circ, const SrsHost &h, bool checked) {
         throw;
     }
     return srs_stream_end(c, st);
+}
+
+uint64_t circuit_check(Ctx &c, const Circuit &C, const fr_t *z_dev, uint64_t *first_bad) {
+    const uint64_t nv = C.n_in + C.n_aux;
+    fr_t *zm = c.scratch[1].as<fr_t>(nv ? nv : 1);
+    unsigned long long *out = c.scratch[9].as<unsigned long long>(2);
+    const unsigned long long init[2] = {0ull, ~0ull};
+    MI_HIP(hipMemcpyAsync(out, init, sizeof init, hipMemcpyHostToDevice, c.stream));
+    k_copy_to_mont<<<grid1(nv), 256, 0, c.stream>>>(z_dev, zm, nv);
+    if (C.n)
+        k_check_rows<<<grid1(C.n), 256, 0, c.stream>>>(C.row_ptr[0], C.col[0], C.coeff[0], C.row_ptr[1], C.col[1],
+                                                      C.coeff[1], C.row_ptr[2], C.col[2], C.coeff[2], zm, C.n, out);
+    MI_HIP(hipGetLastError());
+    unsigned long long h[2];
+    MI_HIP(hipMemcpyAsync(h, out, sizeof h, hipMemcpyDeviceToHost, c.stream));
+    MI_HIP(hipStreamSynchronize(c.stream));
+    if (first_bad) *first_bad = h[1];
+    return h[0];
 }
 
 // ------------------------------------------------------------------------------ fixed-base helper

@@ -12,4 +12,5 @@ from .compound import (MultiProof, partition_count, get_partitions_for_window_po
                        circuit_proofs, seal_commit_phase2_proofs, generate_window_post_proofs,
                        generate_winning_post_proof)
 from . import tree  # noqa: F401  (Poseidon + tree C / tree R-last builders)
+from . import stacked  # noqa: F401  (stacked-PoRep circuit: R1CS + GPU witness)
 from . import sdr  # noqa: F401  (SDR labelling witness: SHA-256 labels of challenged nodes)

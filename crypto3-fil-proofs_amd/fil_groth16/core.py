@@ -77,7 +77,8 @@ class Context:
         return s.value or 0
 
     # ---- device timers (HIP events inside the library; always on) ----
-    STAT_KEYS = ["accum_g1", "accum_g2", "msm_g1", "msm_g2", "sort", "ntt", "prove", "h2d", "poseidon", "tree_h2d"]
+    STAT_KEYS = ["accum_g1", "accum_g2", "msm_g1", "msm_g2", "sort", "ntt", "prove", "h2d", "poseidon", "tree_h2d",
+                 "wit_a", "wit_sha", "wit_pos"]
 
     def reset_stats(self):
         check(lib().mi_ctx_reset_stats(self.h))

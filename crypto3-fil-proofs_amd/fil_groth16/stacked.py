@@ -1,0 +1,288 @@
+"""Stacked-PoRep circuit: R1CS shape and GPU witness generation.
+
+Mirrors the synthesis half of the reference's compound proof for stacked PoRep:
+  StackedCircuit                  StackedCompound::circuit + StackedCircuit::synthesize
+                                  (libs/storage/include/nil/filecoin/storage/proofs/porep/stacked/circuit/
+                                  proof.hpp:98-165; Proof::synthesize, params.hpp:93-238)
+  StackedCircuit.public_inputs    generate_public_inputs (circuit/proof.hpp:186-269)
+  instance_slots                  the circuit Proof built from a vanilla proof (params.hpp:69-90): the openings
+                                  the gadgets consume, in the library's slot layout
+The R1CS is built on the host once per shape (mi_stacked_build; the blank circuit), the witness of every
+partition on the GPU (mi_stacked_witness*).  There is no CPU witness path.
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import check, lib
+from .core import FR_MODULUS, Circuit, _R1CS
+
+
+class _Shape(ctypes.Structure):
+    _fields_ = [("layers", ctypes.c_uint32), ("challenges", ctypes.c_uint32), ("nodes", ctypes.c_uint64),
+                ("base_arity", ctypes.c_uint32), ("sub_arity", ctypes.c_uint32), ("top_arity", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+
+INFO_KEYS = ("constraints", "inputs", "aux", "slots", "stride", "depth_d", "path_c", "ops", "levels", "sha_blocks",
+             "poseidon_hashes", "r1cs_entries")
+
+
+def tree_arities(nodes, base, sub=0, top=0):
+    """tree C / tree R-last level arities, leaf upward (rust-fil-proofs base / sub / top trees)"""
+    per = nodes // ((sub or 1) * (top or 1))
+    out = []
+    while per > 1:
+        out.append(base)
+        per //= base
+    return out + [a for a in (sub, top) if a]
+
+
+class StackedCircuit:
+    """One partition's circuit of a shape: layers (2 or 11), challenges, nodes, tree C / R-last arities."""
+
+    def __init__(self, layers=2, challenges=1, nodes=8, base=8, sub=0, top=0, with_r1cs=True):
+        sh = _Shape(layers, challenges, nodes, base, sub, top, 0)
+        self.h = ctypes.c_void_p()
+        check(lib().mi_stacked_build(ctypes.byref(sh), int(with_r1cs), ctypes.byref(self.h)))
+        out = (ctypes.c_uint64 * len(INFO_KEYS))()
+        check(lib().mi_stacked_info(self.h, out))
+        self.info = dict(zip(INFO_KEYS, list(out)))
+        self.layers, self.challenges, self.nodes = layers, challenges, nodes
+        self.arities = tree_arities(nodes, base, sub, top)
+        self.with_r1cs = with_r1cs
+
+    @property
+    def num_constraints(self):
+        return self.info["constraints"]
+
+    @property
+    def num_inputs(self):
+        return self.info["inputs"]
+
+    @property
+    def num_aux(self):
+        return self.info["aux"]
+
+    @property
+    def num_vars(self):
+        return self.num_inputs + self.num_aux
+
+    def csr(self):
+        """numpy views (valid while this object lives): 3 x (row_ptr u64, col u32, coeff u8[nnz * 32])"""
+        s = _R1CS()
+        check(lib().mi_stacked_r1cs(self.h, ctypes.byref(s)))
+        n = s.num_constraints
+        mats = []
+        for m in range(3):
+            rp = np.ctypeslib.as_array((ctypes.c_uint64 * (n + 1)).from_address(s.row_ptr[m]))
+            nnz = int(rp[-1])
+            col = (np.ctypeslib.as_array((ctypes.c_uint32 * nnz).from_address(s.col[m])) if nnz
+                   else np.zeros(0, np.uint32))
+            co = (np.ctypeslib.as_array((ctypes.c_uint8 * (32 * nnz)).from_address(s.coeff[m])) if nnz
+                  else np.zeros(0, np.uint8))
+            mats.append((rp, col, co))
+        return mats
+
+    def load(self, ctx) -> Circuit:
+        return Circuit(ctx, self.num_constraints, self.num_inputs, self.num_aux, self.csr())
+
+    def public_inputs(self, slots: bytes) -> bytes:
+        out = ctypes.create_string_buffer(32 * (self.num_inputs - 1))
+        check(lib().mi_stacked_public_inputs(self.h, bytes(slots), out))
+        return out.raw
+
+    def witness(self, ctx, slots: bytes) -> bytes:
+        """z = ONE ++ inputs ++ aux (32 B each), computed on the GPU, returned to the host"""
+        out = ctypes.create_string_buffer(32 * self.num_vars)
+        check(lib().mi_stacked_witness(ctx.h, self.h, bytes(slots), out))
+        return out.raw
+
+    def witness_dev(self, ctx, slots_dev_ptr: int, z_dev_ptr: int):
+        check(lib().mi_stacked_witness_dev(ctx.h, self.h, ctypes.c_void_p(slots_dev_ptr), ctypes.c_void_p(z_dev_ptr)))
+
+    def __del__(self):
+        try:
+            lib().mi_stacked_free(self.h)
+        except Exception:
+            pass
+
+
+def circuit_check_dev(ctx, circuit: Circuit, z_dev_ptr: int):
+    """(unsatisfied rows, first unsatisfied row or None) of A z * B z = C z on the device"""
+    out = (ctypes.c_uint64 * 2)()
+    check(lib().mi_circuit_check_dev(ctx.h, circuit.h, ctypes.c_void_p(z_dev_ptr), out))
+    return int(out[0]), (None if out[1] == 2 ** 64 - 1 else int(out[1]))
+
+
+def _fr(x):
+    x = int(x)
+    if not 0 <= x < FR_MODULUS:
+        raise ValueError("not a canonical Fr element")
+    return x.to_bytes(32, "little")
+
+
+def instance_slots(circuit: StackedCircuit, replica_id, comm_d, comm_r, comm_r_last, comm_c, challenges) -> bytes:
+    """Pack one partition's vanilla openings into the library's slot layout (mi355x_groth16.h).  challenges: one
+    dict per challenge with index, data_leaf, d_siblings (tree D, leaf upward), r_siblings / c_siblings (per
+    level the arity - 1 sibling values in position order), and drg / exp: 6 / 8 tuples (index, column,
+    siblings)."""
+    L = circuit.layers
+    out = [_fr(replica_id), _fr(comm_d), _fr(comm_r), _fr(comm_r_last), _fr(comm_c)]
+
+    def sibs(levels):
+        if [len(s) + 1 for s in levels] != circuit.arities:
+            raise ValueError("sibling levels do not match the tree shape")
+        return [_fr(v) for lvl in levels for v in lvl]
+
+    if len(challenges) != circuit.challenges:
+        raise ValueError(f"{circuit.challenges} challenge(s) per partition, got {len(challenges)}")
+    for ch in challenges:
+        out.append(_fr(ch["index"]))
+        out.append(_fr(ch["data_leaf"]))
+        if len(ch["d_siblings"]) != circuit.info["depth_d"]:
+            raise ValueError("tree D path length")
+        out += [_fr(v) for v in ch["d_siblings"]]
+        out += sibs(ch["r_siblings"])
+        out += sibs(ch["c_siblings"])
+        if len(ch["drg"]) != 6 or len(ch["exp"]) != 8:
+            raise ValueError("6 DRG and 8 expander parents per challenge")
+        for idx, column, s in list(ch["drg"]) + list(ch["exp"]):
+            if len(column) != L:
+                raise ValueError("column length != layers")
+            out.append(_fr(idx))
+            out += [_fr(v) for v in column]
+            out += sibs(s)
+    buf = b"".join(out)
+    assert len(buf) == 32 * circuit.info["slots"]
+    return buf
+
+
+# ---------------------------------------------------------------------------------------------- synthetic
+def _sha_node(a: int, b: int) -> int:
+    """tree D node hash: sha256(left LE || right LE), byte 31 &= 0x3f (compute_comm_d, pinned by the
+    reference's vectors in tests/test_cpu_sdr.py)"""
+    import hashlib
+
+    d = bytearray(hashlib.sha256(a.to_bytes(32, "little") + b.to_bytes(32, "little")).digest())
+    d[31] &= 0x3F
+    return int.from_bytes(d, "little")
+
+
+def _sparse_tree(leaves: dict, arities, hash_groups, rand):
+    """Root and openings of a tree over `leaves` (position -> value) whose other nodes are random filler:
+    the paths of all given leaves share one root, as in a real replica's tree.  hash_groups(arity, flat
+    child values) -> parent values."""
+    levels = [dict(leaves)]
+    for a in arities:
+        cur = levels[-1]
+        parents = sorted({p // a for p in cur})
+        flat = []
+        for p in parents:
+            for k in range(a):
+                if p * a + k not in cur:
+                    cur[p * a + k] = rand()
+                flat.append(cur[p * a + k])
+        levels.append(dict(zip(parents, hash_groups(a, flat))))
+    if list(levels[-1]) != [0]:
+        raise ValueError("tree shape does not reduce to one root")
+
+    def path(idx):
+        out, j = [], idx
+        for lvl, a in enumerate(arities):
+            g = j // a
+            out.append([levels[lvl][g * a + k] for k in range(a) if k != j % a])
+            j = g
+        return out
+
+    return levels[-1][0], path
+
+
+def synthetic_instance(ctx, circuit: StackedCircuit, seed: int = 1):
+    """A consistent instance of the circuit's shape without a sector (the bench's 32 GiB-shaped partition and
+    the GPU tests): random replica id, data leaves and parent columns (6 DRG + 8 expander parents at random
+    indices, none of them challenged); each challenged node's labels computed by create_label over its
+    parents' columns on the GPU label kernel (sdr.create_labels: replica_id | layer | node | 37 parents);
+    tree D (SHA-256), tree C (Poseidon column hashes) and tree R-last (encoded = data + last label) built
+    sparsely over the opened leaves with random filler nodes, so every opening of the partition meets one
+    root; comm_r = Poseidon-2(comm_c, comm_r_last).  Returns the instance in instance_slots' format."""
+    from . import sdr, tree
+
+    rng = np.random.default_rng(seed)
+    L, C, nodes = circuit.layers, circuit.challenges, circuit.nodes
+
+    def rand():
+        b = bytearray(rng.bytes(32))
+        b[31] &= 0x1F
+        return int.from_bytes(b, "little")
+
+    def pos_hash(a, flat):
+        return tree.to_ints(tree.poseidon_hash(ctx, a, flat)) if flat else []
+
+    if C + 14 > nodes:
+        raise ValueError("too few nodes for distinct challenges and parents")
+    chal = []
+    while len(chal) < C:
+        x = int(rng.integers(0, nodes))
+        if x not in chal:
+            chal.append(x)
+    taken = set(chal)
+
+    def parent_index():
+        while True:
+            x = int(rng.integers(0, nodes))
+            if x not in taken:
+                return x
+
+    columns, graph = {}, []
+    for c in chal:
+        drg = [parent_index() for _ in range(6)]
+        exp = [parent_index() for _ in range(8)]
+        for p in drg + exp:
+            if p not in columns:
+                columns[p] = [rand() >> 2 for _ in range(L)]  # labels are 254-bit values
+        graph.append((drg, exp))
+    replica_id = rand()
+    rid = replica_id.to_bytes(32, "little")
+    # the challenged columns: layer 1 over the 6 DRG parents, layers 2.. over 6 DRG + 8 expander parents
+    for c in chal:
+        columns[c] = [None] * L
+    for first in (True, False):
+        lay, nod, par = [], [], bytearray()
+        for c, (drg, exp) in zip(chal, graph):
+            for layer in ([1] if first else range(2, L + 1)):
+                ps = [columns[p][layer - 1] for p in drg]
+                if not first:
+                    ps += [columns[p][layer - 2] for p in exp]
+                lay.append(layer)
+                nod.append(c)
+                par += b"".join(v.to_bytes(32, "little") for v in ps)
+        if not lay:
+            continue
+        out = tree.to_ints(sdr.create_labels(ctx, rid, lay, nod, bytes(par), 6 if first else 14))
+        for (layer, c), v in zip(zip(lay, nod), out):
+            columns[c][layer - 1] = v
+    data = {c: rand() for c in chal}
+    col_idx = sorted(columns)
+    col_hash = dict(zip(col_idx, pos_hash(L, [v for i in col_idx for v in columns[i]])))
+    comm_d, d_path = _sparse_tree(data, [2] * circuit.info["depth_d"],
+                                  lambda a, flat: [_sha_node(flat[i], flat[i + 1]) for i in range(0, len(flat), 2)],
+                                  rand)
+    comm_c, c_path = _sparse_tree(col_hash, circuit.arities, pos_hash, rand)
+    enc = {c: (data[c] + columns[c][L - 1]) % FR_MODULUS for c in chal}
+    comm_r_last, r_path = _sparse_tree(enc, circuit.arities, pos_hash, rand)
+    comm_r = pos_hash(2, [comm_c, comm_r_last])[0]
+    challenges = []
+    for c, (drg, exp) in zip(chal, graph):
+        challenges.append({
+            "index": c, "data_leaf": data[c], "d_siblings": [s[0] for s in d_path(c)],
+            "r_siblings": r_path(c), "c_column": columns[c], "c_siblings": c_path(c),
+            "drg": [(p, columns[p], c_path(p)) for p in drg], "exp": [(p, columns[p], c_path(p)) for p in exp]})
+    return {"replica_id": replica_id, "comm_d": comm_d, "comm_r": comm_r, "comm_r_last": comm_r_last,
+            "comm_c": comm_c, "challenges": challenges}
+
+
+def slots_of(circuit: StackedCircuit, inst: dict) -> bytes:
+    """instance_slots over an instance dict (synthetic_instance's / the test oracle's format)"""
+    return instance_slots(circuit, inst["replica_id"], inst["comm_d"], inst["comm_r"], inst["comm_r_last"],
+                          inst["comm_c"], inst["challenges"])

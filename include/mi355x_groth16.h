@@ -271,13 +271,55 @@ int mi_synth_r1cs(const mi_synth *s, mi_r1cs *out);
 int mi_synth_witness(const mi_synth *s, const uint8_t **z, uint64_t *num_vars);
 void mi_synth_free(mi_synth *s);
 
+/* ---- stacked-PoRep circuit: R1CS and GPU witness generation -----------------------
+ * Replaces the synthesis half of compound_proof::circuit_proofs (StackedCompound::circuit + synthesize:
+ * libs/storage/include/nil/filecoin/storage/proofs/porep/stacked/circuit/proof.hpp:98-165, params.hpp:93-238):
+ *   mi_stacked_build   <- the circuit shape (blank-circuit synthesis): the R1CS of one partition over
+ *                         z = ONE ++ inputs ++ aux, identical for every partition of a shape, and the witness
+ *                         program.  layers 2 or 11, nodes a power of two, tree C / R-last arities in {2, 4, 8}
+ *                         (32 GiB: layers 11, challenges 18, nodes 2^30, 8 / 8 / 0).  Host, no device needed.
+ *   mi_stacked_witness <- the assignment half of synthesize: every variable of one partition computed on the
+ *                         GPU from the vanilla proof's openings (the instance slots below).
+ *   mi_stacked_public_inputs <- generate_public_inputs (circuit/proof.hpp:186-269).
+ * Instance slots (32 B each, Fr LE canonical, u64 indices in the low 8 bytes):
+ *   0 replica_id, 1 comm_d, 2 comm_r, 3 comm_r_last, 4 comm_c; challenge c from 5 + c * stride:
+ *   +0 challenge (u64), +1 data leaf, tree D siblings (leaf upward), tree R-last siblings, tree C siblings of
+ *   the challenged column, then 6 DRG and 8 expander parents: index (u64), column (layers labels), tree C
+ *   siblings.  Siblings of an arity-a level: the a - 1 other children in position order.
+ * The layout is pinned by the reference's constraint counts (1,199,620 for 2 layers, 1 challenge, 8 nodes,
+ * base 8; proof.cpp:137-155) and checked row for row against oracle/stacked_circuit.py. */
+typedef struct {
+    uint32_t layers, challenges;
+    uint64_t nodes;
+    uint32_t base_arity, sub_arity, top_arity, reserved;
+} mi_stacked_shape;
+typedef struct mi_stacked mi_stacked;
+/* with_r1cs = 0 builds the witness program only (the R1CS stays with whoever built the key) */
+int mi_stacked_build(const mi_stacked_shape *shape, int with_r1cs, mi_stacked **out);
+/* out: constraints, inputs (with ONE), aux, instance slots, slots per challenge, tree D depth, siblings per
+ * tree C / R-last path, program ops, program levels, SHA-256 blocks, Poseidon hashes, R1CS entries */
+int mi_stacked_info(const mi_stacked *s, uint64_t out[12]);
+/* the R1CS (pointers valid until mi_stacked_free); feed it to mi_circuit_load */
+int mi_stacked_r1cs(const mi_stacked *s, mi_r1cs *out);
+/* (inputs - 1) x 32 B: the public inputs in generate_public_inputs order (without ONE) */
+int mi_stacked_public_inputs(const mi_stacked *s, const uint8_t *slots, uint8_t *out);
+/* z_dev: (inputs + aux) x 32 B on this context's GPU, fully written; slots refused if not canonical or an
+ * index >= nodes (MI_ERR_ARG) */
+int mi_stacked_witness_dev(mi_ctx *ctx, mi_stacked *s, const void *slots_dev, void *z_dev);
+int mi_stacked_witness(mi_ctx *ctx, mi_stacked *s, const uint8_t *slots, uint8_t *z_out);
+void mi_stacked_free(mi_stacked *s);
+/* R1CS satisfaction on the device: out[0] = rows with (A z)(B z) != (C z), out[1] = the first one (~0 if none) */
+int mi_circuit_check_dev(mi_ctx *ctx, const mi_circuit *circuit, const void *z_dev, uint64_t out[2]);
+
 /* ---- device timers (HIP events on the launching stream, resolved at existing sync points, so they
- * stay on inside timed regions).  out = 8 records x {ms, launches, units}:
+ * stay on inside timed regions).  out = 13 records x {ms, launches, units}:
  *   0 k_accum_level0<G1> (units = points)   1 k_accum_level0<G2>   2 whole G1 MSM   3 whole G2 MSM
  *   4 digits + sort + bucket bounds          5 NTT transforms (units = elements)   6 whole prove (units = constraints)
  *   7 witness H2D upload + canonical check on the copy stream (units = bytes)
- *   8 k_poseidon launches (units = hashes)  9 tree builders' label / data uploads (units = bytes) */
-int mi_ctx_get_stats(mi_ctx *ctx, double out[30]);
+ *   8 k_poseidon launches (units = hashes)  9 tree builders' label / data uploads (units = bytes)
+ *  10 stacked witness phase A (units = ops)  11 phase B SHA-256 blocks (units = blocks)
+ *  12 phase B Poseidon gadgets (units = hashes) */
+int mi_ctx_get_stats(mi_ctx *ctx, double out[39]);
 int mi_ctx_reset_stats(mi_ctx *ctx);
 /* work counters since the last reset: out[0] / out[1] = mixed additions (non-zero signed digits)
  * issued by the G1 / G2 bucket accumulation -- the unit of the VALU roofline */
