@@ -127,24 +127,38 @@ def test_stacked_32gib_partition_witness_prove_verify(ctx):
     """BASELINE config 4 on the real circuit: one 32 GiB PoRep partition (11 layers, 18 challenges, 2^30 nodes,
     tree C / R-last 8-8; 130,278,541 constraints, domain 2^27).  The GPU witness of a synthetic partition
     satisfies all rows on the device; the partition proves and pairing-verifies."""
+    import time
+
     import circuits
+
+    t0 = time.perf_counter()
+
+    def note(what):
+        print(f"[32GiB] {what}: {time.perf_counter() - t0:.1f} s", flush=True)
 
     c = stacked.StackedCircuit(11, 18, 1 << 30, 8, 8, 0)
     assert (c.num_constraints, c.num_inputs) == (130_278_541, 328)
+    note(f"R1CS built ({c.info['r1cs_entries']} entries)")
     inst = stacked.synthetic_instance(ctx, c, seed=32)
     slots = stacked.slots_of(c, inst)
+    note("synthetic partition")
     gc = c.load(ctx)
     assert gc.d == 1 << 27
+    note("circuit loaded")
     sd = torch.from_numpy(np.frombuffer(slots, dtype=np.uint8).copy()).cuda()
     z = torch.empty(32 * c.num_vars, dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()
     c.witness_dev(ctx, sd.data_ptr(), z.data_ptr())
+    note("witness")
     assert stacked.circuit_check_dev(ctx, gc, z.data_ptr()) == (0, None)
+    note("R1CS check")
     pub = c.public_inputs(slots)
     assert z[32:32 * c.num_inputs].cpu().numpy().tobytes() == pub
     pk = fg.generate_random_parameters(ctx, gc, circuits.toxic())
+    note("keygen")
     vk, ic = pk.verifying_key()
     proof = fg.prove(ctx, pk, gc, z.data_ptr())
+    note("proof")
     assert fg.verify(vk, ic, pub, proof)
     del pk, gc, z
     torch.cuda.synchronize()
