@@ -596,12 +596,13 @@ def poseidon_hash_circuit(cs, inputs, arity):
 
 
 # ------------------------------------------------------------------------------------------ hashers
-def sha256_hash2(cs, a, b):
-    """storage-proofs-core Sha256Function::hash2_circuit: 255-bit LE decompositions, each padded to whole
-    bytes and bit-reversed per byte, SHA-256, the first 254 output bits (LSB first per byte) packed"""
-    ab = to_bits_le(cs, a)
-    bb = to_bits_le(cs, b)
-    pre = reverse_bit_numbering(ab) + reverse_bit_numbering(bb)
+def sha256_hash_leaves(cs, leaves):
+    """storage-proofs-core Sha256Function::hash_multi_leaf_circuit / hash2_circuit: each leaf's 255-bit LE
+    decomposition padded to whole bytes and bit-reversed per byte, concatenated, SHA-256, the first 254 output
+    bits (LSB first per byte) packed"""
+    pre = []
+    for x in leaves:
+        pre += reverse_bit_numbering(to_bits_le(cs, x))
     out = sha256(cs, pre)
     le = []
     for k in range(0, 256, 8):
@@ -611,8 +612,7 @@ def sha256_hash2(cs, a, b):
 
 def hash_multi_leaf(cs, hasher, arity, leaves):
     if hasher == "sha256":
-        assert arity == 2
-        return sha256_hash2(cs, leaves[0], leaves[1])
+        return sha256_hash_leaves(cs, leaves)
     return poseidon_hash_circuit(cs, leaves, arity)
 
 

@@ -1,0 +1,146 @@
+"""CPU: the stacked-PoRep circuit layout pinned by the reference's constraint counts.
+
+* The oracle's gadget restatement (oracle/stacked_circuit.py) reproduces every count the reference's tests
+  assert: hash_single_column = 598 (libs/storage/test/porep/stacked/circuit/hash.cpp:77), the PoR circuits
+  (libs/storage/test/core/components/por.cpp:89-172, 366-384) and the stacked circuit at 2 layers / 1 challenge
+  for Poseidon base 8, base 2, 8-4 and 8-4-2 trees with 22 inputs (test/porep/stacked/circuit/proof.cpp:137-155).
+* The reference-shape instance satisfies the oracle's R1CS and its inputs equal generate_public_inputs
+  (proof.cpp:122-132).
+* The library's host builder (mi_stacked_build, product) produces the SAME R1CS as the oracle, row for row and
+  coefficient for coefficient, for a 2-challenge partition (which also covers the builder's challenge
+  replication), and the reference counts for all four shapes and the 32 GiB shape.
+"""
+import random
+
+import numpy as np
+import pytest
+
+import fil_groth16 as fg
+from fil_groth16 import stacked
+
+POR = [  # (hasher, (base, sub, top), private, constraints)
+    ("poseidon", (2, 0, 0), False, 1887), ("poseidon", (4, 0, 0), False, 1164), ("poseidon", (8, 0, 0), False, 1063),
+    ("poseidon", (8, 2, 0), False, 1377), ("poseidon", (8, 4, 2), False, 1764), ("poseidon", (8, 8, 0), False, 1593),
+    ("poseidon", (8, 8, 2), False, 1907), ("poseidon", (8, 2, 4), False, 1764),
+    ("poseidon", (2, 0, 0), True, 1886), ("poseidon", (4, 0, 0), True, 1163), ("poseidon", (8, 0, 0), True, 1062),
+    ("sha256", (2, 0, 0), False, 272_295), ("sha256", (4, 0, 0), False, 216_258), ("sha256", (8, 0, 0), False, 250_987),
+]
+STACKED = [((8, 0, 0), 8, 1_199_620), ((2, 0, 0), 8, 1_206_212), ((8, 4, 0), 32, 1_296_576),
+           ((8, 4, 2), 64, 1_346_982)]
+
+
+def test_oracle_hash_single_column_598():
+    import stacked_circuit as sc
+
+    rng = random.Random(1)
+    cs = sc.CS()
+    xs = [cs.alloc(rng.randrange(sc.R)) for _ in range(11)]
+    out = sc.poseidon_hash_circuit(cs, xs, 11)
+    assert cs.n_constraints == 598
+    assert cs.is_satisfied() is None
+    import poseidon_ref
+
+    assert cs.value(out) == poseidon_ref.Poseidon(11).hash([cs.value(x) for x in xs])
+
+
+@pytest.mark.parametrize("hasher,shape,private,want", POR)
+def test_oracle_por_counts(hasher, shape, private, want):
+    """SHA-256 PoR counts pin the bellman SHA-256 gadget (constant folding, MultiEq packing): the hash2 over two
+    255-bit decompositions costs 45,379 constraints.  Poseidon ones pin insert_4 / insert_8 (8 / 22) and the
+    Poseidon circuit of arity 2 / 4 / 8 (311 / 377 / 505)."""
+    import stacked_circuit as sc
+
+    rng = random.Random(2)
+    base, sub, top = shape
+    leaves = 64 * (sub or 1) * (top or 1)
+    levels = sc.tree_levels(leaves, shape)
+    cs = sc.CS(with_constraints=False)
+    leaf, root = cs.alloc(rng.randrange(sc.R)), cs.alloc(rng.randrange(sc.R))
+    sibs = [[rng.randrange(sc.R) for _ in range(a - 1)] for a in levels]
+    sc.por_synthesize(cs, leaf, 5, sibs, root, levels, hasher, private=private)
+    assert cs.n_constraints == want
+    assert len(cs.inputs) == (2 if private else 3)
+
+
+@pytest.mark.parametrize("shape,nodes,want", STACKED)
+def test_oracle_stacked_counts(shape, nodes, want):
+    import stacked_circuit as sc
+    import stacked_instance as si
+
+    inst = si.generate(nodes, 2, shape, 1, seed=3)
+    cs = sc.CS(with_constraints=False)
+    sc.stacked_circuit(cs, inst, 2, nodes, shape)
+    assert (cs.n_constraints, len(cs.inputs)) == (want, 22)
+    assert cs.inputs[1:] == si.public_inputs(inst)
+
+
+@pytest.fixture(scope="module")
+def two_challenges():
+    import stacked_circuit as sc
+    import stacked_instance as si
+
+    inst = si.generate(8, 2, (8, 0, 0), 2, seed=5)
+    cs = sc.CS()
+    sc.stacked_circuit(cs, inst, 2, 8, (8, 0, 0))
+    return inst, cs
+
+
+def test_oracle_stacked_satisfied(two_challenges):
+    inst, cs = two_challenges
+    assert cs.is_satisfied() is None
+    bad = list(cs.aux)
+    cs.aux[len(cs.aux) // 2] ^= 1
+    assert cs.is_satisfied() is not None
+    cs.aux[:] = bad
+
+
+def test_builder_r1cs_equals_oracle(two_challenges):
+    inst, cs = two_challenges
+    c = stacked.StackedCircuit(2, 2, 8, 8, 0, 0)
+    assert (c.num_constraints, c.num_inputs, c.num_aux) == (cs.n_constraints, len(cs.inputs), len(cs.aux))
+    mats, ocsr = c.csr(), cs.to_csr()
+    for m in range(3):
+        rp, col, co = mats[m]
+        orp, ocol, oco = ocsr[m]
+        assert np.array_equal(rp, np.asarray(orp, dtype=np.uint64)), m
+        assert np.array_equal(col, np.asarray(ocol, dtype=np.uint32)), m
+        assert co.tobytes() == b"".join(int(k).to_bytes(32, "little") for k in oco), m
+    slots = stacked.slots_of(c, inst)
+    assert c.public_inputs(slots) == b"".join(v.to_bytes(32, "little") for v in cs.inputs[1:])
+
+
+@pytest.mark.parametrize("shape,nodes,want", STACKED)
+def test_builder_reference_counts(shape, nodes, want):
+    c = stacked.StackedCircuit(2, 1, nodes, *shape, with_r1cs=False)
+    assert (c.num_constraints, c.num_inputs) == (want, 22)
+
+
+def test_builder_32gib_shape_counts():
+    """32 GiB partition: 11 layers, 18 challenges (proofs/parameters.hpp:90-99), 2^30 nodes, tree C / R-last
+    8-8 (SectorShape32GiB).  7,237,665 constraints per challenge + 571 shared: 130,278,541, i.e. the ~1.3e8 of
+    BASELINE config 4, on a 2^27 domain; 328 inputs."""
+    c = stacked.StackedCircuit(11, 18, 1 << 30, 8, 8, 0, with_r1cs=False)
+    assert (c.num_constraints, c.num_inputs) == (130_278_541, 328)
+    assert c.info["sha_blocks"] == 18 * (11 * 20 + 30 * 2)
+    assert c.info["poseidon_hashes"] == 1 + 18 * (15 + 16 * 10)
+
+
+def test_builder_refuses_bad_shapes():
+    for args in [(3, 1, 8, 8, 0, 0), (2, 0, 8, 8, 0, 0), (2, 1, 12, 8, 0, 0), (2, 1, 8, 3, 0, 0), (2, 1, 64, 8, 0, 2)]:
+        with pytest.raises(fg.FilGpuError):
+            stacked.StackedCircuit(*args, with_r1cs=False)
+
+
+def test_instance_slots_layout():
+    import stacked_instance as si
+
+    c = stacked.StackedCircuit(2, 1, 8, 8, 0, 0, with_r1cs=False)
+    inst = si.generate(8, 2, (8, 0, 0), 1, seed=3)
+    slots = stacked.slots_of(c, inst)
+    assert len(slots) == 32 * c.info["slots"] == 32 * (5 + c.info["stride"])
+    ch = inst["challenges"][0]
+    assert int.from_bytes(slots[32 * 5:32 * 6], "little") == ch["index"]
+    assert int.from_bytes(slots[32 * 6:32 * 7], "little") == ch["data_leaf"]
+    with pytest.raises(ValueError):
+        stacked.instance_slots(c, inst["replica_id"], inst["comm_d"], inst["comm_r"], inst["comm_r_last"],
+                               inst["comm_c"], inst["challenges"] * 2)
