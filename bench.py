@@ -367,6 +367,96 @@ def config4_leg(args, fg, synth_mod, ctx):
     return out
 
 
+def stacked_leg(args, fg, ctx, device, world):
+    """SURVEY 8(f)#3 + BASELINE config 4 on the real circuit: one 32 GiB stacked-PoRep partition (11 layers, 18
+    challenges, 2^30 nodes, tree C / R-last 8-8; 130,278,541 constraints, domain 2^27).  The R1CS is built
+    on the host (once per shape) and the proving key generated on the GPU (setup, untimed); then the
+    partition's witness is generated on the GPU from its vanilla openings (a synthetic consistent
+    instance: sparse trees, labels from the label kernel) and proven, every proof pairing-verified.  The
+    witness kernels are HBM-bound by the 32-byte variables they write; the roofline is reported against
+    8 TB/s.  CPU baseline: the oracle's Python synthesis (one thread) on the 2-layer reference shape."""
+    import gc
+
+    import numpy as np
+    import torch
+
+    from fil_groth16 import stacked
+
+    t0 = time.perf_counter()
+    sc_ = stacked.StackedCircuit(args.stacked_layers, args.stacked_challenges, 1 << args.stacked_log_nodes, 8, 8, 0)
+    t_build = time.perf_counter() - t0
+    inst = stacked.synthetic_instance(ctx, sc_, seed=32)
+    slots = stacked.slots_of(sc_, inst)
+    t_inst = time.perf_counter() - t0 - t_build
+    circ = sc_.load(ctx)
+    pk = fg.generate_random_parameters(ctx, circ, splitmix_frs(TOXIC_SEED, 5))
+    ctx.synchronize()
+    t_setup = time.perf_counter() - t0
+    nv = sc_.num_vars
+    sd = torch.from_numpy(np.frombuffer(slots, dtype=np.uint8).copy()).to(device)
+    z = torch.empty(32 * nv, dtype=torch.uint8, device=device)
+    torch.cuda.synchronize()
+    sc_.witness_dev(ctx, sd.data_ptr(), z.data_ptr())  # warm (program upload)
+    bad, _ = stacked.circuit_check_dev(ctx, circ, z.data_ptr())
+    ctx.reset_stats()
+    reps = args.stacked_reps
+    tw = time.perf_counter()
+    for _ in range(reps):
+        sc_.witness_dev(ctx, sd.data_ptr(), z.data_ptr())
+    ctx.synchronize()
+    tw = (time.perf_counter() - tw) / reps
+    st = ctx.stats()
+    blind = splitmix_frs(5000, 2 * (reps + 1))
+    fg.prove(ctx, pk, circ, z.data_ptr(), blind[0], blind[1])
+    ctx.synchronize()
+    tp = time.perf_counter()
+    proofs = []
+    for k in range(reps):
+        sc_.witness_dev(ctx, sd.data_ptr(), z.data_ptr())
+        proofs.append(fg.prove(ctx, pk, circ, z.data_ptr(), blind[2 * k + 2], blind[2 * k + 3]))
+    ctx.synchronize()
+    tp = (time.perf_counter() - tp) / reps
+    vk, ic = pk.verifying_key()
+    pub = sc_.public_inputs(slots)
+    verified = bool(fg.verify_batch(vk, ic, [pub] * len(proofs), proofs))
+    wbytes = 32 * nv
+    res = {"workload": f"32 GiB stacked-PoRep partition: {args.stacked_layers} layers x {args.stacked_challenges} "
+                       f"challenges, 2^{args.stacked_log_nodes} nodes, tree C / R-last 8-8 "
+                       f"({sc_.num_constraints} constraints, {nv} variables, domain 2^{circ.d.bit_length() - 1}); "
+                       f"synthetic consistent instance",
+           "constraints": sc_.num_constraints, "variables": nv, "r1cs_entries": sc_.info["r1cs_entries"],
+           "witness_ms": tw * 1e3, "witness_variables_per_s": nv / tw,
+           "witness_phases_ms_per_partition": {k: st[k]["ms"] / reps for k in ("wit_a", "wit_sha", "wit_pos")},
+           "witness_satisfies_r1cs": bad == 0,
+           "witness_plus_prove_ms": tp * 1e3, "constraints_per_s": sc_.num_constraints / tp,
+           "proofs": len(proofs), "verified": verified,
+           "witness_roofline": {"bound": "hbm", "achieved": wbytes / tw / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": wbytes / tw / 1e9 / HBM_PEAK_GBS,
+                                "algorithmic_bytes": wbytes, "note": "32 B written per variable; reads are the "
+                                "instance slots and operand variables (small)"},
+           "setup_s": {"r1cs_build": t_build, "instance": t_inst, "load_and_keygen": t_setup - t_build - t_inst}}
+    if world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import stacked_circuit as osc
+        import stacked_instance as osi
+
+        oinst = osi.generate(8, 2, (8, 0, 0), 1, seed=3)
+        t1 = time.perf_counter()
+        ocs = osc.CS(with_constraints=False)
+        osc.stacked_circuit(ocs, oinst, 2, 8, (8, 0, 0))
+        dtc = time.perf_counter() - t1
+        nvo = len(ocs.inputs) + len(ocs.aux)
+        res["cpu_baseline"] = {"value": nvo / dtc, "unit": "witness variables/s", "cores": 1, "kind": "port",
+                               "sample": f"oracle/stacked_circuit.py (Python, one thread) synthesising the reference "
+                                         f"test shape (2 layers, 1 challenge, 8 nodes: {nvo} variables) in "
+                                         f"{dtc:.1f} s on {cpu_model()}"}
+        res["gpu_over_cpu_witness"] = res["witness_variables_per_s"] / res["cpu_baseline"]["value"]
+    del pk, circ, z, sd, sc_
+    gc.collect()
+    torch.cuda.synchronize()
+    return res
+
+
 def config5_leg(args, fg, synth_mod, ctx, rank, world, gdev, dist, partitions=10):
     """BASELINE config 5 on the driver's N-GPU run: a Window-PoSt batch of 10 partitions of 32 GiB-sector
     size (2^27-domain synthetic circuit) proven round-robin over the ranks (10 over 8 GPUs: two rounds on
@@ -473,6 +563,11 @@ def main():
     ap.add_argument("--config4-log-rows", type=int, default=27,
                     help="secondary: BASELINE config 4 (2^N domain) after the main run on one GPU (0 skips)")
     ap.add_argument("--config4-steps", type=int, default=2)
+    ap.add_argument("--stacked-log-nodes", type=int, default=30,
+                    help="secondary (one GPU): the 32 GiB stacked-PoRep partition witness + prove (0 skips)")
+    ap.add_argument("--stacked-layers", type=int, default=11)
+    ap.add_argument("--stacked-challenges", type=int, default=18)
+    ap.add_argument("--stacked-reps", type=int, default=2)
     ap.add_argument("--config5-log-rows", type=int, default=27,
                     help="multi-GPU runs: the 10-partition config-5 leg at this domain (0 skips)")
     ap.add_argument("--config5-steps", type=int, default=2)
@@ -672,17 +767,25 @@ def main():
         except Exception as e:  # reported, never fatal to the main measurement
             config5 = {"error": str(e)}
 
-    config4 = None
-    if rank == 0 and world == 1 and args.config4_log_rows:
+    if rank == 0 and world == 1 and (args.config4_log_rows or args.stacked_log_nodes):
         import gc
 
-        del pk, circ, zhost, sc
+        del pk, circ, zhost, sc  # the secondary legs need the HBM
         gc.collect()
         ctx.synchronize()
+    config4 = None
+    if rank == 0 and world == 1 and args.config4_log_rows:
         try:
             config4 = config4_leg(args, fg, synth_mod, ctx)
         except Exception as e:  # reported, never fatal to the config-3 measurement
             config4 = {"value": None, "error": str(e)}
+
+    stacked_res = None
+    if rank == 0 and world == 1 and args.stacked_log_nodes:
+        try:
+            stacked_res = stacked_leg(args, fg, ctx, device, world)
+        except Exception as e:  # reported, never fatal to the config-3 measurement
+            stacked_res = {"error": str(e)}
 
     if rank != 0:
         if dist:
@@ -791,6 +894,7 @@ def main():
         "sdr_labels": sdr,
         "config4": config4,
         "config5": config5,
+        "stacked_porep_32gib": stacked_res,
         "timers_ms": {k: round(v["ms"], 3) for k, v in stats.items()},
         "setup_s": {"synth": t_synth, "circuit_load": t_load, "srs": t_srs},
         "device_gb_after_setup": round(dev_used_gb, 2),
