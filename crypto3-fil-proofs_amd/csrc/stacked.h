@@ -99,8 +99,10 @@ struct Built {
     std::vector<uint32_t> col[3];
     std::vector<fr_t> coeff[3];
     // witness program
-    std::vector<WOp> ops;            // sorted by level
+    std::vector<WOp> ops;            // sorted by (level, kind): kind 0 every non-Poseidon op, 1..4 Poseidon of
+                                     // arity 2 / 4 / 8 / 11 (one kernel per kind)
     std::vector<uint64_t> level_off; // ops of level L: [level_off[L], level_off[L + 1])
+    std::vector<uint64_t> seg_off;   // ops of (level L, kind k): [seg_off[5 L + k], seg_off[5 L + k + 1])
     std::vector<uint64_t> pin;       // Poseidon input variable lists
     std::vector<ShaBlock> blocks;
     std::vector<uint64_t> poseidon_ops, sha_ops;  // op indices (phase B)

@@ -1065,7 +1065,14 @@ Built *build(const Shape &s, bool want_r1cs) {
         const size_t n = b->ops.size();
         std::vector<uint64_t> perm(n), where(n);
         for (size_t i = 0; i < n; i++) perm[i] = i;
-        std::stable_sort(perm.begin(), perm.end(), [&](uint64_t x, uint64_t y) { return b->ops[x].level < b->ops[y].level; });
+        auto kind = [](const WOp &o) -> uint32_t {
+            if (o.type != W_POSEIDON) return 0;
+            return o.n == 2 ? 1 : o.n == 4 ? 2 : o.n == 8 ? 3 : 4;
+        };
+        std::stable_sort(perm.begin(), perm.end(), [&](uint64_t x, uint64_t y) {
+            const WOp &a = b->ops[x], &c = b->ops[y];
+            return a.level != c.level ? a.level < c.level : kind(a) < kind(c);
+        });
         std::vector<WOp> sorted(n);
         for (size_t i = 0; i < n; i++) {
             sorted[i] = b->ops[perm[i]];
@@ -1079,6 +1086,9 @@ Built *build(const Shape &s, bool want_r1cs) {
         b->level_off.assign(maxl + 2, 0);
         for (auto &op : b->ops) b->level_off[op.level + 1]++;
         for (uint32_t l = 0; l <= maxl; l++) b->level_off[l + 1] += b->level_off[l];
+        b->seg_off.assign(5 * (maxl + 1) + 1, 0);
+        for (auto &op : b->ops) b->seg_off[5 * op.level + kind(op) + 1]++;
+        for (size_t q = 0; q + 1 < b->seg_off.size(); q++) b->seg_off[q + 1] += b->seg_off[q];
     } catch (...) {
         delete b;
         throw;

@@ -15,6 +15,7 @@
 #include <stdexcept>
 
 #include "ctx.h"
+#include "poseidon.h"
 #include "poseidon_math.h"
 #include "stacked.h"
 
@@ -23,28 +24,21 @@ namespace stacked {
 
 namespace {
 
-struct PosTab {
-    const fr_t *rc;   // Montgomery, (rf + rp) x t
-    const fr_t *mds;  // Montgomery, t x t
-    fr_t tag;         // Montgomery
-    int rf, rp;
+struct PosKs {
+    PosK k[4];  // arity 2, 4, 8, 11
 };
-struct PosTabs {
-    PosTab t[4];  // arity 2, 4, 8, 11
-};
-__host__ __device__ inline int pos_index(unsigned arity) { return arity == 2 ? 0 : arity == 4 ? 1 : arity == 8 ? 2 : 3; }
 
 struct DevProg {
     WOp *ops = nullptr;
     uint64_t *pin = nullptr;
     ShaBlock *blocks = nullptr;
-    uint64_t *pos_ops = nullptr;
+    uint64_t *pos_ops = nullptr;  // Poseidon op indices grouped by arity (2, 4, 8, 11)
+    uint64_t pos_off[5] = {0, 0, 0, 0, 0};
     uint32_t *states = nullptr;  // 8 words per block: the block's input chaining value
-    fr_t *tabs = nullptr;        // Poseidon constants of all arities (one allocation)
-    PosTabs pt{};
+    PosKs pk{};                  // device views of the production Poseidon tables (poseidon_tables, per ctx)
     int device = -1;
     ~DevProg() {
-        for (void *p : {(void *)ops, (void *)pin, (void *)blocks, (void *)pos_ops, (void *)states, (void *)tabs})
+        for (void *p : {(void *)ops, (void *)pin, (void *)blocks, (void *)pos_ops, (void *)states})
             if (p) hipFree(p);
     }
 };
@@ -275,67 +269,69 @@ __device__ void sha_gadget(Emit &E, const W3 msg[16], const W3 H[8], W3 (*w)[64]
 }
 
 // ---------------------------------------------------------------------------------------- Poseidon
-// literal permutation (ARK, S-box, state' = state * M) in Montgomery form; with E, the gadget's variables
+// The production permutation (poseidon_math.h: 9 x 29-bit lazy Montgomery limbs, folded constants, sparse
+// partial rounds).  Its S-box inputs are the literal permutation's: the full rounds are literal, and in the
+// partial rounds the sparse factorisation keeps element 0 in the literal basis with its folded constant equal
+// to the literal one (A_k = diag(1, M^k)).  The gadget's variables are functions of those inputs only
+// (v, v^2, v^4, v^5), so the expansion emits them as it goes.
+__device__ __forceinline__ void put29(Emit *E, const fr29_t &x) { zput_fr(E->z, E->k++, fr_from_fr29(fr29_from_mont(x))); }
+
 template <int T>
-__device__ fr_t poseidon_run(const PosTab &P, const fr_t *in_mont, Emit *E) {
-    fr_t s[T];
-    s[0] = P.tag;
-#pragma unroll
-    for (int i = 1; i < T; i++) s[i] = in_mont[i - 1];
-    const int half = P.rf / 2;
-    const fr_t *rc = P.rc;
-    for (int rnd = 0; rnd < P.rf + P.rp; rnd++, rc += T) {
-#pragma unroll
-        for (int i = 0; i < T; i++) s[i] = s[i] + rc[i];
-        const bool full = rnd < half || rnd >= half + P.rp;
-#pragma unroll
-        for (int i = 0; i < T; i++) {
-            if (i > 0 && !full) continue;
-            const fr_t x = s[i];
-            const fr_t x2 = x * x, x4 = x2 * x2, x5 = x4 * x;
-            if (E && !(rnd == 0 && i == 0)) {  // the domain tag's first S-box is a constant
-                if (rnd > 0) zput_fr(E->z, E->k++, from_mont(x));
-                zput_fr(E->z, E->k++, from_mont(x2));
-                zput_fr(E->z, E->k++, from_mont(x4));
-                zput_fr(E->z, E->k++, from_mont(x5));
-            }
-            s[i] = x5;
+__device__ fr29_t pos_run(const PosK &k, fr29_t (&s)[T], Emit *E) {
+    const fr29_t *img = k.img;
+    const fr29_t *mds = img + k.off_mds;
+    // one S-box on input x; `first`: a first-round S-box (its input is a linear combination, not allocated)
+    auto sbox = [&](const fr29_t &x, bool first) -> fr29_t {
+        const fr29_t x2 = fr29_sqr(x), x4 = fr29_sqr(x2), x5 = fr29_mul(x4, x);
+        if (E) {
+            if (!first) put29(E, x);
+            put29(E, x2);
+            put29(E, x4);
+            put29(E, x5);
         }
-        fr_t n[T];
-#pragma unroll
-        for (int j = 0; j < T; j++) {
-            fr_t acc = s[0] * P.mds[j];
-#pragma unroll
-            for (int i = 1; i < T; i++) acc = acc + s[i] * P.mds[i * T + j];
-            n[j] = acc;
-        }
-#pragma unroll
-        for (int j = 0; j < T; j++) s[j] = n[j];
+        return x5;
+    };
+    const int half = k.rf / 2;
+    for (int r = 0; r < half; r++) {
+        const fr29_t *rc = img + k.off_rc_first + r * T;
+        sfor<T>([&](auto i) {
+            const fr29_t x = fr29_add(s[i], rc[i]);
+            s[i] = (r == 0 && i == 0) ? fr29_sbox(x) : sbox(x, r == 0);  // the domain tag's first S-box: constant
+        });
+        mat_apply<T>(s, mds);
     }
-    if (E) zput_fr(E->z, E->k++, from_mont(s[1]));
+    const fr29_t *sp = img + k.off_sparse;
+    for (int q = 0; q < k.rp - 1; q++, sp += 2 * T - 1) {
+        s[0] = sbox(fr29_add(s[0], img[k.off_rc_part + q]), false);
+        const fr29_t n0 = fr29_row<T>(sp, s);
+        sfor<T - 1>([&](auto j) { s[j + 1] = fr29_sub_if_ge(fr29_add(s[j + 1], fr29_mul(sp[T + j], s[0])), R2X29); });
+        s[0] = n0;
+    }
+    s[0] = sbox(fr29_add(s[0], img[k.off_rc_part + k.rp - 1]), false);
+    mat_apply<T>(s, img + k.off_dense);
+    for (int r = 0; r < half; r++) {
+        const fr29_t *rc = img + k.off_rc_last + r * T;
+        sfor<T>([&](auto i) { s[i] = sbox(fr29_add(s[i], rc[i]), false); });
+        mat_apply<T>(s, mds);
+    }
+    if (E) put29(E, s[1]);
     return s[1];
 }
 
-template <bool EXPAND>
-__device__ void poseidon_op(const WOp &op, const uint64_t *pin, const PosTabs &pt, fr_t *z) {
-    fr_t in[11];
-    for (unsigned j = 0; j < op.n; j++) in[j] = to_mont(zget(z, pin[op.a + j]));
+template <int T>
+__device__ void pos_op_t(const WOp &op, const uint64_t *pin, const PosK &k, fr_t *z, bool expand) {
+    fr29_t s[T];
+    s[0] = k.img[k.off_tag];
+    for (int j = 1; j < T; j++) s[j] = fr29_mul(fr29_from_fr(zget(z, pin[op.a + j - 1])), k.img[k.off_tag + 1]);
     Emit E{z, op.dst};
-    Emit *ep = EXPAND ? &E : nullptr;
-    fr_t out;
-    switch (op.n) {
-        case 2: out = poseidon_run<3>(pt.t[0], in, ep); break;
-        case 4: out = poseidon_run<5>(pt.t[1], in, ep); break;
-        case 8: out = poseidon_run<9>(pt.t[2], in, ep); break;
-        default: out = poseidon_run<12>(pt.t[3], in, ep); break;
-    }
-    if (!EXPAND) zput_fr(z, op.b, from_mont(out));
+    const fr29_t out = pos_run<T>(k, s, expand ? &E : nullptr);
+    if (!expand) zput_fr(z, op.b, fr_from_fr29(fr29_from_mont(out)));
 }
 
 // ---------------------------------------------------------------------------------------- kernels
 __global__ void __launch_bounds__(64) k_wit_level(const WOp *__restrict__ ops, uint64_t n, const uint8_t *__restrict__ slots,
-                                                  const uint64_t *__restrict__ pin, const ShaBlock *__restrict__ blocks,
-                                                  uint32_t *__restrict__ states, PosTabs pt, fr_t *__restrict__ z) {
+                                                  const ShaBlock *__restrict__ blocks, uint32_t *__restrict__ states,
+                                                  fr_t *__restrict__ z) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const WOp op = ops[i];
@@ -362,7 +358,6 @@ __global__ void __launch_bounds__(64) k_wit_level(const WOp *__restrict__ ops, u
         case W_AND: zput_u32(z, op.dst, zget(z, op.a).v[0] & zget(z, op.b).v[0]); break;
         case W_NOR: zput_u32(z, op.dst, (zget(z, op.a).v[0] | zget(z, op.b).v[0]) ^ 1u); break;
         case W_ADD: zput_fr(z, op.dst, zget(z, op.a) + zget(z, op.b)); break;
-        case W_POSEIDON: poseidon_op<false>(op, pin, pt, z); break;
         case W_SHA: {
             uint32_t st[8];
             for (int q = 0; q < 8; q++) st[q] = kIV[q];
@@ -405,12 +400,24 @@ __global__ void __launch_bounds__(64) k_wit_sha_blocks(const ShaBlock *__restric
     sha_gadget(E, msg, H, wsh);
 }
 
+// Poseidon ops of one arity: phase A (digest only) over ops[0 .. n) or phase B (all variables) over ops[idx[i]]
+template <int T>
 __global__ void __launch_bounds__(64) k_wit_poseidon(const WOp *__restrict__ ops, const uint64_t *__restrict__ idx,
-                                                     uint64_t n, const uint64_t *__restrict__ pin, PosTabs pt,
+                                                     uint64_t n, const uint64_t *__restrict__ pin, PosK k, int expand,
                                                      fr_t *__restrict__ z) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    poseidon_op<true>(ops[idx[i]], pin, pt, z);
+    pos_op_t<T>(ops[idx ? idx[i] : i], pin, k, z, expand != 0);
+}
+void launch_poseidon(int kind, hipStream_t st, const WOp *ops, const uint64_t *idx, uint64_t n, const uint64_t *pin,
+                     const PosKs &pk, int expand, fr_t *z) {
+    const unsigned g = (unsigned)((n + 63) / 64);
+    switch (kind) {
+        case 1: k_wit_poseidon<3><<<g, 64, 0, st>>>(ops, idx, n, pin, pk.k[0], expand, z); break;
+        case 2: k_wit_poseidon<5><<<g, 64, 0, st>>>(ops, idx, n, pin, pk.k[1], expand, z); break;
+        case 3: k_wit_poseidon<9><<<g, 64, 0, st>>>(ops, idx, n, pin, pk.k[2], expand, z); break;
+        default: k_wit_poseidon<12><<<g, 64, 0, st>>>(ops, idx, n, pin, pk.k[3], expand, z); break;
+    }
 }
 
 template <class T>
@@ -431,28 +438,17 @@ DevProg *prog_for(Ctx &c, Built &b) {
         p->ops = upload(b.ops);
         p->pin = upload(b.pin);
         p->blocks = upload(b.blocks);
-        p->pos_ops = upload(b.poseidon_ops);
-        MI_HIP(hipMalloc(&p->states, 32 * (b.blocks.empty() ? 1 : b.blocks.size())));
-        std::vector<fr_t> all;
-        std::vector<size_t> off_rc(4), off_mds(4);
+        std::vector<uint64_t> by;
         const unsigned ar[4] = {2, 4, 8, 11};
-        std::vector<PoseidonHost> hs;
         for (int q = 0; q < 4; q++) {
-            hs.push_back(poseidon_derive(ar[q], poseidon_sbox_field()));
-            off_rc[q] = all.size();
-            for (auto &x : hs[q].plain_rc) all.push_back(to_mont(x));
-            off_mds[q] = all.size();
-            for (auto &x : hs[q].plain_mds) all.push_back(to_mont(x));
+            p->pos_off[q] = by.size();
+            for (uint64_t o : b.poseidon_ops)
+                if (b.ops[o].n == ar[q]) by.push_back(o);
         }
-        p->tabs = upload(all);
-        for (int q = 0; q < 4; q++) {
-            PosTab &t = p->pt.t[q];
-            t.rc = p->tabs + off_rc[q];
-            t.mds = p->tabs + off_mds[q];
-            t.tag = pos_detail::fr_small((1ull << ar[q]) - 1);  // already Montgomery
-            t.rf = hs[q].rf;
-            t.rp = hs[q].rp;
-        }
+        p->pos_off[4] = by.size();
+        p->pos_ops = upload(by);
+        MI_HIP(hipMalloc(&p->states, 32 * (b.blocks.empty() ? 1 : b.blocks.size())));
+        for (int q = 0; q < 4; q++) poseidon_tables(c, ar[q], &p->pk.k[q]);
     } catch (...) {
         delete p;
         throw;
@@ -479,12 +475,18 @@ void witness_dev(Ctx &c, Built &b, const uint8_t *slots_dev, fr_t *z_dev) {
     MI_HIP(hipMemcpyAsync(z_dev, &one, 32, hipMemcpyHostToDevice, st));
     {
         ScopedTimer tm(c, &c.stats.wit_a, b.ops.size());
-        for (size_t L = 0; L + 1 < b.level_off.size(); L++) {
-            const uint64_t o = b.level_off[L], n = b.level_off[L + 1] - o;
-            if (!n) continue;
-            k_wit_level<<<grid64(n), 64, 0, st>>>(p->ops + o, n, slots_dev, p->pin, p->blocks, p->states, p->pt, z_dev);
-            MI_LAUNCHED(c, "k_wit_level");
-        }
+        for (size_t L = 0; L + 1 < b.level_off.size(); L++)
+            for (int kind = 0; kind < 5; kind++) {
+                const uint64_t o = b.seg_off[5 * L + kind], n = b.seg_off[5 * L + kind + 1] - o;
+                if (!n) continue;
+                if (kind == 0) {
+                    k_wit_level<<<grid64(n), 64, 0, st>>>(p->ops + o, n, slots_dev, p->blocks, p->states, z_dev);
+                    MI_LAUNCHED(c, "k_wit_level");
+                } else {
+                    launch_poseidon(kind, st, p->ops + o, nullptr, n, p->pin, p->pk, 0, z_dev);
+                    MI_LAUNCHED(c, "k_wit_poseidon (phase A)");
+                }
+            }
     }
     if (!b.blocks.empty()) {
         ScopedTimer tm(c, &c.stats.wit_sha, b.blocks.size());
@@ -493,9 +495,12 @@ void witness_dev(Ctx &c, Built &b, const uint8_t *slots_dev, fr_t *z_dev) {
     }
     if (!b.poseidon_ops.empty()) {
         ScopedTimer tm(c, &c.stats.wit_pos, b.poseidon_ops.size());
-        k_wit_poseidon<<<grid64(b.poseidon_ops.size()), 64, 0, st>>>(p->ops, p->pos_ops, b.poseidon_ops.size(), p->pin,
-                                                                      p->pt, z_dev);
-        MI_LAUNCHED(c, "k_wit_poseidon");
+        for (int q = 0; q < 4; q++) {
+            const uint64_t n = p->pos_off[q + 1] - p->pos_off[q];
+            if (!n) continue;
+            launch_poseidon(q + 1, st, p->ops, p->pos_ops + p->pos_off[q], n, p->pin, p->pk, 1, z_dev);
+            MI_LAUNCHED(c, "k_wit_poseidon (phase B)");
+        }
     }
     MI_HIP(hipStreamSynchronize(st));
     c.timer.resolve();
