@@ -18,6 +18,7 @@
 #include "poseidon.h"
 #include "poseidon_math.h"
 #include "stacked.h"
+#include "stacked_pos.h"
 
 namespace mi {
 namespace stacked {
@@ -269,63 +270,25 @@ __device__ void sha_gadget(Emit &E, const W3 msg[16], const W3 H[8], W3 (*w)[64]
 }
 
 // ---------------------------------------------------------------------------------------- Poseidon
-// The production permutation (poseidon_math.h: 9 x 29-bit lazy Montgomery limbs, folded constants, sparse
-// partial rounds).  Its S-box inputs are the literal permutation's: the full rounds are literal, and in the
-// partial rounds the sparse factorisation keeps element 0 in the literal basis with its folded constant equal
-// to the literal one (A_k = diag(1, M^k)).  The gadget's variables are functions of those inputs only
-// (v, v^2, v^4, v^5), so the expansion emits them as it goes.
-__device__ __forceinline__ void put29(Emit *E, const fr29_t &x) { zput_fr(E->z, E->k++, fr_from_fr29(fr29_from_mont(x))); }
+struct ZSink {  // writes each emitted variable (canonical) to z
+    fr_t *z;
+    uint64_t k;
+    __device__ __forceinline__ void put(const fr29_t &x) { zput_fr(z, k++, fr_from_fr29(fr29_from_mont(x))); }
+};
 
-template <int T>
-__device__ fr29_t pos_run(const PosK &k, fr29_t (&s)[T], Emit *E) {
-    const fr29_t *img = k.img;
-    const fr29_t *mds = img + k.off_mds;
-    // one S-box on input x; `first`: a first-round S-box (its input is a linear combination, not allocated)
-    auto sbox = [&](const fr29_t &x, bool first) -> fr29_t {
-        const fr29_t x2 = fr29_sqr(x), x4 = fr29_sqr(x2), x5 = fr29_mul(x4, x);
-        if (E) {
-            if (!first) put29(E, x);
-            put29(E, x2);
-            put29(E, x4);
-            put29(E, x5);
-        }
-        return x5;
-    };
-    const int half = k.rf / 2;
-    for (int r = 0; r < half; r++) {
-        const fr29_t *rc = img + k.off_rc_first + r * T;
-        sfor<T>([&](auto i) {
-            const fr29_t x = fr29_add(s[i], rc[i]);
-            s[i] = (r == 0 && i == 0) ? fr29_sbox(x) : sbox(x, r == 0);  // the domain tag's first S-box: constant
-        });
-        mat_apply<T>(s, mds);
-    }
-    const fr29_t *sp = img + k.off_sparse;
-    for (int q = 0; q < k.rp - 1; q++, sp += 2 * T - 1) {
-        s[0] = sbox(fr29_add(s[0], img[k.off_rc_part + q]), false);
-        const fr29_t n0 = fr29_row<T>(sp, s);
-        sfor<T - 1>([&](auto j) { s[j + 1] = fr29_sub_if_ge(fr29_add(s[j + 1], fr29_mul(sp[T + j], s[0])), R2X29); });
-        s[0] = n0;
-    }
-    s[0] = sbox(fr29_add(s[0], img[k.off_rc_part + k.rp - 1]), false);
-    mat_apply<T>(s, img + k.off_dense);
-    for (int r = 0; r < half; r++) {
-        const fr29_t *rc = img + k.off_rc_last + r * T;
-        sfor<T>([&](auto i) { s[i] = sbox(fr29_add(s[i], rc[i]), false); });
-        mat_apply<T>(s, mds);
-    }
-    if (E) put29(E, s[1]);
-    return s[1];
-}
-
-template <int T>
-__device__ void pos_op_t(const WOp &op, const uint64_t *pin, const PosK &k, fr_t *z, bool expand) {
+template <int T, bool EXPAND>
+__device__ __forceinline__ void pos_op_t(const WOp &op, const uint64_t *pin, const PosK &k, fr_t *z) {
+    const fr29_t r2 = k.img[k.off_tag + 1];
     fr29_t s[T];
-    s[0] = k.img[k.off_tag];
-    for (int j = 1; j < T; j++) s[j] = fr29_mul(fr29_from_fr(zget(z, pin[op.a + j - 1])), k.img[k.off_tag + 1]);
-    Emit E{z, op.dst};
-    const fr29_t out = pos_run<T>(k, s, expand ? &E : nullptr);
-    if (!expand) zput_fr(z, op.b, fr_from_fr29(fr29_from_mont(out)));
+    MI_UNROLL for (int l = 0; l < 9; l++) s[0].v[l] = k.img[k.off_tag].v[l];  // limb-wise (a struct copy went to scratch)
+    sfor<T - 1>([&](auto j) { s[j + 1] = fr29_mul(fr29_from_fr(zget(z, pin[op.a + j])), r2); });
+    if (EXPAND) {
+        ZSink E{z, op.dst};
+        pos_run<T, ZSink>(k, s, &E);
+    } else {
+        const fr29_t out = pos_run<T, ZSink>(k, s, nullptr);
+        zput_fr(z, op.b, fr_from_fr29(fr29_from_mont(out)));
+    }
 }
 
 // ---------------------------------------------------------------------------------------- kernels
@@ -400,23 +363,25 @@ __global__ void __launch_bounds__(64) k_wit_sha_blocks(const ShaBlock *__restric
     sha_gadget(E, msg, H, wsh);
 }
 
-// Poseidon ops of one arity: phase A (digest only) over ops[0 .. n) or phase B (all variables) over ops[idx[i]]
-template <int T>
-__global__ void __launch_bounds__(64) k_wit_poseidon(const WOp *__restrict__ ops, const uint64_t *__restrict__ idx,
-                                                     uint64_t n, const uint64_t *__restrict__ pin, PosK k, int expand,
-                                                     fr_t *__restrict__ z) {
+// Poseidon ops of one arity: phase A (digest only) over ops[0 .. n) or phase B (all variables) over ops[idx[i]].
+// Capped at 256 VGPRs (two waves per SIMD): the state spills to scratch for t = 12 rather than using AGPRs.
+template <int T, bool EXPAND>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+k_wit_poseidon(const WOp *__restrict__ ops, const uint64_t *__restrict__ idx, uint64_t n,
+               const uint64_t *__restrict__ pin, PosK k, fr_t *__restrict__ z) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    pos_op_t<T>(ops[idx ? idx[i] : i], pin, k, z, expand != 0);
+    pos_op_t<T, EXPAND>(ops[EXPAND ? idx[i] : i], pin, k, z);
 }
+template <bool EXPAND>
 void launch_poseidon(int kind, hipStream_t st, const WOp *ops, const uint64_t *idx, uint64_t n, const uint64_t *pin,
-                     const PosKs &pk, int expand, fr_t *z) {
+                     const PosKs &pk, fr_t *z) {
     const unsigned g = (unsigned)((n + 63) / 64);
     switch (kind) {
-        case 1: k_wit_poseidon<3><<<g, 64, 0, st>>>(ops, idx, n, pin, pk.k[0], expand, z); break;
-        case 2: k_wit_poseidon<5><<<g, 64, 0, st>>>(ops, idx, n, pin, pk.k[1], expand, z); break;
-        case 3: k_wit_poseidon<9><<<g, 64, 0, st>>>(ops, idx, n, pin, pk.k[2], expand, z); break;
-        default: k_wit_poseidon<12><<<g, 64, 0, st>>>(ops, idx, n, pin, pk.k[3], expand, z); break;
+        case 1: k_wit_poseidon<3, EXPAND><<<g, 64, 0, st>>>(ops, idx, n, pin, pk.k[0], z); break;
+        case 2: k_wit_poseidon<5, EXPAND><<<g, 64, 0, st>>>(ops, idx, n, pin, pk.k[1], z); break;
+        case 3: k_wit_poseidon<9, EXPAND><<<g, 64, 0, st>>>(ops, idx, n, pin, pk.k[2], z); break;
+        default: k_wit_poseidon<12, EXPAND><<<g, 64, 0, st>>>(ops, idx, n, pin, pk.k[3], z); break;
     }
 }
 
@@ -483,7 +448,7 @@ void witness_dev(Ctx &c, Built &b, const uint8_t *slots_dev, fr_t *z_dev) {
                     k_wit_level<<<grid64(n), 64, 0, st>>>(p->ops + o, n, slots_dev, p->blocks, p->states, z_dev);
                     MI_LAUNCHED(c, "k_wit_level");
                 } else {
-                    launch_poseidon(kind, st, p->ops + o, nullptr, n, p->pin, p->pk, 0, z_dev);
+                    launch_poseidon<false>(kind, st, p->ops + o, nullptr, n, p->pin, p->pk, z_dev);
                     MI_LAUNCHED(c, "k_wit_poseidon (phase A)");
                 }
             }
@@ -498,7 +463,7 @@ void witness_dev(Ctx &c, Built &b, const uint8_t *slots_dev, fr_t *z_dev) {
         for (int q = 0; q < 4; q++) {
             const uint64_t n = p->pos_off[q + 1] - p->pos_off[q];
             if (!n) continue;
-            launch_poseidon(q + 1, st, p->ops, p->pos_ops + p->pos_off[q], n, p->pin, p->pk, 1, z_dev);
+            launch_poseidon<true>(q + 1, st, p->ops, p->pos_ops + p->pos_off[q], n, p->pin, p->pk, z_dev);
             MI_LAUNCHED(c, "k_wit_poseidon (phase B)");
         }
     }

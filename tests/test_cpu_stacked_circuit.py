@@ -144,3 +144,31 @@ def test_instance_slots_layout():
     with pytest.raises(ValueError):
         stacked.instance_slots(c, inst["replica_id"], inst["comm_d"], inst["comm_r"], inst["comm_r_last"],
                                inst["comm_c"], inst["challenges"] * 2)
+
+
+def test_poseidon_gadget_emission_on_host(tmp_path):
+    """The GPU witness emits the Poseidon gadget's variables from the production sparse 29-bit permutation
+    (csrc/stacked_pos.h): compiled for the host, its emission equals a literal evaluation of the same variables
+    for every arity, and the variable counts equal the constraint counts 311 / 377 / 505 / 598."""
+    import os
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    exe = str(tmp_path / "stacked_pos_check")
+    subprocess.run([hipcc, "-x", "hip", "--offload-host-only", "-std=c++17", "-O1", "-w", "-I",
+                    os.path.join(root, "crypto3-fil-proofs_amd", "csrc"),
+                    os.path.join(root, "tests", "host", "stacked_pos_check.cpp"), "-o", exe],
+                   check=True, capture_output=True, timeout=600)
+    rng = random.Random(4)
+    R = fg.FR_MODULUS
+    lines, want = [], []
+    for a, n in ((2, 311), (4, 377), (8, 505), (11, 598)):
+        for xs in ([0] * a, [R - 1] * a, [rng.randrange(R) for _ in range(a)]):
+            lines.append(" ".join([str(a)] + ["%x" % x for x in xs]))
+            want.append(f"{n} ok")
+    r = subprocess.run([exe], input="\n".join(lines) + "\n", capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip().split("\n") == want
