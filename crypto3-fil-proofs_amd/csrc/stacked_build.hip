@@ -1089,6 +1089,43 @@ Built *build(const Shape &s, bool want_r1cs) {
         b->seg_off.assign(5 * (maxl + 1) + 1, 0);
         for (auto &op : b->ops) b->seg_off[5 * op.level + kind(op) + 1]++;
         for (size_t q = 0; q + 1 < b->seg_off.size(); q++) b->seg_off[q + 1] += b->seg_off[q];
+        for (uint32_t l = 0; l <= maxl; l++)  // every (level, kind) segment holds exactly its ops
+            for (uint32_t k = 0; k < 5; k++)
+                for (uint64_t i = b->seg_off[5 * l + k]; i < b->seg_off[5 * l + k + 1]; i++)
+                    if (b->ops[i].level != l || kind(b->ops[i]) != k) throw std::logic_error("stacked: op segment");
+        if (b->seg_off.back() != n) throw std::logic_error("stacked: op segments do not cover the program");
+        for (uint64_t o : b->poseidon_ops)
+            if (o >= n || b->ops[o].type != W_POSEIDON) throw std::logic_error("stacked: Poseidon op list");
+        for (const ShaBlock &blk : b->blocks)
+            if (blk.op >= n || b->ops[blk.op].type != W_SHA) throw std::logic_error("stacked: SHA block owner");
+        // every variable is written by exactly one op (the witness program covers z)
+        {
+            std::vector<uint8_t> hit(b->n_in + b->n_aux, 0);
+            hit[0] = 1;
+            auto mark = [&](uint64_t z0, uint64_t cnt) {
+                if (z0 + cnt > hit.size()) throw std::logic_error("stacked: op writes past z");
+                for (uint64_t q = 0; q < cnt; q++) {
+                    if (hit[z0 + q]) throw std::logic_error("stacked: variable written twice");
+                    hit[z0 + q] = 1;
+                }
+            };
+            std::vector<uint64_t> pos_vars(12, 0);
+            for (unsigned a : {2u, 4u, 8u, 11u}) pos_vars[a] = poseidon_constraints(a);
+            for (const WOp &op : b->ops) switch (op.type) {
+                    case W_BITS: case W_DBITS: mark(op.dst, op.n); break;
+                    case W_POSEIDON: mark(op.dst, pos_vars[op.n]); break;
+                    case W_SHA: mark(op.b, 1); break;
+                    default: mark(op.dst, 1); break;
+                }
+            for (size_t k = 0; k < b->blocks.size(); k++) {
+                const uint64_t end = k + 1 < b->blocks.size() && b->blocks[k + 1].op == b->blocks[k].op
+                                         ? b->blocks[k + 1].base
+                                         : b->ops[b->blocks[k].op].b;  // the block's variables run to the next block or the pack
+                mark(b->blocks[k].base, end - b->blocks[k].base);
+            }
+            for (size_t q = 0; q < hit.size(); q++)
+                if (!hit[q]) throw std::logic_error("stacked: variable " + std::to_string(q) + " has no producer");
+        }
     } catch (...) {
         delete b;
         throw;
