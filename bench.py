@@ -625,6 +625,8 @@ def main():
     log(rank, f"setup: synth {t_synth:.1f}s circuit load {t_load:.1f}s srs {'load' if args.params else 'gen'} "
               f"{t_srs:.1f}s; n={n} d={circ.d} |a|={circ.n_a} |b|={circ.n_b}")
 
+    # MI_BENCH_PRIORITY=1: the main leg on the context's high-priority stream (lane A/B)
+    prio = os.environ.get("MI_BENCH_PRIORITY") == "1"
     P = args.partitions
     mine = shard_partitions(P, rank, world) if P else [rank]
     per_step = len(mine)
@@ -636,7 +638,7 @@ def main():
 
     if args.warmup:
         fg.prove_batch(ctx, pk, circ, [zhost] * (args.warmup * per_step),
-                       [blinding(w, p) for w in range(args.warmup) for p in mine])
+                       [blinding(w, p) for w in range(args.warmup) for p in mine], priority=prio)
     ctx.synchronize()
     if dist:
         dist.barrier()
@@ -650,13 +652,14 @@ def main():
         for k in range(args.steps):
             step = args.warmup + k
             multiproofs.append(prove_partitions(
-                lambda ids: fg.prove_batch(ctx, pk, circ, [zhost] * len(ids), [blinding(step, p) for p in ids]),
+                lambda ids: fg.prove_batch(ctx, pk, circ, [zhost] * len(ids), [blinding(step, p) for p in ids],
+                                           priority=prio),
                 P, rank, world, gdev))
         proofs = [mp_[192 * i:192 * (i + 1)] for mp_ in multiproofs for i in range(P)]
     else:
         # K partitions of this rank in one batch: partition k + 1's upload overlaps proof k
         local = fg.prove_batch(ctx, pk, circ, [zhost] * args.steps,
-                               [blinding(args.warmup + k, rank) for k in range(args.steps)])
+                               [blinding(args.warmup + k, rank) for k in range(args.steps)], priority=prio)
         # MultiProof assembly: every rank's proofs gathered in (step, rank) order over RCCL
         proofs = gather_multiproof(local, args.steps * world, rank, world, gdev) if dist else b"".join(local)
         proofs = [proofs[192 * i:192 * (i + 1)] for i in range(len(proofs) // 192)]

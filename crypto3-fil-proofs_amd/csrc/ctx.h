@@ -218,6 +218,11 @@ void bitrev_permute(Ctx &c, fr_t *d, unsigned log_n);
 // iNTT -> coset shift * scale -> NTT in natural order (a, b, c of the QAP), one pass fewer than the
 // two transforms separately
 void ntt_coset_roundtrip(Ctx &c, fr_t *d, unsigned log_n, const fr_t &scale);
+// The QAP tail with a and b already through ntt_coset_roundtrip: cc's coset roundtrip whose last pass also
+// forms h = (a b - cc) zinv and runs the first pass of h's inverse coset transform, then the rest of that
+// transform with scale and the canonical epilogue: a <- H (bit-reversed, canonical), cc clobbered.
+// Returns false (nothing launched) when the domain takes a single pass (log_n <= 10).
+bool ntt_coset_qap(Ctx &c, fr_t *a, const fr_t *b, fr_t *cc, unsigned log_n, const fr_t &scale, const fr_t &zinv);
 void ntt_dif_coset_epilogue(Ctx &c, fr_t *d, unsigned log_n, bool inverse, bool inverse_gen, const fr_t &scale,
                             bool to_canonical);
 // d[pos] *= g^(±bitrev(pos)) * scale (scale may be null)

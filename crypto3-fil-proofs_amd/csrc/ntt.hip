@@ -267,6 +267,56 @@ __global__ void __launch_bounds__(NTT_THREADS) MI_NTT_OCC k_ntt_pass(fr_t *__res
     }
 }
 
+// The outermost pass of the QAP chain, fused (bellman's prover runs
+// coset_fft(c), a = (a b - c) / Z, icoset_fft(a) as separate sweeps): the tile positions of the last DIT
+// pass of c's coset transform are exactly those of the first DIF pass of H's inverse coset transform (pass
+// 0 of the same plan), so one workgroup loads c's tile, finishes its coset NTT in LDS, reads a and b at
+// the same positions (their coset evaluations are final), forms h = (a b - c) zinv, runs the first
+// inverse-transform rounds and writes h over a.  One HBM sweep and the separate division pass fewer per
+// proof; a is read before it is written by the same workgroup only.
+__global__ void __launch_bounds__(NTT_THREADS) MI_NTT_OCC k_ntt_qap(fr_t *__restrict__ ha, const fr_t *__restrict__ bv,
+                                                         const fr_t *__restrict__ cv, unsigned L, unsigned b,
+                                                         unsigned Tlog, const fr29_t *__restrict__ flo,
+                                                         const fr29_t *__restrict__ fhi,
+                                                         const fr29_t *__restrict__ ftw10,
+                                                         const fr29_t *__restrict__ ilo,
+                                                         const fr29_t *__restrict__ ihi,
+                                                         const fr29_t *__restrict__ itw10, fr_t zinv) {
+    __shared__ LdsTile sh;
+    const unsigned tsh = TILE_LOG - b;
+    const fr29_t z29 = fr29_from_fr(zinv);
+    const unsigned T = 1u << Tlog;
+    const unsigned Slog = L - b;  // M = L: one sub-problem, Glog = 0 (plan_passes with two or more passes)
+    const unsigned tile = 1u << (b + Tlog);
+    const uint64_t i20 = (uint64_t)blockIdx.x << Tlog;
+    const unsigned bmask = (1u << b) - 1;
+    for (unsigned e = threadIdx.x; e < tile; e += NTT_THREADS) {  // c, DIT inter-pass twiddle
+        const unsigned t = e & (T - 1), i1 = (e >> Tlog) & bmask;
+        const uint64_t gi = ((uint64_t)i1 << Slog) + i20 + t;
+        fr29_t x = f29(cv[gi]);
+        const uint32_t ex = (uint32_t)(((i20 + t) * brev(i1, b)) << (32 - L));
+        if (ex) x = fr29_mul(x, tw29(flo, fhi, ex));
+        lds_put(sh, e, x);
+    }
+    __syncthreads();
+    ntt_rounds<false>(sh, b, Tlog, tile, ftw10, tsh);
+    for (unsigned e = threadIdx.x; e < tile; e += NTT_THREADS) {  // h = (a b - c) / Z on the coset
+        const unsigned t = e & (T - 1), i1 = (e >> Tlog) & bmask;
+        const uint64_t gi = ((uint64_t)i1 << Slog) + i20 + t;
+        const fr29_t ab = fr29_mul(f29(ha[gi]), f29(bv[gi]));               // < 2r
+        lds_put(sh, e, fr29_mul(fr29_sub_lazy(ab, lds_get(sh, e), R2X29), z29));  // (< 4r) z -> < 2r
+    }
+    __syncthreads();
+    ntt_rounds<true>(sh, b, Tlog, tile, itw10, tsh);
+    for (unsigned e = threadIdx.x; e < tile; e += NTT_THREADS) {  // DIF inter-pass twiddle, store over a
+        const unsigned t = e & (T - 1), i1 = (e >> Tlog) & bmask;
+        const uint64_t gi = ((uint64_t)i1 << Slog) + i20 + t;
+        fr29_t x = lds_get(sh, e);
+        const uint32_t ex = (uint32_t)(((i20 + t) * brev(i1, b)) << (32 - L));
+        if (ex) x = fr29_mul(x, tw29(ilo, ihi, ex));
+        ha[gi] = to_fr(x);
+    }
+}
 
 struct PassPlan {
     unsigned M, b, Tlog, Glog;
@@ -423,7 +473,7 @@ void ntt_free_tables(Ctx &c) {
 }
 
 static void ntt_run(Ctx &c, fr_t *d, unsigned L, bool inverse, bool dif, int epi = 0, bool inv_gen = false,
-                    const fr_t &scale = fr_t::one()) {
+                    const fr_t &scale = fr_t::one(), size_t first_pass = 0) {
     if (L > 32) throw std::runtime_error("ntt: domain larger than 2^32");
     if (L == 0) {
         if (epi) {  // single element: coset factor g^0 = 1
@@ -439,7 +489,7 @@ static void ntt_run(Ctx &c, fr_t *d, unsigned L, bool inverse, bool dif, int epi
     const fr29_t *tw10 = inverse ? c.tw.iv_1024 : c.tw.fw_1024;
     auto plan = plan_passes(L);
     if (dif) {
-        for (size_t i = 0; i < plan.size(); i++) {
+        for (size_t i = first_pass; i < plan.size(); i++) {
             auto &p = plan[i];
             int e = (i + 1 == plan.size()) ? epi : 0;
             k_ntt_pass<true><<<(unsigned)p.blocks, NTT_THREADS, 0, c.stream>>>(d, L, p.M, p.b, p.Tlog, p.Glog,
@@ -489,6 +539,44 @@ void ntt_coset_roundtrip(Ctx &c, fr_t *d, unsigned L, const fr_t &scale) {
                                                                               c.tw.lo29[2], c.tw.hi29[2], scale);
     }
     MI_HIP(hipGetLastError());
+}
+
+bool ntt_coset_qap(Ctx &c, fr_t *a, const fr_t *b, fr_t *cc, unsigned L, const fr_t &scale, const fr_t &zinv) {
+    if (L > 32) throw std::runtime_error("ntt: domain larger than 2^32");
+    auto plan = plan_passes(L);
+    if (plan.size() < 2) return false;  // one pass: the caller runs the unfused chain
+    {
+        ScopedTimer tm(c, &c.stats.ntt, 1ull << L);
+        const size_t last = plan.size() - 1;
+        for (size_t i = 0; i < last; i++) {
+            auto &p = plan[i];
+            k_ntt_pass<true><<<(unsigned)p.blocks, NTT_THREADS, 0, c.stream>>>(cc, L, p.M, p.b, p.Tlog, p.Glog, p.twiddle,
+                                                                                 c.tw.lo29[1], c.tw.hi29[1], c.tw.iv_1024,
+                                                                                 0, c.tw.lo29[2], c.tw.hi29[2], scale);
+        }
+        {
+            auto &p = plan[last];
+            k_ntt_pass<true, true><<<(unsigned)p.blocks, NTT_THREADS, 0, c.stream>>>(
+                cc, L, p.M, p.b, p.Tlog, p.Glog, 0, c.tw.lo29[1], c.tw.hi29[1], c.tw.iv_1024, 1, c.tw.lo29[2],
+                c.tw.hi29[2], scale, c.tw.fw_1024);
+        }
+        for (size_t i = last - 1; i >= 1; i--) {
+            auto &p = plan[i];
+            k_ntt_pass<false><<<(unsigned)p.blocks, NTT_THREADS, 0, c.stream>>>(cc, L, p.M, p.b, p.Tlog, p.Glog,
+                                                                                  p.twiddle, c.tw.lo29[0], c.tw.hi29[0],
+                                                                                  c.tw.fw_1024, 0, c.tw.lo29[2],
+                                                                                  c.tw.hi29[2], scale);
+        }
+        auto &p0 = plan[0];
+        if (p0.M != L || p0.Glog != 0 || !p0.twiddle) throw std::logic_error("ntt: unexpected outer pass shape");
+        k_ntt_qap<<<(unsigned)p0.blocks, NTT_THREADS, 0, c.stream>>>(a, b, cc, L, p0.b, p0.Tlog, c.tw.lo29[0],
+                                                                     c.tw.hi29[0], c.tw.fw_1024, c.tw.lo29[1],
+                                                                     c.tw.hi29[1], c.tw.iv_1024, zinv);
+        MI_HIP(hipGetLastError());
+    }
+    // the rest of H's inverse coset transform: passes 1.. with the icoset epilogue (canonical output)
+    ntt_run(c, a, L, true, true, 2, true, scale, 1);
+    return true;
 }
 
 void ntt_dif_coset_epilogue(Ctx &c, fr_t *d, unsigned log_n, bool inverse, bool inverse_gen, const fr_t &scale,

@@ -945,14 +945,22 @@ ProofSums groth16_sums(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *
             dd.v[0] = (uint32_t)d;
             dd.v[1] = (uint32_t)(d >> 32);
             fr_t dinv = inverse(to_mont(dd));
-            fr_t *vecs[3] = {a, b, cc};
-            for (fr_t *v : vecs) {
-                ntt_coset_roundtrip(c, v, L, dinv);  // ifft, * g^i / d, fft on the coset (natural order)
-            }
             fr_t g = fr_small_mont(7);
             fr_t zinv = inverse(pow_u64(g, d) - fr_t::one());
-            k_qap_divide<<<grid1(d), 256, 0, st>>>(a, b, cc, d, zinv);
-            ntt_dif_coset_epilogue(c, a, L, true, true, dinv, true);  // icoset, canonical H (bit-reversed order)
+            // ifft, * g^i / d, fft on the coset (natural order) for a and b; c's last pass also forms
+            // (a b - c) / Z and starts the inverse coset transform (ntt_coset_qap); MI_QAP_FUSED=0 runs
+            // the separate division pass (A/B)
+            static const bool qap_fused = [] {
+                const char *e = getenv("MI_QAP_FUSED");
+                return !(e && atoi(e) == 0);
+            }();
+            ntt_coset_roundtrip(c, a, L, dinv);
+            ntt_coset_roundtrip(c, b, L, dinv);
+            if (!qap_fused || !ntt_coset_qap(c, a, b, cc, L, dinv, zinv)) {
+                ntt_coset_roundtrip(c, cc, L, dinv);
+                k_qap_divide<<<grid1(d), 256, 0, st>>>(a, b, cc, d, zinv);
+                ntt_dif_coset_epilogue(c, a, L, true, true, dinv, true);  // icoset, canonical H (bit-reversed)
+            }
             uint64_t h_lo, h_cnt = slice(d - 1, h_lo), a_lo, a_cnt = slice(circ.n_a, a_lo);
             msm_g1(c, srs.h_perm + h_lo, a + h_lo, nullptr, h_cnt, &H, srs.h_hi ? srs.h_hi + h_lo : nullptr,
                    srs.in_subgroup);
@@ -1041,7 +1049,14 @@ Ctx &ctx_aux(Ctx &c) {
     int prio = 0, lo = 0, hi = 0;
     MI_HIP(hipStreamGetPriority(c.stream, &prio));
     MI_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    c.aux->stream = (prio == hi && hi != lo) ? c.aux->aux_streams[1] : c.aux->aux_streams[0];
+    // the auxiliary lane follows the caller's priority; MI_LANE_PRIO=aux puts it above a normal main lane,
+    // MI_LANE_PRIO=main keeps it normal under a high-priority main lane (lane-contention A/B)
+    static const int lane_prio = [] {
+        const char *e = getenv("MI_LANE_PRIO");
+        return !e ? 0 : strcmp(e, "aux") == 0 ? 1 : strcmp(e, "main") == 0 ? 2 : 0;
+    }();
+    const bool aux_hi = lane_prio == 1 ? true : lane_prio == 2 ? false : (prio == hi && hi != lo);
+    c.aux->stream = aux_hi ? c.aux->aux_streams[1] : c.aux->aux_streams[0];
     return *c.aux;
 }
 
