@@ -65,6 +65,7 @@ struct mi_srs {
 };
 struct mi_stacked {
     mi::stacked::Built *b;
+    std::vector<mi::fr_t> full[3];  // 32-byte coefficients, materialised on the first mi_stacked_r1cs
 };
 struct mi_srs_stream {
     mi::SrsStream *p;
@@ -1042,6 +1043,21 @@ int mi_stacked_build(const mi_stacked_shape *sh, int with_r1cs, mi_stacked **out
         *out = new mi_stacked{mi::stacked::build(s, with_r1cs != 0)};
     });
 }
+int mi_post_build(const mi_post_shape *sh, int with_r1cs, mi_stacked **out) {
+    return guard([&] {
+        need(sh && out, "null argument");
+        need(sh->sectors > 0, "at least one sector");
+        mi::stacked::Shape s;
+        s.sectors = sh->sectors;
+        s.layers = 0;
+        s.challenges = sh->challenges;
+        s.nodes = sh->nodes;
+        s.base = sh->base_arity;
+        s.sub = sh->sub_arity;
+        s.top = sh->top_arity;
+        *out = new mi_stacked{mi::stacked::build(s, with_r1cs != 0)};
+    });
+}
 int mi_stacked_info(const mi_stacked *s, uint64_t out[12]) {
     return guard([&] {
         need(s && out, "null argument");
@@ -1057,14 +1073,35 @@ int mi_stacked_r1cs(const mi_stacked *s, mi_r1cs *out) {
         need(s && out, "null argument");
         const mi::stacked::Built &b = *s->b;
         need(b.rp[0].size() == b.n_constraints + 1, "circuit was built without its R1CS (with_r1cs = 0)");
+        mi_stacked *w = const_cast<mi_stacked *>(s);
+        for (int m = 0; m < 3; m++)
+            if (w->full[m].size() != b.cidx[m].size()) {
+                w->full[m].resize(b.cidx[m].size());
+                for (size_t e = 0; e < b.cidx[m].size(); e++) w->full[m][e] = b.ctab[b.cidx[m][e]];
+            }
         out->num_constraints = b.n_constraints;
         out->num_inputs = b.n_in;
         out->num_aux = b.n_aux;
         for (int m = 0; m < 3; m++) {
             out->row_ptr[m] = b.rp[m].data();
             out->col[m] = b.col[m].data();
-            out->coeff[m] = (const uint8_t *)b.coeff[m].data();
+            out->coeff[m] = (const uint8_t *)w->full[m].data();
         }
+    });
+}
+int mi_stacked_load(mi_ctx *ctx, const mi_stacked *s, mi_circuit **out) {
+    return guard([&] {
+        need(ctx && s && out, "null argument");
+        const mi::stacked::Built &b = *s->b;
+        need(b.rp[0].size() == b.n_constraints + 1, "circuit was built without its R1CS (with_r1cs = 0)");
+        CtxLock l(ctx);
+        mi::R1csCompact cc{b.n_constraints, b.n_in, b.n_aux, {}, {}, {}, b.ctab.data(), b.ctab.size()};
+        for (int m = 0; m < 3; m++) {
+            cc.row_ptr[m] = b.rp[m].data();
+            cc.col[m] = b.col[m].data();
+            cc.cidx[m] = b.cidx[m].data();
+        }
+        *out = new mi_circuit{mi::circuit_load_compact(ctx->c, cc), ctx->c.device};
     });
 }
 static void stacked_check_slots(const mi::stacked::Built &b, const uint8_t *slots) {
@@ -1072,9 +1109,17 @@ static void stacked_check_slots(const mi::stacked::Built &b, const uint8_t *slot
     for (uint64_t q = 0; q < L.slots; q++)
         need(!mi::geq_raw(mi::fr_from_le(slots + 32 * q), mi::fr_t::modulus_raw()),
              "instance slot " + std::to_string(q) + " is not a canonical Fr element");
-    for (unsigned c = 0; c < b.shape.challenges; c++) {
-        std::vector<uint64_t> idx{L.ch_base(c)};
-        for (unsigned p = 0; p < 14; p++) idx.push_back(L.ch_base(c) + L.off_parent(p, b.shape.layers));
+    std::vector<uint64_t> idx;  // slots holding node indices
+    if (b.shape.sectors) {
+        for (uint64_t s = 0; s < b.shape.sectors; s++)
+            for (unsigned n = 0; n < b.shape.challenges; n++) idx.push_back(L.post_challenge(s, n));
+    } else {
+        for (unsigned c = 0; c < b.shape.challenges; c++) {
+            idx.push_back(L.ch_base(c));
+            for (unsigned p = 0; p < 14; p++) idx.push_back(L.ch_base(c) + L.off_parent(p, b.shape.layers));
+        }
+    }
+    {
         for (uint64_t q : idx) {
             uint64_t v;
             memcpy(&v, slots + 32 * q, 8);

@@ -16,7 +16,14 @@ struct Circuit {
     uint64_t nnz[3] = {0, 0, 0};
     uint64_t *row_ptr[3] = {nullptr, nullptr, nullptr};
     uint32_t *col[3] = {nullptr, nullptr, nullptr};
-    fr_t *coeff[3] = {nullptr, nullptr, nullptr};  // Montgomery
+    // entry e of matrix m has coefficient ctab[cidx[m][e]] (Montgomery; ctab[0] = 1): 8 bytes per entry
+    uint32_t *cidx[3] = {nullptr, nullptr, nullptr};
+    fr_t *ctab = nullptr;
+    uint64_t n_ctab = 0;
+    // witness-map work units (k_eval_blocks): block i of matrix m = rows [blk[m][i], blk[m][i + 1]), at most
+    // EVAL_BLOCK entries and rows, or one longer row alone
+    uint32_t *blk[3] = {nullptr, nullptr, nullptr};
+    uint64_t n_blk[3] = {0, 0, 0};
     // density index lists into z (bellman a_aux_density / b_input_density / b_aux_density)
     uint32_t *idx_a = nullptr, *idx_b = nullptr;
     uint64_t n_a = 0, n_b = 0, n_b_in = 0;
@@ -54,7 +61,18 @@ struct R1csHost {
     const uint8_t *coeff[3];
 };
 
-Circuit *circuit_load(Ctx &c, const R1csHost &cs);
+// the same R1CS with its coefficients as indices into a table of distinct canonical values (ctab[0] = 1):
+// the form the circuit builders produce (stacked.h Built)
+struct R1csCompact {
+    uint64_t n, n_in, n_aux;
+    const uint64_t *row_ptr[3];
+    const uint32_t *col[3];
+    const uint32_t *cidx[3];
+    const fr_t *ctab;  // canonical raw
+    uint64_t n_ctab;
+};
+Circuit *circuit_load(Ctx &c, const R1csHost &cs);  // interns the coefficients, then circuit_load_compact
+Circuit *circuit_load_compact(Ctx &c, const R1csCompact &cs);
 // rows j < n with (A z)_j (B z)_j != (C z)_j (z canonical, device); *first_bad = the first such row or ~0
 uint64_t circuit_check(Ctx &c, const Circuit &C, const fr_t *z_dev, uint64_t *first_bad);
 

@@ -18,7 +18,9 @@
 
 #include <exception>
 #include <cstring>
+#include <string>
 #include <thread>
+#include <unordered_map>
 
 #include "prover.h"
 
@@ -35,40 +37,97 @@ fr_t fr_small_mont(uint32_t v) {
 }
 
 // ------------------------------------------------------------------------------ witness map
-__global__ void k_eval_rows(const uint64_t *__restrict__ rp0, const uint32_t *__restrict__ c0,
-                            const fr_t *__restrict__ k0, const uint64_t *__restrict__ rp1,
-                            const uint32_t *__restrict__ c1, const fr_t *__restrict__ k1,
-                            const uint64_t *__restrict__ rp2, const uint32_t *__restrict__ c2,
-                            const fr_t *__restrict__ k2, const fr_t *__restrict__ zm, uint64_t n, uint64_t n_in,
-                            uint64_t d, fr_t *__restrict__ a, fr_t *__restrict__ b, fr_t *__restrict__ c) {
-    uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= d) return;
-    fr_t va = fr_t::zero(), vb = fr_t::zero(), vc = fr_t::zero();
-    if (j < n) {
-        for (uint64_t e = rp0[j]; e < rp0[j + 1]; e++) va = va + k0[e] * zm[c0[e]];
-        for (uint64_t e = rp1[j]; e < rp1[j + 1]; e++) vb = vb + k1[e] * zm[c1[e]];
-        for (uint64_t e = rp2[j]; e < rp2[j + 1]; e++) vc = vc + k2[e] * zm[c2[e]];
-    } else if (j < n + n_in) {
-        va = zm[j - n];
+// (A z)_j, (B z)_j, (C z)_j for j < n, one matrix per launch.  Real circuits mix rows of 1-3 terms with
+// rows of hundreds (SHA-256 packing, bit decompositions, the Poseidon gadget's linear combinations): one
+// thread per row left most lanes of a wave idle behind its longest row (the stacked circuit's A matrix:
+// 23x the useful work).  So a wave takes a block of consecutive rows holding <= EVAL_BLOCK entries (and
+// rows): its lanes form the products entry-parallel (coalesced col / cidx loads, coefficient table in L2,
+// the multiplication skipped for coefficient 1) into LDS, then sum their rows from LDS.  A row with more
+// entries is a block of its own, reduced across the wave.
+constexpr unsigned EVAL_BLOCK = 256;  // entries (and rows) per wave block: 4 per lane
+
+__device__ __forceinline__ fr_t eval_term(const uint32_t *__restrict__ col, const uint32_t *__restrict__ cidx,
+                                          const fr_t *__restrict__ ctab, const fr_t *__restrict__ zm, uint64_t e) {
+    const uint32_t ci = cidx[e];
+    const fr_t zv = zm[col[e]];
+    return ci == 0 ? zv : ctab[ci] * zv;
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ void __launch_bounds__(256) k_eval_blocks(const uint64_t *__restrict__ rp, const uint32_t *__restrict__ col,
+                                                     const uint32_t *__restrict__ cidx, const fr_t *__restrict__ ctab,
+                                                     const fr_t *__restrict__ zm, const uint32_t *__restrict__ blk,
+                                                     uint64_t nblk, fr_t *__restrict__ out) {
+    __shared__ fr_t prod[4][EVAL_BLOCK];
+    const unsigned w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t b = (uint64_t)blockIdx.x * 4 + w;
+    if (b >= nblk) return;  // whole waves only: no workgroup barrier below
+    const uint32_t r0 = blk[b], r1 = blk[b + 1];
+    const uint64_t e0 = rp[r0], e1 = rp[r1];
+    if (e1 - e0 > EVAL_BLOCK) {  // one long row: lane partial sums, then a butterfly across the wave
+        fr_t acc = fr_t::zero();
+        for (uint64_t e = e0 + lane; e < e1; e += 64) acc = acc + eval_term(col, cidx, ctab, zm, e);
+        MI_UNROLL for (int off = 32; off >= 1; off >>= 1) {
+            fr_t o;
+            MI_UNROLL for (int i = 0; i < 8; i++) o.v[i] = __shfl_xor(acc.v[i], off, 64);
+            acc = acc + o;
+        }
+        if (lane == 0) out[r0] = acc;
+        return;
     }
-    a[j] = va;
-    b[j] = vb;
-    c[j] = vc;
+    fr_t *p = prod[w];
+    MI_UNROLL for (unsigned k = 0; k < EVAL_BLOCK / 64; k++) {
+        const uint64_t e = e0 + lane + 64 * k;
+        if (e < e1) p[lane + 64 * k] = eval_term(col, cidx, ctab, zm, e);
+    }
+    wave_lds_sync();
+    for (uint32_t r = r0 + lane; r < r1; r += 64) {
+        const uint32_t lo = (uint32_t)(rp[r] - e0), hi = (uint32_t)(rp[r + 1] - e0);
+        fr_t s = fr_t::zero();
+        for (uint32_t q = lo; q < hi; q++) s = s + p[q];
+        out[r] = s;
+    }
+}
+
+// rows n .. d - 1: the input rows (A = z_i, bellman's input constraints) and the zero padding
+__global__ void k_eval_tail(const fr_t *__restrict__ zm, uint64_t n, uint64_t n_in, uint64_t d, fr_t *__restrict__ a,
+                            fr_t *__restrict__ b, fr_t *__restrict__ c) {
+    const uint64_t j = n + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= d) return;
+    a[j] = j < n + n_in ? zm[j - n] : fr_t::zero();
+    b[j] = fr_t::zero();
+    c[j] = fr_t::zero();
+}
+
+void eval_witness_map(Ctx &c, const Circuit &C, const fr_t *zm, fr_t *a, fr_t *b, fr_t *cc) {
+    fr_t *outs[3] = {a, b, cc};
+    for (int m = 0; m < 3; m++)
+        if (C.n_blk[m])
+            k_eval_blocks<<<(unsigned)((C.n_blk[m] + 3) / 4), 256, 0, c.stream>>>(
+                C.row_ptr[m], C.col[m], C.cidx[m], C.ctab, zm, C.blk[m], C.n_blk[m], outs[m]);
+    if (C.d > C.n)
+        k_eval_tail<<<(unsigned)((C.d - C.n + 255) / 256), 256, 0, c.stream>>>(zm, C.n, C.n_in, C.d, a, b, cc);
+    MI_HIP(hipGetLastError());
 }
 
 // R1CS satisfaction: rows j with (A z)_j (B z)_j != (C z)_j counted, the first one kept
 __global__ void k_check_rows(const uint64_t *__restrict__ rp0, const uint32_t *__restrict__ c0,
-                             const fr_t *__restrict__ k0, const uint64_t *__restrict__ rp1,
-                             const uint32_t *__restrict__ c1, const fr_t *__restrict__ k1,
+                             const uint32_t *__restrict__ k0, const uint64_t *__restrict__ rp1,
+                             const uint32_t *__restrict__ c1, const uint32_t *__restrict__ k1,
                              const uint64_t *__restrict__ rp2, const uint32_t *__restrict__ c2,
-                             const fr_t *__restrict__ k2, const fr_t *__restrict__ zm, uint64_t n,
-                             unsigned long long *__restrict__ out) {
+                             const uint32_t *__restrict__ k2, const fr_t *__restrict__ ctab,
+                             const fr_t *__restrict__ zm, uint64_t n, unsigned long long *__restrict__ out) {
     uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
     fr_t va = fr_t::zero(), vb = fr_t::zero(), vc = fr_t::zero();
-    for (uint64_t e = rp0[j]; e < rp0[j + 1]; e++) va = va + k0[e] * zm[c0[e]];
-    for (uint64_t e = rp1[j]; e < rp1[j + 1]; e++) vb = vb + k1[e] * zm[c1[e]];
-    for (uint64_t e = rp2[j]; e < rp2[j + 1]; e++) vc = vc + k2[e] * zm[c2[e]];
+    for (uint64_t e = rp0[j]; e < rp0[j + 1]; e++) va = va + ctab[k0[e]] * zm[c0[e]];
+    for (uint64_t e = rp1[j]; e < rp1[j + 1]; e++) vb = vb + ctab[k1[e]] * zm[c1[e]];
+    for (uint64_t e = rp2[j]; e < rp2[j + 1]; e++) vc = vc + ctab[k2[e]] * zm[c2[e]];
     if (!(va * vb == vc)) {
         atomicAdd(&out[0], 1ull);
         atomicMin(&out[1], (unsigned long long)j);
@@ -143,12 +202,12 @@ __global__ void k_col_sums(const uint32_t *__restrict__ start, const uint32_t *_
 }
 // prod[p] = coeff[perm[p]] * lag[rows[perm[p]]]   (entries in column-sorted order)
 __global__ void k_entry_products(const uint32_t *__restrict__ perm, const uint32_t *__restrict__ rows,
-                                 const fr_t *__restrict__ coeff, const fr_t *__restrict__ lag, uint64_t nnz,
-                                 fr_t *__restrict__ prod) {
+                                 const uint32_t *__restrict__ cidx, const fr_t *__restrict__ ctab,
+                                 const fr_t *__restrict__ lag, uint64_t nnz, fr_t *__restrict__ prod) {
     uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= nnz) return;
     uint32_t e = perm[p];
-    prod[p] = coeff[e] * lag[rows[e]];
+    prod[p] = ctab[cidx[e]] * lag[rows[e]];
 }
 __global__ void k_scatter_runs(const uint32_t *__restrict__ keys, const fr_t *__restrict__ vals,
                                const uint32_t *__restrict__ nruns, fr_t *__restrict__ out) {
@@ -396,8 +455,10 @@ Circuit::~Circuit() {
     for (int m = 0; m < 3; m++) {
         if (row_ptr[m]) hipFree(row_ptr[m]);
         if (col[m]) hipFree(col[m]);
-        if (coeff[m]) hipFree(coeff[m]);
+        if (cidx[m]) hipFree(cidx[m]);
+        if (blk[m]) hipFree(blk[m]);
     }
+    if (ctab) hipFree(ctab);
     if (idx_a) hipFree(idx_a);
     if (idx_b) hipFree(idx_b);
 }
@@ -407,10 +468,36 @@ Srs::~Srs() {
         if (p) hipFree(p);
 }
 
-Circuit *circuit_load(Ctx &c, const R1csHost &cs) {
+namespace {
+// witness-map blocks of one matrix (k_eval_blocks): consecutive rows while the block holds at most
+// EVAL_BLOCK entries and rows; a row with more entries stands alone
+std::vector<uint32_t> eval_blocks(const uint64_t *rp, uint64_t n) {
+    std::vector<uint32_t> b;
+    uint64_t r = 0;
+    while (r < n) {
+        b.push_back((uint32_t)r);
+        const uint64_t e0 = rp[r];
+        uint64_t q = r + 1;
+        if (rp[q] - e0 <= EVAL_BLOCK)
+            while (q < n && q - r < EVAL_BLOCK && rp[q + 1] - e0 <= EVAL_BLOCK) q++;
+        r = q;
+    }
+    b.push_back((uint32_t)n);
+    return b;
+}
+}  // namespace
+
+Circuit *circuit_load_compact(Ctx &c, const R1csCompact &cs) {
     if (cs.n_in < 1) throw std::invalid_argument("circuit must have at least the ONE input");
     uint64_t nv = cs.n_in + cs.n_aux;
     if (nv >= 0x80000000ull) throw std::invalid_argument("too many variables");
+    if (cs.n >= 0xffffffffull) throw std::invalid_argument("too many constraints");
+    if (!cs.n_ctab || !cs.ctab) throw std::invalid_argument("empty coefficient table");
+    {
+        fr_t one = fr_t::zero();
+        one.v[0] = 1;
+        if (memcmp(cs.ctab[0].v, one.v, 32) != 0) throw std::invalid_argument("coefficient table must start with 1");
+    }
     Circuit *C = new Circuit();
     try {
         C->n = cs.n;
@@ -422,34 +509,62 @@ Circuit *circuit_load(Ctx &c, const R1csHost &cs) {
         C->d = 1ull << C->log_d;
         if (C->log_d > 31) throw std::invalid_argument("domain too large");
         std::vector<uint8_t> a_den(cs.n_aux, 0), b_in(cs.n_in, 0), b_aux(cs.n_aux, 0);
+        std::vector<uint32_t> blocks[3];
+        std::string err[3];
+        {  // validation, density and witness-map blocks: one host thread per matrix
+            std::vector<std::thread> th;
+            for (int m = 0; m < 3; m++)
+                th.emplace_back([&, m] {
+                    const uint64_t *rp = cs.row_ptr[m];
+                    if (rp[0] != 0) {
+                        err[m] = "row_ptr[0] must be 0";
+                        return;
+                    }
+                    for (uint64_t j = 0; j < cs.n; j++)
+                        if (rp[j + 1] < rp[j]) {
+                            err[m] = "row_ptr not monotone";
+                            return;
+                        }
+                    const uint64_t nnz = rp[cs.n];
+                    for (uint64_t e = 0; e < nnz; e++) {
+                        const uint32_t v = cs.col[m][e];
+                        if (v >= nv) {
+                            err[m] = "column index out of range";
+                            return;
+                        }
+                        if (cs.cidx[m][e] >= cs.n_ctab) {
+                            err[m] = "coefficient index out of range";
+                            return;
+                        }
+                        if (m == 0 && v >= cs.n_in) a_den[v - cs.n_in] = 1;
+                        if (m == 1) (v < cs.n_in ? b_in[v] : b_aux[v - cs.n_in]) = 1;
+                    }
+                    blocks[m] = eval_blocks(rp, cs.n);
+                });
+            for (auto &t : th) t.join();
+            for (auto &e : err)
+                if (!e.empty()) throw std::invalid_argument(e);
+        }
         for (int m = 0; m < 3; m++) {
-            uint64_t nnz = cs.row_ptr[m][cs.n];
+            const uint64_t nnz = cs.row_ptr[m][cs.n];
             C->nnz[m] = nnz;
-            if (cs.row_ptr[m][0] != 0) throw std::invalid_argument("row_ptr[0] must be 0");
-            for (uint64_t j = 0; j < cs.n; j++)
-                if (cs.row_ptr[m][j + 1] < cs.row_ptr[m][j]) throw std::invalid_argument("row_ptr not monotone");
-            for (uint64_t e = 0; e < nnz; e++) {
-                uint32_t v = cs.col[m][e];
-                if (v >= nv) throw std::invalid_argument("column index out of range");
-                if (m == 0 && v >= cs.n_in) a_den[v - cs.n_in] = 1;
-                if (m == 1) {
-                    if (v < cs.n_in)
-                        b_in[v] = 1;
-                    else
-                        b_aux[v - cs.n_in] = 1;
-                }
-            }
             C->row_ptr[m] = dalloc<uint64_t>(cs.n + 1);
             MI_HIP(hipMemcpy(C->row_ptr[m], cs.row_ptr[m], 8 * (cs.n + 1), hipMemcpyHostToDevice));
+            C->n_blk[m] = blocks[m].size() - 1;
+            C->blk[m] = dalloc<uint32_t>(blocks[m].size());
+            MI_HIP(hipMemcpy(C->blk[m], blocks[m].data(), 4 * blocks[m].size(), hipMemcpyHostToDevice));
             if (nnz) {
                 C->col[m] = dalloc<uint32_t>(nnz);
-                C->coeff[m] = dalloc<fr_t>(nnz);
+                C->cidx[m] = dalloc<uint32_t>(nnz);
                 MI_HIP(hipMemcpy(C->col[m], cs.col[m], 4 * nnz, hipMemcpyHostToDevice));
-                MI_HIP(hipMemcpy(C->coeff[m], cs.coeff[m], 32 * nnz, hipMemcpyHostToDevice));
-                fr_canonicalize(c, C->coeff[m], nnz);
-                fr_to_mont_inplace(c, C->coeff[m], nnz);
+                MI_HIP(hipMemcpy(C->cidx[m], cs.cidx[m], 4 * nnz, hipMemcpyHostToDevice));
             }
         }
+        C->n_ctab = cs.n_ctab;
+        C->ctab = dalloc<fr_t>(cs.n_ctab);
+        MI_HIP(hipMemcpy(C->ctab, cs.ctab, 32 * cs.n_ctab, hipMemcpyHostToDevice));
+        fr_canonicalize(c, C->ctab, cs.n_ctab);
+        fr_to_mont_inplace(c, C->ctab, cs.n_ctab);
         std::vector<uint32_t> ia, ib;
         for (uint64_t i = 0; i < cs.n_in; i++) ia.push_back((uint32_t)i);
         for (uint64_t i = 0; i < cs.n_aux; i++)
@@ -473,6 +588,96 @@ Circuit *circuit_load(Ctx &c, const R1csHost &cs) {
         throw;
     }
     return C;
+}
+
+// Full-coefficient R1CS (the C-ABI's mi_r1cs): the 32-byte coefficients interned into a table (1 first),
+// chunk-parallel with a per-chunk table merged afterwards (circuits use few distinct coefficients, so the
+// per-entry cost is one small hash lookup behind a last-value check)
+Circuit *circuit_load(Ctx &c, const R1csHost &cs) {
+    struct Key {
+        uint64_t w[4];
+        bool operator==(const Key &o) const { return !memcmp(w, o.w, 32); }
+    };
+    struct KH {
+        size_t operator()(const Key &k) const {
+            return (size_t)((k.w[0] ^ (k.w[1] * 0x9e3779b97f4a7c15ull) ^ (k.w[2] << 7) ^ (k.w[3] >> 3)) *
+                            0xff51afd7ed558ccdull);
+        }
+    };
+    auto key_at = [](const uint8_t *p) {
+        Key k;
+        memcpy(k.w, p, 32);
+        return k;
+    };
+    std::vector<uint32_t> cidx[3];
+    std::vector<Key> table;
+    std::unordered_map<Key, uint32_t, KH> index;
+    Key one{{1, 0, 0, 0}};
+    table.push_back(one);
+    index.emplace(one, 0);
+    const unsigned nt = 16;
+    for (int m = 0; m < 3; m++) {
+        const uint64_t nnz = cs.n ? cs.row_ptr[m][cs.n] : 0;
+        cidx[m].resize(nnz);
+        if (!nnz) continue;
+        const uint8_t *co = cs.coeff[m];
+        std::vector<std::vector<Key>> local(nt);
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < nt; t++)
+            th.emplace_back([&, t] {  // local indices first
+                std::unordered_map<Key, uint32_t, KH> li;
+                const uint64_t lo = nnz * t / nt, hi = nnz * (t + 1) / nt;
+                Key last{};
+                uint32_t last_i = ~0u;
+                for (uint64_t e = lo; e < hi; e++) {
+                    const Key k = key_at(co + 32 * e);
+                    if (last_i != ~0u && k == last) {
+                        cidx[m][e] = last_i;
+                        continue;
+                    }
+                    auto it = li.find(k);
+                    uint32_t i;
+                    if (it == li.end()) {
+                        i = (uint32_t)local[t].size();
+                        local[t].push_back(k);
+                        li.emplace(k, i);
+                    } else {
+                        i = it->second;
+                    }
+                    cidx[m][e] = i;
+                    last = k;
+                    last_i = i;
+                }
+            });
+        for (auto &t : th) t.join();
+        th.clear();
+        std::vector<std::vector<uint32_t>> remap(nt);
+        for (unsigned t = 0; t < nt; t++)
+            for (const Key &k : local[t]) {
+                auto it = index.find(k);
+                if (it == index.end()) {
+                    if (table.size() >= 0xffffffffull) throw std::invalid_argument("too many distinct coefficients");
+                    it = index.emplace(k, (uint32_t)table.size()).first;
+                    table.push_back(k);
+                }
+                remap[t].push_back(it->second);
+            }
+        for (unsigned t = 0; t < nt; t++)
+            th.emplace_back([&, t] {
+                const uint64_t lo = nnz * t / nt, hi = nnz * (t + 1) / nt;
+                for (uint64_t e = lo; e < hi; e++) cidx[m][e] = remap[t][cidx[m][e]];
+            });
+        for (auto &t : th) t.join();
+    }
+    std::vector<fr_t> ctab(table.size());
+    for (size_t i = 0; i < table.size(); i++) memcpy(ctab[i].v, table[i].w, 32);
+    R1csCompact cc{cs.n, cs.n_in, cs.n_aux, {}, {}, {}, ctab.data(), ctab.size()};
+    for (int m = 0; m < 3; m++) {
+        cc.row_ptr[m] = cs.row_ptr[m];
+        cc.col[m] = cs.col[m];
+        cc.cidx[m] = cidx[m].data();
+    }
+    return circuit_load_compact(c, cc);
 }
 
 // Proving-key upload as a stream of chunks (mi_srs_stream_*; srs_load is begin + whole queries + end).
@@ -640,8 +845,9 @@ uint64_t circuit_check(Ctx &c, const Circuit &C, const fr_t *z_dev, uint64_t *fi
     MI_HIP(hipMemcpyAsync(out, init, sizeof init, hipMemcpyHostToDevice, c.stream));
     k_copy_to_mont<<<grid1(nv), 256, 0, c.stream>>>(z_dev, zm, nv);
     if (C.n)
-        k_check_rows<<<grid1(C.n), 256, 0, c.stream>>>(C.row_ptr[0], C.col[0], C.coeff[0], C.row_ptr[1], C.col[1],
-                                                      C.coeff[1], C.row_ptr[2], C.col[2], C.coeff[2], zm, C.n, out);
+        k_check_rows<<<grid1(C.n), 256, 0, c.stream>>>(C.row_ptr[0], C.col[0], C.cidx[0], C.row_ptr[1], C.col[1],
+                                                      C.cidx[1], C.row_ptr[2], C.col[2], C.cidx[2], C.ctab, zm, C.n,
+                                                      out);
     MI_HIP(hipGetLastError());
     unsigned long long h[2];
     MI_HIP(hipMemcpyAsync(h, out, sizeof h, hipMemcpyDeviceToHost, c.stream));
@@ -806,7 +1012,7 @@ Srs *srs_generate(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5]) {
             // column sums by reduce-by-key over the column-sorted products: load-balanced whatever
             // the column lengths (ONE appears in ~half the rows of B)
             fr_t *prod = c.scratch[13].as<fr_t>(nnz);
-            k_entry_products<<<grid1(nnz), 256, 0, st>>>(perm, rows, circ.coeff[m], lag, nnz, prod);
+            k_entry_products<<<grid1(nnz), 256, 0, st>>>(perm, rows, circ.cidx[m], circ.ctab, lag, nnz, prod);
             uint32_t *ukeys = c.scratch[5].as<uint32_t>(nnz);
             fr_t *uvals = c.scratch[14].as<fr_t>(nnz);
             uint32_t *nruns = c.scratch[6].as<uint32_t>(4);
@@ -937,10 +1143,7 @@ ProofSums groth16_sums(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *
             fr_t *zm = c.scratch[20].as<fr_t>(nv + 3 * d);
             fr_t *a = zm + nv, *b = a + d, *cc = b + d;
             k_copy_to_mont<<<grid1(nv), 256, 0, st>>>(z_dev, zm, nv);
-            k_eval_rows<<<grid1(d), 256, 0, st>>>(circ.row_ptr[0], circ.col[0], circ.coeff[0], circ.row_ptr[1],
-                                                  circ.col[1], circ.coeff[1], circ.row_ptr[2], circ.col[2],
-                                                  circ.coeff[2], zm, circ.n, circ.n_in, d, a, b, cc);
-            MI_HIP(hipGetLastError());
+            eval_witness_map(c, circ, zm, a, b, cc);
             fr_t dd = fr_t::zero();
             dd.v[0] = (uint32_t)d;
             dd.v[1] = (uint32_t)(d >> 32);

@@ -32,9 +32,12 @@ namespace stacked {
 
 struct Shape {
     unsigned layers = 2;       // SDR layers (columns of `layers` labels; 11 at 32 GiB)
-    unsigned challenges = 1;   // challenges per partition (18 at 32 GiB: proofs/parameters.hpp:90-99)
+    unsigned challenges = 1;   // challenges per partition (18 at 32 GiB: proofs/parameters.hpp:90-99); PoSt:
+                               // challenges per sector (Window PoSt: 10)
     uint64_t nodes = 8;        // sector nodes (2^30 at 32 GiB)
     unsigned base = 8, sub = 0, top = 0;  // tree C / tree R-last arities (32 GiB: 8, 8, 0)
+    unsigned sectors = 0;      // 0: the stacked PoRep circuit; > 0: the Fallback PoSt circuit over this many
+                               // sectors (Window PoSt at 32 GiB: 2349, constants.hpp:85-89)
 };
 
 // instance data: an array of 32-byte slots (Fr little-endian canonical; u64 values in the low 8 bytes)
@@ -45,13 +48,20 @@ struct Shape {
 //     tree C siblings of the challenged column (same count)
 //     6 DRG parents, then 8 expander parents, each: index (u64), column (layers labels, layer 1 first),
 //     tree C siblings
+//
+// Fallback PoSt instance (sectors > 0): per sector s, from s * stride:
+//   +0 comm_r  +1 comm_c  +2 comm_r_last, then per challenge n, from 3 + n * (2 + path_c):
+//     +0 challenged leaf index (u64)  +1 leaf  +2 .. tree R-last siblings (position order, leaf upward)
 struct Layout {
     unsigned depth_d = 0;               // binary tree D levels
     std::vector<unsigned> c_arities;    // tree C / R-last level arities, leaf upward
     uint64_t path_c = 0;                // siblings per tree C / R-last path
     uint64_t stride = 0;                // slots per challenge
     uint64_t slots = 0;                 // total slots
+    uint64_t unit0 = 5;                 // first slot of the replicated unit (challenge; PoSt: sector 0)
     uint64_t ch_base(unsigned c) const { return 5 + (uint64_t)c * stride; }
+    uint64_t post_sector(uint64_t s) const { return s * stride; }
+    uint64_t post_challenge(uint64_t s, unsigned n) const { return s * stride + 3 + (uint64_t)n * (2 + path_c); }
     uint64_t off_d() const { return 2; }
     uint64_t off_r() const { return 2 + depth_d; }
     uint64_t off_cx() const { return 2 + depth_d + path_c; }
@@ -94,10 +104,13 @@ struct Built {
     Shape shape;
     Layout lay;
     uint64_t n_in = 0, n_aux = 0, n_constraints = 0;
-    // R1CS over z = ONE ++ inputs ++ aux, coefficients canonical little-endian (fr_t raw limbs)
+    // R1CS over z = ONE ++ inputs ++ aux; entry e of matrix m has coefficient ctab[cidx[m][e]] (canonical
+    // little-endian fr_t raw limbs; ctab[0] = 1).  A circuit has few distinct coefficients (about 1.5 K for
+    // the stacked circuit: powers of two, the Poseidon constants), so an entry costs 8 bytes, not 36.
     std::vector<uint64_t> rp[3];
     std::vector<uint32_t> col[3];
-    std::vector<fr_t> coeff[3];
+    std::vector<uint32_t> cidx[3];
+    std::vector<fr_t> ctab;
     // witness program
     std::vector<WOp> ops;            // sorted by (level, kind): kind 0 every non-Poseidon op, 1..4 Poseidon of
                                      // arity 2 / 4 / 8 / 11 (one kernel per kind)
@@ -114,10 +127,14 @@ struct Built {
 
 // Builds the R1CS and the witness program of one partition of `s` (throws std::invalid_argument on a shape
 // the circuit cannot take: layers 2 or 11 (Poseidon column arity), power-of-two node count matching the
-// tree shape, arities in {2, 4, 8}).
+// tree shape, arities in {2, 4, 8}).  With s.sectors > 0 the circuit is FallbackPoStCircuit::synthesize
+// (rust-fil-proofs storage-proofs-post fallback/circuit.rs; the reference keeps its data types,
+// post/fallback/circuit.hpp:38-86): per sector comm_c, comm_r_last, comm_r (an input), Poseidon-2(comm_c,
+// comm_r_last) == comm_r, and one private tree R-last PoR per challenge (path packed into one input).
 Built *build(const Shape &s, bool want_r1cs = true);
 
-// generate_public_inputs order (circuit/proof.hpp:186-269) from the instance slots, without ONE
+// generate_public_inputs order (circuit/proof.hpp:186-269; PoSt: per sector comm_r, then the challenged leaf
+// index of each inclusion proof) from the instance slots, without ONE
 void public_inputs(const Built &b, const uint8_t *slots, std::vector<fr_t> &out);
 
 // The witness of one partition on the GPU: slots_dev = the instance (Layout), z_dev = (n_in + n_aux) x 32 B,

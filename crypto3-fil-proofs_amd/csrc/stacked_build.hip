@@ -7,10 +7,12 @@
 #include <algorithm>
 #include <array>
 #include <map>
-#include <cstring>
 #include <stdexcept>
 #include <string>
+#include <cstring>
+#include <mutex>
 #include <thread>
+#include <unordered_map>
 
 #include "poseidon_math.h"
 #include "stacked.h"
@@ -50,6 +52,12 @@ Layout layout_for(const Shape &s) {
     if (s.top && !s.sub) throw std::invalid_argument("stacked: a top tree needs a sub tree");
     L.c_arities = tree_arities(s.nodes, s.base, s.sub, s.top);
     for (unsigned a : L.c_arities) L.path_c += a - 1;
+    if (s.sectors) {  // Fallback PoSt: sectors x (comm_r, comm_c, comm_r_last, challenges x (index, leaf, path))
+        L.stride = 3 + (uint64_t)s.challenges * (2 + L.path_c);
+        L.slots = (uint64_t)s.sectors * L.stride;
+        L.unit0 = 0;
+        return L;
+    }
     L.stride = 2 + L.depth_d + 2 * L.path_c + 14ull * (1 + s.layers + L.path_c);
     L.slots = 5 + (uint64_t)s.challenges * L.stride;
     return L;
@@ -104,6 +112,51 @@ const Poseidon &poseidon_consts(unsigned arity) {
     return cache.emplace(arity, std::move(p)).first->second;
 }
 
+// Process-wide coefficient pool (canonical values -> dense indices, 0 = one): templates are cached across
+// builds with their coefficients already interned, and each Built takes a snapshot of the pool.
+struct CoefPool {
+    struct H {
+        size_t operator()(const fr_t &x) const {
+            uint64_t h = 0x9e3779b97f4a7c15ull;
+            for (int i = 0; i < 8; i++) h = (h ^ x.v[i]) * 0x100000001b3ull;
+            return (size_t)h;
+        }
+    };
+    struct E {
+        bool operator()(const fr_t &a, const fr_t &b) const { return memcmp(a.v, b.v, 32) == 0; }
+    };
+    std::mutex mu;
+    std::vector<fr_t> tab;
+    std::unordered_map<fr_t, uint32_t, H, E> idx;
+    CoefPool() {
+        fr_t one = fr_t::zero();
+        one.v[0] = 1;
+        intern(one);
+    }
+    uint32_t intern(const fr_t &canonical) {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = idx.find(canonical);
+        if (it != idx.end()) return it->second;
+        if (tab.size() >= 0xffffffffull) throw std::runtime_error("stacked: coefficient pool full");
+        const uint32_t i = (uint32_t)tab.size();
+        tab.push_back(canonical);
+        idx.emplace(canonical, i);
+        return i;
+    }
+    fr_t at(uint32_t i) {
+        std::lock_guard<std::mutex> g(mu);
+        return tab[i];
+    }
+    std::vector<fr_t> snapshot() {
+        std::lock_guard<std::mutex> g(mu);
+        return tab;
+    }
+};
+CoefPool &pool() {
+    static CoefPool p;
+    return p;
+}
+
 void canon(LC &lc) {
     std::sort(lc.begin(), lc.end(), [](const Term &x, const Term &y) { return x.z < y.z; });
     size_t o = 0;
@@ -148,7 +201,7 @@ struct CS {
             canon(*m[q]);
             for (auto &t : *m[q]) {
                 out->col[q].push_back((uint32_t)t.z);
-                out->coeff[q].push_back(from_mont(t.k));
+                out->cidx[q].push_back(pool().intern(from_mont(t.k)));
             }
             out->rp[q].push_back(out->col[q].size());
         }
@@ -474,10 +527,10 @@ struct Template {
     std::vector<Row> rows;  // as recorded (symbolic ids, Montgomery); released by flatten()
     uint64_t n_int = 0;
     std::vector<uint64_t> outs;  // symbolic ids of the outputs (SHA: 256 state bits as Is; Poseidon: digest)
-    // flat form: per row and matrix the end offset of its terms; ids and canonical coefficients
+    // flat form: per row and matrix the end offset of its terms; ids and pooled coefficient indices
     std::vector<uint32_t> ends;  // 3 per row
     std::vector<uint64_t> ids;
-    std::vector<fr_t> ks;
+    std::vector<uint32_t> ks;
     void flatten() {
         for (const Row &r : rows)
             for (const LC *lc : {&r.a, &r.b, &r.c}) {
@@ -485,7 +538,7 @@ struct Template {
                 canon(x);  // symbolic ids are distinct per operand; instantiate merges repeated operands
                 for (auto &t : x) {
                     ids.push_back(t.z);
-                    ks.push_back(from_mont(t.k));
+                    ks.push_back(pool().intern(from_mont(t.k)));
                 }
                 ends.push_back((uint32_t)ids.size());
             }
@@ -558,7 +611,7 @@ uint64_t instantiate(CS &cs, const Template &T, const std::vector<uint64_t> &ext
     Built &b = *cs.out;
     struct ZK {
         uint64_t z;
-        fr_t k;
+        uint32_t k;  // pooled coefficient index
     };
     static thread_local std::vector<ZK> buf;
     uint32_t beg = 0;
@@ -580,15 +633,23 @@ uint64_t instantiate(CS &cs, const Template &T, const std::vector<uint64_t> &ext
                 for (size_t i = 0; i < buf.size();) {
                     ZK t = buf[i];
                     size_t j = i + 1;
-                    for (; j < buf.size() && buf[j].z == t.z; j++) t.k = t.k + buf[j].k;  // mod r, any representation
-                    if (!t.k.is_zero()) buf[o++] = t;
+                    if (j < buf.size() && buf[j].z == t.z) {  // repeated operand: the summed coefficient (mod r)
+                        fr_t k = pool().at(t.k);
+                        for (; j < buf.size() && buf[j].z == t.z; j++) k = k + pool().at(buf[j].k);
+                        if (k.is_zero()) {
+                            i = j;
+                            continue;
+                        }
+                        t.k = pool().intern(k);
+                    }
+                    buf[o++] = t;
                     i = j;
                 }
                 buf.resize(o);
             }
             for (auto &t : buf) {
                 b.col[q].push_back((uint32_t)t.z);
-                b.coeff[q].push_back(t.k);
+                b.cidx[q].push_back(t.k);
             }
             b.rp[q].push_back(b.col[q].size());
         }
@@ -609,7 +670,8 @@ struct Synth {
     explicit Synth(Built &bb, bool keep) : b(bb), g(cs) {
         cs.out = &bb;
         cs.keep = keep;
-        cs.n_in_total = 4 + 18ull * bb.shape.challenges;
+        cs.n_in_total = bb.shape.sectors ? 1 + (uint64_t)bb.shape.sectors * (1 + bb.shape.challenges)
+                                         : 4 + 18ull * bb.shape.challenges;
         for (int m = 0; m < 3; m++) b.rp[m].assign(1, 0);
     }
     uint32_t level_of(uint64_t z) const {
@@ -888,30 +950,29 @@ struct Synth {
         uint64_t aux0 = 0, in0 = 0, row0[3] = {0, 0, 0}, ops0 = 0, blocks0 = 0, pin0 = 0, pos0 = 0, sha0 = 0, ncons0 = 0;
     } mark;
 
-    // copies of challenge 0 for challenges 1 .. C - 1: challenge-local aux variables shift by c x (aux per
-    // challenge), local inputs by 18 c, challenge slots by c x stride; rows keep their canonical order (the
-    // shift is monotone and leaves global variables below local ones)
-    void replicate() {
-        const unsigned C = b.shape.challenges;
+    // copies of unit 0 (a challenge; PoSt: a sector) for units 1 .. C - 1: unit-local aux variables shift by
+    // c x (aux per unit), local inputs by c x (inputs per unit), unit slots by c x stride; rows keep their
+    // canonical order (the shift is monotone and leaves global variables below local ones)
+    void replicate(unsigned C, uint64_t inputs_per_unit) {
         const uint64_t nin = cs.n_in_total;
         const uint64_t A = cs.next_aux - mark.aux0, I = cs.next_input - mark.in0;
-        const uint64_t zl = nin + mark.aux0;  // first challenge-local aux z
-        const uint64_t S = b.lay.stride;
-        if (I != 18) throw std::logic_error("stacked: 18 inputs per challenge expected");
+        const uint64_t zl = nin + mark.aux0;  // first unit-local aux z
+        const uint64_t S = b.lay.stride, U0 = b.lay.unit0;
+        if (I != inputs_per_unit) throw std::logic_error("stacked: unexpected input count per replicated unit");
         if (C == 1) return;
         auto zmap = [&](uint64_t z, uint64_t c) -> uint64_t {
             if (z >= zl) return z + c * A;
             if (z >= mark.in0 && z < mark.in0 + I) return z + c * I;
             return z;
         };
-        auto smap = [&](uint64_t slot, uint64_t c) -> uint64_t { return slot >= 5 ? slot + c * S : slot; };
+        auto smap = [&](uint64_t slot, uint64_t c) -> uint64_t { return slot >= U0 ? slot + c * S : slot; };
         // R1CS
         if (cs.keep) {
             std::vector<std::thread> th;
             for (int m = 0; m < 3; m++) {
                 auto &rp = b.rp[m];
                 auto &col = b.col[m];
-                auto &co = b.coeff[m];
+                auto &co = b.cidx[m];
                 const uint64_t r0 = mark.row0[m], r1 = rp.size() - 1, nr = r1 - r0;
                 const uint64_t e0 = rp[r0], e1 = rp[r1], ne = e1 - e0;
                 rp.resize(rp.size() + (C - 1) * nr);
@@ -925,7 +986,7 @@ struct Synth {
                             for (uint64_t r = 1; r <= nr; r++) b.rp[m][ro + r] = b.rp[m][r0 + r] + c * ne;
                             for (uint64_t e = 0; e < ne; e++) {
                                 b.col[m][eo + e] = (uint32_t)zmap(b.col[m][e0 + e], c);
-                                b.coeff[m][eo + e] = b.coeff[m][e0 + e];
+                                b.cidx[m][eo + e] = b.cidx[m][e0 + e];
                             }
                         }
                     });
@@ -972,6 +1033,39 @@ struct Synth {
         cs.next_input += (C - 1) * I;
     }
 
+    void set_mark() {
+        mark.aux0 = cs.next_aux;
+        mark.in0 = cs.next_input;
+        for (int m = 0; m < 3; m++) mark.row0[m] = b.rp[m].size() - 1;
+        mark.ops0 = b.ops.size();
+        mark.blocks0 = b.blocks.size();
+        mark.pin0 = b.pin.size();
+        mark.pos0 = b.poseidon_ops.size();
+        mark.sha0 = b.sha_ops.size();
+        mark.ncons0 = b.n_constraints;
+    }
+
+    // FallbackPoStCircuit::synthesize: sector 0 is synthesised, sectors 1.. are its shifted copies
+    void run_post() {
+        const Shape &s = b.shape;
+        const Layout &L = b.lay;
+        set_mark();
+        const uint64_t sb = L.post_sector(0);
+        const uint64_t comm_c = alloc_data(sb + 1);
+        const uint64_t comm_r_last = alloc_data(sb + 2);
+        const uint64_t comm_r = alloc_data(sb + 0);
+        inputize(comm_r);
+        const uint64_t h = poseidon({comm_c, comm_r_last});  // hash2_circuit
+        equal(comm_r, h);
+        for (unsigned n = 0; n < s.challenges; n++) {  // PoRCircuit (private): leaf, path, root = comm_r_last
+            const uint64_t cb = L.post_challenge(0, n);
+            const uint64_t leaf = alloc_data(cb + 1);
+            por(leaf, cb, cb + 2, L.c_arities, false, comm_r_last);
+        }
+        replicate(s.sectors, 1 + s.challenges);
+        if (cs.next_input != cs.n_in_total) throw std::logic_error("post: input count differs from the shape");
+    }
+
     void run() {
         const Shape &s = b.shape;
         const Layout &L = b.lay;
@@ -989,15 +1083,7 @@ struct Synth {
         std::vector<unsigned> d_ar(L.depth_d, 2);
         // challenge 0 is synthesised; challenges 1.. have the identical shape and are copies of it with the
         // challenge-local variables, inputs and instance slots shifted (replicate())
-        mark.aux0 = cs.next_aux;
-        mark.in0 = cs.next_input;
-        for (int m = 0; m < 3; m++) mark.row0[m] = b.rp[m].size() - 1;
-        mark.ops0 = b.ops.size();
-        mark.blocks0 = b.blocks.size();
-        mark.pin0 = b.pin.size();
-        mark.pos0 = b.poseidon_ops.size();
-        mark.sha0 = b.sha_ops.size();
-        mark.ncons0 = b.n_constraints;
+        set_mark();
         for (unsigned c = 0; c < 1; c++) {
             const uint64_t cb = L.ch_base(c);
             const uint64_t data_leaf = alloc_data(cb + 1);
@@ -1042,7 +1128,7 @@ struct Synth {
             const uint64_t colh = poseidon(labels);
             por(colh, cb, cb + L.off_cx(), L.c_arities, false, comm_c);
         }
-        replicate();
+        replicate(s.challenges, 18);
         if (cs.next_input != cs.n_in_total) throw std::logic_error("stacked: input count differs from the shape");
     }
 };
@@ -1051,16 +1137,23 @@ struct Synth {
 
 Built *build(const Shape &s, bool want_r1cs) {
     init_consts();
-    if (s.layers != 2 && s.layers != 11) throw std::invalid_argument("stacked: layers must be 2 or 11 (column hash arity)");
+    if (!s.sectors && s.layers != 2 && s.layers != 11)
+        throw std::invalid_argument("stacked: layers must be 2 or 11 (column hash arity)");
     if (!s.challenges) throw std::invalid_argument("stacked: at least one challenge");
+    if (s.sectors && (uint64_t)s.sectors * (1 + s.challenges) >= (1ull << 31))
+        throw std::invalid_argument("post: too many sectors x challenges");
     Built *b = new Built();
     try {
         b->shape = s;
         b->lay = layout_for(s);
         Synth sy(*b, want_r1cs);
-        sy.run();
+        if (s.sectors)
+            sy.run_post();
+        else
+            sy.run();
         b->n_in = sy.cs.n_in_total;
         b->n_aux = sy.cs.next_aux;
+        b->ctab = pool().snapshot();
         // order the program by level (stable), remapping the op references of blocks and the phase-B lists
         const size_t n = b->ops.size();
         std::vector<uint64_t> perm(n), where(n);
@@ -1148,10 +1241,17 @@ void public_inputs(const Built &b, const uint8_t *slots, std::vector<fr_t> &out)
         return x;
     };
     out.clear();
+    const Layout &L = b.lay;
+    if (b.shape.sectors) {
+        for (uint64_t s = 0; s < b.shape.sectors; s++) {
+            out.push_back(fr_at(L.post_sector(s)));  // comm_r
+            for (unsigned n = 0; n < b.shape.challenges; n++) out.push_back(u64_at(L.post_challenge(s, n)));
+        }
+        return;
+    }
     out.push_back(fr_at(0));
     out.push_back(fr_at(1));
     out.push_back(fr_at(2));
-    const Layout &L = b.lay;
     for (unsigned c = 0; c < b.shape.challenges; c++) {
         const uint64_t cb = L.ch_base(c);
         out.push_back(u64_at(cb));  // tree D path (packed index bits)

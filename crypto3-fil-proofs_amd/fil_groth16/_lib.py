@@ -31,7 +31,7 @@ EXPORTS = [
     "mi_tree_d_build_dev", "mi_srs_msm_info", "mi_points_check_subgroup", "mi_points_info",
     "mi_groth16_prove_random", "mi_groth16_prove_dev_random", "mi_groth16_prove_batch_random",
     "mi_srs_stream_begin", "mi_srs_stream_part", "mi_srs_stream_end", "mi_srs_stream_abort", "mi_srs_export_query_dev",
-    "mi_stacked_build", "mi_stacked_info", "mi_stacked_r1cs", "mi_stacked_public_inputs", "mi_stacked_witness_dev",
+    "mi_stacked_build", "mi_post_build", "mi_stacked_info", "mi_stacked_r1cs", "mi_stacked_load", "mi_stacked_public_inputs", "mi_stacked_witness_dev",
     "mi_stacked_witness", "mi_stacked_free", "mi_circuit_check_dev",
 ]
 
@@ -87,6 +87,8 @@ def lib():
         "mi_srs_free": ([vp], None),
         "mi_srs_msm_info": ([vp, vp], c_int),
         "mi_stacked_build": ([vp, c_int, pp], c_int),
+        "mi_post_build": ([vp, c_int, pp], c_int),
+        "mi_stacked_load": ([vp, vp, pp], c_int),
         "mi_stacked_info": ([vp, vp], c_int),
         "mi_stacked_r1cs": ([vp, vp], c_int),
         "mi_stacked_public_inputs": ([vp, vp, vp], c_int),

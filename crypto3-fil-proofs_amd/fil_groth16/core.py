@@ -184,6 +184,17 @@ class Circuit:
             s.coeff[m] = k.ctypes.data if len(k) else None
         self.h = ctypes.c_void_p()
         check(lib().mi_circuit_load(ctx.h, ctypes.byref(s), ctypes.byref(self.h)))
+        self._info()
+
+    @classmethod
+    def from_handle(cls, ctx: Context, h):
+        """wrap a circuit the library uploaded itself (mi_stacked_load)"""
+        self = cls.__new__(cls)
+        self.ctx, self.h = ctx, h
+        self._info()
+        return self
+
+    def _info(self):
         info = (ctypes.c_uint64 * 9)()
         check(lib().mi_circuit_info(self.h, info))
         (self.num_constraints, self.num_inputs, self.num_aux, self.d, self.n_a, self.n_b,

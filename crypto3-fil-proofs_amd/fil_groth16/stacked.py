@@ -1,14 +1,19 @@
-"""Stacked-PoRep circuit: R1CS shape and GPU witness generation.
+"""Stacked-PoRep and Fallback-PoSt circuits: R1CS shape and GPU witness generation.
 
-Mirrors the synthesis half of the reference's compound proof for stacked PoRep:
+Mirrors the synthesis half of the reference's compound proofs:
   StackedCircuit                  StackedCompound::circuit + StackedCircuit::synthesize
                                   (libs/storage/include/nil/filecoin/storage/proofs/porep/stacked/circuit/
                                   proof.hpp:98-165; Proof::synthesize, params.hpp:93-238)
   StackedCircuit.public_inputs    generate_public_inputs (circuit/proof.hpp:186-269)
   instance_slots                  the circuit Proof built from a vanilla proof (params.hpp:69-90): the openings
                                   the gadgets consume, in the library's slot layout
-The R1CS is built on the host once per shape (mi_stacked_build; the blank circuit), the witness of every
-partition on the GPU (mi_stacked_witness*).  There is no CPU witness path.
+  FallbackPoStCircuit             FallbackPoStCircuit / Sector (post/fallback/circuit.hpp:38-86; the synthesize
+                                  body is rust-fil-proofs storage-proofs-post fallback/circuit.rs): Window and
+                                  Winning PoSt partitions
+  generate_leaf_challenge         post/fallback/vanilla.hpp:398-411
+  post_slots                      a partition's sector proofs (vanilla.hpp:188-251) in the slot layout
+The R1CS is built on the host once per shape (mi_stacked_build / mi_post_build; the blank circuit), the
+witness of every partition on the GPU (mi_stacked_witness*).  There is no CPU witness path.
 """
 import ctypes
 
@@ -38,18 +43,19 @@ def tree_arities(nodes, base, sub=0, top=0):
     return out + [a for a in (sub, top) if a]
 
 
-class StackedCircuit:
-    """One partition's circuit of a shape: layers (2 or 11), challenges, nodes, tree C / R-last arities."""
+class _PostShape(ctypes.Structure):
+    _fields_ = [("sectors", ctypes.c_uint32), ("challenges", ctypes.c_uint32), ("nodes", ctypes.c_uint64),
+                ("base_arity", ctypes.c_uint32), ("sub_arity", ctypes.c_uint32), ("top_arity", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
 
-    def __init__(self, layers=2, challenges=1, nodes=8, base=8, sub=0, top=0, with_r1cs=True):
-        sh = _Shape(layers, challenges, nodes, base, sub, top, 0)
-        self.h = ctypes.c_void_p()
-        check(lib().mi_stacked_build(ctypes.byref(sh), int(with_r1cs), ctypes.byref(self.h)))
+
+class _BuiltCircuit:
+    """A circuit built by the library (R1CS + GPU witness program); subclasses name the shape."""
+
+    def _finish(self, with_r1cs):
         out = (ctypes.c_uint64 * len(INFO_KEYS))()
         check(lib().mi_stacked_info(self.h, out))
         self.info = dict(zip(INFO_KEYS, list(out)))
-        self.layers, self.challenges, self.nodes = layers, challenges, nodes
-        self.arities = tree_arities(nodes, base, sub, top)
         self.with_r1cs = with_r1cs
 
     @property
@@ -85,7 +91,10 @@ class StackedCircuit:
         return mats
 
     def load(self, ctx) -> Circuit:
-        return Circuit(ctx, self.num_constraints, self.num_inputs, self.num_aux, self.csr())
+        """the circuit on the device, uploaded from the builder's compact form (mi_stacked_load)"""
+        h = ctypes.c_void_p()
+        check(lib().mi_stacked_load(ctx.h, self.h, ctypes.byref(h)))
+        return Circuit.from_handle(ctx, h)
 
     def public_inputs(self, slots: bytes) -> bytes:
         out = ctypes.create_string_buffer(32 * (self.num_inputs - 1))
@@ -106,6 +115,137 @@ class StackedCircuit:
             lib().mi_stacked_free(self.h)
         except Exception:
             pass
+
+
+class StackedCircuit(_BuiltCircuit):
+    """One partition's circuit of a shape: layers (2 or 11), challenges, nodes, tree C / R-last arities."""
+
+    def __init__(self, layers=2, challenges=1, nodes=8, base=8, sub=0, top=0, with_r1cs=True):
+        sh = _Shape(layers, challenges, nodes, base, sub, top, 0)
+        self.h = ctypes.c_void_p()
+        check(lib().mi_stacked_build(ctypes.byref(sh), int(with_r1cs), ctypes.byref(self.h)))
+        self.layers, self.challenges, self.nodes = layers, challenges, nodes
+        self.arities = tree_arities(nodes, base, sub, top)
+        self._finish(with_r1cs)
+
+
+class FallbackPoStCircuit(_BuiltCircuit):
+    """One Fallback PoSt partition: `sectors` sectors x `challenges` private tree R-last inclusion proofs
+    (Window PoSt at 32 GiB: 2349 x 10 over 2^30-node 8-8-0 trees = 125,279,217 constraints, constants.hpp:85-89;
+    Winning PoSt: 1 sector x 66 challenges)."""
+
+    def __init__(self, sectors=1, challenges=1, nodes=64, base=8, sub=0, top=0, with_r1cs=True):
+        sh = _PostShape(sectors, challenges, nodes, base, sub, top, 0)
+        self.h = ctypes.c_void_p()
+        check(lib().mi_post_build(ctypes.byref(sh), int(with_r1cs), ctypes.byref(self.h)))
+        self.sectors, self.challenges, self.nodes = sectors, challenges, nodes
+        self.arities = tree_arities(nodes, base, sub, top)
+        self._finish(with_r1cs)
+
+
+def generate_leaf_challenge(randomness: int, sector_id: int, leaf_challenge_index: int, nodes: int) -> int:
+    """post/fallback/vanilla.hpp:398-411: SHA-256(randomness (32 B LE) || sector_id u64 LE || index u64 LE),
+    the first 8 bytes as a little-endian u64, mod the sector's node count"""
+    import hashlib
+
+    h = hashlib.sha256(int(randomness).to_bytes(32, "little") + int(sector_id).to_bytes(8, "little") +
+                       int(leaf_challenge_index).to_bytes(8, "little")).digest()
+    return int.from_bytes(h[:8], "little") % nodes
+
+
+def post_challenges(randomness: int, sector_ids, challenges: int, nodes: int, partition: int = 0,
+                    sectors_per_partition: int = None):
+    """the challenged leaves of one partition's sectors (prove_all_partitions, vanilla.hpp:222-236): sector i of
+    partition j, challenge n -> generate_leaf_challenge(randomness, id, (j * sectors + i) * challenges + n)"""
+    per = sectors_per_partition or len(sector_ids)
+    return [[generate_leaf_challenge(randomness, sid, (partition * per + i) * challenges + n, nodes)
+             for n in range(challenges)] for i, sid in enumerate(sector_ids)]
+
+
+def post_slots(circuit: FallbackPoStCircuit, sectors) -> bytes:
+    """Pack a partition's sector proofs into the slot layout (mi355x_groth16.h, mi_post_build).  sectors: one
+    dict per sector with comm_r, comm_c, comm_r_last and challenges: [{index, leaf, siblings}] (siblings per
+    tree level, the arity - 1 other children in position order).  Fewer sectors than the circuit takes are
+    padded by repeating the last one (prove_all_partitions, vanilla.hpp:241-245)."""
+    if not sectors or len(sectors) > circuit.sectors:
+        raise ValueError(f"1 .. {circuit.sectors} sectors per partition, got {len(sectors)}")
+    sectors = list(sectors) + [sectors[-1]] * (circuit.sectors - len(sectors))
+    out = []
+    for sec in sectors:
+        out += [_fr(sec["comm_r"]), _fr(sec["comm_c"]), _fr(sec["comm_r_last"])]
+        if len(sec["challenges"]) != circuit.challenges:
+            raise ValueError(f"{circuit.challenges} challenge(s) per sector, got {len(sec['challenges'])}")
+        for ch in sec["challenges"]:
+            if [len(s) + 1 for s in ch["siblings"]] != circuit.arities:
+                raise ValueError("sibling levels do not match the tree shape")
+            out += [_fr(ch["index"]), _fr(ch["leaf"])]
+            out += [_fr(v) for lvl in ch["siblings"] for v in lvl]
+    buf = b"".join(out)
+    assert len(buf) == 32 * circuit.info["slots"]
+    return buf
+
+
+def synthetic_post_instance(ctx, circuit: FallbackPoStCircuit, seed: int = 1, partition: int = 0):
+    """A consistent Fallback PoSt partition without sectors on disk (the bench's Window-PoSt partition and
+    the GPU tests): random randomness, sector ids, comm_c and challenged leaves; challenges derived by
+    generate_leaf_challenge; each sector's tree R-last built sparsely over its challenged leaves with random
+    filler nodes (Poseidon on the GPU, one batched call per tree level over all sectors); comm_r =
+    Poseidon-2(comm_c, comm_r_last).  Returns (randomness, sectors in post_slots' format)."""
+    from . import tree
+
+    rng = np.random.default_rng(seed)
+    S, C, nodes, ar = circuit.sectors, circuit.challenges, circuit.nodes, circuit.arities
+
+    def rand_many(k):
+        b = rng.integers(0, 256, size=(k, 32), dtype=np.uint8)
+        b[:, 31] &= 0x1F
+        return [int.from_bytes(r.tobytes(), "little") for r in b]
+
+    def pos_hash(a, flat):
+        return tree.to_ints(tree.poseidon_hash(ctx, a, flat)) if flat else []
+
+    randomness = rand_many(1)[0]
+    ids = [int(x) for x in rng.choice(2 ** 40, size=S, replace=False)]
+    chal = post_challenges(randomness, ids, C, nodes, partition, S)
+    levels = []  # per sector: list of {position: value} per tree level
+    for s in range(S):
+        leaves = {}
+        vals = rand_many(len(set(chal[s])))
+        for idx, v in zip(sorted(set(chal[s])), vals):
+            leaves[idx] = v
+        levels.append([leaves])
+    for a in ar:  # one GPU call per level over every sector's sparse tree
+        flat, parents = [], []
+        for s in range(S):
+            cur = levels[s][-1]
+            ps = sorted({p // a for p in cur})
+            missing = [p * a + k for p in ps for k in range(a) if p * a + k not in cur]
+            for q, v in zip(missing, rand_many(len(missing))):
+                cur[q] = v
+            for p in ps:
+                flat += [cur[p * a + k] for k in range(a)]
+            parents.append(ps)
+        hashed = pos_hash(a, flat)
+        o = 0
+        for s in range(S):
+            levels[s].append(dict(zip(parents[s], hashed[o:o + len(parents[s])])))
+            o += len(parents[s])
+    comm_r_last = [levels[s][-1][0] for s in range(S)]
+    comm_c = rand_many(S)
+    comm_r = pos_hash(2, [v for s in range(S) for v in (comm_c[s], comm_r_last[s])])
+    sectors = []
+    for s in range(S):
+        chs = []
+        for idx in chal[s]:
+            path, j = [], idx
+            for lvl, a in enumerate(ar):
+                g = j // a
+                path.append([levels[s][lvl][g * a + k] for k in range(a) if k != j % a])
+                j = g
+            chs.append({"index": idx, "leaf": levels[s][0][idx], "siblings": path})
+        sectors.append({"id": ids[s], "comm_r": comm_r[s], "comm_c": comm_c[s], "comm_r_last": comm_r_last[s],
+                        "challenges": chs})
+    return randomness, sectors
 
 
 def circuit_check_dev(ctx, circuit: Circuit, z_dev_ptr: int):

@@ -299,8 +299,12 @@ int mi_stacked_build(const mi_stacked_shape *shape, int with_r1cs, mi_stacked **
 /* out: constraints, inputs (with ONE), aux, instance slots, slots per challenge, tree D depth, siblings per
  * tree C / R-last path, program ops, program levels, SHA-256 blocks, Poseidon hashes, R1CS entries */
 int mi_stacked_info(const mi_stacked *s, uint64_t out[12]);
-/* the R1CS (pointers valid until mi_stacked_free); feed it to mi_circuit_load */
+/* the R1CS with 32-byte coefficients (materialised on the first call; pointers valid until mi_stacked_free):
+ * the form mi_circuit_load and external tools take */
 int mi_stacked_r1cs(const mi_stacked *s, mi_r1cs *out);
+/* the circuit uploaded straight from the builder's compact form (column + coefficient-table index per entry,
+ * 8 B instead of 36): mi_circuit_load without the host-side 32-byte coefficient arrays */
+int mi_stacked_load(mi_ctx *ctx, const mi_stacked *s, mi_circuit **out);
 /* (inputs - 1) x 32 B: the public inputs in generate_public_inputs order (without ONE) */
 int mi_stacked_public_inputs(const mi_stacked *s, const uint8_t *slots, uint8_t *out);
 /* z_dev: (inputs + aux) x 32 B on this context's GPU, fully written; slots refused if not canonical or an
@@ -308,6 +312,25 @@ int mi_stacked_public_inputs(const mi_stacked *s, const uint8_t *slots, uint8_t 
 int mi_stacked_witness_dev(mi_ctx *ctx, mi_stacked *s, const void *slots_dev, void *z_dev);
 int mi_stacked_witness(mi_ctx *ctx, mi_stacked *s, const uint8_t *slots, uint8_t *z_out);
 void mi_stacked_free(mi_stacked *s);
+/* ---- Fallback PoSt circuit (Window / Winning PoSt; SURVEY.md 8(a) a2 + 8(f)#3) ------------------------------
+ * Replaces the synthesis half of FallbackPoStCompound's circuit_proofs (the reference keeps the circuit's
+ * data, post/fallback/circuit.hpp:38-86 Sector / FallbackPoStCircuit, and the vanilla side,
+ * post/fallback/vanilla.hpp:188-251 prove_all_partitions, :398-411 generate_leaf_challenge; the synthesize
+ * body is rust-fil-proofs storage-proofs-post fallback/circuit.rs): per sector comm_c, comm_r_last, comm_r
+ * (public), Poseidon-2(comm_c, comm_r_last) == comm_r, and one private tree R-last inclusion proof per
+ * challenge.  The same mi_stacked object and calls (info, r1cs, public_inputs, witness, free) serve it.
+ * Instance slots: sector s from s * stride: +0 comm_r, +1 comm_c, +2 comm_r_last, then challenge n from
+ * +3 + n * (2 + siblings): challenged leaf index (u64), leaf, tree R-last siblings (leaf upward, position
+ * order).  Pinned by the reference's partition sizes (constants.hpp:85-89): 2349 sectors x 10 challenges at
+ * 32 GiB (8-8-0 trees, 2^30 nodes) = 125,279,217 constraints; 2300 x 10 at 64 GiB (8-8-2, 2^31) = 129,887,900.
+ * Public inputs: per sector comm_r, then the challenged leaf indices. */
+typedef struct {
+    uint32_t sectors, challenges; /* sectors per partition, challenges per sector */
+    uint64_t nodes;               /* nodes per sector */
+    uint32_t base_arity, sub_arity, top_arity, reserved;
+} mi_post_shape;
+int mi_post_build(const mi_post_shape *shape, int with_r1cs, mi_stacked **out);
+
 /* R1CS satisfaction on the device: out[0] = rows with (A z)(B z) != (C z), out[1] = the first one (~0 if none) */
 int mi_circuit_check_dev(mi_ctx *ctx, const mi_circuit *circuit, const void *z_dev, uint64_t out[2]);
 

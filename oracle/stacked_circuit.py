@@ -737,3 +737,34 @@ def challenge_synthesize(cs, ch, layers, comm_d, comm_c, comm_r_last, rid_bits, 
     # the challenged column's hash over the labels just recomputed, included in tree C
     col_hash = poseidon_hash_circuit(cs, labels, layers)
     por_synthesize(cs, col_hash, ch["index"], ch["c_siblings"], comm_c, c_levels, "poseidon")
+
+
+# ------------------------------------------------------------------------------------------ Fallback PoSt
+def fallback_post_circuit(cs, inst, shape):
+    """FallbackPoStCircuit::synthesize over a partition's sectors (the reference carries the data,
+    post/fallback/circuit.hpp:38-86; the body restated here is rust-fil-proofs storage-proofs-post
+    fallback/circuit.rs Sector::synthesize): comm_c, comm_r_last and comm_r allocated in that order, comm_r
+    inputized, hash2(comm_c, comm_r_last) == comm_r, then one private PoR per challenge whose root is the
+    allocated comm_r_last.  Pinned by the reference's partition sizes (constants.hpp:85-89): 2349 sectors x 10
+    challenges over 2^30-node 8-8-0 trees = 125,279,217 constraints (tests/test_cpu_post_circuit.py)."""
+    levels = tree_levels(inst["nodes"], shape)
+    for sec in inst["sectors"]:
+        comm_c = cs.alloc(sec["comm_c"])
+        comm_r_last = cs.alloc(sec["comm_r_last"])
+        comm_r = cs.alloc(sec["comm_r"])
+        inputize(cs, comm_r)
+        h = poseidon_hash_circuit(cs, [comm_c, comm_r_last], 2)
+        equal(cs, comm_r, h)
+        for ch in sec["challenges"]:
+            leaf = cs.alloc(ch["leaf"])
+            por_synthesize(cs, leaf, ch["index"], ch["siblings"], comm_r_last, levels, "poseidon")
+    return cs
+
+
+def post_constraints(sectors, challenges, levels):
+    """closed form of fallback_post_circuit's size: per sector 1 (comm_r input) + 311 (Poseidon-2) + 1
+    (equality), per challenge sum over levels of (index bits + insert + Poseidon) + 1 (path input) + 1 (root)"""
+    ins = {2: 2, 4: 8, 8: 22}
+    nb = {2: 1, 4: 2, 8: 3}
+    por = sum(nb[a] + ins[a] + poseidon_constraints(a) for a in levels) + 2
+    return sectors * (1 + poseidon_constraints(2) + 1 + challenges * por)

@@ -1,5 +1,7 @@
 """stacked_instance.py -- TEST INFRASTRUCTURE ONLY: small, fully built stacked-PoRep instances (a replica with
-real trees) whose vanilla openings satisfy the stacked circuit, and the reference's public-input order.
+real trees) whose vanilla openings satisfy the stacked circuit, and the reference's public-input order; the
+same for Fallback PoSt partitions (generate_post: sectors with full trees R-last, challenges derived by
+generate_leaf_challenge, post/fallback/vanilla.hpp:398-411).
 
   * tree D: binary SHA-256 tree over the data nodes (node hash = sha256(left LE || right LE) with byte 31 &=
     0x3f; pinned by the reference's compute_comm_d vectors, tests/test_cpu_sdr.py);
@@ -134,4 +136,45 @@ def public_inputs(inst):
         out += [p for p, _, _ in ch["drg"]]
         out += [p for p, _, _ in ch["exp"]]
         out += [c, c, c]  # the challenge (UInt64), tree R-last path, tree C path
+    return out
+
+
+# ------------------------------------------------------------------------------------------ Fallback PoSt
+def generate_leaf_challenge(randomness, sector_id, leaf_challenge_index, nodes):
+    """post/fallback/vanilla.hpp:398-411"""
+    h = hashlib.sha256(randomness.to_bytes(32, "little") + sector_id.to_bytes(8, "little") +
+                       leaf_challenge_index.to_bytes(8, "little")).digest()
+    return int.from_bytes(h[:8], "little") % nodes
+
+
+def generate_post(n_sectors, challenges, nodes, shape, seed=1, partition=0):
+    """A Fallback PoSt partition over fully built trees R-last: per sector random leaves (the encoded replica
+    nodes), the (base, sub, top) Poseidon tree, a random comm_c, comm_r = Poseidon-2(comm_c, comm_r_last); the
+    challenged leaves of sector i are generate_leaf_challenge(randomness, id, (partition * S + i) * C + n)
+    (prove_all_partitions, vanilla.hpp:222-236)."""
+    rng = random.Random(seed)
+    fr = lambda: rng.randrange(R)
+    randomness = fr()
+    sectors = []
+    for i in range(n_sectors):
+        sid = rng.randrange(2 ** 40)
+        leaves = [fr() for _ in range(nodes)]
+        rows, ar = build_tree(leaves, shape, lambda a, xs: poseidon(a, xs))
+        comm_r_last, comm_c = rows[-1][0], fr()
+        chs = []
+        for n in range(challenges):
+            idx = generate_leaf_challenge(randomness, sid, (partition * n_sectors + i) * challenges + n, nodes)
+            chs.append({"index": idx, "leaf": leaves[idx], "siblings": siblings(rows, ar, idx)})
+        sectors.append({"id": sid, "comm_c": comm_c, "comm_r_last": comm_r_last,
+                        "comm_r": poseidon(2, [comm_c, comm_r_last]), "challenges": chs})
+    return {"randomness": randomness, "sectors": sectors, "nodes": nodes, "shape": shape}
+
+
+def post_public_inputs(inst):
+    """FallbackPoStCompound::generate_public_inputs (without ONE): per sector comm_r, then per challenge the
+    private PoR's packed path = the challenged leaf index"""
+    out = []
+    for sec in inst["sectors"]:
+        out.append(sec["comm_r"])
+        out += [ch["index"] for ch in sec["challenges"]]
     return out
