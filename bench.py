@@ -457,88 +457,117 @@ def stacked_leg(args, fg, ctx, device, world):
     return res
 
 
-def config5_leg(args, fg, synth_mod, ctx, rank, world, gdev, dist, partitions=10):
-    """BASELINE config 5 on the driver's N-GPU run: a Window-PoSt batch of 10 partitions of 32 GiB-sector
-    size (2^27-domain synthetic circuit) proven round-robin over the ranks (10 over 8 GPUs: two rounds on
-    ranks 0 and 1; post.cpp:37-46, constants.hpp:88), the 10 x 192-byte multi-proof all-gathered over
-    RCCL.  Every rank builds its own circuit and key (independent partitions over one SRS); the makespan is
-    the max over ranks; rank 0 pairing-verifies every gathered proof.  Host memory per rank is bounded by
-    one synthetic circuit (freed after upload) plus the pinned witness; below that the leg falls back to
-    2^26 and says so."""
+def window_post_leg(args, fg, ctx, device, rank, world, gdev, dist):
+    """The Window-PoSt circuit itself: partitions of --post-sectors 32 GiB sectors x
+    --post-challenges challenges (2349 x 10 = 125,279,217 constraints, constants.hpp:85-89; domain 2^27).
+    Setup (untimed): the R1CS built on the host and uploaded in compact form, the proving key generated on the
+    GPU from the fixed toxic waste (the same SRS on every rank), one synthetic partition instance per
+    partition (sparse trees R-last, challenges by generate_leaf_challenge) resident in HBM.  Timed: per
+    partition the GPU witness (mi_stacked_witness_dev) and the proof.
+      world == 1: --post-reps partitions back to back on one GPU (the per-partition rate of config 5).
+      world > 1 : BASELINE config 5 -- --post-partitions (10) partitions round-robin over the ranks (two rounds
+                  on ranks 0 and 1 at 8 GPUs), the P x 192-byte multi-proof all-gathered over RCCL, the makespan
+                  max over ranks; rank 0 pairing-verifies every gathered proof against each partition's inputs."""
     import gc
 
     import numpy as np
     import torch
 
+    from fil_groth16 import stacked
     from fil_groth16.compound import shard_partitions
     from fil_groth16.distributed import prove_partitions
 
-    lr = args.config5_log_rows
-    need_gb = 30.0 * 2.0 ** (lr - 27)  # host CSR + witness of one synthetic circuit, plus the pinned copy
+    S, C, nodes = args.post_sectors, args.post_challenges, 1 << args.post_log_nodes
     try:
         avail_gb = int(next(l for l in open("/proc/meminfo") if l.startswith("MemAvailable")).split()[1]) / 1e6
     except (OSError, StopIteration):
         avail_gb = None
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
-    fallback = None
-    if avail_gb is not None and lr > 26 and avail_gb < local_world * need_gb:
-        fallback = f"MemAvailable {avail_gb:.0f} GB < {local_world} ranks x {need_gb:.0f} GB: 2^26"
-        lr = 26
+    need_gb = 25.0 * S / 2349  # compact R1CS build peak + instances, per rank
+    if avail_gb is not None and avail_gb < local_world * need_gb:
+        return {"skipped": f"MemAvailable {avail_gb:.0f} GB < {local_world} ranks x {need_gb:.0f} GB"}
     t0 = time.perf_counter()
-    sc = synth_mod.SynthCircuit(lr, args.n_in, args.seed)
-    circ = sc.load(ctx)
+    pc = stacked.FallbackPoStCircuit(S, C, nodes, 8, 8, 0)
+    t_build = time.perf_counter() - t0
+    circ = pc.load(ctx)
     pk = fg.generate_random_parameters(ctx, circ, splitmix_frs(TOXIC_SEED, 5))
-    z = fg.HostBuffer(32 * sc.num_vars)
-    np.copyto(z.array, sc.z_array())
-    n, n_in = sc.n, sc.n_in
-    del sc
-    gc.collect()
+    P = args.post_partitions if world > 1 else args.post_reps
+    mine = shard_partitions(P, rank, world) if world > 1 else list(range(P))
+    slots, sdev = {}, {}
+    for p in (range(P) if rank == 0 else mine):  # rank 0 also needs every partition's public inputs
+        _, sectors = stacked.synthetic_post_instance(ctx, pc, seed=4000 + p, partition=p)
+        slots[p] = stacked.post_slots(pc, sectors)
+        if p in mine:
+            sdev[p] = torch.from_numpy(np.frombuffer(slots[p], dtype=np.uint8).copy()).to(device)
+    z = torch.empty(32 * pc.num_vars, dtype=torch.uint8, device=device)
     ctx.synchronize()
+    torch.cuda.synchronize()
     t_setup = time.perf_counter() - t0
-    mine = shard_partitions(partitions, rank, world)
-    blind = splitmix_frs(9000 + rank, 2 * (len(mine) * (args.config5_steps + 1) + 1))
-    fg.prove_batch(ctx, pk, circ, [z], [(blind[0], blind[1])])  # warm-up
+    blind = splitmix_frs(9000 + rank, 2 * (len(mine) * (args.config5_steps + 1) + 2))
+    state = {"k": 2}
+
+    def prove_ids(ids):
+        out = []
+        for p in ids:
+            pc.witness_dev(ctx, sdev[p].data_ptr(), z.data_ptr())
+            k = state["k"]
+            state["k"] += 2
+            out.append(fg.prove(ctx, pk, circ, z.data_ptr(), blind[k], blind[k + 1]))
+        return out
+
+    if mine:  # warm-up (program upload, plans)
+        pc.witness_dev(ctx, sdev[mine[0]].data_ptr(), z.data_ptr())
+        fg.prove(ctx, pk, circ, z.data_ptr(), blind[0], blind[1])
     ctx.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    ctx.reset_stats()
+    steps = args.config5_steps if world > 1 else 1
     t1 = time.perf_counter()
     multi = []
-    for k in range(args.config5_steps):
-        off = 2 + 2 * k * len(mine)
-        multi.append(prove_partitions(
-            lambda ids: fg.prove_batch(ctx, pk, circ, [z] * len(ids),
-                                       [(blind[off + 2 * i], blind[off + 2 * i + 1]) for i in range(len(ids))]),
-            partitions, rank, world, gdev))
+    for _ in range(steps):
+        if world > 1:
+            multi.append(prove_partitions(prove_ids, P, rank, world, gdev))
+        else:
+            multi.append(b"".join(prove_ids(mine)))
     ctx.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t1
     mine_dt = dt
+    st = ctx.stats()
     if dist:
         tt = torch.tensor([dt], dtype=torch.float64, device=gdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
-    counts = [len(shard_partitions(partitions, r, world)) for r in range(world)]
     out = None
     if rank == 0:
         vk, ic = pk.verifying_key()
-        pub = z.array[32:32 * n_in].tobytes()
-        proofs = [m[192 * i:192 * (i + 1)] for m in multi for i in range(partitions)]
-        verified = bool(fg.verify_batch(vk, ic, [pub] * len(proofs), proofs))
-        makespan = dt / args.config5_steps
-        size = "32 GiB-sector partition size" if lr >= 27 else "REDUCED size, not the config-5 shape"
-        out = {"workload": f"BASELINE config 5: Window-PoSt batch of {partitions} partitions x synthetic "
-                           f"2^{lr}-domain R1CS ({n} constraints each, {size}), round-robin "
-                           f"over {world} GPU(s), {partitions} x 192-byte multi-proof all-gathered",
-               "partitions": partitions, "n_gpus": world, "per_rank_partitions": counts,
-               "steps": args.config5_steps, "makespan_s": makespan, "proofs_per_s": partitions / makespan,
-               "constraints_per_s": partitions * n / makespan, "rank0_busy_s": mine_dt / args.config5_steps,
-               "verified": verified, "verified_proofs": len(proofs), "setup_s": t_setup,
-               "host_mem_available_gb": avail_gb, "fallback": fallback}
-    del pk, circ, z
+        proofs = [m[192 * i:192 * (i + 1)] for m in multi for i in range(P)]
+        pubs = [pc.public_inputs(slots[i]) for _ in multi for i in range(P)]
+        verified = bool(fg.verify_batch(vk, ic, pubs, proofs))
+        per_step = dt / steps
+        n = pc.num_constraints
+        out = {"workload": f"Window-PoSt partitions of the real circuit: {S} sectors x {C} challenges over 2^"
+                           f"{args.post_log_nodes}-node 8-8-0 trees R-last ({n} constraints, {pc.num_inputs} inputs, "
+                           f"domain 2^{circ.d.bit_length() - 1}); synthetic consistent partitions; timed = GPU "
+                           f"witness + proof per partition" +
+                           (f"; BASELINE config 5: {P} partitions round-robin over {world} GPUs, {P} x 192-byte "
+                            f"multi-proof all-gathered" if world > 1 else f"; {P} partitions on one GPU"),
+               "partitions": P, "n_gpus": world, "constraints": n, "steps": steps,
+               "makespan_s": per_step, "proofs_per_s": P / per_step, "constraints_per_s": P * n / per_step,
+               "ms_per_partition_rank0": 1e3 * mine_dt / steps / max(1, len(mine)),
+               "witness_ms_per_partition_rank0": (st["wit_a"]["ms"] + st["wit_sha"]["ms"] + st["wit_pos"]["ms"]) /
+                                                 max(1, steps * len(mine)),
+               "verified": verified, "verified_proofs": len(proofs),
+               "setup_s": {"r1cs_build": t_build, "total": t_setup}, "host_mem_available_gb": avail_gb}
+        if world > 1:
+            out["per_rank_partitions"] = [len(shard_partitions(P, r, world)) for r in range(world)]
+    del pk, circ, z, sdev, pc
     gc.collect()
+    torch.cuda.synchronize()
     return out
 
 
@@ -568,9 +597,13 @@ def main():
     ap.add_argument("--stacked-layers", type=int, default=11)
     ap.add_argument("--stacked-challenges", type=int, default=18)
     ap.add_argument("--stacked-reps", type=int, default=2)
-    ap.add_argument("--config5-log-rows", type=int, default=27,
-                    help="multi-GPU runs: the 10-partition config-5 leg at this domain (0 skips)")
-    ap.add_argument("--config5-steps", type=int, default=2)
+    ap.add_argument("--post-sectors", type=int, default=2349,
+                    help="Window-PoSt partition: sectors (0 skips the Window-PoSt / config-5 leg)")
+    ap.add_argument("--post-challenges", type=int, default=10)
+    ap.add_argument("--post-log-nodes", type=int, default=30)
+    ap.add_argument("--post-partitions", type=int, default=10, help="multi-GPU runs: config 5's partition count")
+    ap.add_argument("--post-reps", type=int, default=2, help="one GPU: Window-PoSt partitions proven (witness + proof)")
+    ap.add_argument("--config5-steps", type=int, default=1)
     ap.add_argument("--tree-log-nodes", type=int, default=21,
                     help="secondary: tree C over 2^N columns x 11 layers (N a multiple of 3; 0 skips)")
     ap.add_argument("--sdr-log-labels", type=int, default=24,
@@ -759,18 +792,18 @@ def main():
             cpu = {"value": None, "unit": "constraints/s", "cores": None, "kind": "port", "sample": f"failed: {e}"}
 
     config5 = None
-    if world > 1 and not P and args.config5_log_rows:
+    if world > 1 and not P and args.post_sectors:
         import gc
 
         del pk, circ, zhost, sc
         gc.collect()
         ctx.synchronize()
         try:
-            config5 = config5_leg(args, fg, synth_mod, ctx, rank, world, gdev, dist)
+            config5 = window_post_leg(args, fg, ctx, device, rank, world, gdev, dist)
         except Exception as e:  # reported, never fatal to the main measurement
             config5 = {"error": str(e)}
 
-    if rank == 0 and world == 1 and (args.config4_log_rows or args.stacked_log_nodes):
+    if rank == 0 and world == 1 and (args.config4_log_rows or args.stacked_log_nodes or args.post_sectors):
         import gc
 
         del pk, circ, zhost, sc  # the secondary legs need the HBM
@@ -789,6 +822,13 @@ def main():
             stacked_res = stacked_leg(args, fg, ctx, device, world)
         except Exception as e:  # reported, never fatal to the config-3 measurement
             stacked_res = {"error": str(e)}
+
+    post_res = None
+    if rank == 0 and world == 1 and args.post_sectors and args.post_reps:
+        try:
+            post_res = window_post_leg(args, fg, ctx, device, rank, world, None, None)
+        except Exception as e:  # reported, never fatal to the config-3 measurement
+            post_res = {"error": str(e)}
 
     if rank != 0:
         if dist:
@@ -898,6 +938,7 @@ def main():
         "config4": config4,
         "config5": config5,
         "stacked_porep_32gib": stacked_res,
+        "window_post_32gib": post_res,
         "timers_ms": {k: round(v["ms"], 3) for k, v in stats.items()},
         "setup_s": {"synth": t_synth, "circuit_load": t_load, "srs": t_srs},
         "device_gb_after_setup": round(dev_used_gb, 2),

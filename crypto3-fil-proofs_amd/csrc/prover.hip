@@ -896,12 +896,18 @@ void build_hi_tables(Ctx &c, Srs &S) {
         uint64_t n;
         g1_affine_t **dst;
     } qs[] = {{S.h_perm, S.n_h, &S.h_hi}, {S.l, S.n_l, &S.l_hi}, {S.a, S.n_a, &S.a_hi}};
-    if (msm_glv_mode() == 2) {  // auto: tables only while they leave half of the free HBM to the prover
+    if (msm_glv_mode() == 2) {  // auto: tables only while they leave the prover its working set
         uint64_t need = 0;
         for (auto &q : qs) need += q.src ? q.n * sizeof(g1_affine_t) : 0;
         size_t free_b = 0, total_b = 0;
         MI_HIP(hipMemGetInfo(&free_b, &total_b));
-        if (need > free_b / 2) return;  // the MSMs take the GLV split instead
+        // a proof's scratch: the Montgomery witness and the three QAP vectors (32 (m + 3 d) bytes), and per
+        // lane one split-mode MSM plan (keys / values sorted and unsorted over ~6 windows of 2 n half-scalar
+        // points, chunk partials and sort space) over the larger of h and l: measured 109 GB in all for a
+        // 2^27-domain Window-PoSt partition (tools/post_mem.py), i.e. ~350 B per point and lane
+        const uint64_t big = S.d > S.n_l ? S.d : S.n_l;
+        const uint64_t work = 32 * (S.n_l + 3 * S.d) + 2 * 360 * big;
+        if (need + work + (1ull << 30) > free_b) return;  // the MSMs take the GLV split instead
     }
     for (auto &q : qs) {
         if (!q.src || !q.n) continue;
@@ -1061,6 +1067,10 @@ Srs *srs_generate(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5]) {
         hipFree(pw);
         hipFree(t1);
         hipFree(t2);
+        // the column sums' sort and reduce-by-key buffers scale with the R1CS entries (tens of GB for a
+        // 32 GiB partition): key generation is one-time, so give them back before the table decision and
+        // the first proof
+        for (auto &b : c.scratch) b.release();
         // verifying key
         S->alpha_g1 = host_mul_affine(g1, toxic_canonical[1]);
         S->beta_g1 = host_mul_affine(g1, toxic_canonical[2]);
