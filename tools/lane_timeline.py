@@ -28,7 +28,7 @@ CLASSES = [
                                 "k_flag_multi", "k_tree_count", "k_tree_heads", "merge_sort", "scan",
                                 "init_lookback", "partition", "reduce_config", "transform")),
     ("fills / copies", ("__amd_rocclr",)),
-    ("witness map", ("k_eval_rows", "k_copy_to_mont")),
+    ("witness map", ("k_eval_rows", "k_eval_blocks", "k_eval_tail", "k_copy_to_mont")),
 ]
 
 
