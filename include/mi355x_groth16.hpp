@@ -59,6 +59,8 @@ private:
 class circuit {
 public:
     circuit(context &ctx, const mi_r1cs &cs) { check(mi_circuit_load(ctx.get(), &cs, &h_)); }
+    // a stacked-PoRep / Fallback-PoSt circuit built by the library, uploaded in its compact form
+    circuit(context &ctx, const mi_stacked *built) { check(mi_stacked_load(ctx.get(), built, &h_)); }
     ~circuit() { mi_circuit_free(h_); }
     circuit(const circuit &) = delete;
     circuit &operator=(const circuit &) = delete;
