@@ -115,6 +115,7 @@ def cpu_baseline(args, fg, synth_mod, ctx):
         t0 = time.perf_counter()
         proof_cpu = op.prove(zb, r, s)[0]
         dt = time.perf_counter() - t0
+        log(0, f"cpu baseline: 2^{lr} rows in {dt:.1f} s")
         proof_gpu = fg.prove(ctx, pk, circ, zb, r, s)
         samples.append({"log_rows": lr, "constraints": sc.n, "seconds": dt, "constraints_per_s": sc.n / dt,
                         "gpu_proof_bytes_identical": proof_cpu == proof_gpu})
@@ -345,6 +346,7 @@ def config4_leg(args, fg, synth_mod, ctx):
     pk = fg.generate_random_parameters(ctx, circ, splitmix_frs(TOXIC_SEED, 5))
     ctx.synchronize()
     t_setup = time.perf_counter() - t0
+    log(0, f"config 4 setup {t_setup:.1f} s")
     z = fg.HostBuffer(32 * sc.num_vars)
     np.copyto(z.array, sc.z_array())
     blind = splitmix_frs(4000, 2 * (1 + args.config4_steps))
@@ -392,6 +394,7 @@ def stacked_leg(args, fg, ctx, device, world):
     pk = fg.generate_random_parameters(ctx, circ, splitmix_frs(TOXIC_SEED, 5))
     ctx.synchronize()
     t_setup = time.perf_counter() - t0
+    log(0, f"stacked setup {t_setup:.1f} s")
     nv = sc_.num_vars
     sd = torch.from_numpy(np.frombuffer(slots, dtype=np.uint8).copy()).to(device)
     z = torch.empty(32 * nv, dtype=torch.uint8, device=device)
@@ -503,6 +506,7 @@ def window_post_leg(args, fg, ctx, device, rank, world, gdev, dist):
     ctx.synchronize()
     torch.cuda.synchronize()
     t_setup = time.perf_counter() - t0
+    log(rank, f"Window-PoSt setup {t_setup:.1f} s (R1CS {t_build:.1f} s, key, {len(slots)} partition instances)")
     blind = splitmix_frs(9000 + rank, 2 * (len(mine) * (args.config5_steps + 1) + 2))
     state = {"k": 2}
 
@@ -710,6 +714,7 @@ def main():
 
     # the C2 self-check policy (api/seal.hpp:310-313), outside the timer: every gathered proof is
     # pairing-verified (one batch multi-pairing with OS-random weights) and the last one singly
+    log(rank, f"main leg: {1e3 * dt / args.steps:.1f} ms per step, {proofs_total} proofs")
     t_ver = time.perf_counter()
     verified = bool(fg.verify_batch(vk, ic, [pub_inputs] * len(proofs), proofs)) and \
         bool(fg.verify(vk, ic, pub_inputs, proofs[-1]))
@@ -772,9 +777,11 @@ def main():
 
     # tree C over one 2^tree_log_nodes-node sub-tree (device-resident labels), and the
     # oracle's CPU Poseidon on a sample of the same columns
+    log(rank, "secondary: MSM / configs[1] micro done")
     tree = None
     if args.tree_log_nodes and rank == 0:
         tree = tree_c_leg(args, fg, ctx, device, world)
+        log(rank, "tree C leg done")
 
     # SDR labelling-witness labels (SHA-256 over gathered parents)
     sdr = None
@@ -783,6 +790,7 @@ def main():
             sdr = sdr_leg(args, fg, ctx, device, world)
         except Exception as e:  # reported, never fatal to the main measurement
             sdr = {"error": str(e)}
+        log(rank, "SDR label leg done")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -799,6 +807,7 @@ def main():
         gc.collect()
         ctx.synchronize()
         try:
+            log(rank, "config 5 leg (Window-PoSt partitions) ...")
             config5 = window_post_leg(args, fg, ctx, device, rank, world, gdev, dist)
         except Exception as e:  # reported, never fatal to the main measurement
             config5 = {"error": str(e)}
@@ -812,6 +821,7 @@ def main():
     config4 = None
     if rank == 0 and world == 1 and args.config4_log_rows:
         try:
+            log(rank, "config 4 leg ...")
             config4 = config4_leg(args, fg, synth_mod, ctx)
         except Exception as e:  # reported, never fatal to the config-3 measurement
             config4 = {"value": None, "error": str(e)}
@@ -819,6 +829,7 @@ def main():
     stacked_res = None
     if rank == 0 and world == 1 and args.stacked_log_nodes:
         try:
+            log(rank, "stacked PoRep leg ...")
             stacked_res = stacked_leg(args, fg, ctx, device, world)
         except Exception as e:  # reported, never fatal to the config-3 measurement
             stacked_res = {"error": str(e)}
@@ -826,6 +837,7 @@ def main():
     post_res = None
     if rank == 0 and world == 1 and args.post_sectors and args.post_reps:
         try:
+            log(rank, "Window-PoSt leg ...")
             post_res = window_post_leg(args, fg, ctx, device, rank, world, None, None)
         except Exception as e:  # reported, never fatal to the config-3 measurement
             post_res = {"error": str(e)}
