@@ -1654,6 +1654,7 @@ int mi_sdr_labels_dev(mi_ctx *ctx, const uint8_t replica_id[32], uint64_t count,
         CtxLock l(ctx);
         mi::sdr_labels_dev(ctx->c, mi::sdr_replica(replica_id), (const uint32_t *)layers_dev,
                            (const uint64_t *)nodes_dev, parents_dev, n_parents, count, labels_dev);
+        MI_HIP(hipStreamSynchronize(ctx->c.stream));  // labels_dev complete on return, like the other _dev calls
     });
 }
 
@@ -1708,6 +1709,7 @@ int mi_sdr_labeling_proofs_dev(mi_ctx *ctx, const uint8_t replica_id[32], unsign
                                   (const uint32_t *)layers_dev, (const uint64_t *)challenges_dev,
                                   (const uint32_t *)parent_idx_dev, n_base, n_exp, count, labels_dev,
                                   parents_out_dev);
+        MI_HIP(hipStreamSynchronize(c.stream));
     });
 }
 
@@ -1747,6 +1749,14 @@ int mi_tree_inclusion_paths_dev(mi_ctx *ctx, unsigned arity, const void *leaves_
                            (mi::fr_t *)leaf_out_dev, (mi::fr_t *)siblings_out_dev);
         MI_HIP(hipStreamSynchronize(c.stream));
     });
+}
+int mi_tree_d_inclusion_paths_dev(mi_ctx *ctx, const void *leaves_dev, uint64_t leaf_count, const void *tree_dev,
+                                  uint64_t count, const void *challenges_dev, void *leaf_out_dev,
+                                  void *siblings_out_dev) {
+    // tree D keeps every row (binary SHA-256; rebuilding discarded rows would need the SHA-256 hasher), so its
+    // openings are pure reads of the cached rows: arity 2, rows_to_discard 0, nothing recomputed
+    return mi_tree_inclusion_paths_dev(ctx, 2, leaves_dev, leaf_count, 0, tree_dev, count, challenges_dev,
+                                       leaf_out_dev, siblings_out_dev);
 }
 
 int mi_tree_d_build_dev(mi_ctx *ctx, const void *leaves_dev, uint64_t leaf_count, void *tree_dev) {

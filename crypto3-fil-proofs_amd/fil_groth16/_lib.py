@@ -27,7 +27,7 @@ EXPORTS = [
     "mi_poseidon_constants", "mi_poseidon_hash", "mi_poseidon_hash_dev", "mi_tree_cache_size",
     "mi_tree_build", "mi_tree_build_dev", "mi_tree_c_build", "mi_tree_c_build_dev",
     "mi_tree_r_last_build", "mi_tree_r_last_build_dev",
-    "mi_sdr_labels", "mi_sdr_labels_dev", "mi_sdr_labeling_proofs_dev", "mi_tree_inclusion_paths_dev",
+    "mi_sdr_labels", "mi_sdr_labels_dev", "mi_sdr_labeling_proofs_dev", "mi_tree_inclusion_paths_dev", "mi_tree_d_inclusion_paths_dev",
     "mi_tree_d_build_dev", "mi_srs_msm_info", "mi_points_check_subgroup", "mi_points_info",
     "mi_groth16_prove_random", "mi_groth16_prove_dev_random", "mi_groth16_prove_batch_random",
     "mi_srs_stream_begin", "mi_srs_stream_part", "mi_srs_stream_end", "mi_srs_stream_abort", "mi_srs_export_query_dev",
@@ -153,6 +153,7 @@ def lib():
         "mi_tree_r_last_build": ([vp, u64, vp, vp, ctypes.c_uint, ctypes.c_uint, vp], c_int),
         "mi_tree_r_last_build_dev": ([vp, u64, vp, vp, ctypes.c_uint, ctypes.c_uint, vp], c_int),
         "mi_tree_inclusion_paths_dev": ([vp, ctypes.c_uint, vp, u64, ctypes.c_uint, vp, u64, vp, vp, vp], c_int),
+        "mi_tree_d_inclusion_paths_dev": ([vp, vp, u64, vp, u64, vp, vp, vp], c_int),
         "mi_tree_d_build_dev": ([vp, vp, u64, vp], c_int),
         "mi_sdr_labels": ([vp, vp, u64, vp, vp, vp, ctypes.c_uint, vp], c_int),
         "mi_sdr_labels_dev": ([vp, vp, u64, vp, vp, vp, ctypes.c_uint, vp], c_int),

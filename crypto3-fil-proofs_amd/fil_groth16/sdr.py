@@ -115,5 +115,15 @@ class EncodingProof:
 
 def build_tree_d_dev(ctx, leaves_ptr: int, leafs: int, tree_ptr: int) -> None:
     """tree D over 32-byte data nodes on the device (node = SHA256(left || right), byte 31 &= 0x3f): every row
-    above the leaves, bottom-up, leafs - 1 entries.  Openings: tree.gen_proofs_dev(arity=2, rows_to_discard=0)."""
+    above the leaves, bottom-up, leafs - 1 entries.  Openings: tree_d_proofs_dev."""
     check(lib().mi_tree_d_build_dev(ctx.h, ctypes.c_void_p(leaves_ptr), leafs, ctypes.c_void_p(tree_ptr)))
+
+
+def tree_d_proofs_dev(ctx, leaves_ptr: int, leafs: int, tree_ptr: int, count: int, challenges_ptr: int,
+                      leaf_out_ptr: int, siblings_out_ptr: int) -> None:
+    """Inclusion proofs in a device-resident tree D (MerkleTree_gen_proof(tree_d), vanilla/proof.hpp:139-140):
+    the layouts of tree.gen_proofs_dev at arity 2; every row is cached, so nothing is rebuilt (a rebuild would
+    need SHA-256, and tree.gen_proofs_dev rebuilds discarded rows with Poseidon)."""
+    vp = ctypes.c_void_p
+    check(lib().mi_tree_d_inclusion_paths_dev(ctx.h, vp(leaves_ptr), leafs, vp(tree_ptr), count, vp(challenges_ptr),
+                                              vp(leaf_out_ptr), vp(siblings_out_ptr)))

@@ -400,7 +400,8 @@ int mi_tree_r_last_build_dev(mi_ctx *ctx, uint64_t nodes, const void *labels_dev
  * siblings_out[(i * H + j) * (arity - 1) ..] = the arity - 1 siblings of c_i's ancestor in row j (0 = leaves,
  * H = log_arity(leaf_count) rows), in position order skipping its own slot (that slot is digit j of c_i in
  * base arity).  tree_dev is the cached rows of mi_tree_build_dev / mi_tree_c_build_dev / mi_tree_r_last_build_dev
- * with the same rows_to_discard; discarded rows are rebuilt per challenge from the leaves.  Replaces
+ * with the same rows_to_discard; discarded rows are rebuilt per challenge from the leaves WITH POSEIDON (trees C
+ * and R-last; a SHA-256 tree D goes through mi_tree_d_inclusion_paths_dev, which never rebuilds).  Replaces
  * MerkleTree_gen_proof (tree D / tree C openings, porep/stacked/vanilla/proof.hpp:139-140, column_proof.hpp
  * make_proof) and MerkleTree_gen_cached_proof (tree R-last, proof.hpp:183-186).  A challenge >= leaf_count is
  * refused with MI_ERR_ARG before any read. */
@@ -429,9 +430,13 @@ int mi_sdr_labels_dev(mi_ctx *ctx, const uint8_t replica_id[32], uint64_t count,
 /* tree D (comm_d): the binary SHA-256 tree over the sector's 32-byte data nodes, node = SHA256(left || right)
  * with byte 31 &= 0x3f (Sha256Hasher, truncated into Fr); tree_dev receives every row above the leaves,
  * bottom-up, leaf_count - 1 entries (mi_tree_cache_size(leaf_count, 2, 0)).  leaf_count a power of two.
- * Openings: mi_tree_inclusion_paths_dev(arity 2, rows_to_discard 0).  Replaces the tree D build of
- * transform_and_replicate_layers / MerkleTree_gen_proof(tree_d) (porep/stacked/vanilla/proof.hpp:139-140). */
+ * Openings: mi_tree_d_inclusion_paths_dev (the layouts of mi_tree_inclusion_paths_dev at arity 2, every row
+ * cached).  Replaces the tree D build of transform_and_replicate_layers / MerkleTree_gen_proof(tree_d)
+ * (porep/stacked/vanilla/proof.hpp:139-140).  The SDR and tree _dev calls return with their outputs written. */
 int mi_tree_d_build_dev(mi_ctx *ctx, const void *leaves_dev, uint64_t leaf_count, void *tree_dev);
+int mi_tree_d_inclusion_paths_dev(mi_ctx *ctx, const void *leaves_dev, uint64_t leaf_count, const void *tree_dev,
+                                  uint64_t count, const void *challenges_dev, void *leaf_out_dev,
+                                  void *siblings_out_dev);
 int mi_sdr_labeling_proofs_dev(mi_ctx *ctx, const uint8_t replica_id[32], unsigned n_layers,
                                uint64_t nodes_per_layer, const void *layer_labels_dev, uint64_t count,
                                const void *layers_dev, const void *challenges_dev, const void *parent_idx_dev,

@@ -185,8 +185,8 @@ def test_tree_d_vs_hashlib_and_openings(ctx, n):
     d_leaf = torch.zeros(32 * 3, dtype=torch.uint8, device=dev)
     d_sib = torch.zeros(32 * 3 * H, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
-    fg.tree.gen_proofs_dev(ctx, 2, d_leaves.data_ptr(), n, 0, d_tree.data_ptr(), 3, d_chal.data_ptr(),
-                           d_leaf.data_ptr(), d_sib.data_ptr())
+    fg.sdr.tree_d_proofs_dev(ctx, d_leaves.data_ptr(), n, d_tree.data_ptr(), 3, d_chal.data_ptr(),
+                             d_leaf.data_ptr(), d_sib.data_ptr())
     ctx.synchronize()
     sib = d_sib.cpu().numpy().tobytes()
     for i, c in enumerate(int(x) for x in chal):
