@@ -468,9 +468,12 @@ def window_post_leg(args, fg, ctx, device, rank, world, gdev, dist):
     partition (sparse trees R-last, challenges by generate_leaf_challenge) resident in HBM.  Timed: per
     partition the GPU witness (mi_stacked_witness_dev) and the proof.
       world == 1: --post-reps partitions back to back on one GPU (the per-partition rate of config 5).
-      world > 1 : BASELINE config 5 -- --post-partitions (10) partitions round-robin over the ranks (two rounds
-                  on ranks 0 and 1 at 8 GPUs), the P x 192-byte multi-proof all-gathered over RCCL, the makespan
-                  max over ranks; rank 0 pairing-verifies every gathered proof against each partition's inputs."""
+      world > 1 : BASELINE config 5 -- --post-partitions (10) partitions over the ranks: P - P % W round-robin as
+                  whole proofs, the P % W tail partitions each over a group of ranks in latency mode (at 8 GPUs:
+                  partitions 0-7 whole, 8 and 9 over four GPUs each; MI_C5_SCHEDULE=roundrobin leaves them
+                  to a second round on ranks 0 and 1); the P x 192-byte multi-proof (whole proofs + shares)
+                  all-gathered over RCCL, the makespan max over ranks; rank 0 pairing-verifies every gathered
+                  proof against each partition's inputs."""
     import gc
 
     import numpy as np
@@ -478,7 +481,7 @@ def window_post_leg(args, fg, ctx, device, rank, world, gdev, dist):
 
     from fil_groth16 import stacked
     from fil_groth16.compound import shard_partitions
-    from fil_groth16.distributed import prove_partitions
+    from fil_groth16.distributed import balanced_schedule, prove_partitions, prove_partitions_balanced
 
     S, C, nodes = args.post_sectors, args.post_challenges, 1 << args.post_log_nodes
     try:
@@ -495,7 +498,14 @@ def window_post_leg(args, fg, ctx, device, rank, world, gdev, dist):
     circ = pc.load(ctx)
     pk = fg.generate_random_parameters(ctx, circ, splitmix_frs(TOXIC_SEED, 5))
     P = args.post_partitions if world > 1 else args.post_reps
-    mine = shard_partitions(P, rank, world) if world > 1 else list(range(P))
+    # config 5's schedule: "balanced" (default) proves the P % W tail partitions in latency mode over rank
+    # groups (distributed.balanced_schedule); "roundrobin" leaves them to a last round on P % W ranks
+    schedule = os.environ.get("MI_C5_SCHEDULE", "balanced") if world > 1 else "local"
+    whole, tail = balanced_schedule(P, world) if schedule == "balanced" else \
+        ([shard_partitions(P, r, world) for r in range(world)], [])
+    if world == 1:
+        whole = [list(range(P))]
+    mine = whole[rank] + [p for p, rs in tail if rank in rs]
     slots, sdev = {}, {}
     for p in (range(P) if rank == 0 else mine):  # rank 0 also needs every partition's public inputs
         _, sectors = stacked.synthetic_post_instance(ctx, pc, seed=4000 + p, partition=p)
@@ -519,9 +529,22 @@ def window_post_leg(args, fg, ctx, device, rank, world, gdev, dist):
             out.append(fg.prove(ctx, pk, circ, z.data_ptr(), blind[k], blind[k + 1]))
         return out
 
+    vk, ic = pk.verifying_key()
+
+    def share_fn(p, k, g):
+        pc.witness_dev(ctx, sdev[p].data_ptr(), z.data_ptr())
+        return fg.prove_share(ctx, pk, circ, z.data_ptr(), k, g)
+
+    def assemble_fn(p, shares):  # the same blinding on every rank of the group
+        return fg.assemble(vk, shares, *splitmix_frs(9500 + p, 2))
+
     if mine:  # warm-up (program upload, plans)
         pc.witness_dev(ctx, sdev[mine[0]].data_ptr(), z.data_ptr())
-        fg.prove(ctx, pk, circ, z.data_ptr(), blind[0], blind[1])
+        if whole[rank]:
+            fg.prove(ctx, pk, circ, z.data_ptr(), blind[0], blind[1])
+        for p, rs in tail:
+            if rank in rs:
+                share_fn(p, rs.index(rank), len(rs))
     ctx.synchronize()
     if dist:
         dist.barrier()
@@ -532,7 +555,8 @@ def window_post_leg(args, fg, ctx, device, rank, world, gdev, dist):
     multi = []
     for _ in range(steps):
         if world > 1:
-            multi.append(prove_partitions(prove_ids, P, rank, world, gdev))
+            multi.append(prove_partitions_balanced(prove_ids, share_fn, assemble_fn, P, rank, world, gdev)
+                         if tail else prove_partitions(prove_ids, P, rank, world, gdev))
         else:
             multi.append(b"".join(prove_ids(mine)))
     ctx.synchronize()
@@ -542,13 +566,32 @@ def window_post_leg(args, fg, ctx, device, rank, world, gdev, dist):
     dt = time.perf_counter() - t1
     mine_dt = dt
     st = ctx.stats()
+    # one GPU: the latency-mode shares the balanced config-5 schedule gives a tail partition, timed one after
+    # another (slowest share = that group's tail on g GPUs), assembled and compared with the whole proof
+    shares_res = None
+    if world == 1 and args.post_share_groups and mine:
+        p0 = mine[0]
+        rs0 = splitmix_frs(9500 + p0, 2)
+        pc.witness_dev(ctx, sdev[p0].data_ptr(), z.data_ptr())
+        ref = fg.prove(ctx, pk, circ, z.data_ptr(), *rs0)
+        shares_res = {}
+        for g in [int(x) for x in args.post_share_groups.split(",") if x]:
+            share_fn(p0, 0, g)  # warm (slice plans)
+            ctx.synchronize()
+            ts, shs = [], []
+            for k in range(g):
+                t2 = time.perf_counter()
+                shs.append(share_fn(p0, k, g))
+                ctx.synchronize()
+                ts.append(time.perf_counter() - t2)
+            shares_res[str(g)] = {"share_ms": [1e3 * x for x in ts], "slowest_ms": 1e3 * max(ts),
+                                  "assembled_equals_whole_proof": fg.assemble(vk, shs, *rs0) == ref}
     if dist:
         tt = torch.tensor([dt], dtype=torch.float64, device=gdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     out = None
     if rank == 0:
-        vk, ic = pk.verifying_key()
         proofs = [m[192 * i:192 * (i + 1)] for m in multi for i in range(P)]
         pubs = [pc.public_inputs(slots[i]) for _ in multi for i in range(P)]
         verified = bool(fg.verify_batch(vk, ic, pubs, proofs))
@@ -558,7 +601,7 @@ def window_post_leg(args, fg, ctx, device, rank, world, gdev, dist):
                            f"{args.post_log_nodes}-node 8-8-0 trees R-last ({n} constraints, {pc.num_inputs} inputs, "
                            f"domain 2^{circ.d.bit_length() - 1}); synthetic consistent partitions; timed = GPU "
                            f"witness + proof per partition" +
-                           (f"; BASELINE config 5: {P} partitions round-robin over {world} GPUs, {P} x 192-byte "
+                           (f"; BASELINE config 5: {P} partitions over {world} GPUs ({schedule} schedule), {P} x 192-byte "
                             f"multi-proof all-gathered" if world > 1 else f"; {P} partitions on one GPU"),
                "partitions": P, "n_gpus": world, "constraints": n, "steps": steps,
                "makespan_s": per_step, "proofs_per_s": P / per_step, "constraints_per_s": P * n / per_step,
@@ -567,8 +610,21 @@ def window_post_leg(args, fg, ctx, device, rank, world, gdev, dist):
                                                  max(1, steps * len(mine)),
                "verified": verified, "verified_proofs": len(proofs),
                "setup_s": {"r1cs_build": t_build, "total": t_setup}, "host_mem_available_gb": avail_gb}
+        if shares_res:
+            tp1 = 1e3 * mine_dt / steps / max(1, len(mine))
+            out["latency_mode_shares"] = shares_res
+            out["config5_projection"] = {
+                "note": "projected from this GPU's times (witness + share per rank, ranks independent): 10 "
+                        "partitions; balanced = P - P % W whole partitions round-robin, then each of the P % W "
+                        "tail partitions over W / (P % W) GPUs in latency mode",
+                "w8_roundrobin_makespan_ms": 2 * tp1,
+                "w8_balanced_makespan_ms": tp1 + shares_res["4"]["slowest_ms"] if "4" in shares_res else None,
+                "w4_roundrobin_makespan_ms": 3 * tp1,
+                "w4_balanced_makespan_ms": 2 * tp1 + shares_res["2"]["slowest_ms"] if "2" in shares_res else None}
         if world > 1:
-            out["per_rank_partitions"] = [len(shard_partitions(P, r, world)) for r in range(world)]
+            out["schedule"] = schedule
+            out["per_rank_partitions"] = [len(w) for w in whole]
+            out["split_partitions"] = [{"partition": p, "ranks": rs} for p, rs in tail]
     del pk, circ, z, sdev, pc
     gc.collect()
     torch.cuda.synchronize()
@@ -608,6 +664,8 @@ def main():
     ap.add_argument("--post-partitions", type=int, default=10, help="multi-GPU runs: config 5's partition count")
     ap.add_argument("--post-reps", type=int, default=2, help="one GPU: Window-PoSt partitions proven (witness + proof)")
     ap.add_argument("--config5-steps", type=int, default=1)
+    ap.add_argument("--post-share-groups", default="4,2",
+                    help="one GPU: time the latency-mode shares of one Window-PoSt partition for these group sizes")
     ap.add_argument("--tree-log-nodes", type=int, default=21,
                     help="secondary: tree C over 2^N columns x 11 layers (N a multiple of 3; 0 skips)")
     ap.add_argument("--sdr-log-labels", type=int, default=24,

@@ -53,6 +53,92 @@ def prove_partitions(prove_fn, num_partitions: int, rank: int, world: int, devic
     return gather_multiproof(local, num_partitions, rank, world, device)
 
 
+def balanced_schedule(num_partitions: int, world: int):
+    """Config-5 schedule without an idle tail.  Round-robin leaves P % W partitions for a last round in which
+    W - P % W GPUs idle (10 partitions on 8 GPUs: two full rounds on ranks 0 and 1, six GPUs waiting).  Here
+    the first P - P % W partitions go round-robin as whole proofs, and each of the R = P % W remaining ones
+    is proven by a GROUP of ranks in latency mode (mi_groth16_prove_share: every rank of a group its slice
+    of the five MSMs, the shares assembled on the host).  Groups partition the ranks: sizes W // R, the
+    first W % R of them one larger.  A group of one rank proves its partition whole.
+    -> (whole, tail): whole[r] = partitions rank r proves whole; tail = [(partition, [ranks])]."""
+    if num_partitions < 0 or world < 1:
+        raise ValueError("need num_partitions >= 0 and world >= 1")
+    R = num_partitions % world
+    full = num_partitions - R
+    whole = [list(range(r, full, world)) for r in range(world)]
+    tail, start = [], 0
+    for j in range(R):
+        g = world // R + (1 if j < world % R else 0)
+        tail.append((full + j, list(range(start, start + g))))
+        start += g
+    for p, ranks in tail:
+        if len(ranks) == 1:  # a group of one: a whole proof
+            whole[ranks[0]].append(p)
+    tail = [(p, ranks) for p, ranks in tail if len(ranks) > 1]
+    return whole, tail
+
+
+def agree_blinding(count: int, rank: int, device="cpu"):
+    """``count`` (r, s) pairs drawn by rank 0 from the OS CSPRNG and broadcast, so that every rank of a group
+    assembles the same proof from the gathered shares (bellman create_random_proof draws r, s once per
+    proof; here the proof is assembled on several ranks)."""
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    from .core import FR_MODULUS
+
+    t = torch.from_numpy(np.frombuffer(os.urandom(128 * count), dtype=np.uint8).copy()) if rank == 0 else \
+        torch.zeros(128 * count, dtype=torch.uint8)
+    t = t.to(device)
+    dist.broadcast(t, 0)
+    raw = t.cpu().numpy().tobytes()
+    ints = [int.from_bytes(raw[64 * i:64 * (i + 1)], "little") % FR_MODULUS for i in range(2 * count)]
+    return [(ints[2 * i], ints[2 * i + 1]) for i in range(count)]
+
+
+def prove_partitions_balanced(prove_fn, share_fn, assemble_fn, num_partitions: int, rank: int, world: int,
+                              device="cpu"):
+    """prove_partitions with the balanced_schedule: ``prove_fn(ids) -> [192-byte proofs]`` for this rank's
+    whole partitions, ``share_fn(partition, k, g) -> 576-byte share`` for its slice k of g of a tail
+    partition, ``assemble_fn(partition, shares) -> 192-byte proof`` (fg.assemble with that partition's
+    blinding, identical on every rank).  One all-gather carries every rank's whole proofs and its share;
+    each rank then assembles the tail proofs itself.  Returns the P x 192-byte multi-proof (partition
+    order) on every rank, byte-identical to prove_partitions' for the same blinding."""
+    import torch
+    import torch.distributed as dist
+
+    whole, tail = balanced_schedule(num_partitions, world)
+    kmax = max((len(w) for w in whole), default=0)
+    local = list(prove_fn(whole[rank])) if whole[rank] else []
+    if len(local) != len(whole[rank]) or any(len(p) != PROOF_BYTES for p in local):
+        raise ValueError(f"rank {rank}: prove_fn returned {len(local)} proofs for {len(whole[rank])} partitions")
+    rec = np.zeros(kmax * PROOF_BYTES + SHARE_BYTES, dtype=np.uint8)
+    for i, p in enumerate(local):
+        rec[i * PROOF_BYTES:(i + 1) * PROOF_BYTES] = np.frombuffer(p, dtype=np.uint8)
+    for p, ranks in tail:
+        if rank in ranks:
+            share = share_fn(p, ranks.index(rank), len(ranks))
+            if len(share) != SHARE_BYTES:
+                raise ValueError(f"shares are {SHARE_BYTES} bytes")
+            rec[kmax * PROOF_BYTES:] = np.frombuffer(share, dtype=np.uint8)
+    t = torch.from_numpy(rec).to(device)
+    if world > 1:
+        bufs = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(bufs, t)
+        allr = [b.cpu().numpy() for b in bufs]
+    else:
+        allr = [rec]
+    out = {}
+    for r in range(world):
+        for i, p in enumerate(whole[r]):
+            out[p] = allr[r][i * PROOF_BYTES:(i + 1) * PROOF_BYTES].tobytes()
+    for p, ranks in tail:
+        out[p] = assemble_fn(p, [allr[r][kmax * PROOF_BYTES:].tobytes() for r in ranks])
+    return b"".join(out[p] for p in range(num_partitions))
+
+
 def gather_shares(share: bytes, world: int, device="cpu"):
     """All-gather one MI_SHARE_BYTES record per rank (the latency mode's only exchange, 576 B per GPU)."""
     import torch

@@ -161,6 +161,98 @@ def test_gloo_partition_runner(tmp_path, oracle, world, num_partitions):
     assert all(o == serial for o in outs)
 
 
+def test_balanced_schedule():
+    """Config 5 on 8 GPUs: partitions 0-7 whole, 8 and 9 each over a group of four ranks; every partition
+    exactly once, every rank in at most one group, groups of one collapse into whole proofs."""
+    from fil_groth16.distributed import balanced_schedule
+
+    whole, tail = balanced_schedule(10, 8)
+    assert whole == [[r] for r in range(8)]
+    assert tail == [(8, [0, 1, 2, 3]), (9, [4, 5, 6, 7])]
+    assert balanced_schedule(10, 4) == ([[0, 4], [1, 5], [2, 6], [3, 7]], [(8, [0, 1]), (9, [2, 3])])
+    assert balanced_schedule(10, 2) == ([[0, 2, 4, 6, 8], [1, 3, 5, 7, 9]], [])
+    assert balanced_schedule(3, 2) == ([[0], [1]], [(2, [0, 1])])
+    assert balanced_schedule(2, 3) == ([[], [], [1]], [(0, [0, 1])])  # groups [0, 1] and [2]: rank 2 proves 1 whole
+    for P in range(0, 13):
+        for W in range(1, 9):
+            whole, tail = balanced_schedule(P, W)
+            ids = sorted([p for w in whole for p in w] + [p for p, _ in tail])
+            assert ids == list(range(P))
+            grouped = [r for _, rs in tail for r in rs]
+            assert len(grouped) == len(set(grouped)) and all(len(rs) > 1 for _, rs in tail)
+            # makespan in units of one whole proof: never worse than round-robin
+            assert max(len(w) for w in whole) <= -(-P // W)
+
+
+def _balanced_worker(rank, world, port, num_partitions, outdir):
+    """The balanced config-5 runner with the oracle standing in for the GPU prover: whole partitions by the
+    oracle prove, tail partitions by oracle shares (split_oracle) assembled through the C ABI."""
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "crypto3-fil-proofs_amd"), os.path.join(root, "oracle"),
+              os.path.join(root, "tests", "golden"), os.path.join(root, "tests")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+
+    import circuits
+    import fil_groth16 as fg
+    import oracle_py
+    import split_oracle
+    from fil_groth16.distributed import agree_blinding, prove_partitions_balanced
+
+    oracle_py.set_threads(1)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n_in, n_aux, rows, z = circuits.random_circuit(63, 40)
+    mats = circuits.to_csr(rows)
+    P = oracle_py.OracleParams(oracle_py.OracleCircuit(len(rows), n_in, n_aux, mats), circuits.toxic())
+    zb = circuits.z_bytes(z)
+    vk = P.export()["vk"]
+    log = []
+
+    def prove_fn(ids):
+        log.extend(("whole", p) for p in ids)
+        return [P.prove(zb, 300 + p, 400 + p)[0] for p in ids]
+
+    def share_fn(p, k, g):
+        log.append(("share", p, k, g))
+        return split_oracle.shares(oracle_py, P, n_in, n_aux, mats, zb, g)[k]
+
+    buf = prove_partitions_balanced(prove_fn, share_fn, lambda p, sh: fg.assemble(vk, sh, 300 + p, 400 + p),
+                                    num_partitions, rank, world)
+    rs = agree_blinding(2, rank)
+    with open(os.path.join(outdir, f"b{rank}.bin"), "wb") as f:
+        f.write(buf)
+    with open(os.path.join(outdir, f"log{rank}.txt"), "w") as f:
+        f.write(repr(log) + "\n" + repr(rs))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,num_partitions", [(2, 3), (3, 5), (4, 2)])
+def test_gloo_balanced_runner(tmp_path, oracle, world, num_partitions):
+    """Tail partitions split over rank groups (latency-mode shares + host assembly) give the same multi-proof
+    bytes as the serial prove on every rank; the blinding rank 0 draws reaches every rank unchanged."""
+    import circuits
+    from fil_groth16.distributed import balanced_schedule
+
+    mp.spawn(_balanced_worker, args=(world, _free_port(), num_partitions, str(tmp_path)), nprocs=world, join=True)
+    outs = [open(tmp_path / f"b{r}.bin", "rb").read() for r in range(world)]
+    logs = [open(tmp_path / f"log{r}.txt").read().split("\n") for r in range(world)]
+    whole, tail = balanced_schedule(num_partitions, world)
+    assert tail, "the case must exercise a split partition"
+    for r in range(world):
+        exp = [("whole", p) for p in whole[r]] + [("share", p, rs.index(r), len(rs)) for p, rs in tail if r in rs]
+        assert logs[r][0] == repr(exp)
+    assert len({l[1] for l in logs}) == 1  # agree_blinding: identical pairs on every rank
+    n_in, n_aux, rows, z = circuits.random_circuit(63, 40)
+    P = oracle.OracleParams(oracle.OracleCircuit(len(rows), n_in, n_aux, circuits.to_csr(rows)), circuits.toxic())
+    zb = circuits.z_bytes(z)
+    serial = b"".join(P.prove(zb, 300 + p, 400 + p)[0] for p in range(num_partitions))
+    assert all(o == serial for o in outs)
+
+
 def _srs_worker(rank, world, port, outdir):
     import sys
 
