@@ -10,8 +10,27 @@
 
 namespace mi {
 
+// Stored bases are gathered at random by the bucket accumulation, one record per mixed addition.  A
+// 112-byte G1 record straddles two 128-byte lines for 7 of 8 records; padded to an aligned 128 bytes
+// (G2: 224 -> 256, two lines) every gather fetches the minimum number of lines.  The gathered bytes
+// cost power, not cycles: the accumulation's cycles per addition are unchanged, but the core clock
+// under load rises from 2.08 to 2.18 GHz, +6 % mixed additions per second
+// (microbench/maddloop.hip, profiles/r03_maddloop2.jsonl).  In registers the padding does not exist.
 template <class F>
-struct alignas(16) Affine {
+struct AffineAlign {
+    static constexpr size_t value = 16;
+};
+template <>
+struct AffineAlign<fq_t> {
+    static constexpr size_t value = 128;
+};
+template <>
+struct AffineAlign<fq2_t> {
+    static constexpr size_t value = 256;
+};
+
+template <class F>
+struct alignas(AffineAlign<F>::value) Affine {
     F x, y;
     MI_HD bool is_inf() const { return x.is_zero() && y.is_zero(); }
     MI_HD static Affine inf() { return {F::zero(), F::zero()}; }

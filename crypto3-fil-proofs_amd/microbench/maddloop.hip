@@ -1,0 +1,251 @@
+// maddloop.hip -- how close k_accum_level0<G1> runs to the ceiling of its own group law on gfx950.
+// Standalone diagnostic (not part of the library):
+//   reg    : every lane repeats the library's XYZZ += affine (madd-2008-s, lazy forms, xyzz_add_affine_inl)
+//            on a point held in registers -- the compiled group law with no memory traffic at all;
+//   gather : the same loop, but each addition gathers its 112-byte point from a 2^24-point table at a
+//            random index (as the level-0 chunks do), with the kernel's one-ahead software pipeline;
+//            gather128 / gather96: the same with 128-byte aligned records / 96-byte packed records.
+// Both run at the kernel's occupancy cap (amdgpu_waves_per_eu(2)).  A diagnostic build stamps s_memtime /
+// s_memrealtime around the loop once per wave: the in-kernel clock is delta(memtime) / delta(realtime) x
+// 100 MHz (MI355X_MICROARCH.md, DVFS item 6), so the cycles per wave-madd per SIMD can be compared with
+// the ISA issue model (3,546 v_mad_u64_u32 at 4 cycles + 1,824 other VALU at 2 cycles = 17.8 k cycles).
+// Inputs are random field elements (not curve points): the formula's instruction stream is the same, and
+// P = U2 - X1 is never zero, so every addition takes the general branch.
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 maddloop.hip -o maddloop && ./maddloop
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../csrc/curve.h"
+
+using namespace mi;
+
+#define CHECK(x)                                                                          \
+    do {                                                                                  \
+        hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess) {                                                           \
+            printf("HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+            exit(1);                                                                      \
+        }                                                                                 \
+    } while (0)
+
+__device__ __forceinline__ uint64_t stamp_time() {
+    uint64_t t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+__device__ __forceinline__ uint64_t stamp_real() {
+    uint64_t t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+
+// point record layouts for the gather form: the earlier library's 112-byte record (7 x 16 B, straddling a
+// 128-byte line for 7 of 8 records), the same padded to an aligned 128-byte line, and 96 bytes of packed
+// 32-bit words (the canonical width) unpacked to 14 x 29-bit limbs in registers
+struct alignas(16) Rec112 {  // the round-2 / round-3 library record (curve.h Affine before the padding)
+    fq_t x, y;
+};
+struct alignas(128) Rec128 {
+    fq_t x, y;
+    uint32_t pad[4];
+};
+struct alignas(32) Rec96 {
+    uint32_t w[24];
+};
+__device__ __forceinline__ fq_t unpack29(const uint32_t *w) {
+    fq_t r;
+#pragma unroll
+    for (int i = 0; i < 14; i++) {
+        const int bit = 29 * i, k = bit >> 5, sh = bit & 31;
+        uint64_t x = w[k];
+        if (k + 1 < 12) x |= (uint64_t)w[k + 1] << 32;
+        r.v[i] = (uint32_t)(x >> sh) & Fq29::M;
+    }
+    return r;
+}
+template <class T>
+__device__ __forceinline__ Affine<fq_t> ld(const T *t, uint32_t i) {
+    if constexpr (sizeof(T) == 112) {
+        return {t[i].x, t[i].y};
+    } else if constexpr (sizeof(T) == 128) {
+        return {t[i].x, t[i].y};
+    } else {
+        const Rec96 r = t[i];
+        return {unpack29(r.w), unpack29(r.w + 12)};
+    }
+}
+
+template <bool GATHER, class T = Rec112>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+k_madd(const T *__restrict__ table, uint32_t table_mask, const uint32_t *__restrict__ idx, int iters,
+       XYZZ<fq_t> *__restrict__ out, uint64_t *__restrict__ stamps) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const Affine<fq_t> p0 = ld(table, tid & table_mask);
+    XYZZ<fq_t> acc = {p0.x, p0.y, fq_t::one(), fq_t::one()};
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t t0 = stamp_time(), r0 = stamp_real();
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (GATHER) {
+        const uint32_t *ix = idx + (uint64_t)tid * iters;
+        uint32_t v = ix[0], vn = iters > 1 ? ix[1] : 0u;
+        Affine<fq_t> a = ld(table, v & table_mask);
+        for (int p = 0; p < iters; p++) {
+            Affine<fq_t> an = a;
+            uint32_t vnn = 0;
+            if (p + 1 < iters) {
+                an = ld(table, vn & table_mask);
+                if (p + 2 < iters) vnn = ix[p + 2];
+            }
+            if (v >> 31) a.y = lazy_neg(a.y);
+            acc = xyzz_add_affine_inl(acc, a);
+            a = an;
+            v = vn;
+            vn = vnn;
+        }
+    } else {
+        Affine<fq_t> a = ld(table, (tid + 1) & table_mask);
+        for (int p = 0; p < iters; p++) {
+            a.y = lazy_neg(a.y);  // the kernel's sign handling (2p - (2p - y) = y: alternates the sign)
+            acc = xyzz_add_affine_inl(acc, a);
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t t1 = stamp_time(), r1 = stamp_real();
+    __builtin_amdgcn_sched_barrier(0);
+    out[tid] = acc;
+    if ((threadIdx.x & 63) == 0) {
+        const uint32_t w = tid >> 6;
+        stamps[2 * w] = t1 - t0;
+        stamps[2 * w + 1] = r1 - r0;
+    }
+}
+
+static uint32_t rng32(uint64_t &s) {
+    s += 0x9E3779B97F4A7C15ull;
+    uint64_t z = s;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return (uint32_t)(z ^ (z >> 31));
+}
+
+template <bool G, class T = Rec112>
+static void run(const char *name, const T *table, uint32_t mask, const uint32_t *idx, int iters,
+                int blocks, XYZZ<fq_t> *out, uint64_t *stamps, double seconds) {
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    // warm the clock: back-to-back launches for ~`seconds` (DVFS settles under sustained load)
+    int launches = 0;
+    CHECK(hipEventRecord(e0));
+    float ms = 0;
+    while (ms < 1e3 * seconds) {
+        k_madd<G, T><<<blocks, 256>>>(table, mask, idx, iters, out, stamps);
+        launches++;
+        CHECK(hipEventRecord(e1));
+        CHECK(hipEventSynchronize(e1));
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+    }
+    const int reps = 5;
+    CHECK(hipEventRecord(e0));
+    for (int r = 0; r < reps; r++) k_madd<G, T><<<blocks, 256>>>(table, mask, idx, iters, out, stamps);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    CHECK(hipGetLastError());
+    const int waves = blocks * 4;
+    std::vector<uint64_t> st(2 * waves);
+    CHECK(hipMemcpy(st.data(), stamps, st.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<double> ghz, cyc;
+    for (int w = 0; w < waves; w++) {
+        ghz.push_back((double)st[2 * w] / ((double)st[2 * w + 1] / 100e6) / 1e9);
+        cyc.push_back((double)st[2 * w] / iters);
+    }
+    std::sort(ghz.begin(), ghz.end());
+    std::sort(cyc.begin(), cyc.end());
+    const double per_launch = ms / reps;
+    const double madds = (double)blocks * 256 * iters;
+    // two waves per SIMD share it: SIMD cycles per wave-madd = wave cycles per madd / 2
+    printf("{\"form\": \"%s\", \"iters\": %d, \"blocks\": %d, \"ms_per_launch\": %.3f, \"gmadd_per_s\": %.3f, "
+           "\"clock_ghz_median\": %.3f, \"wave_cycles_per_madd_median\": %.0f, "
+           "\"simd_cycles_per_wave_madd\": %.0f, \"issue_model_cycles\": 17832, \"frac_of_issue_model\": %.3f, "
+           "\"warm_launches\": %d}\n",
+           name, iters, blocks, per_launch, madds / (per_launch * 1e-3) / 1e9, ghz[waves / 2], cyc[waves / 2],
+           cyc[waves / 2] / 2, 17832.0 / (cyc[waves / 2] / 2), launches);
+    fflush(stdout);
+}
+
+int main(int argc, char **argv) {
+    const int iters = argc > 1 ? atoi(argv[1]) : 64;
+    const double warm_s = argc > 2 ? atof(argv[2]) : 2.0;
+    hipDeviceProp_t prop;
+    CHECK(hipGetDeviceProperties(&prop, 0));
+    // 2 waves per SIMD x 4 SIMDs per CU = 8 waves = 2 workgroups of 256 per CU; 8 rounds of the chip
+    const int blocks = prop.multiProcessorCount * 2 * 8;
+    const uint32_t tbits = 24, tn = 1u << tbits;
+    std::vector<Rec112> h(tn);
+    uint64_t s = 12345;
+    for (uint32_t i = 0; i < tn; i++) {
+        for (int k = 0; k < 14; k++) {
+            h[i].x.v[k] = rng32(s) & Fq29::M;
+            h[i].y.v[k] = rng32(s) & Fq29::M;
+        }
+        h[i].x.v[13] &= 0xf;  // below 2^381 < 2p
+        h[i].y.v[13] &= 0xf;
+    }
+    Rec112 *dt;
+    XYZZ<fq_t> *dout;
+    uint32_t *didx;
+    uint64_t *dst;
+    const uint64_t nthreads = (uint64_t)blocks * 256;
+    std::vector<uint32_t> ix(nthreads * iters);
+    for (auto &v : ix) v = rng32(s);  // random point, random sign bit
+    CHECK(hipMalloc(&dt, sizeof(Rec112) * tn));
+    CHECK(hipMalloc(&dout, sizeof(XYZZ<fq_t>) * nthreads));
+    CHECK(hipMalloc(&didx, 4 * ix.size()));
+    CHECK(hipMalloc(&dst, 16 * nthreads / 64));
+    CHECK(hipMemcpy(dt, h.data(), sizeof(Rec112) * tn, hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(didx, ix.data(), 4 * ix.size(), hipMemcpyHostToDevice));
+    printf("{\"device\": \"%s\", \"cus\": %d, \"record_bytes\": [%zu, %zu, %zu]}\n", prop.name,
+           prop.multiProcessorCount, sizeof(Rec112), sizeof(Rec128), sizeof(Rec96));
+    run<false>("reg", dt, tn - 1, didx, iters, blocks, dout, dst, warm_s);
+    run<true>("gather", dt, tn - 1, didx, iters, blocks, dout, dst, warm_s);
+    // the same points as 128-byte aligned records and as 96-byte packed words
+    std::vector<Rec128> h128(tn);
+    std::vector<Rec96> h96(tn);
+    for (uint32_t i = 0; i < tn; i++) {
+        h128[i].x = h[i].x;
+        h128[i].y = h[i].y;
+        for (int c = 0; c < 2; c++) {
+            const fq_t &f = c ? h[i].y : h[i].x;
+            uint32_t w[12] = {0};
+            for (int k = 0; k < 14; k++) {
+                const int bit = 29 * k, j = bit >> 5, sh = bit & 31;
+                w[j] |= f.v[k] << sh;
+                if (sh > 3 && j + 1 < 12) w[j + 1] |= f.v[k] >> (32 - sh);
+            }
+            for (int j = 0; j < 12; j++) h96[i].w[12 * c + j] = w[j];
+        }
+    }
+    Rec128 *d128;
+    Rec96 *d96;
+    CHECK(hipMalloc(&d128, sizeof(Rec128) * tn));
+    CHECK(hipMalloc(&d96, sizeof(Rec96) * tn));
+    CHECK(hipMemcpy(d128, h128.data(), sizeof(Rec128) * tn, hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(d96, h96.data(), sizeof(Rec96) * tn, hipMemcpyHostToDevice));
+    run<true, Rec128>("gather128", d128, tn - 1, didx, iters, blocks, dout, dst, warm_s);
+    run<true, Rec96>("gather96", d96, tn - 1, didx, iters, blocks, dout, dst, warm_s);
+    run<true>("gather", dt, tn - 1, didx, iters, blocks, dout, dst, warm_s);
+    run<false>("reg", dt, tn - 1, didx, iters, blocks, dout, dst, warm_s);
+    CHECK(hipFree(d128));
+    CHECK(hipFree(d96));
+    CHECK(hipFree(dt));
+    CHECK(hipFree(dout));
+    CHECK(hipFree(didx));
+    CHECK(hipFree(dst));
+    return 0;
+}
