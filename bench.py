@@ -933,6 +933,19 @@ def main():
     # secondary (binding) roofline: Fq multiplications per second vs the MAD-issue bound, over the mixed
     # additions the accumulation actually issued (non-zero signed digits, counted by the library)
     madds_per_launch = dom.get("madds", 0) / max(dom["launches"], 1)
+    # the ceiling of the kernel's own group law on this chip: the maddloop microbenchmark's gathered-record
+    # rate for the library's record layout (microbench/maddloop.hip; in-kernel clock, two waves per SIMD)
+    ceiling = None
+    if os.path.isdir(prof_dir) and grp == "G1":
+        for fn in sorted(os.listdir(prof_dir), reverse=True):
+            if fn.startswith("r03_maddloop") and fn.endswith(".jsonl"):
+                rows = [json.loads(l) for l in open(os.path.join(prof_dir, fn)) if l.strip().startswith("{")]
+                g = [r for r in rows if r.get("form") == "gather128"]
+                if g:
+                    ceiling = {"source": f"profiles/{fn}", "form": "gather128 (the library's padded 128-byte records)",
+                               "gmadd_per_s": max(r["gmadd_per_s"] for r in g),
+                               "clock_ghz": max(r["clock_ghz_median"] for r in g)}
+                    break
     fq_muls = madds_per_launch * FQ_MUL_PER_MIXED_ADD[grp]
     valu_ach = fq_muls / (avg_ms * 1e-3) if avg_ms > 0 and fq_muls else None
     valu_peak = MAD_RATE / FQ_MUL_MADS
@@ -991,6 +1004,8 @@ def main():
             "unit": "Fq-mul/s",
             "frac": valu_ach / valu_peak if valu_ach else None,
             "madds_per_launch": madds_per_launch,
+            "group_law_ceiling": dict(ceiling, frac=(madds_per_launch / (avg_ms * 1e-3) / 1e9) / ceiling["gmadd_per_s"])
+            if ceiling and avg_ms > 0 and madds_per_launch else None,
             "spec_issue": {"peak_lane_instr_per_s": SPEC_VALU_LANE_INSTR,
                            "instr_per_mixed_add": G1_MADD_VALU_INSTR if grp == "G1" else None,
                            "frac": (madds_per_launch * G1_MADD_VALU_INSTR / (avg_ms * 1e-3) / SPEC_VALU_LANE_INSTR)

@@ -4,7 +4,8 @@
 //            on a point held in registers -- the compiled group law with no memory traffic at all;
 //   gather : the same loop, but each addition gathers its 112-byte point from a 2^24-point table at a
 //            random index (as the level-0 chunks do), with the kernel's one-ahead software pipeline;
-//            gather128 / gather96: the same with 128-byte aligned records / 96-byte packed records.
+//            gather128 / gather96: the same with 128-byte aligned records / 96-byte packed records;
+//   g2_*   : the G2 lane-pair addition (g2pair.h) with 224-byte / aligned 256-byte records, and in registers.
 // Both run at the kernel's occupancy cap (amdgpu_waves_per_eu(2)).  A diagnostic build stamps s_memtime /
 // s_memrealtime around the loop once per wave: the in-kernel clock is delta(memtime) / delta(realtime) x
 // 100 MHz (MI355X_MICROARCH.md, DVFS item 6), so the cycles per wave-madd per SIMD can be compared with
@@ -18,9 +19,10 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 #include <vector>
 
-#include "../csrc/curve.h"
+#include "../csrc/g2pair.h"
 
 using namespace mi;
 
@@ -125,6 +127,68 @@ k_madd(const T *__restrict__ table, uint32_t table_mask, const uint32_t *__restr
     }
 }
 
+// G2 on lane pairs (g2pair.h), as k_accum_level0<G2>: each lane of a pair gathers its Fq half of the point
+// (x.c_k, y.c_k); the record is 224 bytes (the earlier layout) or padded to an aligned 256 bytes.
+struct alignas(16) Rec224 {
+    fq_t c[4];  // x.c0, x.c1, y.c0, y.c1
+};
+struct alignas(256) Rec256 {
+    fq_t c[4];
+    uint32_t pad[8];
+};
+template <bool GATHER, class T>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+k_madd_g2(const T *__restrict__ table, uint32_t table_mask, const uint32_t *__restrict__ idx, int iters,
+          XYZZ<fq2_t> *__restrict__ out, uint64_t *__restrict__ stamps) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, pair = tid >> 1, half = tid & 1;
+    auto ld2 = [&](uint32_t i) -> Affine<fq2h_t> {
+        const fq_t *f = table[i].c + half;
+        return {{f[0]}, {f[2]}};
+    };
+    const Affine<fq2h_t> p0 = ld2(pair & table_mask);
+    XYZZ<fq2h_t> acc = {p0.x, p0.y, fq2h_t::one(), fq2h_t::one()};
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t t0 = stamp_time(), r0 = stamp_real();
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (GATHER) {
+        const uint32_t *ix = idx + (uint64_t)pair * iters;
+        uint32_t v = ix[0], vn = iters > 1 ? ix[1] : 0u;
+        Affine<fq2h_t> a = ld2(v & table_mask);
+        for (int p = 0; p < iters; p++) {
+            Affine<fq2h_t> an = a;
+            uint32_t vnn = 0;
+            if (p + 1 < iters) {
+                an = ld2(vn & table_mask);
+                if (p + 2 < iters) vnn = ix[p + 2];
+            }
+            if (v >> 31) a.y = lazy_neg(a.y);
+            acc = xyzz_add_affine_inl(acc, a);
+            a = an;
+            v = vn;
+            vn = vnn;
+        }
+    } else {
+        Affine<fq2h_t> a = ld2((pair + 1) & table_mask);
+        for (int p = 0; p < iters; p++) {
+            a.y = lazy_neg(a.y);
+            acc = xyzz_add_affine_inl(acc, a);
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t t1 = stamp_time(), r1 = stamp_real();
+    __builtin_amdgcn_sched_barrier(0);
+    fq_t *o = reinterpret_cast<fq_t *>(out + pair) + half;
+    o[0] = acc.X.v;
+    o[2] = acc.Y.v;
+    o[4] = acc.ZZ.v;
+    o[6] = acc.ZZZ.v;
+    if ((threadIdx.x & 63) == 0) {
+        const uint32_t w = tid >> 6;
+        stamps[2 * w] = t1 - t0;
+        stamps[2 * w + 1] = r1 - r0;
+    }
+}
+
 static uint32_t rng32(uint64_t &s) {
     s += 0x9E3779B97F4A7C15ull;
     uint64_t z = s;
@@ -133,9 +197,9 @@ static uint32_t rng32(uint64_t &s) {
     return (uint32_t)(z ^ (z >> 31));
 }
 
-template <bool G, class T = Rec112>
-static void run(const char *name, const T *table, uint32_t mask, const uint32_t *idx, int iters,
-                int blocks, XYZZ<fq_t> *out, uint64_t *stamps, double seconds) {
+template <class Launch>
+static void run_with(const char *name, Launch launch, int iters, int blocks, int lanes_per_madd, double model_cycles,
+                     uint64_t *stamps, double seconds) {
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
     CHECK(hipEventCreate(&e1));
@@ -144,7 +208,7 @@ static void run(const char *name, const T *table, uint32_t mask, const uint32_t 
     CHECK(hipEventRecord(e0));
     float ms = 0;
     while (ms < 1e3 * seconds) {
-        k_madd<G, T><<<blocks, 256>>>(table, mask, idx, iters, out, stamps);
+        launch();
         launches++;
         CHECK(hipEventRecord(e1));
         CHECK(hipEventSynchronize(e1));
@@ -152,7 +216,7 @@ static void run(const char *name, const T *table, uint32_t mask, const uint32_t 
     }
     const int reps = 5;
     CHECK(hipEventRecord(e0));
-    for (int r = 0; r < reps; r++) k_madd<G, T><<<blocks, 256>>>(table, mask, idx, iters, out, stamps);
+    for (int r = 0; r < reps; r++) launch();
     CHECK(hipEventRecord(e1));
     CHECK(hipEventSynchronize(e1));
     CHECK(hipEventElapsedTime(&ms, e0, e1));
@@ -168,14 +232,14 @@ static void run(const char *name, const T *table, uint32_t mask, const uint32_t 
     std::sort(ghz.begin(), ghz.end());
     std::sort(cyc.begin(), cyc.end());
     const double per_launch = ms / reps;
-    const double madds = (double)blocks * 256 * iters;
+    const double madds = (double)blocks * 256 / lanes_per_madd * iters;
     // two waves per SIMD share it: SIMD cycles per wave-madd = wave cycles per madd / 2
     printf("{\"form\": \"%s\", \"iters\": %d, \"blocks\": %d, \"ms_per_launch\": %.3f, \"gmadd_per_s\": %.3f, "
            "\"clock_ghz_median\": %.3f, \"wave_cycles_per_madd_median\": %.0f, "
-           "\"simd_cycles_per_wave_madd\": %.0f, \"issue_model_cycles\": 17832, \"frac_of_issue_model\": %.3f, "
+           "\"simd_cycles_per_wave_madd\": %.0f, \"issue_model_cycles\": %.0f, \"frac_of_issue_model\": %.3f, "
            "\"warm_launches\": %d}\n",
            name, iters, blocks, per_launch, madds / (per_launch * 1e-3) / 1e9, ghz[waves / 2], cyc[waves / 2],
-           cyc[waves / 2] / 2, 17832.0 / (cyc[waves / 2] / 2), launches);
+           cyc[waves / 2] / 2, model_cycles, model_cycles / (cyc[waves / 2] / 2), launches);
     fflush(stdout);
 }
 
@@ -212,8 +276,6 @@ int main(int argc, char **argv) {
     CHECK(hipMemcpy(didx, ix.data(), 4 * ix.size(), hipMemcpyHostToDevice));
     printf("{\"device\": \"%s\", \"cus\": %d, \"record_bytes\": [%zu, %zu, %zu]}\n", prop.name,
            prop.multiProcessorCount, sizeof(Rec112), sizeof(Rec128), sizeof(Rec96));
-    run<false>("reg", dt, tn - 1, didx, iters, blocks, dout, dst, warm_s);
-    run<true>("gather", dt, tn - 1, didx, iters, blocks, dout, dst, warm_s);
     // the same points as 128-byte aligned records and as 96-byte packed words
     std::vector<Rec128> h128(tn);
     std::vector<Rec96> h96(tn);
@@ -237,12 +299,51 @@ int main(int argc, char **argv) {
     CHECK(hipMalloc(&d96, sizeof(Rec96) * tn));
     CHECK(hipMemcpy(d128, h128.data(), sizeof(Rec128) * tn, hipMemcpyHostToDevice));
     CHECK(hipMemcpy(d96, h96.data(), sizeof(Rec96) * tn, hipMemcpyHostToDevice));
-    run<true, Rec128>("gather128", d128, tn - 1, didx, iters, blocks, dout, dst, warm_s);
-    run<true, Rec96>("gather96", d96, tn - 1, didx, iters, blocks, dout, dst, warm_s);
-    run<true>("gather", dt, tn - 1, didx, iters, blocks, dout, dst, warm_s);
-    run<false>("reg", dt, tn - 1, didx, iters, blocks, dout, dst, warm_s);
+    auto g1 = [&](const char *name, auto gather, auto *table) {
+        using T = std::remove_pointer_t<decltype(table)>;
+        run_with(name, [&] { k_madd<decltype(gather)::value, T><<<blocks, 256>>>(table, tn - 1, didx, iters, dout, dst); },
+                 iters, blocks, 1, 17832.0, dst, warm_s);
+    };
+    g1("gather128", std::true_type{}, d128);
+    g1("gather96", std::true_type{}, d96);
+    g1("gather", std::true_type{}, dt);
+    g1("reg", std::false_type{}, dt);
     CHECK(hipFree(d128));
     CHECK(hipFree(d96));
+    // G2 on lane pairs: the same random elements as Fq2 coordinates, 2^23 records; one madd per lane pair.
+    // Issue model: ISA count of the compiled loop body is not taken here, so the fraction is left to
+    // the G1 rows (model_cycles 0 prints 0).
+    {
+        const uint32_t tn2 = 1u << 23;
+        std::vector<Rec224> h224(tn2);
+        std::vector<Rec256> h256(tn2);
+        for (uint32_t i = 0; i < tn2; i++) {
+            h224[i].c[0] = h[2 * i].x;
+            h224[i].c[1] = h[2 * i].y;
+            h224[i].c[2] = h[2 * i + 1].x;
+            h224[i].c[3] = h[2 * i + 1].y;
+            for (int q = 0; q < 4; q++) h256[i].c[q] = h224[i].c[q];
+        }
+        Rec224 *d224;
+        Rec256 *d256;
+        XYZZ<fq2_t> *dout2;
+        CHECK(hipMalloc(&d224, sizeof(Rec224) * tn2));
+        CHECK(hipMalloc(&d256, sizeof(Rec256) * tn2));
+        CHECK(hipMalloc(&dout2, sizeof(XYZZ<fq2_t>) * nthreads / 2));
+        CHECK(hipMemcpy(d224, h224.data(), sizeof(Rec224) * tn2, hipMemcpyHostToDevice));
+        CHECK(hipMemcpy(d256, h256.data(), sizeof(Rec256) * tn2, hipMemcpyHostToDevice));
+        auto g2 = [&](const char *name, auto gather, auto *table) {
+            using T = std::remove_pointer_t<decltype(table)>;
+            run_with(name, [&] { k_madd_g2<decltype(gather)::value, T><<<blocks, 256>>>(table, tn2 - 1, didx, iters, dout2, dst); },
+                     iters, blocks, 2, 0.0, dst, warm_s);
+        };
+        g2("g2_gather224", std::true_type{}, d224);
+        g2("g2_gather256", std::true_type{}, d256);
+        g2("g2_reg", std::false_type{}, d256);
+        CHECK(hipFree(d224));
+        CHECK(hipFree(d256));
+        CHECK(hipFree(dout2));
+    }
     CHECK(hipFree(dt));
     CHECK(hipFree(dout));
     CHECK(hipFree(didx));
