@@ -10,12 +10,14 @@
 
 namespace mi {
 
-// Stored bases are gathered at random by the bucket accumulation, one record per mixed addition.  A
-// 112-byte G1 record straddles two 128-byte lines for 7 of 8 records; padded to an aligned 128 bytes
-// (G2: 224 -> 256, two lines) every gather fetches the minimum number of lines.  The gathered bytes
-// cost power, not cycles: the accumulation's cycles per addition are unchanged, but the core clock
-// under load rises from 2.08 to 2.18 GHz, +6 % mixed additions per second
-// (microbench/maddloop.hip, profiles/r03_maddloop2.jsonl).  In registers the padding does not exist.
+// Stored G1 bases are gathered at random by the bucket accumulation, one record per mixed addition. A
+// 112-byte record straddles two 128-byte lines for 7 of 8 records; padded to an aligned 128 bytes every
+// gather fetches one line.  The gathered bytes cost power, not cycles: the accumulation's cycles per
+// addition are unchanged, but the core clock under load rises from 2.08 to 2.18 GHz, +6 % mixed additions
+// per second (microbench/maddloop.hip, profiles/r03_maddloop2.jsonl).  G2 records stay 224 bytes: an
+// aligned 256-byte form measured no gain for the lane-pair addition (1.73 vs 1.71 G madd/s,
+// profiles/r03_maddloop3.jsonl), whose VALU work per gathered byte is 3x G1's, and would cost the 32 GiB
+// Window-PoSt key 2 GB.  In registers the padding does not exist.
 template <class F>
 struct AffineAlign {
     static constexpr size_t value = 16;
@@ -23,10 +25,6 @@ struct AffineAlign {
 template <>
 struct AffineAlign<fq_t> {
     static constexpr size_t value = 128;
-};
-template <>
-struct AffineAlign<fq2_t> {
-    static constexpr size_t value = 256;
 };
 
 template <class F>

@@ -905,9 +905,12 @@ void build_hi_tables(Ctx &c, Srs &S) {
         // lane one split-mode MSM plan (keys / values sorted and unsorted over ~6 windows of 2 n half-scalar
         // points, chunk partials and sort space) over the larger of h and l: measured 109 GB in all for a
         // 2^27-domain Window-PoSt partition (tools/post_mem.py), i.e. ~350 B per point and lane
+        // Reserve that estimate + 10 % + 8 GB: the padded 128 / 256-byte records (curve.h) left the 32 GiB
+        // Window-PoSt partition with tables 6 GB short of its working set (out of memory in the prove)
+        // under the round-3 estimate + 1 GB, and earlier legs' buffers fragment what is free.
         const uint64_t big = S.d > S.n_l ? S.d : S.n_l;
         const uint64_t work = 32 * (S.n_l + 3 * S.d) + 2 * 360 * big;
-        if (need + work + (1ull << 30) > free_b) return;  // the MSMs take the GLV split instead
+        if (need + work + work / 10 + (8ull << 30) > free_b) return;  // the MSMs take the GLV split instead
     }
     for (auto &q : qs) {
         if (!q.src || !q.n) continue;
@@ -1071,6 +1074,8 @@ Srs *srs_generate(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5]) {
         // 32 GiB partition): key generation is one-time, so give them back before the table decision and
         // the first proof
         for (auto &b : c.scratch) b.release();
+        if (c.aux)  // and the auxiliary lane's arena (earlier proofs' B / L plans)
+            for (auto &b : c.aux->scratch) b.release();
         // verifying key
         S->alpha_g1 = host_mul_affine(g1, toxic_canonical[1]);
         S->beta_g1 = host_mul_affine(g1, toxic_canonical[2]);
