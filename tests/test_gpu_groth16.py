@@ -338,6 +338,59 @@ def test_prove_split_two_processes(oracle, tmp_path):
     assert outs[0] == outs[1] == op.prove(circuits.z_bytes(z), 21, 22)[0]
 
 
+def _balanced_gpu_worker(rank, world, port, outdir):
+    import os
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "crypto3-fil-proofs_amd"), os.path.join(root, "tests", "golden")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+
+    import circuits
+    import fil_groth16 as fg
+    from fil_groth16.distributed import prove_partitions_balanced
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    c = fg.Context(0)
+    n_in, n_aux, rws, z = circuits.random_circuit(85, 2500, n_in=5, n_free=32)
+    gc = fg.Circuit(c, len(rws), n_in, n_aux, circuits.to_csr(rws))
+    pk = fg.generate_random_parameters(c, gc, circuits.toxic())
+    zb = circuits.z_bytes(z)
+    vk, _ = pk.verifying_key()
+    buf = prove_partitions_balanced(
+        lambda ids: fg.prove_batch(c, pk, gc, [zb] * len(ids), [(31 + p, 41 + p) for p in ids]),
+        lambda p, k, g: fg.prove_share(c, pk, gc, zb, k, g),
+        lambda p, sh: fg.assemble(vk, sh, 31 + p, 41 + p), 3, rank, world)
+    with open(os.path.join(outdir, f"b{rank}.bin"), "wb") as f:
+        f.write(buf)
+    dist.barrier()
+    dist.destroy_process_group()
+    del pk, gc
+    c.close()
+
+
+def test_balanced_partitions_two_processes(oracle, tmp_path):
+    """The balanced config-5 runner on the GPU with one process per rank (both on this box's GPU, gloo for the
+    all-gather): 3 partitions over 2 ranks -- 0 and 1 proven whole, 2 split into two latency-mode shares and
+    assembled on both ranks -- give the oracle's serial multi-proof on every rank."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    mp.spawn(_balanced_gpu_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    outs = [open(tmp_path / f"b{k}.bin", "rb").read() for k in range(2)]
+    n_in, n_aux, rws, z = circuits.random_circuit(85, 2500, n_in=5, n_free=32)
+    op = oracle.OracleParams(oracle.OracleCircuit(len(rws), n_in, n_aux, circuits.to_csr(rws)), circuits.toxic())
+    zb = circuits.z_bytes(z)
+    assert outs[0] == outs[1] == b"".join(op.prove(zb, 31 + p, 41 + p)[0] for p in range(3))
+
+
 def _srs_bcast_gpu_worker(rank, world, port, outdir):
     import os
     import sys
