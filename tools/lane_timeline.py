@@ -60,6 +60,20 @@ def main():
     for r in sel:
         by[r[3]].append(r)
     print(f"proof window {(t1 - t0) / 1e6:.1f} ms")
+    # union of the kernels' busy intervals over all streams: the window minus this is time with no kernel
+    # running at all (host synchronisations, launch gaps)
+    union, cur_s, cur_e = 0, None, None
+    for _, s, e, _ in sorted(sel, key=lambda r: r[1]):
+        e = min(e, t1)
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                union += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    if cur_e is not None:
+        union += cur_e - cur_s
+    print(f"device busy (union over streams) {union / 1e6:.1f} ms, idle {(t1 - t0 - union) / 1e6:.1f} ms")
     for st, rs in sorted(by.items()):
         busy = sum(e - s for _, s, e, _ in rs) / 1e6
         print(f"stream {st}: {len(rs)} launches, busy {busy:.1f} ms, span {(rs[-1][2] - rs[0][1]) / 1e6:.1f} ms")
