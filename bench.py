@@ -17,6 +17,11 @@ the ranks (10 over 8 GPUs: two rounds on ranks 0 and 1) and all-gathers the P x 
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--log-rows 26] [--partitions P]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Launch: under torch.distributed.run (WORLD_SIZE set) each process is one rank, and WORLD_SIZE must equal
+--gpus.  Without a launcher, --gpus N > 1 makes this process a parent that, before touching the GPU, starts
+N rank processes of itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / a free MASTER_PORT),
+forwards rank 0's JSON line and exits non-zero if any rank fails (spawn_ranks).
 """
 import argparse
 import json
@@ -631,6 +636,127 @@ def window_post_leg(args, fg, ctx, device, rank, world, gdev, dist):
     return out
 
 
+def spawn_ranks(n, argv):
+    """`bench.py --gpus N` with no launcher: N child ranks of this script, one per GPU (LOCAL_RANK = rank),
+    rendezvous on 127.0.0.1.  This process never touches the GPU (no torch import), so starting children is
+    safe.  Rank 0's stdout (the JSON line) is forwarded; every rank's stderr passes through.  If any rank exits
+    non-zero the others are stopped (they would wait in a collective) and the parent exits with that code."""
+    import socket
+    import subprocess
+    import threading
+
+    port = os.environ.get("MASTER_PORT")
+    if not port:
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = str(sk.getsockname()[1])
+    procs, lines = [], []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr))
+    import signal
+
+    def stop(signum, _frame):  # a time limit on the parent ends the ranks too
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        sys.exit(128 + signum)
+
+    signal.signal(signal.SIGTERM, stop)
+    signal.signal(signal.SIGINT, stop)
+    reader = threading.Thread(target=lambda: lines.extend(procs[0].stdout), daemon=True)
+    reader.start()
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            print(f"[bench] a rank exited with {rc}; stopping the others", file=sys.stderr, flush=True)
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            break
+        if all(c == 0 for c in codes):
+            break
+        time.sleep(0.2)
+    reader.join(timeout=10)
+    for ln in lines:
+        sys.stdout.write(ln.decode() if isinstance(ln, bytes) else ln)
+    sys.stdout.flush()
+    return rc
+
+
+def winning_post_leg(args, fg, ctx, device):
+    """SURVEY 8(a) a2 generate_winning_post (api/post.hpp:178-230) on the real circuit at the reference's shape:
+    winning_post_setup_params (parameters.hpp:58-68) turns 66 challenges over 1 sector into 66 circuit sectors x
+    1 challenge over the one replica (2^30-node 8-8-0 tree R-last at 32 GiB: 370,590 constraints, 133 inputs,
+    domain 2^19).  Winning PoSt is the latency-critical single-GPU path (SURVEY CS-3): timed = GPU witness +
+    proof of one partition, --winning-reps times back to back (latency per proof, not throughput), every proof
+    pairing-verified after the timer."""
+    import gc
+
+    import numpy as np
+    import torch
+
+    from fil_groth16 import stacked
+
+    t0 = time.perf_counter()
+    wc = stacked.WinningPoStCircuit(1 << args.winning_log_nodes, 8, 8, 0)
+    t_build = time.perf_counter() - t0
+    _, sectors = stacked.synthetic_winning_post_instance(ctx, wc, seed=66)
+    slots = stacked.post_slots(wc, sectors)
+    circ = wc.load(ctx)
+    pk = fg.generate_random_parameters(ctx, circ, splitmix_frs(TOXIC_SEED, 5))
+    sd = torch.from_numpy(np.frombuffer(slots, dtype=np.uint8).copy()).to(device)
+    z = torch.empty(32 * wc.num_vars, dtype=torch.uint8, device=device)
+    torch.cuda.synchronize()
+    t_setup = time.perf_counter() - t0
+    reps = args.winning_reps
+    blind = splitmix_frs(6600, 2 * (reps + 3))
+    for w in range(2):  # warm-up: program upload, plans, scratch
+        wc.witness_dev(ctx, sd.data_ptr(), z.data_ptr())
+        fg.prove(ctx, pk, circ, z.data_ptr(), blind[2 * w], blind[2 * w + 1])
+    ctx.synchronize()
+    ctx.reset_stats()
+    lat, proofs = [], []
+    for k in range(reps):
+        t1 = time.perf_counter()
+        wc.witness_dev(ctx, sd.data_ptr(), z.data_ptr())
+        proofs.append(fg.prove(ctx, pk, circ, z.data_ptr(), blind[2 * k + 4], blind[2 * k + 5]))
+        lat.append(time.perf_counter() - t1)
+    st = ctx.stats()
+    vk, ic = pk.verifying_key()
+    pub = wc.public_inputs(slots)
+    verified = bool(fg.verify_batch(vk, ic, [pub] * len(proofs), proofs))
+    lat_s = sorted(lat)
+    med = lat_s[len(lat_s) // 2]
+    n = wc.num_constraints
+    out = {"workload": f"Winning PoSt (generate_winning_post) at the reference shape: {wc.sectors} circuit sectors x "
+                       f"{wc.challenges} challenge over one replica, 2^{args.winning_log_nodes}-node 8-8-0 tree R-last "
+                       f"({n} constraints, {wc.num_inputs} inputs, domain 2^{circ.d.bit_length() - 1}); synthetic "
+                       f"consistent replica; timed = GPU witness + proof, one partition per call",
+           "constraints": n, "inputs": wc.num_inputs, "domain": circ.d, "reps": reps,
+           "latency_ms_median": med * 1e3, "latency_ms_mean": 1e3 * sum(lat) / reps, "latency_ms_min": lat_s[0] * 1e3,
+           "constraints_per_s": n / med, "verified": verified, "verified_proofs": len(proofs),
+           "device_ms_per_proof": {k: round(st[k]["ms"] / reps, 3) for k in
+                                   ("prove", "msm_g1", "msm_g2", "accum_g1", "accum_g2", "sort", "ntt", "wit_a",
+                                    "wit_sha", "wit_pos")},
+           "setup_s": {"r1cs_build": t_build, "total": t_setup}}
+    del pk, circ, z, sd, wc
+    gc.collect()
+    torch.cuda.synchronize()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -666,11 +792,23 @@ def main():
     ap.add_argument("--config5-steps", type=int, default=1)
     ap.add_argument("--post-share-groups", default="4,2",
                     help="one GPU: time the latency-mode shares of one Window-PoSt partition for these group sizes")
+    ap.add_argument("--winning-log-nodes", type=int, default=30,
+                    help="one GPU: Winning-PoSt latency over a 2^N-node sector (N = 3 (mod 3) for 8-8-0; 0 skips)")
+    ap.add_argument("--winning-reps", type=int, default=10)
     ap.add_argument("--tree-log-nodes", type=int, default=21,
                     help="secondary: tree C over 2^N columns x 11 layers (N a multiple of 3; 0 skips)")
     ap.add_argument("--sdr-log-labels", type=int, default=24,
                     help="secondary: SDR labelling-proof labels of 2^N challenges (0 skips)")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" in os.environ:
+        if int(os.environ["WORLD_SIZE"]) != args.gpus:
+            raise SystemExit(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} from the launcher but --gpus "
+                             f"{args.gpus}: they must agree")
+    elif args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -870,7 +1008,8 @@ def main():
         except Exception as e:  # reported, never fatal to the main measurement
             config5 = {"error": str(e)}
 
-    if rank == 0 and world == 1 and (args.config4_log_rows or args.stacked_log_nodes or args.post_sectors):
+    if rank == 0 and world == 1 and (args.config4_log_rows or args.stacked_log_nodes or args.post_sectors or
+                                     args.winning_log_nodes):
         import gc
 
         del pk, circ, zhost, sc  # the secondary legs need the HBM
@@ -891,6 +1030,14 @@ def main():
             stacked_res = stacked_leg(args, fg, ctx, device, world)
         except Exception as e:  # reported, never fatal to the config-3 measurement
             stacked_res = {"error": str(e)}
+
+    winning = None
+    if rank == 0 and world == 1 and args.winning_log_nodes:
+        try:
+            log(rank, "Winning-PoSt leg ...")
+            winning = winning_post_leg(args, fg, ctx, device)
+        except Exception as e:  # reported, never fatal to the config-3 measurement
+            winning = {"error": str(e)}
 
     post_res = None
     if rank == 0 and world == 1 and args.post_sectors and args.post_reps:
@@ -914,8 +1061,12 @@ def main():
     avg_ms = dom["ms"] / max(dom["launches"], 1)
     units_per_launch = dom["units"] / max(dom["launches"], 1)
     achieved = bytes_per_unit * units_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else None
-    # HBM traffic per launch from the committed rocprofv3 PMC summary of the same kernel/workload
-    traffic, traffic_src = None, None
+    # HBM traffic of the dominant kernel from the committed rocprofv3 PMC summary of the same workload (FETCH_SIZE
+    # and WRITE_SIZE passes, per point): bytes per launch = per-point bytes x points per launch, and as a rate
+    # over this run's average launch time (GB/s, the unit of `achieved`).  Raw FETCH_SIZE and the gfx950 x2
+    # correction (MI355X_MICROARCH.md) are reported separately; `traffic` is the corrected rate, an upper bound
+    # for this gather-bound kernel.
+    traffic, traffic_detail = None, None
     prof_dir = os.path.join(ROOT, "profiles")
     if os.path.isdir(prof_dir):
         for fn in sorted(os.listdir(prof_dir), reverse=True):
@@ -925,8 +1076,22 @@ def main():
                     dk = ps.get("dominant_kernel", {})
                     if grp == "G1" and "hbm_bytes_per_point" in dk and ps.get("workload") == \
                             workload_name(args.log_rows):
-                        traffic = dk["hbm_bytes_per_point"] * units_per_launch
-                        traffic_src = fn
+                        wr = dk.get("write_bytes_per_point", 0.0)
+                        raw_b = (dk.get("fetch_bytes_raw_per_point", 0.0) + wr) * units_per_launch
+                        cor_b = dk["hbm_bytes_per_point"] * units_per_launch
+                        sec = avg_ms * 1e-3
+                        traffic = cor_b / sec / 1e9 if sec > 0 else None
+                        traffic_detail = {
+                            "unit": "GB/s", "bytes_per_launch_raw": raw_b, "bytes_per_launch_corrected": cor_b,
+                            "gbps_raw": raw_b / sec / 1e9 if sec > 0 else None, "gbps_corrected": traffic,
+                            "bytes_per_point_raw": raw_b / units_per_launch if units_per_launch else None,
+                            "bytes_per_point_corrected": dk["hbm_bytes_per_point"],
+                            "source": f"profiles/{fn}", "profiled_at_commit": ps.get("commit"),
+                            "profiled_launch_avg_ms": dk.get("timed_step_launch_avg_ms"),
+                            "note": "FETCH_SIZE (+ WRITE_SIZE) per point from separate --pmc passes x points per "
+                                    "launch of this run; corrected = FETCH x 2 (gfx950, stated for streaming "
+                                    "reads; an upper bound for these 128-B record gathers), rate over this run's "
+                                    "average launch time"}
                         break
                 except Exception:
                     pass
@@ -988,8 +1153,8 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS if achieved else None,
             "traffic": traffic,
-            "traffic_source": f"profiles/{traffic_src} (FETCH_SIZE + WRITE_SIZE per point x points per launch; "
-                              f"see the summary for the gfx950 correction applied)" if traffic_src else None,
+            "traffic_unit": "GB/s",
+            "traffic_detail": traffic_detail,
             "avg_launch_ms": avg_ms,
             "units_per_launch": units_per_launch,
             "algorithmic_bytes_per_unit": bytes_per_unit,
@@ -1024,6 +1189,7 @@ def main():
         "config5": config5,
         "stacked_porep_32gib": stacked_res,
         "window_post_32gib": post_res,
+        "winning_post_32gib": winning,
         "timers_ms": {k: round(v["ms"], 3) for k, v in stats.items()},
         "setup_s": {"synth": t_synth, "circuit_load": t_load, "srs": t_srs},
         "device_gb_after_setup": round(dev_used_gb, 2),

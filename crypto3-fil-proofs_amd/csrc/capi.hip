@@ -76,8 +76,17 @@ struct mi_points {
     uint64_t n;
     int is_g2;
     int owns;
-    const void *hi = nullptr;  // 2^128 multiples (split-mode MSM table), proving-key queries h, l, a only
+    const void *hi = nullptr;  // 2^128 multiples (split-mode MSM table) of caller-uploaded points (none today)
     int subgroup = 0;          // every point known to be in the prime-order subgroup (GLV split allowed)
+    // a proving-key query (mi_points_from_srs): its split table is looked up at use, since a proof that runs
+    // out of memory may release the key's tables (prover.hip groth16_sums)
+    const mi::Srs *srs = nullptr;
+    int which = -1;
+    const void *table() const {
+        if (!srs) return hi;
+        return which == 0 ? (const void *)srs->h_hi : which == 1 ? (const void *)srs->l_hi
+                                                    : which == 2 ? (const void *)srs->a_hi : nullptr;
+    }
 };
 
 namespace {
@@ -184,11 +193,30 @@ void write_be32(FILE *f, uint64_t v) {
     write_all(f, b, 4);
 }
 
+// Selects a context's device for the length of one C-ABI call and gives the calling thread its previous
+// device back afterwards, so a call never moves the caller's (e.g. torch's) current device.
+struct DeviceScope {
+    int prev = -1;
+    // strict: throw when the device cannot be selected (entries under guard); the free functions pass false
+    explicit DeviceScope(int device, bool strict = true) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        hipError_t e = hipSetDevice(device);
+        if (strict && e != hipSuccess) {
+            if (prev >= 0) (void)hipSetDevice(prev);
+            prev = -1;
+            MI_HIP(e);
+        }
+    }
+    ~DeviceScope() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
 struct CtxLock {
     mi_ctx *ctx;
     std::lock_guard<std::recursive_mutex> lk;
-    CtxLock(mi_ctx *c, int priority = 0) : ctx(c), lk(c->c.mu) {
-        MI_HIP(hipSetDevice(c->c.device));
+    DeviceScope dev;
+    CtxLock(mi_ctx *c, int priority = 0) : ctx(c), lk(c->c.mu), dev(c->c.device) {
         c->c.stream = priority ? c->high : c->normal;
     }
 };
@@ -356,7 +384,7 @@ int mi_ctx_create(int device, mi_ctx **out) {
         int n = 0;
         if (hipGetDeviceCount(&n) != hipSuccess || n == 0) throw std::runtime_error("no HIP device available");
         need(device >= 0 && device < n, "device index out of range");
-        MI_HIP(hipSetDevice(device));
+        DeviceScope dev(device);
         mi_ctx *c = new mi_ctx();
         try {
             c->c.device = device;
@@ -380,7 +408,7 @@ int mi_ctx_create(int device, mi_ctx **out) {
 
 void mi_ctx_destroy(mi_ctx *ctx) {
     if (!ctx) return;
-    hipSetDevice(ctx->c.device);
+    DeviceScope dev(ctx->c.device, false);
     hipDeviceSynchronize();
     ctx->up.release();
     mi::ntt_free_tables(ctx->c);
@@ -454,7 +482,7 @@ int mi_circuit_info(const mi_circuit *c, uint64_t out[9]) {
 
 void mi_circuit_free(mi_circuit *c) {
     if (!c) return;
-    hipSetDevice(c->device);
+    DeviceScope dev(c->device, false);
     delete c->p;
     delete c;
 }
@@ -523,8 +551,11 @@ int mi_srs_stream_end(mi_srs_stream *st, mi_srs **out) {
 }
 void mi_srs_stream_abort(mi_srs_stream *st) {
     if (!st) return;
-    hipSetDevice(st->ctx->c.device);
-    mi::srs_stream_abort(st->p);
+    try {
+        CtxLock l(st->ctx);  // the context's device and lock, like every other stream entry
+        mi::srs_stream_abort(st->p);
+    } catch (...) {
+    }
     delete st;
 }
 
@@ -645,7 +676,7 @@ int mi_srs_export_query(mi_ctx *ctx, const mi_srs *srs, int which, uint8_t *out,
 
 void mi_srs_free(mi_srs *s) {
     if (!s) return;
-    hipSetDevice(s->device);
+    DeviceScope dev(s->device, false);
     delete s->p;
     delete s;
 }
@@ -882,13 +913,15 @@ int mi_points_from_srs(mi_ctx *ctx, const mi_srs *srs, int which, mi_points **ou
         need(ctx && srs && out, "null argument");
         const mi::Srs &s = *srs->p;
         switch (which) {
-            case 0: *out = new mi_points{s.h_perm, s.n_h, 0, 0, s.h_hi, s.in_subgroup}; break;
-            case 1: *out = new mi_points{s.l, s.n_l, 0, 0, s.l_hi, s.in_subgroup}; break;
-            case 2: *out = new mi_points{s.a, s.n_a, 0, 0, s.a_hi, s.in_subgroup}; break;
+            case 0: *out = new mi_points{s.h_perm, s.n_h, 0, 0, nullptr, s.in_subgroup}; break;
+            case 1: *out = new mi_points{s.l, s.n_l, 0, 0, nullptr, s.in_subgroup}; break;
+            case 2: *out = new mi_points{s.a, s.n_a, 0, 0, nullptr, s.in_subgroup}; break;
             case 3: *out = new mi_points{s.b_g1, s.n_b, 0, 0, nullptr, s.in_subgroup}; break;
             case 4: *out = new mi_points{s.b_g2, s.n_b, 1, 0, nullptr, s.in_subgroup}; break;
             default: throw std::invalid_argument("which must be 0..4");
         }
+        (*out)->srs = &s;
+        (*out)->which = which;
     });
 }
 int mi_points_check_subgroup(mi_ctx *ctx, mi_points *p) {
@@ -916,7 +949,7 @@ int mi_points_info(const mi_points *p, uint64_t out[3]) {
     return guard([&] {
         need(p && out, "null argument");
         out[0] = p->n;
-        out[1] = p->hi ? 1 : 0;
+        out[1] = p->table() ? 1 : 0;
         out[2] = p->subgroup ? 1 : 0;
     });
 }
@@ -933,9 +966,11 @@ int mi_msm_g1_dev(mi_ctx *ctx, const mi_points *bases, const void *scalars_dev, 
         need(!bases->is_g2, "G2 bases passed to mi_msm_g1_dev");
         need(n <= bases->n, "n exceeds the number of bases");
         CtxLock l(ctx);
+        std::shared_lock<std::shared_mutex> in_use;  // a key's query: its split table stays while this MSM runs
+        if (bases->srs) in_use = std::shared_lock<std::shared_mutex>(bases->srs->use_mu);
         mi::g1_xyzz_t r;
         mi::msm_g1(ctx->c, (const mi::g1_affine_t *)bases->dev, (const mi::fr_t *)scalars_dev, nullptr, n, &r,
-                   (const mi::g1_affine_t *)bases->hi, bases->subgroup != 0);
+                   (const mi::g1_affine_t *)bases->table(), bases->subgroup != 0);
         mi::g1_encode(mi::xyzz_to_affine(r), out96);
     });
 }
@@ -1215,6 +1250,14 @@ int mi_ctx_get_work(mi_ctx *ctx, uint64_t out[2]) {
         CtxLock l(ctx);
         out[0] = ctx->c.stats.madds_g1;
         out[1] = ctx->c.stats.madds_g2;
+    });
+}
+int mi_ctx_get_fallbacks(mi_ctx *ctx, uint64_t out[2]) {
+    return guard([&] {
+        need(ctx && out, "null argument");
+        CtxLock l(ctx);
+        out[0] = ctx->c.stats.oom_retries;
+        out[1] = ctx->c.stats.oom_freed_bytes;
     });
 }
 unsigned mi_msm_window_bits(uint64_t n) { return mi::msm_window_bits(n); }

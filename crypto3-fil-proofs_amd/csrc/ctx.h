@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -90,6 +91,8 @@ struct Stats {
     KStat wit_sha;             // stacked witness phase B, SHA-256 gadget blocks (units = blocks)
     KStat wit_pos;             // stacked witness phase B, Poseidon gadgets (units = hashes)
     uint64_t madds_g1 = 0, madds_g2 = 0;  // mixed additions issued by k_accum_level0 (non-zero digits)
+    uint64_t oom_retries = 0;      // proofs re-run after an out-of-memory error (prover.hip groth16_sums)
+    uint64_t oom_freed_bytes = 0;  // split tables + scratch released for those retries
     static constexpr int NK = 13;
     void merge(const Stats &o) {
         madds_g1 += o.madds_g1;
@@ -152,7 +155,13 @@ struct EventTimer {
     }
 };
 
+inline uint64_t next_ctx_uid() {
+    static std::atomic<uint64_t> n{1};
+    return n.fetch_add(1);
+}
+
 struct Ctx {
+    const uint64_t uid = next_ctx_uid();  // never reused: keys per-context device state held by shared objects
     int device = 0;
     hipStream_t stream = nullptr;
     std::recursive_mutex mu;

@@ -2,6 +2,8 @@
 #pragma once
 #include <stdint.h>
 
+#include <shared_mutex>
+
 #include <vector>
 
 #include "ctx.h"
@@ -51,6 +53,14 @@ struct Srs {
     // every query point is known to lie in the prime-order subgroup (generated from toxic waste, or
     // loaded with checked = 1): the condition for the GLV split in auto mode (msm_g1 `subgroup`)
     bool in_subgroup = false;
+    // Every live key is registered with its device: a proof that runs out of memory may release the split
+    // tables of any key on its device (groth16_sums).  Provers and MSMs over the key's points hold use_mu
+    // shared; releasing another key's tables takes it exclusive, and only when no one is using that key.
+    int device = -1;
+    mutable std::shared_mutex use_mu;
+    explicit Srs(int dev);
+    Srs(const Srs &) = delete;
+    Srs &operator=(const Srs &) = delete;
     ~Srs();
 };
 
@@ -125,6 +135,9 @@ ProofPoints groth16_prove(Ctx &c, const Srs &srs, const Circuit &circ, const fr_
 // rank's share of the MSMs (rank < world); the witness map and NTT chain run in full on every rank
 ProofSums groth16_sums(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, unsigned rank = 0,
                        unsigned world = 1);
+// releases the 2^128 split tables of a key (its G1 MSMs then take the GLV split); returns the bytes freed.  The
+// caller holds the key exclusively (use_mu) or owns it outright.
+uint64_t srs_drop_split_tables(Srs &S);
 // A = alpha + A_sum + r delta, B = beta + B2_sum + s delta, C = H + L + s A + r B1 - r s delta (host)
 ProofPoints groth16_assemble(const AssemblyKey &k, const ProofSums &sums, const fr_t &r, const fr_t &s);
 AssemblyKey assembly_key(const Srs &srs);

@@ -18,6 +18,7 @@
 
 #include <exception>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -462,7 +463,25 @@ Circuit::~Circuit() {
     if (idx_a) hipFree(idx_a);
     if (idx_b) hipFree(idx_b);
 }
+namespace {
+std::mutex g_keys_mu;
+std::vector<Srs *> g_keys;  // every live proving key (Srs::device says where it lives)
+}  // namespace
+
+Srs::Srs(int dev) : device(dev) {
+    std::lock_guard<std::mutex> lk(g_keys_mu);
+    g_keys.push_back(this);
+}
+
 Srs::~Srs() {
+    {
+        std::lock_guard<std::mutex> lk(g_keys_mu);
+        for (size_t i = 0; i < g_keys.size(); i++)
+            if (g_keys[i] == this) {
+                g_keys.erase(g_keys.begin() + i);
+                break;
+            }
+    }
     void *ps[] = {h_perm, l, a, b_g1, b_g2, at, bt, ct, h_hi, l_hi, a_hi};
     for (void *p : ps)
         if (p) hipFree(p);
@@ -693,7 +712,7 @@ const char *kQueryName[5] = {"h", "l", "a", "b_g1", "b_g2"};
 
 SrsStream *srs_stream_begin(Ctx &c, const Circuit *circ, const SrsHost &h, bool checked) {
     SrsStream *st = new SrsStream();
-    Srs *S = st->S = new Srs();
+    Srs *S = st->S = new Srs(c.device);
     try {
         st->checked = checked;
         if (h.n_h < 1) throw std::invalid_argument("empty h query");
@@ -921,7 +940,7 @@ void build_hi_tables(Ctx &c, Srs &S) {
 }  // namespace
 
 Srs *srs_generate(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5]) {
-    Srs *S = new Srs();
+    Srs *S = new Srs(c.device);
     hipStream_t st = c.stream;
     try {
         const uint64_t d = circ.d, n = circ.n, nv = circ.n_in + circ.n_aux;
@@ -1092,8 +1111,12 @@ Srs *srs_generate(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5]) {
 }
 
 // ================================================================================ prove
-ProofSums groth16_sums(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, unsigned rank,
-                       unsigned world) {
+namespace {
+// One attempt at a proof's MSM sums.  inject_oom (tests, MI_INJECT_PROVE_OOM): the main lane throws the
+// out-of-memory error a scratch hipMalloc would, after the NTT chain, while the auxiliary lane runs.
+ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, unsigned rank,
+                            unsigned world, bool inject_oom) {
+    std::shared_lock<std::shared_mutex> in_use(srs.use_mu);
     if (srs.d != circ.d || srs.n_l != circ.n_aux || srs.n_a != circ.n_a || srs.n_b != circ.n_b)
         throw std::invalid_argument("SRS does not match circuit");
     if (world == 0 || rank >= world) throw std::invalid_argument("share rank out of range");
@@ -1179,6 +1202,8 @@ ProofSums groth16_sums(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *
                 k_qap_divide<<<grid1(d), 256, 0, st>>>(a, b, cc, d, zinv);
                 ntt_dif_coset_epilogue(c, a, L, true, true, dinv, true);  // icoset, canonical H (bit-reversed)
             }
+            if (inject_oom)
+                throw hip_error(hipErrorOutOfMemory, "hipMalloc failed: out of memory (injected, MI_INJECT_PROVE_OOM)");
             uint64_t h_lo, h_cnt = slice(d - 1, h_lo), a_lo, a_cnt = slice(circ.n_a, a_lo);
             msm_g1(c, srs.h_perm + h_lo, a + h_lo, nullptr, h_cnt, &H, srs.h_hi ? srs.h_hi + h_lo : nullptr,
                    srs.in_subgroup);
@@ -1207,6 +1232,85 @@ ProofSums groth16_sums(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *
     MI_HIP(hipStreamSynchronize(st));
     c.timer.resolve();
     return out;
+}
+
+}  // namespace
+
+uint64_t srs_drop_split_tables(Srs &S) {
+    uint64_t freed = 0;
+    const struct {
+        g1_affine_t **p;
+        uint64_t n;
+    } ts[] = {{&S.h_hi, S.n_h}, {&S.l_hi, S.n_l}, {&S.a_hi, S.n_a}};
+    for (auto &t : ts)
+        if (*t.p) {
+            (void)hipFree(*t.p);
+            *t.p = nullptr;
+            freed += t.n * sizeof(g1_affine_t);
+        }
+    return freed;
+}
+
+namespace {
+// the split tables of every key on `device` that no one is using right now, the proving key first
+uint64_t release_device_tables(int device, const Srs &first) {
+    std::lock_guard<std::mutex> lk(g_keys_mu);
+    std::vector<Srs *> order;
+    for (Srs *k : g_keys)
+        if (k == &first) order.insert(order.begin(), k);
+        else if (k->device == device) order.push_back(k);
+    uint64_t freed = 0;
+    for (Srs *k : order) {
+        if (!k->h_hi && !k->l_hi && !k->a_hi) continue;
+        std::unique_lock<std::shared_mutex> ex(k->use_mu, std::try_to_lock);
+        if (ex.owns_lock()) freed += srs_drop_split_tables(*k);
+    }
+    return freed;
+}
+
+// releases a context's grow-only scratch (both lanes), except the witness slots of the batch uploader (21, 22:
+// the next partition may be uploading into the other one) and any buffer holding `keep` (the proof's witness)
+uint64_t release_prover_scratch(Ctx &c, const void *keep) {
+    uint64_t freed = 0;
+    auto rel = [&](Ctx &x, int upto) {
+        for (int i = 0; i < upto; i++) {
+            DevBuf &b = x.scratch[i];
+            if (!b.p) continue;
+            const char *lo = (const char *)b.p;
+            if ((const char *)keep >= lo && (const char *)keep < lo + b.cap) continue;
+            freed += b.cap;
+            b.release();
+        }
+    };
+    rel(c, 21);
+    if (c.aux) rel(*c.aux, 24);
+    return freed;
+}
+}  // namespace
+
+// A proof whose working set does not fit next to the resident keys degrades instead of failing: on an
+// out-of-memory error the attempt is drained, the 2^128 split tables of the keys on this device (the proving
+// key's first, then every other key no one is using: several keys stay resident side by side, as the
+// reference's GROTH_PARAM_MEMORY_CACHE keeps them, caches.hpp:48-116) and this context's idle scratch are
+// released, and the proof runs again; its G1 MSMs take the GLV split, which needs no table (glv.h).  The MSM
+// sums are unique group elements, so the retried proof is byte-identical.  A second out-of-memory error
+// propagates.
+ProofSums groth16_sums(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, unsigned rank,
+                       unsigned world) {
+    const bool inject = getenv("MI_INJECT_PROVE_OOM") != nullptr;
+    try {
+        return groth16_sums_once(c, srs, circ, z_dev, rank, world, inject);
+    } catch (const hip_error &e) {
+        if (e.code != hipErrorOutOfMemory) throw;
+        (void)hipStreamSynchronize(c.stream);
+        if (c.aux) (void)hipStreamSynchronize(c.aux->stream);
+        (void)hipGetLastError();  // the failed allocation's error, so the retry's launch checks start clean
+        uint64_t freed = release_device_tables(c.device, srs);
+        freed += release_prover_scratch(c, z_dev);
+        c.stats.oom_retries += 1;
+        c.stats.oom_freed_bytes += freed;
+        return groth16_sums_once(c, srs, circ, z_dev, rank, world, false);
+    }
 }
 
 AssemblyKey assembly_key(const Srs &srs) {

@@ -22,6 +22,8 @@
 // level and 2 per tree C level.  Phase B is one launch per heavy op kind.
 #pragma once
 #include <cstdint>
+#include <mutex>
+#include <utility>
 #include <vector>
 
 #include "field.h"
@@ -119,9 +121,15 @@ struct Built {
     std::vector<uint64_t> pin;       // Poseidon input variable lists
     std::vector<ShaBlock> blocks;
     std::vector<uint64_t> poseidon_ops, sha_ops;  // op indices (phase B)
-    // device copy of the program (stacked_witness.hip), uploaded on first use on device `dev_device`
-    void *dev_prog = nullptr;
-    int dev_device = -1;
+    // device copies of the program (stacked_witness.hip), one per context (Ctx::uid) that ran the witness,
+    // uploaded on first use.  Each holds that context's Poseidon table views and its own SHA chaining-value
+    // scratch, so contexts on one or several devices never share device state; calls through one context are
+    // serialised by its lock, and dev_mu guards the list itself.
+    std::mutex dev_mu;
+    std::vector<std::pair<uint64_t, void *>> dev_progs;
+    Built() = default;
+    Built(const Built &) = delete;
+    Built &operator=(const Built &) = delete;
     ~Built();
 };
 

@@ -394,9 +394,9 @@ T *upload(const std::vector<T> &v) {
 }
 
 DevProg *prog_for(Ctx &c, Built &b) {
-    if (b.dev_prog && b.dev_device == c.device) return (DevProg *)b.dev_prog;
-    delete (DevProg *)b.dev_prog;
-    b.dev_prog = nullptr;
+    std::lock_guard<std::mutex> lk(b.dev_mu);
+    for (auto &e : b.dev_progs)
+        if (e.first == c.uid) return (DevProg *)e.second;
     DevProg *p = new DevProg();
     try {
         p->device = c.device;
@@ -414,12 +414,11 @@ DevProg *prog_for(Ctx &c, Built &b) {
         p->pos_ops = upload(by);
         MI_HIP(hipMalloc(&p->states, 32 * (b.blocks.empty() ? 1 : b.blocks.size())));
         for (int q = 0; q < 4; q++) poseidon_tables(c, ar[q], &p->pk.k[q]);
+        b.dev_progs.emplace_back(c.uid, p);
     } catch (...) {
         delete p;
         throw;
     }
-    b.dev_prog = p;
-    b.dev_device = c.device;
     return p;
 }
 
@@ -427,7 +426,9 @@ unsigned grid64(uint64_t n) { return (unsigned)((n + 63) / 64); }
 
 }  // namespace
 
-Built::~Built() { delete (DevProg *)dev_prog; }
+Built::~Built() {
+    for (auto &e : dev_progs) delete (DevProg *)e.second;
+}
 
 void witness_dev(Ctx &c, Built &b, const uint8_t *slots_dev, fr_t *z_dev) {
     DevProg *p = prog_for(c, b);

@@ -14,7 +14,7 @@
   generate_winning_post_proof     generate_winning_post (api/post.hpp:178-230): one partition
   shard_partitions                one process per GPU: partition k goes to rank k % world
 """
-from .core import PROOF_BYTES, prove_batch, verify_batch
+from .core import PROOF_BYTES, prove, prove_batch, verify_batch
 
 
 def partition_count(partitions: int) -> int:
@@ -74,19 +74,31 @@ def circuit_proofs(ctx, pk, circuit, witnesses, blindings=None, priority=False):
         raise ValueError("Cannot create a circuit proof over missing vanilla proofs")
     if blindings is not None and len(witnesses) != len(blindings):
         raise ValueError("one (r, s) pair per partition is required")
-    return prove_batch(ctx, pk, circuit, list(witnesses), blindings, priority=priority)
+    ws = list(witnesses)
+    on_device = [isinstance(z, int) for z in ws]
+    if any(on_device):  # witnesses already in HBM (e.g. the library-built circuits' GPU witness): one prove each
+        if not all(on_device):
+            raise TypeError("witnesses must be all host buffers or all device pointers")
+        return [prove(ctx, pk, circuit, z, *(blindings[k] if blindings is not None else (None, None)),
+                      priority=priority) for k, z in enumerate(ws)]
+    return prove_batch(ctx, pk, circuit, ws, blindings, priority=priority)
 
 
 def seal_commit_phase2_proofs(ctx, pk, circuit, witnesses, blindings=None, num_inputs=None,
-                              priority=False) -> bytes:
+                              priority=False, public_inputs=None) -> bytes:
     """api/seal.hpp:296-313: prove every partition, pack the MultiProof buffer and refuse to return
-    one that does not verify.  ``witnesses`` are full assignments (ONE first); the public inputs of
-    partition k are its witness entries 1 .. num_inputs - 1."""
+    one that does not verify.  ``witnesses`` are full assignments (ONE first), in host memory or as device
+    pointers; the public inputs of partition k are its witness entries 1 .. num_inputs - 1 (device
+    witnesses: given as ``public_inputs``, e.g. StackedCircuit.public_inputs of each partition's slots)."""
     if num_inputs is None:
         num_inputs = circuit.num_inputs
     proofs = circuit_proofs(ctx, pk, circuit, witnesses, blindings, priority=priority)
     mp = MultiProof(proofs, pk.verifying_key())
-    inputs = [bytes(z[32:32 * num_inputs]) for z in witnesses]
+    if public_inputs is None:
+        if any(isinstance(z, int) for z in witnesses):
+            raise ValueError("device witnesses: pass public_inputs (one 32 x (num_inputs - 1)-byte vector each)")
+        public_inputs = [bytes(z[32:32 * num_inputs]) for z in witnesses]
+    inputs = list(public_inputs)
     if not mp.verify(inputs):
         raise RuntimeError("post-seal verification sanity check failed")
     return mp.to_bytes()

@@ -94,6 +94,13 @@ class Context:
         st["accum_g1"]["madds"], st["accum_g2"]["madds"] = int(w[0]), int(w[1])
         return st
 
+    def fallbacks(self) -> dict:
+        """proofs re-run after an out-of-memory error with their key's split tables released, since the last
+        reset_stats (mi_ctx_get_fallbacks)"""
+        w = (ctypes.c_uint64 * 2)()
+        check(lib().mi_ctx_get_fallbacks(self.h, w))
+        return {"oom_retries": int(w[0]), "freed_bytes": int(w[1])}
+
     # ---- building blocks ----
     def msm_g1(self, bases96: bytes, scalars32: bytes) -> bytes:
         n = len(scalars32) // 32
@@ -449,7 +456,10 @@ class HostBuffer:
 
 
 def _host_ptr(z, nbytes):
-    """(address, keepalive) of a host witness without copying it: HostBuffer, numpy array or bytes."""
+    """(address, keepalive) of a host witness without copying it: HostBuffer, numpy array or bytes.  A device
+    pointer (int) is refused: the batch entry uploads host witnesses (use prove / circuit_proofs for those)."""
+    if isinstance(z, int):
+        raise TypeError("prove_batch takes host witnesses; a device pointer (int) goes through prove()")
     if isinstance(z, HostBuffer):
         assert z.nbytes >= nbytes
         return z.ptr, z

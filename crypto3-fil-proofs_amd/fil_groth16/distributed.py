@@ -13,11 +13,37 @@ from .compound import shard_partitions
 from .core import PROOF_BYTES, SHARE_BYTES
 
 
+def _group_active(world: int) -> bool:
+    """True when a process group is initialised (then every exchange goes through it, a world of one
+    included: that is how a one-GPU box runs the RCCL path); it must have ``world`` ranks."""
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()):
+        if world > 1:
+            raise RuntimeError(f"world size {world} needs an initialised process group")
+        return False
+    if dist.get_world_size() != world:
+        raise ValueError(f"process group has {dist.get_world_size()} ranks, caller says {world}")
+    return True
+
+
+def _all_gather(t, world: int):
+    """all_gather of one tensor per rank over the process group (RCCL for device tensors with "nccl"),
+    returned as host numpy arrays in rank order; a plain copy without a group."""
+    import torch
+    import torch.distributed as dist
+
+    if not _group_active(world):
+        return [t.cpu().numpy()]
+    bufs = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(bufs, t)
+    return [b.cpu().numpy() for b in bufs]
+
+
 def gather_multiproof(local_proofs, num_partitions: int, rank: int, world: int, device="cpu"):
     """local_proofs: this rank's proofs, in the order of shard_partitions(num_partitions, rank, world).
     Returns the P x 192-byte multi-proof (partition order) on every rank."""
     import torch
-    import torch.distributed as dist
 
     mine = shard_partitions(num_partitions, rank, world)
     if len(local_proofs) != len(mine):
@@ -28,13 +54,7 @@ def gather_multiproof(local_proofs, num_partitions: int, rank: int, world: int, 
         if len(p) != PROOF_BYTES:
             raise ValueError("proofs are 192 bytes")
         buf[i] = np.frombuffer(p, dtype=np.uint8)
-    t = torch.from_numpy(buf).to(device)
-    if world > 1:
-        bufs = [torch.empty_like(t) for _ in range(world)]
-        dist.all_gather(bufs, t)
-        allp = [b.cpu().numpy() for b in bufs]
-    else:
-        allp = [t.cpu().numpy()]
+    allp = _all_gather(torch.from_numpy(buf).to(device), world)
     out = bytearray()
     for p in range(num_partitions):
         out += allp[p % world][p // world].tobytes()
@@ -107,7 +127,6 @@ def prove_partitions_balanced(prove_fn, share_fn, assemble_fn, num_partitions: i
     each rank then assembles the tail proofs itself.  Returns the P x 192-byte multi-proof (partition
     order) on every rank, byte-identical to prove_partitions' for the same blinding."""
     import torch
-    import torch.distributed as dist
 
     whole, tail = balanced_schedule(num_partitions, world)
     kmax = max((len(w) for w in whole), default=0)
@@ -123,13 +142,7 @@ def prove_partitions_balanced(prove_fn, share_fn, assemble_fn, num_partitions: i
             if len(share) != SHARE_BYTES:
                 raise ValueError(f"shares are {SHARE_BYTES} bytes")
             rec[kmax * PROOF_BYTES:] = np.frombuffer(share, dtype=np.uint8)
-    t = torch.from_numpy(rec).to(device)
-    if world > 1:
-        bufs = [torch.empty_like(t) for _ in range(world)]
-        dist.all_gather(bufs, t)
-        allr = [b.cpu().numpy() for b in bufs]
-    else:
-        allr = [rec]
+    allr = _all_gather(torch.from_numpy(rec).to(device), world)
     out = {}
     for r in range(world):
         for i, p in enumerate(whole[r]):
@@ -142,16 +155,11 @@ def prove_partitions_balanced(prove_fn, share_fn, assemble_fn, num_partitions: i
 def gather_shares(share: bytes, world: int, device="cpu"):
     """All-gather one MI_SHARE_BYTES record per rank (the latency mode's only exchange, 576 B per GPU)."""
     import torch
-    import torch.distributed as dist
 
     if len(share) != SHARE_BYTES:
         raise ValueError(f"shares are {SHARE_BYTES} bytes")
     t = torch.from_numpy(np.frombuffer(share, dtype=np.uint8).copy()).to(device)
-    if world == 1:
-        return [share]
-    bufs = [torch.empty_like(t) for _ in range(world)]
-    dist.all_gather(bufs, t)
-    return [b.cpu().numpy().tobytes() for b in bufs]
+    return [b.tobytes() for b in _all_gather(t, world)]
 
 
 def prove_split(ctx, pk, circuit, z, r, s, rank: int, world: int, device="cpu", want_raw=False):
@@ -171,21 +179,23 @@ SRS_PARTS = ("vk", "ic", "h", "l", "a", "b_g1", "b_g2")
 _POINT_BYTES = {"vk": 1, "ic": 96, "h": 96, "l": 96, "a": 96, "b_g1": 96, "b_g2": 192}
 
 
-def _broadcast_chunks(sizes, rank, src, device, chunk_bytes, source, sink):
+def _broadcast_chunks(sizes, rank, src, device, chunk_bytes, source, sink, relay=False):
     """Broadcast every part of ``sizes`` (name -> bytes) from ``src`` in chunks of whole points of at most
     ``chunk_bytes``: ``source(name, offset, nbytes) -> uint8 tensor on device`` on the source rank,
-    ``sink(name, offset, tensor)`` on the others.  Only one chunk is in flight per rank."""
+    ``sink(name, offset, tensor)`` on the others (relay: the one rank of a world of one does both, the
+    broadcast tensor going to its own sink).  Only one chunk is in flight per rank."""
     import torch
     import torch.distributed as dist
 
+    is_src = relay or rank == src
     for k, n in sizes:
         esz = _POINT_BYTES[k]
         step = max(esz, chunk_bytes // esz * esz)
         for off in range(0, n, step):
             m = min(step, n - off)
-            t = source(k, off, m) if rank == src else torch.empty(m, dtype=torch.uint8, device=device)
+            t = source(k, off, m) if is_src else torch.empty(m, dtype=torch.uint8, device=device)
             dist.broadcast(t, src)
-            if rank != src:
+            if relay or rank != src:
                 sink(k, off, t)
 
 
@@ -225,7 +235,7 @@ def broadcast_srs_parts(parts, rank: int, world: int, src: int = 0, device="cpu"
 
 
 def broadcast_proving_key(ctx, pk, circuit, rank: int, world: int, src: int = 0, device="cpu", checked=False,
-                          chunk_bytes: int = 1 << 30):
+                          chunk_bytes: int = 1 << 30, self_relay: bool = False):
     """Rank ``src`` holds ``pk`` (e.g. ProvingKey.load_params from a v28 file); every other rank receives the
     key over the process group and loads it into its own GPU through the streaming loader
     (mi_srs_stream_*), chunk by chunk with the same rules as mi_srs_load (``checked``: subgroup checks).
@@ -235,40 +245,50 @@ def broadcast_proving_key(ctx, pk, circuit, rank: int, world: int, src: int = 0,
     With backend "nccl" (``device`` a CUDA device) the source encodes each chunk on its GPU
     (mi_srs_export_query_dev), RCCL moves it over xGMI, and the receiver decodes it in place from device
     memory: no rank holds the key in host memory.  With gloo the chunks travel through host tensors, one
-    chunk at a time.  Memory per rank beyond the key itself: one chunk.  Returns this rank's ProvingKey."""
+    chunk at a time.  Memory per rank beyond the key itself: one chunk.  Returns this rank's ProvingKey.
+
+    ``self_relay`` (a world of one with an initialised group): the one rank is source and receiver, every
+    chunk goes through the group's broadcast and is decoded into a second key, which is returned.  That
+    runs the whole device path -- export, RCCL broadcast, on-device decode -- on a one-GPU box."""
     import torch
 
     from .core import ProvingKey
 
-    if world == 1:
+    relay = bool(self_relay) and world == 1
+    if world == 1 and not relay:
         return pk
+    if relay and not _group_active(1):
+        raise RuntimeError("self_relay needs an initialised process group")
+    is_src, is_dst = (True, True) if relay else (rank == src, rank != src)
     on_gpu = torch.device(device).type == "cuda"
     sizes = None
-    if rank == src:
+    if is_src:
         vk, ic = pk.verifying_key()
         sizes = [len(vk), len(ic), 96 * pk.n_h, 96 * pk.n_l, 96 * pk.n_a, 96 * pk.n_b, 192 * pk.n_b]
     sizes = _broadcast_sizes(sizes, rank, src, device)
-    small = {"vk": None, "ic": None}
-    if rank == src:
-        small = {"vk": vk, "ic": ic}
-        source_small = lambda k, off, m: torch.frombuffer(bytearray(small[k][off:off + m]), dtype=torch.uint8).to(device)
-    else:
-        small = {"vk": bytearray(sizes[0]), "ic": bytearray(sizes[1])}
-        source_small = None
+    small_src = {"vk": vk, "ic": ic} if is_src else None
+    small = {"vk": bytearray(sizes[0]), "ic": bytearray(sizes[1])}
+    gpu = torch.device("cuda", ctx.device) if hasattr(ctx, "device") else torch.device("cuda")
+
+    def source_small(k, off, m):
+        return torch.frombuffer(bytearray(small_src[k][off:off + m]), dtype=torch.uint8).to(device)
 
     def sink_small(k, off, t):
         small[k][off:off + t.numel()] = memoryview(t.cpu().numpy())
 
-    _broadcast_chunks([("vk", sizes[0]), ("ic", sizes[1])], rank, src, device, chunk_bytes, source_small, sink_small)
-    queries = list(zip(SRS_PARTS[2:], sizes[2:]))
     which = {k: i for i, k in enumerate(SRS_PARTS[2:])}
-    gpu = torch.device("cuda", ctx.device) if hasattr(ctx, "device") else torch.device("cuda")
-    if rank == src:
-        def source(k, off, m):
-            t = torch.empty(m, dtype=torch.uint8, device=gpu)
-            pk.export_query_dev(which[k], off // _POINT_BYTES[k], m // _POINT_BYTES[k], t.data_ptr())
-            return t if on_gpu else t.cpu()
 
+    def source(k, off, m):
+        t = torch.empty(m, dtype=torch.uint8, device=gpu)
+        # the library writes t on its own stream: torch's stream must be done with this memory first
+        torch.cuda.current_stream(gpu).synchronize()
+        pk.export_query_dev(which[k], off // _POINT_BYTES[k], m // _POINT_BYTES[k], t.data_ptr())
+        return t if on_gpu else t.cpu()
+
+    _broadcast_chunks([("vk", sizes[0]), ("ic", sizes[1])], rank, src, device, chunk_bytes,
+                      source_small if is_src else None, sink_small if is_dst else None, relay)
+    queries = list(zip(SRS_PARTS[2:], sizes[2:]))
+    if not is_dst:
         _broadcast_chunks(queries, rank, src, device, chunk_bytes, source, None)
         return pk
     counts = [n // _POINT_BYTES[k] for k, n in queries]
@@ -282,7 +302,7 @@ def broadcast_proving_key(ctx, pk, circuit, rank: int, world: int, src: int = 0,
             stream.part(which[k], off // _POINT_BYTES[k], t.numpy(), t.numel() // _POINT_BYTES[k], on_device=False)
 
     try:
-        _broadcast_chunks(queries, rank, src, device, chunk_bytes, None, sink)
+        _broadcast_chunks(queries, rank, src, device, chunk_bytes, source if relay else None, sink, relay)
     except BaseException:
         stream.abort()
         raise

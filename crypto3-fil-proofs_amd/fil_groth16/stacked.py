@@ -10,6 +10,9 @@ Mirrors the synthesis half of the reference's compound proofs:
   FallbackPoStCircuit             FallbackPoStCircuit / Sector (post/fallback/circuit.hpp:38-86; the synthesize
                                   body is rust-fil-proofs storage-proofs-post fallback/circuit.rs): Window and
                                   Winning PoSt partitions
+  winning_post_setup_params       proofs/parameters.hpp:58-68: Winning PoSt's 66 challenges over 1 sector become
+                                  66 circuit sectors x 1 challenge (WinningPoStCircuit)
+  winning_post_sectors            generate_winning_post's replica repetition (api/post.hpp:205-218)
   generate_leaf_challenge         post/fallback/vanilla.hpp:398-411
   post_slots                      a partition's sector proofs (vanilla.hpp:188-251) in the slot layout
 The R1CS is built on the host once per shape (mi_stacked_build / mi_post_build; the blank circuit), the
@@ -132,7 +135,7 @@ class StackedCircuit(_BuiltCircuit):
 class FallbackPoStCircuit(_BuiltCircuit):
     """One Fallback PoSt partition: `sectors` sectors x `challenges` private tree R-last inclusion proofs
     (Window PoSt at 32 GiB: 2349 x 10 over 2^30-node 8-8-0 trees = 125,279,217 constraints, constants.hpp:85-89;
-    Winning PoSt: 1 sector x 66 challenges)."""
+    Winning PoSt: 66 sectors x 1 challenge, WinningPoStCircuit)."""
 
     def __init__(self, sectors=1, challenges=1, nodes=64, base=8, sub=0, top=0, with_r1cs=True):
         sh = _PostShape(sectors, challenges, nodes, base, sub, top, 0)
@@ -141,6 +144,44 @@ class FallbackPoStCircuit(_BuiltCircuit):
         self.sectors, self.challenges, self.nodes = sectors, challenges, nodes
         self.arities = tree_arities(nodes, base, sub, top)
         self._finish(with_r1cs)
+
+
+WINNING_POST_CHALLENGE_COUNT = 66  # constants.hpp:54
+WINNING_POST_SECTOR_COUNT = 1  # constants.hpp:55
+
+
+def winning_post_setup_params(challenge_count: int = WINNING_POST_CHALLENGE_COUNT,
+                              sector_count: int = WINNING_POST_SECTOR_COUNT):
+    """proofs/parameters.hpp:58-68 winning_post_setup_params -> (param_sector_count, param_challenge_count):
+    the post_config's challenges over its sectors become challenge_count / sector_count circuit sectors of
+    challenge_count / param_sector_count challenges each (66 / 1 -> 66 sectors x 1 challenge)."""
+    if sector_count <= 0 or challenge_count <= 0 or challenge_count % sector_count:
+        raise ValueError("sector count must divide challenge count")
+    param_sector_count = challenge_count // sector_count
+    param_challenge_count = challenge_count // param_sector_count
+    if param_sector_count * param_challenge_count != challenge_count:
+        raise ValueError("invalid parameters calculated")
+    return param_sector_count, param_challenge_count
+
+
+class WinningPoStCircuit(FallbackPoStCircuit):
+    """The Winning PoSt circuit: FallbackPoSt set up with winning_post_setup_params (parameters.hpp:58-68), one
+    partition (partitions unset, api/post.hpp:193).  At 32 GiB (2^30-node 8-8-0 trees R-last): 66 sectors x 1
+    challenge = 370,590 constraints, 1 + 66 x 2 = 133 public inputs, domain 2^19."""
+
+    def __init__(self, nodes, base=8, sub=8, top=0, challenge_count=WINNING_POST_CHALLENGE_COUNT,
+                 sector_count=WINNING_POST_SECTOR_COUNT, with_r1cs=True):
+        ps, pc = winning_post_setup_params(challenge_count, sector_count)
+        super().__init__(ps, pc, nodes, base, sub, top, with_r1cs)
+        self.replicas = sector_count
+
+
+def winning_post_sectors(replicas, param_sector_count: int):
+    """api/post.hpp:205-218: for i in 0..param_sector_count, for each replica (in sector-id order): one
+    public/private sector -- the post_config's replicas repeated param_sector_count times (66 copies of the one
+    Winning-PoSt replica).  The reference's C++ sizes its vectors and then pushes behind them; the sector list
+    it means (rust-fil-proofs winning_post.rs) is this one."""
+    return [r for _ in range(param_sector_count) for r in replicas]
 
 
 def generate_leaf_challenge(randomness: int, sector_id: int, leaf_challenge_index: int, nodes: int) -> int:
@@ -185,16 +226,21 @@ def post_slots(circuit: FallbackPoStCircuit, sectors) -> bytes:
     return buf
 
 
-def synthetic_post_instance(ctx, circuit: FallbackPoStCircuit, seed: int = 1, partition: int = 0):
-    """A consistent Fallback PoSt partition without sectors on disk (the bench's Window-PoSt partition and
-    the GPU tests): random randomness, sector ids, comm_c and challenged leaves; challenges derived by
-    generate_leaf_challenge; each sector's tree R-last built sparsely over its challenged leaves with random
-    filler nodes (Poseidon on the GPU, one batched call per tree level over all sectors); comm_r =
-    Poseidon-2(comm_c, comm_r_last).  Returns (randomness, sectors in post_slots' format)."""
+def synthetic_post_instance(ctx, circuit: FallbackPoStCircuit, seed: int = 1, partition: int = 0, replicas=None):
+    """A consistent Fallback PoSt partition without sectors on disk (the bench's Window- and Winning-PoSt
+    partitions and the GPU tests): random randomness, sector ids, comm_c and challenged leaves; challenges derived
+    by generate_leaf_challenge; each replica's tree R-last built sparsely over its challenged leaves with random
+    filler nodes (Poseidon on the GPU, one batched call per tree level over all replicas); comm_r =
+    Poseidon-2(comm_c, comm_r_last).  replicas: distinct sectors behind the circuit's sector slots (default one
+    per slot; Winning PoSt: 1, slot s holding replica s % replicas as winning_post_sectors lays them out).
+    Returns (randomness, sectors in post_slots' format)."""
     from . import tree
 
     rng = np.random.default_rng(seed)
     S, C, nodes, ar = circuit.sectors, circuit.challenges, circuit.nodes, circuit.arities
+    Q = S if replicas is None else int(replicas)
+    if not 1 <= Q <= S:
+        raise ValueError(f"1 .. {S} replicas behind {S} sector slots, got {Q}")
 
     def rand_many(k):
         b = rng.integers(0, 256, size=(k, 32), dtype=np.uint8)
@@ -205,47 +251,54 @@ def synthetic_post_instance(ctx, circuit: FallbackPoStCircuit, seed: int = 1, pa
         return tree.to_ints(tree.poseidon_hash(ctx, a, flat)) if flat else []
 
     randomness = rand_many(1)[0]
-    ids = [int(x) for x in rng.choice(2 ** 40, size=S, replace=False)]
-    chal = post_challenges(randomness, ids, C, nodes, partition, S)
-    levels = []  # per sector: list of {position: value} per tree level
-    for s in range(S):
-        leaves = {}
-        vals = rand_many(len(set(chal[s])))
-        for idx, v in zip(sorted(set(chal[s])), vals):
-            leaves[idx] = v
+    ids = [int(x) for x in rng.choice(2 ** 40, size=Q, replace=False)]
+    slot_ids = winning_post_sectors(ids, S // Q) + ids[:S % Q]
+    chal = post_challenges(randomness, slot_ids, C, nodes, partition, S)
+    levels = []  # per replica: list of {position: value} per tree level
+    for q in range(Q):
+        want = sorted({i for s in range(q, S, Q) for i in chal[s]})
+        leaves = dict(zip(want, rand_many(len(want))))
         levels.append([leaves])
-    for a in ar:  # one GPU call per level over every sector's sparse tree
+    for a in ar:  # one GPU call per level over every replica's sparse tree
         flat, parents = [], []
-        for s in range(S):
-            cur = levels[s][-1]
+        for q in range(Q):
+            cur = levels[q][-1]
             ps = sorted({p // a for p in cur})
             missing = [p * a + k for p in ps for k in range(a) if p * a + k not in cur]
-            for q, v in zip(missing, rand_many(len(missing))):
-                cur[q] = v
+            for m, v in zip(missing, rand_many(len(missing))):
+                cur[m] = v
             for p in ps:
                 flat += [cur[p * a + k] for k in range(a)]
             parents.append(ps)
         hashed = pos_hash(a, flat)
         o = 0
-        for s in range(S):
-            levels[s].append(dict(zip(parents[s], hashed[o:o + len(parents[s])])))
-            o += len(parents[s])
-    comm_r_last = [levels[s][-1][0] for s in range(S)]
-    comm_c = rand_many(S)
-    comm_r = pos_hash(2, [v for s in range(S) for v in (comm_c[s], comm_r_last[s])])
+        for q in range(Q):
+            levels[q].append(dict(zip(parents[q], hashed[o:o + len(parents[q])])))
+            o += len(parents[q])
+    comm_r_last = [levels[q][-1][0] for q in range(Q)]
+    comm_c = rand_many(Q)
+    comm_r = pos_hash(2, [v for q in range(Q) for v in (comm_c[q], comm_r_last[q])])
     sectors = []
     for s in range(S):
+        q = s % Q
         chs = []
         for idx in chal[s]:
             path, j = [], idx
             for lvl, a in enumerate(ar):
                 g = j // a
-                path.append([levels[s][lvl][g * a + k] for k in range(a) if k != j % a])
+                path.append([levels[q][lvl][g * a + k] for k in range(a) if k != j % a])
                 j = g
-            chs.append({"index": idx, "leaf": levels[s][0][idx], "siblings": path})
-        sectors.append({"id": ids[s], "comm_r": comm_r[s], "comm_c": comm_c[s], "comm_r_last": comm_r_last[s],
+            chs.append({"index": idx, "leaf": levels[q][0][idx], "siblings": path})
+        sectors.append({"id": ids[q], "comm_r": comm_r[q], "comm_c": comm_c[q], "comm_r_last": comm_r_last[q],
                         "challenges": chs})
     return randomness, sectors
+
+
+def synthetic_winning_post_instance(ctx, circuit: WinningPoStCircuit, seed: int = 1):
+    """A Winning-PoSt partition as generate_winning_post builds it (api/post.hpp:178-230): the post_config's
+    replica(s) (synthetic, sparse tree R-last) repeated over the circuit's param_sector_count sector slots,
+    slot i challenged at generate_leaf_challenge(randomness, id, i * challenges + n)."""
+    return synthetic_post_instance(ctx, circuit, seed, 0, replicas=getattr(circuit, "replicas", 1))
 
 
 def circuit_check_dev(ctx, circuit: Circuit, z_dev_ptr: int):

@@ -347,6 +347,12 @@ int mi_ctx_reset_stats(mi_ctx *ctx);
 /* work counters since the last reset: out[0] / out[1] = mixed additions (non-zero signed digits)
  * issued by the G1 / G2 bucket accumulation -- the unit of the VALU roofline */
 int mi_ctx_get_work(mi_ctx *ctx, uint64_t out[2]);
+/* memory fallbacks since the last reset: out[0] = proofs that hit an out-of-memory error and were re-run after
+ * their key's 2^128 split tables and the idle scratch were released (the retried proof takes the GLV split and
+ * is byte-identical; a second failure is returned as MI_ERR_INTERNAL), out[1] = bytes released for them.
+ * Replaces failing outright when several keys share one GPU, as GROTH_PARAM_MEMORY_CACHE keeps them
+ * (libs/filecoin/include/nil/filecoin/proofs/caches.hpp:48-116). */
+int mi_ctx_get_fallbacks(mi_ctx *ctx, uint64_t out[2]);
 /* msm window size chosen for n points (exposed for tests / reports) */
 unsigned mi_msm_window_bits(uint64_t n);
 

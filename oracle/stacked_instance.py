@@ -178,3 +178,44 @@ def post_public_inputs(inst):
         out.append(sec["comm_r"])
         out += [ch["index"] for ch in sec["challenges"]]
     return out
+
+
+def winning_post_setup_params(challenge_count=66, sector_count=1):
+    """proofs/parameters.hpp:58-68 (constants.hpp:54-55: 66 challenges, 1 sector) -> (param_sector_count,
+    param_challenge_count)"""
+    assert challenge_count % sector_count == 0, "sector count must divide challenge count"
+    ps = challenge_count // sector_count
+    pc = challenge_count // ps
+    assert ps * pc == challenge_count, "invalid parameters calculated"
+    return ps, pc
+
+
+def generate_winning_post(nodes, shape, seed=1, challenge_count=66, sector_count=1):
+    """A Winning-PoSt partition over fully built trees R-last, as generate_winning_post lays it out
+    (api/post.hpp:190-230): the sector_count replicas (random leaves, the (base, sub, top) Poseidon tree, random
+    comm_c) repeated over param_sector_count circuit sectors; circuit sector i, challenge n opens
+    generate_leaf_challenge(randomness, id, i * param_challenge_count + n) (prove_all_partitions,
+    vanilla.hpp:222-236, one partition)."""
+    ps, pc = winning_post_setup_params(challenge_count, sector_count)
+    rng = random.Random(seed)
+    fr = lambda: rng.randrange(R)
+    randomness = fr()
+    reps = []
+    for _ in range(sector_count):
+        sid = rng.randrange(2 ** 40)
+        leaves = [fr() for _ in range(nodes)]
+        rows, ar = build_tree(leaves, shape, lambda a, xs: poseidon(a, xs))
+        comm_c = fr()
+        reps.append((sid, leaves, rows, ar, comm_c))
+    sectors = []
+    for i in range(ps):
+        for sid, leaves, rows, ar, comm_c in reps:
+            k = len(sectors)
+            chs = []
+            for n in range(pc):
+                idx = generate_leaf_challenge(randomness, sid, k * pc + n, nodes)
+                chs.append({"index": idx, "leaf": leaves[idx], "siblings": siblings(rows, ar, idx)})
+            comm_r_last = rows[-1][0]
+            sectors.append({"id": sid, "comm_c": comm_c, "comm_r_last": comm_r_last,
+                            "comm_r": poseidon(2, [comm_c, comm_r_last]), "challenges": chs})
+    return {"randomness": randomness, "sectors": sectors, "nodes": nodes, "shape": shape}

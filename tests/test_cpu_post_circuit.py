@@ -113,3 +113,60 @@ def test_builder_refuses_bad_post_shapes():
     for args in [(0, 1, 64, 8, 0, 0), (1, 0, 64, 8, 0, 0), (1, 1, 48, 8, 0, 0), (1, 1, 64, 3, 0, 0)]:
         with pytest.raises(fg.FilGpuError):
             stacked.FallbackPoStCircuit(*args, with_r1cs=False)
+
+
+# ------------------------------------------------------------------------------------------ Winning PoSt
+def test_winning_post_setup_params():
+    """proofs/parameters.hpp:58-68: 66 challenges over 1 sector -> 66 circuit sectors x 1 challenge"""
+    import stacked_instance as si
+
+    for cc, sc, want in ((66, 1, (66, 1)), (66, 2, (33, 2)), (66, 66, (1, 66)), (10, 5, (2, 5))):
+        assert stacked.winning_post_setup_params(cc, sc) == want
+        assert si.winning_post_setup_params(cc, sc) == want
+    for cc, sc in ((66, 4), (66, 0), (0, 1)):
+        with pytest.raises(ValueError):
+            stacked.winning_post_setup_params(cc, sc)
+    assert (stacked.WINNING_POST_CHALLENGE_COUNT, stacked.WINNING_POST_SECTOR_COUNT) == (66, 1)
+    assert stacked.winning_post_sectors(["r"], 3) == ["r"] * 3
+    assert stacked.winning_post_sectors(["a", "b"], 2) == ["a", "b", "a", "b"]
+
+
+def test_builder_winning_post_32gib_shape():
+    """The 32 GiB Winning-PoSt circuit: 66 sectors x 1 challenge over 2^30-node 8-8-0 trees R-last.  Per
+    sector 1 + 311 + 1, per challenge 10 levels x (3 + 22 + 505) + 2: 66 x 5,615 = 370,590 constraints;
+    inputs ONE + 66 x (comm_r, challenge) = 133 (against 1 + 1 x 67 = 68 for the 1 x 66 shape)."""
+    import stacked_circuit as sc
+
+    c = stacked.WinningPoStCircuit(1 << 30, 8, 8, 0, with_r1cs=False)
+    assert (c.sectors, c.challenges) == (66, 1)
+    assert c.num_constraints == 370_590 == sc.post_constraints(66, 1, sc.tree_levels(1 << 30, (8, 8, 0)))
+    assert c.num_inputs == 133
+    assert c.info["poseidon_hashes"] == 66 * (1 + 10)
+    # the domain the prover takes: constraints + inputs rows -> 2^19
+    assert (c.num_constraints + c.num_inputs - 1).bit_length() == 19
+
+
+def test_builder_winning_post_r1cs_equals_oracle():
+    """The builder's Winning-PoSt R1CS equals the oracle's synthesis of generate_winning_post's layout, row for row;
+    the public inputs are every sector slot's comm_r (the one replica's) then its challenged leaf."""
+    import stacked_circuit as sc
+    import stacked_instance as si
+
+    inst = si.generate_winning_post(64, (8, 0, 0), seed=12)
+    assert len(inst["sectors"]) == 66 and all(len(s["challenges"]) == 1 for s in inst["sectors"])
+    assert len({s["comm_r"] for s in inst["sectors"]}) == 1
+    cs = sc.CS()
+    sc.fallback_post_circuit(cs, inst, (8, 0, 0))
+    assert cs.is_satisfied() is None
+    c = stacked.WinningPoStCircuit(64, 8, 0, 0)
+    assert (c.num_constraints, c.num_inputs, c.num_aux) == (cs.n_constraints, len(cs.inputs), len(cs.aux))
+    mats, ocsr = c.csr(), cs.to_csr()
+    for m in range(3):
+        rp, col, co = mats[m]
+        orp, ocol, oco = ocsr[m]
+        assert np.array_equal(rp, np.asarray(orp, dtype=np.uint64)), m
+        assert np.array_equal(col, np.asarray(ocol, dtype=np.uint32)), m
+        assert co.tobytes() == b"".join(int(k).to_bytes(32, "little") for k in oco), m
+    slots = stacked.post_slots(c, inst["sectors"])
+    assert c.public_inputs(slots) == b"".join(v.to_bytes(32, "little") for v in cs.inputs[1:])
+    assert cs.inputs[1:] == si.post_public_inputs(inst)

@@ -200,3 +200,54 @@ def test_srs_stream_load_chunks_host_and_device(ctx, oracle):
         st.part(q, 0, bytes(data), counts[q])
     with pytest.raises(fg.FilGpuError, match="subgroup"):
         st.end()
+
+
+# The reference's Fr32 canonicality edge (libs/storage/test/core/fr32.cpp:51-86, bytes_into_fr accept /
+# refuse) and the api tripwire (libs/filecoin/test/api/mod.cpp:35-44: all-zero converts, all-0xFF does not),
+# as 32-byte little-endian encodings with the reference's expected verdict.
+FR32_VECTORS = [
+    ("fr32.cpp:52 bytes 0..31", bytes(range(32)), True),
+    ("fr32.cpp:58 ff..ff,115", b"\xff" * 31 + bytes([115]), False),
+    ("fr32.cpp:65 ff..ff,114", b"\xff" * 31 + bytes([114]), True),
+    ("fr32.cpp:72 ff..ff,236,115", b"\xff" * 30 + bytes([236, 115]), True),
+    ("fr32.cpp:79 ff..ff,237,115", b"\xff" * 30 + bytes([237, 115]), False),
+    ("mod.cpp:36 all zero", bytes(32), True),
+    ("mod.cpp:41 all 0xff", b"\xff" * 32, False),
+]
+
+
+@pytest.mark.parametrize("name,enc,ok", FR32_VECTORS, ids=[v[0] for v in FR32_VECTORS])
+def test_fr32_reference_vectors_through_the_c_abi(ctx, case, name, enc, ok):
+    """Each vector as a witness entry (host and device witness, prove_batch, prove_share) and as an instance
+    slot of the library-built PoSt circuit (mi_stacked_public_inputs, mi_stacked_witness, _dev): accepted
+    exactly when the reference accepts it, refused with MI_ERR_ARG ("canonical") otherwise."""
+    from fil_groth16 import stacked
+
+    assert (int.from_bytes(enc, "little") < R) == ok
+    gc, pk, z = case["gc"], case["pk"], case["z"]
+    good = circuits.z_bytes(z)
+    zb = bytearray(good)
+    zb[32:64] = enc  # input 1
+    zb = bytes(zb)
+    calls = [lambda: fg.prove(ctx, pk, gc, zb, 1, 2),
+             lambda: fg.prove(ctx, pk, gc, _dev(zb).data_ptr(), 1, 2),
+             lambda: fg.prove_batch(ctx, pk, gc, [good, zb], [(1, 2), (3, 4)]),
+             lambda: fg.prove_share(ctx, pk, gc, zb, 0, 2),
+             lambda: fg.prove_share(ctx, pk, gc, _dev(zb).data_ptr(), 1, 2)]
+    pc = stacked.FallbackPoStCircuit(1, 1, 64, 8, 0, 0, with_r1cs=False)
+    import stacked_instance as si
+
+    slots = bytearray(stacked.post_slots(pc, si.generate_post(1, 1, 64, (8, 0, 0), seed=2)["sectors"]))
+    slots[32 * 1:32 * 2] = enc  # comm_c of the sector (a free field element of the instance)
+    slots = bytes(slots)
+    zdev = _dev(bytes(32 * pc.num_vars))
+    calls += [lambda: pc.public_inputs(slots), lambda: pc.witness(ctx, slots),
+              lambda: pc.witness_dev(ctx, _dev(slots).data_ptr(), zdev.data_ptr())]
+    for i, call in enumerate(calls):
+        if ok:
+            call()
+        else:
+            with pytest.raises(fg.FilGpuError, match="canonical") as e:
+                call()
+            assert e.value.code == MI_ERR_ARG, i
+    assert fg.prove(ctx, pk, gc, good, 1, 2) == case["op"].prove(good, 1, 2)[0]

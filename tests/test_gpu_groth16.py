@@ -132,6 +132,40 @@ def test_groth16_split_msm_vs_oracle(ctx, oracle, monkeypatch, split):
     assert fg.assemble(vk, shares, r, s) == op.prove(zb, r, s)[0]
 
 
+def test_prove_out_of_memory_degrades_to_glv(ctx, oracle, monkeypatch):
+    """A proof whose scratch allocation fails (MI_INJECT_PROVE_OOM: the main lane raises hipMalloc's
+    out-of-memory error after the NTT chain while the auxiliary lane runs) is re-run in-process after the key's
+    2^128 split tables are released: the bytes equal the oracle's, the key reports no tables afterwards, and
+    the context counts the retry.  Every prove entry (host / device witness, batch, share) recovers alike."""
+    monkeypatch.setenv("MI_MSM_SPLIT", "2")  # split mode at this size, so the tables are in use
+    n_in, n_aux, rws, z = circuits.random_circuit(36, 5000, n_in=6, n_free=32)
+    oc, gc = _load(ctx, oracle, n_in, n_aux, rws, z)
+    tox = circuits.toxic(36)
+    pk = fg.generate_random_parameters(ctx, gc, tox)
+    assert pk.msm_info() == {"split_tables": True, "subgroup": True}
+    op = oracle.OracleParams(oc, tox)
+    zb = circuits.z_bytes(z)
+    want = [op.prove(zb, 10 + k, 20 + k)[0] for k in range(3)]
+    assert fg.prove(ctx, pk, gc, zb, 10, 20) == want[0]
+    ctx.reset_stats()
+    monkeypatch.setenv("MI_INJECT_PROVE_OOM", "1")
+    assert fg.prove(ctx, pk, gc, zb, 10, 20) == want[0]
+    fb = ctx.fallbacks()
+    assert fb["oom_retries"] == 1 and fb["freed_bytes"] > 0
+    assert pk.msm_info() == {"split_tables": False, "subgroup": True}
+    import torch
+
+    zd = torch.from_numpy(np.frombuffer(zb, dtype=np.uint8).copy()).cuda()
+    assert fg.prove(ctx, pk, gc, zd.data_ptr(), 11, 21) == want[1]
+    assert fg.prove_batch(ctx, pk, gc, [zb, zb], [(10, 20), (12, 22)]) == [want[0], want[2]]
+    vk, _ = pk.verifying_key()
+    assert fg.assemble(vk, [fg.prove_share(ctx, pk, gc, zb, k, 2) for k in range(2)], 10, 20) == want[0]
+    assert ctx.fallbacks()["oom_retries"] == 6
+    monkeypatch.delenv("MI_INJECT_PROVE_OOM")
+    ctx.reset_stats()
+    assert fg.prove(ctx, pk, gc, zb, 12, 22) == want[2] and ctx.fallbacks()["oom_retries"] == 0
+
+
 def test_prove_batch_and_priority(ctx, oracle):
     n_in, n_aux, rws, z = circuits.random_circuit(41, 300)
     oc, gc = _load(ctx, oracle, n_in, n_aux, rws, z)

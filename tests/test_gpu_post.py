@@ -119,3 +119,61 @@ def test_post_32gib_window_partition_prove_verify(ctx):
     assert fg.verify(vk, ic, pub, proof)
     del pk, gc, z
     torch.cuda.synchronize()
+
+
+# ------------------------------------------------------------------------------------------ Winning PoSt
+def test_winning_post_small_witness_prove_verify(ctx, oracle):
+    """Winning PoSt at the reference's shape (parameters.hpp:58-68: 66 sectors x 1 challenge, the one replica
+    repeated as api/post.hpp:205-218 does) over a 64-node tree: GPU witness == oracle synthesis, satisfied on
+    the device, proven and pairing-verified through generate_winning_post_proof."""
+    import circuits
+    import stacked_instance as si
+
+    from fil_groth16.compound import generate_winning_post_proof
+
+    shape = (8, 0, 0)
+    c = stacked.WinningPoStCircuit(64, *shape)
+    inst = si.generate_winning_post(64, shape, seed=12)
+    slots = stacked.post_slots(c, inst["sectors"])
+    got = c.witness(ctx, slots)
+    assert got == _oracle_z(inst, shape)
+    pub = c.public_inputs(slots)
+    assert got[32:32 * c.num_inputs] == pub
+    gc = c.load(ctx)
+    zd = torch.from_numpy(np.frombuffer(got, dtype=np.uint8).copy()).cuda()
+    assert stacked.circuit_check_dev(ctx, gc, zd.data_ptr()) == (0, None)
+    pk = fg.generate_random_parameters(ctx, gc, circuits.toxic())
+    vk, ic = pk.verifying_key()
+    proof = generate_winning_post_proof(ctx, pk, gc, 1, 1, got)
+    assert len(proof) == 192 and fg.verify(vk, ic, pub, proof)
+    assert fg.prove(ctx, pk, gc, zd.data_ptr(), 5, 6) == oracle.OracleParams(
+        oracle.OracleCircuit(c.num_constraints, c.num_inputs, c.num_aux, c.csr()), circuits.toxic()).prove(got, 5, 6)[0]
+
+
+def test_winning_post_32gib_prove_verify(ctx, oracle):
+    """The 32 GiB Winning-PoSt partition (66 x 1 over a 2^30-node 8-8-0 tree R-last: 370,590 constraints,
+    133 inputs, domain 2^19) from the synthetic generator: the GPU witness equals the oracle's synthesis over
+    the same openings, satisfies every row on the device, and the proof pairing-verifies."""
+    import circuits
+
+    shape, nodes = (8, 8, 0), 1 << 30
+    c = stacked.WinningPoStCircuit(nodes, *shape)
+    assert (c.num_constraints, c.num_inputs) == (370_590, 133)
+    _, sectors = stacked.synthetic_winning_post_instance(ctx, c, seed=13)
+    assert len({s["comm_r"] for s in sectors}) == 1
+    slots = stacked.post_slots(c, sectors)
+    sd = torch.from_numpy(np.frombuffer(slots, dtype=np.uint8).copy()).cuda()
+    z = torch.empty(32 * c.num_vars, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    c.witness_dev(ctx, sd.data_ptr(), z.data_ptr())
+    gc = c.load(ctx)
+    assert gc.d == 1 << 19
+    assert stacked.circuit_check_dev(ctx, gc, z.data_ptr()) == (0, None)
+    inst = {"sectors": sectors, "nodes": nodes, "shape": shape}
+    assert z.cpu().numpy().tobytes() == _oracle_z(inst, shape)
+    pub = c.public_inputs(slots)
+    pk = fg.generate_random_parameters(ctx, gc, circuits.toxic())
+    vk, ic = pk.verifying_key()
+    proof = fg.prove(ctx, pk, gc, z.data_ptr())
+    assert fg.verify(vk, ic, pub, proof)
+    assert not fg.verify(vk, ic, pub[:-32] + bytes(32), proof)
