@@ -486,7 +486,8 @@ def window_post_leg(args, fg, ctx, device, rank, world, gdev, dist):
 
     from fil_groth16 import stacked
     from fil_groth16.compound import shard_partitions
-    from fil_groth16.distributed import balanced_schedule, prove_partitions, prove_partitions_balanced
+    from fil_groth16.distributed import (agree_float, balanced_schedule, calibrate_lead_share, latency_ranges,
+                                         lead_share_from_times, prove_partitions, prove_partitions_balanced)
 
     S, C, nodes = args.post_sectors, args.post_challenges, 1 << args.post_log_nodes
     try:
@@ -536,13 +537,31 @@ def window_post_leg(args, fg, ctx, device, rank, world, gdev, dist):
 
     vk, ic = pk.verifying_key()
 
+    # latency-mode groups compute H once (MI_C5_LATENCY=h_once, default): the group's lead rank runs the witness
+    # map, the NTT chain and the whole H MSM plus a calibrated fraction of L, A, B; the others split the rest
+    # (distributed.latency_ranges).  MI_C5_LATENCY=slices: every rank repeats H and takes equal slices.
+    latency = os.environ.get("MI_C5_LATENCY", "h_once")
+    sizes = (pk.n_h, pk.n_l, pk.n_a, pk.n_b)
+    calib = {}
+
     def share_fn(p, k, g):
         pc.witness_dev(ctx, sdev[p].data_ptr(), z.data_ptr())
-        return fg.prove_share(ctx, pk, circ, z.data_ptr(), k, g)
+        if latency == "slices":
+            return fg.prove_share(ctx, pk, circ, z.data_ptr(), k, g)
+        rg = latency_ranges(sizes, g, lead_share_from_times(calib["t_h_ms"], calib["t_lab_ms"], g))
+        return fg.prove_share_ranges(ctx, pk, circ, z.data_ptr(), rg[k])
 
     def assemble_fn(p, shares):  # the same blinding on every rank of the group
         return fg.assemble(vk, shares, *splitmix_frs(9500 + p, 2))
 
+    if latency != "slices" and (tail or (world == 1 and args.post_share_groups)):
+        # one GPU's times of the two halves of a proof (H part; L, A, B part), rank 0's agreed by every rank
+        if mine:
+            pc.witness_dev(ctx, sdev[mine[0]].data_ptr(), z.data_ptr())
+            _, t = calibrate_lead_share(ctx, pk, circ, z.data_ptr(), 2)
+        else:
+            t = {"t_h_ms": 0.0, "t_lab_ms": 0.0}
+        calib = {k: agree_float(v, rank, gdev) if dist else v for k, v in t.items()}
     if mine:  # warm-up (program upload, plans)
         pc.witness_dev(ctx, sdev[mine[0]].data_ptr(), z.data_ptr())
         if whole[rank]:
@@ -590,7 +609,10 @@ def window_post_leg(args, fg, ctx, device, rank, world, gdev, dist):
                 ctx.synchronize()
                 ts.append(time.perf_counter() - t2)
             shares_res[str(g)] = {"share_ms": [1e3 * x for x in ts], "slowest_ms": 1e3 * max(ts),
-                                  "assembled_equals_whole_proof": fg.assemble(vk, shs, *rs0) == ref}
+                                  "assembled_equals_whole_proof": fg.assemble(vk, shs, *rs0) == ref,
+                                  "mode": latency}
+            if latency != "slices":
+                shares_res[str(g)]["lead_share"] = lead_share_from_times(calib["t_h_ms"], calib["t_lab_ms"], g)
     if dist:
         tt = torch.tensor([dt], dtype=torch.float64, device=gdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -618,16 +640,23 @@ def window_post_leg(args, fg, ctx, device, rank, world, gdev, dist):
         if shares_res:
             tp1 = 1e3 * mine_dt / steps / max(1, len(mine))
             out["latency_mode_shares"] = shares_res
+            if calib:
+                out["latency_mode_calibration_ms"] = calib
             out["config5_projection"] = {
                 "note": "projected from this GPU's times (witness + share per rank, ranks independent): 10 "
                         "partitions; balanced = P - P % W whole partitions round-robin, then each of the P % W "
-                        "tail partitions over W / (P % W) GPUs in latency mode",
+                        "tail partitions over W / (P % W) GPUs in latency mode (" + latency + ": " +
+                        ("the group's lead rank alone computes H" if latency != "slices" else
+                         "every rank repeats H, equal slices") + ")",
                 "w8_roundrobin_makespan_ms": 2 * tp1,
                 "w8_balanced_makespan_ms": tp1 + shares_res["4"]["slowest_ms"] if "4" in shares_res else None,
                 "w4_roundrobin_makespan_ms": 3 * tp1,
                 "w4_balanced_makespan_ms": 2 * tp1 + shares_res["2"]["slowest_ms"] if "2" in shares_res else None}
         if world > 1:
             out["schedule"] = schedule
+            out["latency_mode"] = latency if tail else None
+            if calib:
+                out["latency_mode_calibration_ms"] = calib
             out["per_rank_partitions"] = [len(w) for w in whole]
             out["split_partitions"] = [{"partition": p, "ranks": rs} for p, rs in tail]
     del pk, circ, z, sdev, pc

@@ -845,6 +845,42 @@ int mi_groth16_prove_share_dev(mi_ctx *ctx, const mi_srs *srs, const mi_circuit 
     });
 }
 
+static mi::SumRanges ranges_of(const uint64_t r[8]) {
+    mi::SumRanges g;
+    for (int q = 0; q < 4; q++) {
+        g.lo[q] = r[2 * q];
+        g.cnt[q] = r[2 * q + 1];
+    }
+    return g;
+}
+
+int mi_groth16_prove_share_ranges(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circ, const uint8_t *z,
+                                  const uint64_t ranges[8], int priority, uint8_t *share) {
+    return guard([&] {
+        need(ctx && srs && circ && z && ranges && share, "null argument");
+        CtxLock l(ctx, priority);
+        uint64_t nv = circ->p->n_in + circ->p->n_aux;
+        mi::fr_t *zd = witness_upload(ctx, 0, z, nv);
+        witness_ready(ctx, 0, nv);
+        mi::sums_encode(mi::groth16_sums_ranges(ctx->c, *srs->p, *circ->p, zd, ranges_of(ranges)), share);
+    });
+}
+
+int mi_groth16_prove_share_ranges_dev(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circ, const void *z_dev,
+                                      const uint64_t ranges[8], int priority, uint8_t *share) {
+    return guard([&] {
+        need(ctx && srs && circ && z_dev && ranges && share, "null argument");
+        CtxLock l(ctx, priority);
+        uint64_t nv = circ->p->n_in + circ->p->n_aux;
+        DevWitnessCheck chk(ctx, (const mi::fr_t *)z_dev, nv);
+        uint8_t sh[MI_SHARE_BYTES];
+        mi::sums_encode(mi::groth16_sums_ranges(ctx->c, *srs->p, *circ->p, (const mi::fr_t *)z_dev, ranges_of(ranges)),
+                        sh);
+        chk.verdict(nv);
+        memcpy(share, sh, MI_SHARE_BYTES);
+    });
+}
+
 int mi_groth16_assemble(const uint8_t *vk, const uint8_t *shares, uint64_t count, const uint8_t r[32],
                         const uint8_t s[32], uint8_t *proof, uint8_t *raw) {
     return guard([&] {

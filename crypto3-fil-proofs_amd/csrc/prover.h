@@ -132,12 +132,27 @@ struct AssemblyKey {
 // z_dev: (n_in + n_aux) canonical Fr on the device (z[0] must be ONE).  r, s canonical.
 ProofPoints groth16_prove(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, const fr_t &r,
                           const fr_t &s);
-// rank's share of the MSMs (rank < world); the witness map and NTT chain run in full on every rank
+// rank's share of the MSMs (rank < world): the contiguous slice [n k / W, n (k + 1) / W) of every query; the
+// witness map and NTT chain run in full on every rank whose H slice is not empty
 ProofSums groth16_sums(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, unsigned rank = 0,
                        unsigned world = 1);
+// The MSM sums over explicit ranges [lo, lo + cnt) of the queries 0 H (d - 1 points, the key's bit-reversed h
+// order), 1 L (aux variables), 2 A (a query), 3 B (b query: B_G1 and B_G2 over the same range).  Any set of
+// ranges that partitions every query gives shares that add up to the whole proof's sums.  The witness map and
+// the NTT chain run only when the H range is not empty, so a latency-mode group can compute H on one rank and
+// spread L, A and B over the others (fil_groth16.distributed.latency_ranges).
+struct SumRanges {
+    uint64_t lo[4] = {0, 0, 0, 0}, cnt[4] = {0, 0, 0, 0};
+};
+ProofSums groth16_sums_ranges(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, const SumRanges &rg);
+SumRanges share_ranges(const Circuit &circ, unsigned rank, unsigned world);
 // releases the 2^128 split tables of a key (its G1 MSMs then take the GLV split); returns the bytes freed.  The
 // caller holds the key exclusively (use_mu) or owns it outright.
 uint64_t srs_drop_split_tables(Srs &S);
+// After an out-of-memory error: drain the context's lanes, then release the split tables of every key on its
+// device that no one is using (`first` before the others; may be null) and the context's idle scratch, except a
+// buffer holding `keep`.  Returns the bytes freed.
+uint64_t release_for_retry(Ctx &c, const Srs *first, const void *keep);
 // A = alpha + A_sum + r delta, B = beta + B2_sum + s delta, C = H + L + s A + r B1 - r s delta (host)
 ProofPoints groth16_assemble(const AssemblyKey &k, const ProofSums &sums, const fr_t &r, const fr_t &s);
 AssemblyKey assembly_key(const Srs &srs);

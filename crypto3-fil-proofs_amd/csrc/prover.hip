@@ -844,16 +844,32 @@ void srs_stream_abort(SrsStream *st) {
     delete st;
 }
 
-Srs *srs_load(Ctx &c, const Circuit *circ, const SrsHost &h, bool checked) {
+namespace {
+Srs *srs_load_once(Ctx &c, const Circuit *circ, const SrsHost &h, bool checked) {
     SrsStream *st = srs_stream_begin(c, circ, h, checked);
     const uint8_t *q[5] = {h.h, h.l, h.a, h.b_g1, h.b_g2};
     try {
         for (int k = 0; k < 5; k++) srs_stream_part(c, *st, k, 0, q[k], st->n[k], false);
     } catch (...) {
+        (void)hipStreamSynchronize(c.stream);
         srs_stream_abort(st);
         throw;
     }
     return srs_stream_end(c, st);
+}
+}  // namespace
+
+// a load out of memory releases the other keys' split tables and the idle scratch and loads once more
+// (srs_generate's rule)
+Srs *srs_load(Ctx &c, const Circuit *circ, const SrsHost &h, bool checked) {
+    try {
+        return srs_load_once(c, circ, h, checked);
+    } catch (const hip_error &e) {
+        if (e.code != hipErrorOutOfMemory) throw;
+        c.stats.oom_retries += 1;
+        c.stats.oom_freed_bytes += release_for_retry(c, nullptr, nullptr);
+        return srs_load_once(c, circ, h, checked);
+    }
 }
 
 uint64_t circuit_check(Ctx &c, const Circuit &C, const fr_t *z_dev, uint64_t *first_bad) {
@@ -931,17 +947,43 @@ void build_hi_tables(Ctx &c, Srs &S) {
         const uint64_t work = 32 * (S.n_l + 3 * S.d) + 2 * 360 * big;
         if (need + work + work / 10 + (8ull << 30) > free_b) return;  // the MSMs take the GLV split instead
     }
-    for (auto &q : qs) {
-        if (!q.src || !q.n) continue;
-        *q.dst = dalloc<g1_affine_t>(q.n);
-        g1_shift128(c, q.src, q.n, *q.dst);
+    // the tables are an optimisation: if one cannot be allocated (the free-memory estimate was wrong, or memory
+    // is fragmented), the key keeps none and its MSMs take the GLV split
+    try {
+        for (auto &q : qs) {
+            if (!q.src || !q.n) continue;
+            *q.dst = dalloc<g1_affine_t>(q.n);
+            g1_shift128(c, q.src, q.n, *q.dst);
+        }
+    } catch (const hip_error &e) {
+        if (e.code != hipErrorOutOfMemory) throw;
+        (void)hipStreamSynchronize(c.stream);
+        (void)hipGetLastError();
+        srs_drop_split_tables(S);
     }
 }
 }  // namespace
 
-Srs *srs_generate(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5]) {
+namespace {
+// a device temporary freed on every path (keygen retries after an out-of-memory error must not leak)
+struct DevTemp {
+    void *p = nullptr;
+    template <class T>
+    T *alloc(uint64_t count) {
+        p = dalloc<T>(count);
+        return (T *)p;
+    }
+    void reset() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+    }
+    ~DevTemp() { reset(); }
+};
+
+Srs *srs_generate_once(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5]) {
     Srs *S = new Srs(c.device);
     hipStream_t st = c.stream;
+    DevTemp pw_t, ks_t, t1_t, t2_t;
     try {
         const uint64_t d = circ.d, n = circ.n, nv = circ.n_in + circ.n_aux;
         const unsigned L = circ.log_d;
@@ -963,13 +1005,13 @@ Srs *srs_generate(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5]) {
         fr_t *dlo = c.scratch[12].as<fr_t>(65536 * 2), *dhi = dlo + 65536;
         MI_HIP(hipMemcpyAsync(dlo, lo.data(), 32 * 65536, hipMemcpyHostToDevice, st));
         MI_HIP(hipMemcpyAsync(dhi, hi.data(), 32 * 65536, hipMemcpyHostToDevice, st));
-        fr_t *pw = dalloc<fr_t>(d);
+        fr_t *pw = pw_t.alloc<fr_t>(d);
         k_powers<<<grid1(d), 256, 0, st>>>(dlo, dhi, d, pw);
         fr_t tau_d = pow_u64(tau, d);
         fr_t t_tau = tau_d - fr_t::one();
         fr_t delta_inv = inverse(delta), gamma_inv = inverse(gamma);
         // h query scalars (bit-reversed order) -> points
-        fr_t *ks = dalloc<fr_t>(nv > d ? nv : d);
+        fr_t *ks = ks_t.alloc<fr_t>(nv > d ? nv : d);
         k_h_scalars<<<grid1(d - 1), 256, 0, st>>>(pw, L, d - 1, t_tau * delta_inv, ks);
         // Lagrange coefficients L_j(tau) = ifft(powers)
         ntt_dif(c, pw, L, true);
@@ -1007,8 +1049,8 @@ Srs *srs_generate(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5]) {
             g1_decode_host(g1b, g1);
             g2_decode_host(g2b, g2);
         }
-        g1_affine_t *t1 = dalloc<g1_affine_t>(32 * 255);
-        g2_affine_t *t2 = dalloc<g2_affine_t>(32 * 255);
+        g1_affine_t *t1 = t1_t.alloc<g1_affine_t>(32 * 255);
+        g2_affine_t *t2 = t2_t.alloc<g2_affine_t>(32 * 255);
         k_fb_table<fq_t><<<grid1(32 * 255), 256, 0, st>>>(g1, t1);
         k_fb_table<fq2_t><<<grid1(32 * 255), 256, 0, st>>>(g2, t2);
         MI_HIP(hipGetLastError());
@@ -1085,10 +1127,10 @@ Srs *srs_generate(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5]) {
             fixed_base_affine<fq2_t>(c, t2, ks, circ.n_b, S->b_g2);
         }
         MI_HIP(hipStreamSynchronize(st));
-        hipFree(ks);
-        hipFree(pw);
-        hipFree(t1);
-        hipFree(t2);
+        ks_t.reset();
+        pw_t.reset();
+        t1_t.reset();
+        t2_t.reset();
         // the column sums' sort and reduce-by-key buffers scale with the R1CS entries (tens of GB for a
         // 32 GiB partition): key generation is one-time, so give them back before the table decision and
         // the first proof
@@ -1104,30 +1146,45 @@ Srs *srs_generate(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5]) {
         S->delta_g2 = host_mul_affine(g2, toxic_canonical[4]);
         build_hi_tables(c, *S);
     } catch (...) {
+        (void)hipStreamSynchronize(st);  // no kernel may still write the buffers freed below
         delete S;
         throw;
     }
     return S;
+}
+}  // namespace
+
+// Key generation out of memory (several keys resident, earlier proofs' scratch): release the split tables of the
+// keys on this device that no one is using and this context's idle scratch, and generate once more.
+Srs *srs_generate(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5]) {
+    try {
+        return srs_generate_once(c, circ, toxic_canonical);
+    } catch (const hip_error &e) {
+        if (e.code != hipErrorOutOfMemory) throw;
+        c.stats.oom_retries += 1;
+        c.stats.oom_freed_bytes += release_for_retry(c, nullptr, nullptr);
+        return srs_generate_once(c, circ, toxic_canonical);
+    }
 }
 
 // ================================================================================ prove
 namespace {
 // One attempt at a proof's MSM sums.  inject_oom (tests, MI_INJECT_PROVE_OOM): the main lane throws the
 // out-of-memory error a scratch hipMalloc would, after the NTT chain, while the auxiliary lane runs.
-ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, unsigned rank,
-                            unsigned world, bool inject_oom) {
+ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, const SumRanges &rg,
+                            bool inject_oom) {
     std::shared_lock<std::shared_mutex> in_use(srs.use_mu);
     if (srs.d != circ.d || srs.n_l != circ.n_aux || srs.n_a != circ.n_a || srs.n_b != circ.n_b)
         throw std::invalid_argument("SRS does not match circuit");
-    if (world == 0 || rank >= world) throw std::invalid_argument("share rank out of range");
+    const uint64_t totals[4] = {circ.d - 1, circ.n_aux, circ.n_a, circ.n_b};
+    for (int q = 0; q < 4; q++)
+        if (rg.lo[q] > totals[q] || rg.cnt[q] > totals[q] - rg.lo[q])
+            throw std::invalid_argument("MSM range past the end of its query");
     hipStream_t st = c.stream;
     const uint64_t d = circ.d, nv = circ.n_in + circ.n_aux;
     const unsigned L = circ.log_d;
-    // this rank's contiguous slice [lo, lo + cnt) of a query of n points
-    auto slice = [&](uint64_t n, uint64_t &lo) {
-        lo = n * rank / world;
-        return n * (rank + 1) / world - lo;
-    };
+    // the witness map and the NTT chain run only when this share holds part of the H MSM
+    const bool need_h = rg.cnt[0] > 0;
     ProofSums out;
     g1_xyzz_t &H = out.H, &Lq = out.L, &As = out.A, &B1 = out.B1;
     g2_xyzz_t &B2 = out.B2;
@@ -1152,7 +1209,7 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
                 MI_HIP(hipSetDevice(c.device));
                 // B_G1 and B_G2 share the scalars (z over the B-density): sort them once
                 auto run_b = [&] {
-                    uint64_t lo, cnt = slice(circ.n_b, lo);
+                    const uint64_t lo = rg.lo[3], cnt = rg.cnt[3];
                     MsmPlan pb;
                     msm_prepare(x, z_dev, circ.idx_b + lo, cnt, pb);
                     msm_g1_planned(x, pb, srs.b_g1 + lo, &B1);
@@ -1165,7 +1222,7 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
                     return !(e && strcmp(e, "l_first") == 0);
                 }();
                 if (b_first) run_b();
-                uint64_t l_lo, l_cnt = slice(circ.n_aux, l_lo);
+                const uint64_t l_lo = rg.lo[1], l_cnt = rg.cnt[1];
                 msm_g1(x, srs.l + l_lo, z_dev + circ.n_in + l_lo, nullptr, l_cnt, &Lq,
                        srs.l_hi ? srs.l_hi + l_lo : nullptr, srs.in_subgroup);
                 if (!b_first) run_b();
@@ -1178,8 +1235,11 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
         if (!one_lane) lane = std::thread(aux_work);
         std::exception_ptr err_main;
         try {
+            fr_t *a = nullptr;
+            if (need_h) {
             fr_t *zm = c.scratch[20].as<fr_t>(nv + 3 * d);
-            fr_t *a = zm + nv, *b = a + d, *cc = b + d;
+            a = zm + nv;
+            fr_t *b = a + d, *cc = b + d;
             k_copy_to_mont<<<grid1(nv), 256, 0, st>>>(z_dev, zm, nv);
             eval_witness_map(c, circ, zm, a, b, cc);
             fr_t dd = fr_t::zero();
@@ -1202,11 +1262,15 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
                 k_qap_divide<<<grid1(d), 256, 0, st>>>(a, b, cc, d, zinv);
                 ntt_dif_coset_epilogue(c, a, L, true, true, dinv, true);  // icoset, canonical H (bit-reversed)
             }
+            }
             if (inject_oom)
                 throw hip_error(hipErrorOutOfMemory, "hipMalloc failed: out of memory (injected, MI_INJECT_PROVE_OOM)");
-            uint64_t h_lo, h_cnt = slice(d - 1, h_lo), a_lo, a_cnt = slice(circ.n_a, a_lo);
-            msm_g1(c, srs.h_perm + h_lo, a + h_lo, nullptr, h_cnt, &H, srs.h_hi ? srs.h_hi + h_lo : nullptr,
-                   srs.in_subgroup);
+            const uint64_t h_lo = rg.lo[0], h_cnt = rg.cnt[0], a_lo = rg.lo[2], a_cnt = rg.cnt[2];
+            if (need_h)
+                msm_g1(c, srs.h_perm + h_lo, a + h_lo, nullptr, h_cnt, &H, srs.h_hi ? srs.h_hi + h_lo : nullptr,
+                       srs.in_subgroup);
+            else
+                H = g1_xyzz_t::inf();
             msm_g1(c, srs.a + a_lo, z_dev, circ.idx_a + a_lo, a_cnt, &As, srs.a_hi ? srs.a_hi + a_lo : nullptr,
                    srs.in_subgroup);
         } catch (...) {
@@ -1253,11 +1317,11 @@ uint64_t srs_drop_split_tables(Srs &S) {
 
 namespace {
 // the split tables of every key on `device` that no one is using right now, the proving key first
-uint64_t release_device_tables(int device, const Srs &first) {
+uint64_t release_device_tables(int device, const Srs *first) {
     std::lock_guard<std::mutex> lk(g_keys_mu);
     std::vector<Srs *> order;
     for (Srs *k : g_keys)
-        if (k == &first) order.insert(order.begin(), k);
+        if (k == first) order.insert(order.begin(), k);
         else if (k->device == device) order.push_back(k);
     uint64_t freed = 0;
     for (Srs *k : order) {
@@ -1288,6 +1352,13 @@ uint64_t release_prover_scratch(Ctx &c, const void *keep) {
 }
 }  // namespace
 
+uint64_t release_for_retry(Ctx &c, const Srs *first, const void *keep) {
+    (void)hipStreamSynchronize(c.stream);
+    if (c.aux) (void)hipStreamSynchronize(c.aux->stream);
+    (void)hipGetLastError();  // the failed allocation's error, so the retry's launch checks start clean
+    return release_device_tables(c.device, first) + release_prover_scratch(c, keep);
+}
+
 // A proof whose working set does not fit next to the resident keys degrades instead of failing: on an
 // out-of-memory error the attempt is drained, the 2^128 split tables of the keys on this device (the proving
 // key's first, then every other key no one is using: several keys stay resident side by side, as the
@@ -1295,22 +1366,32 @@ uint64_t release_prover_scratch(Ctx &c, const void *keep) {
 // released, and the proof runs again; its G1 MSMs take the GLV split, which needs no table (glv.h).  The MSM
 // sums are unique group elements, so the retried proof is byte-identical.  A second out-of-memory error
 // propagates.
-ProofSums groth16_sums(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, unsigned rank,
-                       unsigned world) {
+ProofSums groth16_sums_ranges(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, const SumRanges &rg) {
     const bool inject = getenv("MI_INJECT_PROVE_OOM") != nullptr;
     try {
-        return groth16_sums_once(c, srs, circ, z_dev, rank, world, inject);
+        return groth16_sums_once(c, srs, circ, z_dev, rg, inject);
     } catch (const hip_error &e) {
         if (e.code != hipErrorOutOfMemory) throw;
-        (void)hipStreamSynchronize(c.stream);
-        if (c.aux) (void)hipStreamSynchronize(c.aux->stream);
-        (void)hipGetLastError();  // the failed allocation's error, so the retry's launch checks start clean
-        uint64_t freed = release_device_tables(c.device, srs);
-        freed += release_prover_scratch(c, z_dev);
         c.stats.oom_retries += 1;
-        c.stats.oom_freed_bytes += freed;
-        return groth16_sums_once(c, srs, circ, z_dev, rank, world, false);
+        c.stats.oom_freed_bytes += release_for_retry(c, &srs, z_dev);
+        return groth16_sums_once(c, srs, circ, z_dev, rg, false);
     }
+}
+
+SumRanges share_ranges(const Circuit &circ, unsigned rank, unsigned world) {
+    if (world == 0 || rank >= world) throw std::invalid_argument("share rank out of range");
+    const uint64_t totals[4] = {circ.d - 1, circ.n_aux, circ.n_a, circ.n_b};
+    SumRanges r;
+    for (int q = 0; q < 4; q++) {  // rank's contiguous slice [n k / W, n (k + 1) / W) of every query
+        r.lo[q] = totals[q] * rank / world;
+        r.cnt[q] = totals[q] * (rank + 1) / world - r.lo[q];
+    }
+    return r;
+}
+
+ProofSums groth16_sums(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, unsigned rank,
+                       unsigned world) {
+    return groth16_sums_ranges(c, srs, circ, z_dev, share_ranges(circ, rank, world));
 }
 
 AssemblyKey assembly_key(const Srs &srs) {

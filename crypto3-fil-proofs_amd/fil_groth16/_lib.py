@@ -23,6 +23,7 @@ EXPORTS = [
     "mi_params_inspect", "mi_params_load", "mi_params_write", "mi_vk_write",
     "mi_groth16_verify", "mi_groth16_verify_batch", "mi_pairing",
     "mi_groth16_prove_share", "mi_groth16_prove_share_dev", "mi_groth16_assemble",
+    "mi_groth16_prove_share_ranges", "mi_groth16_prove_share_ranges_dev",
     "mi_host_alloc", "mi_host_free", "mi_groth16_verify_batch_seeded",
     "mi_poseidon_constants", "mi_poseidon_hash", "mi_poseidon_hash_dev", "mi_tree_cache_size",
     "mi_tree_build", "mi_tree_build_dev", "mi_tree_c_build", "mi_tree_c_build_dev",
@@ -111,6 +112,8 @@ def lib():
         "mi_groth16_prove_batch": ([vp, vp, vp, u64, vp, u8p, c_int, vp], c_int),
         "mi_groth16_prove_share": ([vp, vp, vp, u8p, ctypes.c_uint32, ctypes.c_uint32, c_int, vp], c_int),
         "mi_groth16_prove_share_dev": ([vp, vp, vp, vp, ctypes.c_uint32, ctypes.c_uint32, c_int, vp], c_int),
+        "mi_groth16_prove_share_ranges": ([vp, vp, vp, vp, vp, c_int, vp], c_int),
+        "mi_groth16_prove_share_ranges_dev": ([vp, vp, vp, vp, vp, c_int, vp], c_int),
         "mi_groth16_assemble": ([u8p, u8p, u64, u8p, u8p, vp, vp], c_int),
         "mi_groth16_trapdoor_dlogs": ([vp, vp, vp, vp, u8p, u8p, vp], c_int),
         "mi_msm_g1": ([vp, u8p, u8p, u64, vp], c_int),

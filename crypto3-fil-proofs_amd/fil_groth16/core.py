@@ -491,6 +491,24 @@ def prove_batch(ctx: Context, pk: ProvingKey, circuit: Circuit, zs, rs=None, pri
     return [out.raw[i * PROOF_BYTES:(i + 1) * PROOF_BYTES] for i in range(count)]
 
 
+def prove_share_ranges(ctx: Context, pk: ProvingKey, circuit: Circuit, z, ranges, priority=False) -> bytes:
+    """A latency-mode share over explicit query ranges: ranges = [(first, count)] for H (d - 1 points, h order),
+    L, A and B (B_G1 and B_G2); H is computed (witness map + NTT chain) only when its count is non-zero.
+    z as for ``prove``.  Shares whose ranges partition every query go to ``assemble``."""
+    flat = [int(v) for fc in ranges for v in fc]
+    if len(flat) != 8:
+        raise ValueError("four (first, count) ranges: H, L, A, B")
+    arr = (ctypes.c_uint64 * 8)(*flat)
+    out = ctypes.create_string_buffer(SHARE_BYTES)
+    if isinstance(z, int):
+        check(lib().mi_groth16_prove_share_ranges_dev(ctx.h, pk.h, circuit.h, ctypes.c_void_p(z), arr, int(priority),
+                                                      out))
+    else:
+        assert len(z) == 32 * circuit.num_vars, "witness length must be (num_inputs + num_aux) * 32"
+        check(lib().mi_groth16_prove_share_ranges(ctx.h, pk.h, circuit.h, bytes(z), arr, int(priority), out))
+    return out.raw
+
+
 def prove_share(ctx: Context, pk: ProvingKey, circuit: Circuit, z, rank: int, world: int, priority=False) -> bytes:
     """Single-proof latency mode: this rank's share of the five MSMs of one proof
     (SHARE_BYTES). z as for ``prove``. The shares of ranks 0..world-1 go to ``assemble``."""

@@ -152,6 +152,76 @@ def prove_partitions_balanced(prove_fn, share_fn, assemble_fn, num_partitions: i
     return b"".join(out[p] for p in range(num_partitions))
 
 
+def latency_ranges(sizes, group: int, lead_share: float = 0.0):
+    """Query ranges of a latency-mode group of ``group`` ranks that computes H once (every rank of a
+    group used to repeat the witness map and the NTT chain, ~317 ms per share of a 32 GiB Window-PoSt
+    partition).  sizes = (n_h, n_l, n_a, n_b) of the proving key (ProvingKey.n_h ...).  Rank 0 of the group
+    takes the whole H query -- it alone runs the witness map and the NTT chain -- plus the fraction
+    ``lead_share`` of L, A and B; ranks 1 .. g - 1 split the rest of L, A and B into equal contiguous slices.
+    Returns one [(first, count)] x 4 (H, L, A, B) list per rank; together they partition every query, so the
+    assembled proof equals the one-GPU proof (mi_groth16_prove_share_ranges)."""
+    if group < 1:
+        raise ValueError("a group has at least one rank")
+    if not 0.0 <= lead_share <= 1.0:
+        raise ValueError("lead_share is a fraction")
+    n_h, n_l, n_a, n_b = (int(x) for x in sizes)
+    if group == 1:
+        return [[(0, n_h), (0, n_l), (0, n_a), (0, n_b)]]
+    out = [[(0, n_h)] + [None] * 3] + [[(n_h, 0)] + [None] * 3 for _ in range(group - 1)]
+    for q, n in ((1, n_l), (2, n_a), (3, n_b)):
+        n0 = int(round(n * lead_share))
+        out[0][q] = (0, n0)
+        rest = n - n0
+        for k in range(1, group):
+            lo = n0 + rest * (k - 1) // (group - 1)
+            hi = n0 + rest * k // (group - 1)
+            out[k][q] = (lo, hi - lo)
+    return out
+
+
+def lead_share_from_times(t_h: float, t_lab: float, group: int) -> float:
+    """The lead rank's fraction of L, A and B that evens a group out: t_h = the H part alone (witness map, NTT
+    chain, H MSM), t_lab = L, A and B alone, both on one GPU.  Lead: t_h + f t_lab; others: (1 - f) t_lab / (g - 1);
+    equal at f = (t_lab - (g - 1) t_h) / (g t_lab), clamped to [0, 1] (0: H alone already outweighs a slice)."""
+    if group <= 1 or t_lab <= 0:
+        return 1.0
+    return min(1.0, max(0.0, (t_lab - (group - 1) * t_h) / (group * t_lab)))
+
+
+def calibrate_lead_share(ctx, pk, circuit, z, group: int, reps: int = 1):
+    """Times the two halves of one proof on this GPU (after one warm call each) and returns
+    (lead_share_from_times, {"t_h_ms", "t_lab_ms"}).  z: host bytes or a device pointer."""
+    import time
+
+    from .core import prove_share_ranges
+
+    sizes = (pk.n_h, pk.n_l, pk.n_a, pk.n_b)
+    h_only = [(0, sizes[0]), (0, 0), (0, 0), (0, 0)]
+    lab = [(0, 0), (0, sizes[1]), (0, sizes[2]), (0, sizes[3])]
+    t = {}
+    for name, rg in (("t_h_ms", h_only), ("t_lab_ms", lab)):
+        prove_share_ranges(ctx, pk, circuit, z, rg)
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            prove_share_ranges(ctx, pk, circuit, z, rg)
+        ctx.synchronize()
+        t[name] = 1e3 * (time.perf_counter() - t0) / reps
+    return lead_share_from_times(t["t_h_ms"], t["t_lab_ms"], group), t
+
+
+def agree_float(x, rank: int, device="cpu") -> float:
+    """rank 0's value of x on every rank (one broadcast); x itself without a process group"""
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()):
+        return float(x)
+    t = torch.tensor([float(x) if rank == 0 else 0.0], dtype=torch.float64).to(device)
+    dist.broadcast(t, 0)
+    return float(t.cpu().item())
+
+
 def gather_shares(share: bytes, world: int, device="cpu"):
     """All-gather one MI_SHARE_BYTES record per rank (the latency mode's only exchange, 576 B per GPU)."""
     import torch

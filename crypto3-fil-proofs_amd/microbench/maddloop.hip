@@ -19,6 +19,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 #include <vector>
 
@@ -189,6 +190,128 @@ k_madd_g2(const T *__restrict__ table, uint32_t table_mask, const uint32_t *__re
     }
 }
 
+// ---- batch-affine accumulation (VERDICT r3 "measure, do not estimate") ----
+// Each lane keeps K affine accumulators in HBM (coalesced [k][lane] layout) and per step adds one gathered
+// point to each: forward pass d_k = x2 - x1, prefix products P_k (stored), ONE Fermat inversion of P_(K-1),
+// backward pass 1 / d_k = inv * P_(k-1), inv *= d_k, then lambda = (y2 - y1) / d_k, x3 = lambda^2 - x1 - x2,
+// y3 = lambda (x1 - x3) - y1 (the point is gathered again in the backward pass rather than stored).
+// Field products per addition: 6 (G1: 5 M + 1 S) plus the inversion's ~575 over K; XYZZ's madd-2008-s is 10.
+// HBM per addition: acc read twice + written once, point gathered twice, prefix written + read.
+__device__ __forceinline__ uint32_t hidx(uint32_t tid, uint32_t s, uint32_t k) {
+    uint32_t h = tid * 0x9E3779B1u ^ (s * 0x85EBCA77u + k * 0xC2B2AE3Du);
+    h ^= h >> 15;
+    h *= 0x2C1B3C6Du;
+    h ^= h >> 12;
+    return h;
+}
+template <int K, class T>
+__global__ void __launch_bounds__(256) k_ba_g1(const T *__restrict__ table, uint32_t mask, int steps,
+                                               fq_t *__restrict__ ax, fq_t *__restrict__ ay,
+                                               fq_t *__restrict__ pre, uint64_t *__restrict__ stamps) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t Tn = (uint64_t)gridDim.x * blockDim.x;
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t t0 = stamp_time(), r0 = stamp_real();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll 1
+    for (int s = 0; s < steps; s++) {
+        fq_t P = fq_t::one();
+#pragma unroll 1
+        for (int k = 0; k < K; k++) {
+            const uint32_t v = hidx(tid, s, k);
+            const Affine<fq_t> a = ld(table, v & mask);
+            P = P * (a.x - ax[k * Tn + tid]);
+            pre[k * Tn + tid] = P;
+        }
+        fq_t inv = inverse_inl(P);
+#pragma unroll 1
+        for (int k = K - 1; k >= 0; k--) {
+            const uint32_t v = hidx(tid, s, k);
+            Affine<fq_t> a = ld(table, v & mask);
+            if (v >> 31) a.y = -a.y;
+            const fq_t x1 = ax[k * Tn + tid], y1 = ay[k * Tn + tid];
+            const fq_t d = a.x - x1;
+            const fq_t ik = k ? inv * pre[(k - 1) * Tn + tid] : inv;
+            inv = inv * d;
+            const fq_t lam = (a.y - y1) * ik;
+            const fq_t x3 = sqr(lam) - x1 - a.x;
+            ay[k * Tn + tid] = lam * (x1 - x3) - y1;
+            ax[k * Tn + tid] = x3;
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t t1 = stamp_time(), r1 = stamp_real();
+    __builtin_amdgcn_sched_barrier(0);
+    if ((threadIdx.x & 63) == 0) {
+        const uint32_t w = tid >> 6;
+        stamps[2 * w] = t1 - t0;
+        stamps[2 * w + 1] = r1 - r0;
+    }
+}
+// the same over Fq2 (one lane per G2 addition; Karatsuba 3-product Fq2 multiplication, Fq2 inversion = one Fq
+// inversion of the norm): 17 Fq products per addition plus ~580 / K, against 28 for the XYZZ lane-pair form
+template <int K, class T>
+__global__ void __launch_bounds__(256) k_ba_g2(const T *__restrict__ table, uint32_t mask, int steps,
+                                               fq2_t *__restrict__ ax, fq2_t *__restrict__ ay,
+                                               fq2_t *__restrict__ pre, uint64_t *__restrict__ stamps) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t Tn = (uint64_t)gridDim.x * blockDim.x;
+    auto ld2 = [&](uint32_t i) -> Affine<fq2_t> {
+        const T &r = table[i];
+        return {{r.c[0], r.c[1]}, {r.c[2], r.c[3]}};
+    };
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t t0 = stamp_time(), r0 = stamp_real();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll 1
+    for (int s = 0; s < steps; s++) {
+        fq2_t P = fq2_t::one();
+#pragma unroll 1
+        for (int k = 0; k < K; k++) {
+            const uint32_t v = hidx(tid, s, k);
+            const Affine<fq2_t> a = ld2(v & mask);
+            P = P * (a.x - ax[k * Tn + tid]);
+            pre[k * Tn + tid] = P;
+        }
+        fq2_t inv = inverse_inl(P);
+#pragma unroll 1
+        for (int k = K - 1; k >= 0; k--) {
+            const uint32_t v = hidx(tid, s, k);
+            Affine<fq2_t> a = ld2(v & mask);
+            if (v >> 31) a.y = -a.y;
+            const fq2_t x1 = ax[k * Tn + tid], y1 = ay[k * Tn + tid];
+            const fq2_t d = a.x - x1;
+            const fq2_t ik = k ? inv * pre[(k - 1) * Tn + tid] : inv;
+            inv = inv * d;
+            const fq2_t lam = (a.y - y1) * ik;
+            const fq2_t x3 = sqr(lam) - x1 - a.x;
+            ay[k * Tn + tid] = lam * (x1 - x3) - y1;
+            ax[k * Tn + tid] = x3;
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t t1 = stamp_time(), r1 = stamp_real();
+    __builtin_amdgcn_sched_barrier(0);
+    if ((threadIdx.x & 63) == 0) {
+        const uint32_t w = tid >> 6;
+        stamps[2 * w] = t1 - t0;
+        stamps[2 * w + 1] = r1 - r0;
+    }
+}
+
+// random field elements (14 limbs below 2^381, not reduced) as batch-affine accumulator starts, on the device
+template <class F>
+__global__ void k_fill(F *__restrict__ out, uint64_t n, uint32_t seed) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t *w = reinterpret_cast<uint32_t *>(out + i);
+    constexpr int L = sizeof(F) / 4;
+    for (int q = 0; q < L; q++) {
+        uint32_t h = hidx((uint32_t)i, seed, q) ^ (uint32_t)(i >> 32);
+        w[q] = (q % 14 == 13) ? (h & 0xf) : (h & Fq29::M);
+    }
+}
+
 static uint32_t rng32(uint64_t &s) {
     s += 0x9E3779B97F4A7C15ull;
     uint64_t z = s;
@@ -246,6 +369,7 @@ static void run_with(const char *name, Launch launch, int iters, int blocks, int
 int main(int argc, char **argv) {
     const int iters = argc > 1 ? atoi(argv[1]) : 64;
     const double warm_s = argc > 2 ? atof(argv[2]) : 2.0;
+    const bool only_ba = argc > 3 && strcmp(argv[3], "ba") == 0;  // the XYZZ gather baselines + batch-affine forms
     hipDeviceProp_t prop;
     CHECK(hipGetDeviceProperties(&prop, 0));
     // 2 waves per SIMD x 4 SIMDs per CU = 8 waves = 2 workgroups of 256 per CU; 8 rounds of the chip
@@ -305,9 +429,37 @@ int main(int argc, char **argv) {
                  iters, blocks, 1, 17832.0, dst, warm_s);
     };
     g1("gather128", std::true_type{}, d128);
-    g1("gather96", std::true_type{}, d96);
-    g1("gather", std::true_type{}, dt);
-    g1("reg", std::false_type{}, dt);
+    if (!only_ba) {
+        g1("gather96", std::true_type{}, d96);
+        g1("gather", std::true_type{}, dt);
+        g1("reg", std::false_type{}, dt);
+    }
+    // batch-affine G1: blocks of 256 threads, occupancy left to the compiler; K accumulators per lane in HBM
+    {
+        const int bblocks = prop.multiProcessorCount * 8;
+        const uint64_t bt = (uint64_t)bblocks * 256;
+        const int KMAX = 256;
+        fq_t *ax, *ay, *pre;
+        CHECK(hipMalloc(&ax, sizeof(fq_t) * bt * KMAX));
+        CHECK(hipMalloc(&ay, sizeof(fq_t) * bt * KMAX));
+        CHECK(hipMalloc(&pre, sizeof(fq_t) * bt * KMAX));
+        // accumulators start as table points (random field elements)
+        k_fill<<<(unsigned)((bt * KMAX + 255) / 256), 256>>>(ax, bt * KMAX, 1);
+        k_fill<<<(unsigned)((bt * KMAX + 255) / 256), 256>>>(ay, bt * KMAX, 2);
+        CHECK(hipDeviceSynchronize());
+        auto ba = [&](const char *name, auto kc, int steps) {
+            constexpr int K = decltype(kc)::value;
+            run_with(name, [&] { k_ba_g1<K, Rec128><<<bblocks, 256>>>(d128, tn - 1, steps, ax, ay, pre, dst); },
+                     steps * K, bblocks, 1, 0.0, dst, warm_s);
+        };
+        ba("ba_g1_k32", std::integral_constant<int, 32>{}, 4);
+        ba("ba_g1_k64", std::integral_constant<int, 64>{}, 2);
+        ba("ba_g1_k128", std::integral_constant<int, 128>{}, 1);
+        ba("ba_g1_k256", std::integral_constant<int, 256>{}, 1);
+        CHECK(hipFree(ax));
+        CHECK(hipFree(ay));
+        CHECK(hipFree(pre));
+    }
     CHECK(hipFree(d128));
     CHECK(hipFree(d96));
     // G2 on lane pairs: the same random elements as Fq2 coordinates, 2^23 records; one madd per lane pair.
@@ -337,9 +489,33 @@ int main(int argc, char **argv) {
             run_with(name, [&] { k_madd_g2<decltype(gather)::value, T><<<blocks, 256>>>(table, tn2 - 1, didx, iters, dout2, dst); },
                      iters, blocks, 2, 0.0, dst, warm_s);
         };
-        g2("g2_gather224", std::true_type{}, d224);
+        if (!only_ba) g2("g2_gather224", std::true_type{}, d224);
         g2("g2_gather256", std::true_type{}, d256);
-        g2("g2_reg", std::false_type{}, d256);
+        if (!only_ba) g2("g2_reg", std::false_type{}, d256);
+        {
+            const int bblocks = prop.multiProcessorCount * 8;
+            const uint64_t bt = (uint64_t)bblocks * 256;
+            const int KMAX = 256;
+            fq2_t *ax, *ay, *pre;
+            CHECK(hipMalloc(&ax, sizeof(fq2_t) * bt * KMAX));
+            CHECK(hipMalloc(&ay, sizeof(fq2_t) * bt * KMAX));
+            CHECK(hipMalloc(&pre, sizeof(fq2_t) * bt * KMAX));
+            k_fill<<<(unsigned)((bt * KMAX + 255) / 256), 256>>>(ax, bt * KMAX, 3);
+            k_fill<<<(unsigned)((bt * KMAX + 255) / 256), 256>>>(ay, bt * KMAX, 4);
+            CHECK(hipDeviceSynchronize());
+            auto ba2 = [&](const char *name, auto kc, int steps) {
+                constexpr int K = decltype(kc)::value;
+                run_with(name, [&] { k_ba_g2<K, Rec256><<<bblocks, 256>>>(d256, tn2 - 1, steps, ax, ay, pre, dst); },
+                         steps * K, bblocks, 1, 0.0, dst, warm_s);
+            };
+            ba2("ba_g2_k32", std::integral_constant<int, 32>{}, 2);
+            ba2("ba_g2_k64", std::integral_constant<int, 64>{}, 1);
+            ba2("ba_g2_k128", std::integral_constant<int, 128>{}, 1);
+            ba2("ba_g2_k256", std::integral_constant<int, 256>{}, 1);
+            CHECK(hipFree(ax));
+            CHECK(hipFree(ay));
+            CHECK(hipFree(pre));
+        }
         CHECK(hipFree(d224));
         CHECK(hipFree(d256));
         CHECK(hipFree(dout2));

@@ -228,6 +228,15 @@ int mi_groth16_prove_share(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *cir
                            uint32_t rank, uint32_t world, int priority, uint8_t share_out[MI_SHARE_BYTES]);
 int mi_groth16_prove_share_dev(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circuit, const void *z_dev,
                                uint32_t rank, uint32_t world, int priority, uint8_t share_out[MI_SHARE_BYTES]);
+/* A share over explicit query ranges: ranges[2q], ranges[2q + 1] = first point, count of query q = 0 H (the
+ * d - 1 points in the key's bit-reversed h order), 1 L (aux), 2 A (a query), 3 B (b query; B_G1 and B_G2 over
+ * the same range).  The witness map and the NTT chain run only when the H count is non-zero, so a latency-mode
+ * group computes H once (on the rank that holds the whole H range) and spreads L, A and B over the others;
+ * shares whose ranges partition every query assemble into the proof mi_groth16_prove makes. */
+int mi_groth16_prove_share_ranges(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circuit, const uint8_t *z,
+                                  const uint64_t ranges[8], int priority, uint8_t share_out[MI_SHARE_BYTES]);
+int mi_groth16_prove_share_ranges_dev(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circuit, const void *z_dev,
+                                      const uint64_t ranges[8], int priority, uint8_t share_out[MI_SHARE_BYTES]);
 /* host only (no device): vk = MI_VK_BYTES uncompressed, shares = count x MI_SHARE_BYTES (any order) */
 int mi_groth16_assemble(const uint8_t *vk, const uint8_t *shares, uint64_t count, const uint8_t r[32],
                         const uint8_t s[32], uint8_t proof_out[MI_PROOF_BYTES], uint8_t *raw_out);
@@ -347,9 +356,11 @@ int mi_ctx_reset_stats(mi_ctx *ctx);
 /* work counters since the last reset: out[0] / out[1] = mixed additions (non-zero signed digits)
  * issued by the G1 / G2 bucket accumulation -- the unit of the VALU roofline */
 int mi_ctx_get_work(mi_ctx *ctx, uint64_t out[2]);
-/* memory fallbacks since the last reset: out[0] = proofs that hit an out-of-memory error and were re-run after
- * their key's 2^128 split tables and the idle scratch were released (the retried proof takes the GLV split and
- * is byte-identical; a second failure is returned as MI_ERR_INTERNAL), out[1] = bytes released for them.
+/* memory fallbacks since the last reset: out[0] = proofs, key generations and key loads that hit an
+ * out-of-memory error and were re-run after the 2^128 split tables of the device's keys (the one being proven
+ * first; keys in use by another context are left alone) and the context's idle scratch were released (a retried
+ * proof takes the GLV split and is byte-identical; a second failure is returned as MI_ERR_INTERNAL), out[1] =
+ * bytes released for them.
  * Replaces failing outright when several keys share one GPU, as GROTH_PARAM_MEMORY_CACHE keeps them
  * (libs/filecoin/include/nil/filecoin/proofs/caches.hpp:48-116). */
 int mi_ctx_get_fallbacks(mi_ctx *ctx, uint64_t out[2]);

@@ -60,3 +60,32 @@ def shares(oracle, params, n_in, n_aux, mats, z: bytes, world: int):
         assert len(rec) == SHARE_BYTES
         out.append(rec)
     return out
+
+
+def shares_ranges(oracle, params, n_in, n_aux, mats, z: bytes, ranges_list):
+    """Oracle shares over explicit query ranges (what mi_groth16_prove_share_ranges computes): one
+    [(first, count)] x 4 list (H in the bit-reversed h order, L, A, B) per share."""
+    ex = params.export()
+    _, _, hb = params.prove(z, 0, 0, want_h=True)
+    idx_a, idx_b = densities(n_in, n_aux, mats)
+    zs = np.frombuffer(z, dtype=np.uint8).reshape(-1, 32)
+
+    def msm(bases, esz, scal, lo, cnt, g2=False):
+        if cnt == 0:
+            return G2_INF if g2 else G1_INF
+        fn = oracle.msm_g2 if g2 else oracle.msm_g1
+        return fn(bases[esz * lo:esz * (lo + cnt)], scal[32 * lo:32 * (lo + cnt)])
+
+    zaux, za, zb = zs[n_in:].tobytes(), zs[idx_a].tobytes(), zs[idx_b].tobytes()
+    log_d = params.d.bit_length() - 1
+    rev = [int(format(i, f"0{log_d}b")[::-1], 2) for i in range(params.d - 1)] if log_d else []
+    hq = np.frombuffer(ex["h"], dtype=np.uint8).reshape(-1, 96)
+    hc = np.frombuffer(hb, dtype=np.uint8).reshape(-1, 32)
+    h_perm, hb_perm = hq[rev].tobytes(), hc[rev].tobytes()
+    out = []
+    for (h, l, a, b) in ranges_list:
+        rec = msm(h_perm, 96, hb_perm, *h) + msm(ex["l"], 96, zaux, *l) + msm(ex["a"], 96, za, *a)
+        rec += msm(ex["b_g1"], 96, zb, *b) + msm(ex["b_g2"], 192, zb, *b, g2=True)
+        assert len(rec) == SHARE_BYTES
+        out.append(rec)
+    return out

@@ -299,3 +299,89 @@ def test_gloo_srs_broadcast(tmp_path):
     assert all(len(ex[k]) > 1000 or k == "vk" for k in ("h", "l", "a", "b_g2"))
     exp = ",".join(hashlib.sha256(bytes(ex[k])).hexdigest() for k in SRS_PARTS)
     assert outs == [exp] * world
+
+
+# ------------------------------------------------------------------ latency groups that compute H once
+@pytest.mark.parametrize("g", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("lead", [0.0, 0.146, 0.5, 1.0])
+def test_latency_ranges_partition_every_query(g, lead):
+    """Rank 0 of a group takes the whole H query (it alone runs the witness map + NTT chain) and `lead` of L, A,
+    B; the others split the rest: every query is covered exactly once, in contiguous order."""
+    from fil_groth16.distributed import latency_ranges
+
+    sizes = (1023, 1000, 977, 501)
+    rg = latency_ranges(sizes, g, lead)
+    assert len(rg) == g
+    for q, n in enumerate(sizes):
+        pos = 0
+        for k in range(g):
+            lo, cnt = rg[k][q]
+            assert lo == pos and cnt >= 0
+            pos += cnt
+        assert pos == n
+    assert rg[0][0] == (0, sizes[0]) and all(rg[k][0][1] == 0 for k in range(1, g))
+    if g > 1:
+        counts = [rg[k][1][1] for k in range(1, g)]
+        assert max(counts) - min(counts) <= 1
+
+
+def test_lead_share_from_times():
+    from fil_groth16.distributed import lead_share_from_times
+
+    assert lead_share_from_times(467.0, 1284.0, 4) == 0.0  # H alone outweighs a third of L/A/B
+    f = lead_share_from_times(467.0, 1284.0, 2)
+    assert abs((467.0 + f * 1284.0) - (1 - f) * 1284.0) < 1e-6
+    assert lead_share_from_times(0.0, 100.0, 4) == 0.25 and lead_share_from_times(5.0, 100.0, 1) == 1.0
+
+
+def _ranges_worker(rank, world, port, outdir):
+    """The balanced runner whose tail groups use latency_ranges (H once per group), oracle range shares."""
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "crypto3-fil-proofs_amd"), os.path.join(root, "oracle"),
+              os.path.join(root, "tests", "golden"), os.path.join(root, "tests")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+
+    import circuits
+    import fil_groth16 as fg
+    import oracle_py
+    import split_oracle
+    from fil_groth16.distributed import agree_float, latency_ranges, prove_partitions_balanced
+
+    oracle_py.set_threads(1)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n_in, n_aux, rows, z = circuits.random_circuit(64, 40)
+    mats = circuits.to_csr(rows)
+    P = oracle_py.OracleParams(oracle_py.OracleCircuit(len(rows), n_in, n_aux, mats), circuits.toxic())
+    zb = circuits.z_bytes(z)
+    ex = P.export()
+    idx_a, idx_b = split_oracle.densities(n_in, n_aux, mats)
+    sizes = (P.d - 1, n_aux, len(idx_a), len(idx_b))
+    lead = agree_float(0.3 if rank == 0 else 0.9, rank)  # rank 0's value reaches every rank
+
+    def share_fn(p, k, g):
+        rg = latency_ranges(sizes, g, lead)
+        return split_oracle.shares_ranges(oracle_py, P, n_in, n_aux, mats, zb, [rg[k]])[0]
+
+    buf = prove_partitions_balanced(lambda ids: [P.prove(zb, 300 + p, 400 + p)[0] for p in ids], share_fn,
+                                    lambda p, sh: fg.assemble(ex["vk"], sh, 300 + p, 400 + p), 5, rank, world)
+    with open(os.path.join(outdir, f"r{rank}.bin"), "wb") as f:
+        f.write(buf + repr(lead).encode())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_balanced_runner_h_once(tmp_path, oracle):
+    """5 partitions over 3 ranks: 3 whole, 2 tail partitions over groups whose lead rank alone computes H; the
+    multi-proof equals the serial one on every rank."""
+    import circuits
+
+    mp.spawn(_ranges_worker, args=(3, _free_port(), str(tmp_path)), nprocs=3, join=True)
+    n_in, n_aux, rows, z = circuits.random_circuit(64, 40)
+    P = oracle.OracleParams(oracle.OracleCircuit(len(rows), n_in, n_aux, circuits.to_csr(rows)), circuits.toxic())
+    zb = circuits.z_bytes(z)
+    serial = b"".join(P.prove(zb, 300 + p, 400 + p)[0] for p in range(5)) + repr(0.3).encode()
+    assert all(open(tmp_path / f"r{r}.bin", "rb").read() == serial for r in range(3))

@@ -313,6 +313,42 @@ def test_prove_share_vs_oracle_shares(ctx, oracle, rows, seed, worlds):
         fg.prove_share(ctx, pk, gc, zb, 2, 2)  # rank >= world
 
 
+@pytest.mark.parametrize("rows,seed", [(700, 86), (16000, 87)])
+def test_prove_share_ranges_vs_oracle(ctx, oracle, rows, seed):
+    """Latency groups that compute H once (mi_groth16_prove_share_ranges, distributed.latency_ranges): every
+    range share equals the oracle's sums over the same ranges, byte for byte, whether or not it holds H (only
+    the shares with an H range run the witness map and NTT chain), and the shares of a partition assemble into
+    the one-GPU proof.  Also an irregular partition (H split over two shares, empty ranges) and the device
+    witness entry."""
+    import torch
+
+    import split_oracle
+    from fil_groth16.distributed import latency_ranges
+
+    n_in, n_aux, rws, z = circuits.random_circuit(seed, rows, n_in=6, n_free=32)
+    mats = circuits.to_csr(rws)
+    oc, gc = _load(ctx, oracle, n_in, n_aux, rws, z)
+    tox = circuits.toxic(seed)
+    pk = fg.generate_random_parameters(ctx, gc, tox)
+    op = oracle.OracleParams(oc, tox)
+    zb = circuits.z_bytes(z)
+    r, s = circuits.blinding(seed)
+    vk, _ = pk.verifying_key()
+    one = fg.prove(ctx, pk, gc, zb, r, s)
+    sizes = (pk.n_h, pk.n_l, pk.n_a, pk.n_b)
+    h, l, a, b = sizes
+    parts = [latency_ranges(sizes, 3, 0.2), latency_ranges(sizes, 4, 0.0), latency_ranges(sizes, 2, 0.35),
+             [[(0, h // 3), (0, 0), (0, a), (0, 0)], [(h // 3, h - h // 3), (0, l), (a, 0), (0, b // 2)],
+              [(h, 0), (l, 0), (a, 0), (b // 2, b - b // 2)], [(0, 0), (0, 0), (0, 0), (0, 0)]]]
+    zd = torch.from_numpy(np.frombuffer(zb, dtype=np.uint8).copy()).cuda()
+    for i, rg in enumerate(parts):
+        shares = [fg.prove_share_ranges(ctx, pk, gc, zd.data_ptr() if i % 2 else zb, x) for x in rg]
+        assert shares == split_oracle.shares_ranges(oracle, op, n_in, n_aux, mats, zb, rg), i
+        assert fg.assemble(vk, shares, r, s) == one, i
+    with pytest.raises(fg.FilGpuError, match="range"):
+        fg.prove_share_ranges(ctx, pk, gc, zb, [(1, h), (0, 0), (0, 0), (0, 0)])
+
+
 def test_prove_share_device_witness(ctx, oracle):
     import torch
 
