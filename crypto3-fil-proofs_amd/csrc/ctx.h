@@ -32,17 +32,28 @@ struct hip_error : std::runtime_error {
                                           " at " + __FILE__ + ":" + std::to_string(__LINE__));    \
     } while (0)
 
-// A device buffer that only grows (no hipMalloc inside the timed steady state).
+// A device buffer that only grows (no hipMalloc inside the timed steady state).  A growth that fails leaves
+// the buffer empty (p = nullptr, cap = 0) -- never a null pointer behind a stale capacity, which a later
+// smaller request would hand to a kernel -- and throws the out-of-memory error (prover.hip retries on it).
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
     void *get(size_t bytes) {
         if (bytes > cap) {
-            if (p) MI_HIP(hipFree(p));
-            p = nullptr;
-            size_t want = bytes + bytes / 8;
-            MI_HIP(hipMalloc(&p, want));
-            cap = want;
+            release();
+            const size_t want = bytes + bytes / 8;
+            void *q = nullptr;
+            hipError_t e = hipMalloc(&q, want);
+            size_t got = want;
+            if (e != hipSuccess) {  // the 1/8 growth slack is optional: try the exact size before giving up
+                (void)hipGetLastError();
+                q = nullptr;
+                e = hipMalloc(&q, bytes);
+                got = bytes;
+            }
+            if (e != hipSuccess) MI_HIP(e);
+            p = q;
+            cap = got;
         }
         return p;
     }
@@ -51,7 +62,7 @@ struct DevBuf {
         return (T *)get(count * sizeof(T));
     }
     void release() {
-        if (p) hipFree(p);
+        if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
     }

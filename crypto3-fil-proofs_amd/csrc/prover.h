@@ -48,6 +48,7 @@ struct Srs {
     std::vector<g1_affine_t> ic;
     // trapdoor evaluations (only when generated from known toxic waste): per-variable u,v,w(tau)
     fr_t *at = nullptr, *bt = nullptr, *ct = nullptr;
+    uint64_t n_vars = 0;  // length of at / bt / ct
     fr_t toxic[5];
     bool has_trapdoor = false;
     // every query point is known to lie in the prime-order subgroup (generated from toxic waste, or

@@ -1058,6 +1058,7 @@ Srs *srs_generate_once(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5
         S->h_perm = dalloc<g1_affine_t>(d - 1);
         fixed_base_affine<fq_t>(c, t1, ks, d - 1, S->h_perm);
         // QAP evaluations per variable: column sums of coeff * L_row(tau)
+        S->n_vars = nv;
         S->at = dalloc<fr_t>(nv);
         S->bt = dalloc<fr_t>(nv);
         S->ct = dalloc<fr_t>(nv);
@@ -1169,8 +1170,9 @@ Srs *srs_generate(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5]) {
 
 // ================================================================================ prove
 namespace {
-// One attempt at a proof's MSM sums.  inject_oom (tests, MI_INJECT_PROVE_OOM): the main lane throws the
-// out-of-memory error a scratch hipMalloc would, after the NTT chain, while the auxiliary lane runs.
+// One attempt at a proof's MSM sums.  inject_oom (tests, MI_INJECT_PROVE_OOM): after the NTT chain, while the
+// auxiliary lane runs, the main lane asks a scratch buffer for more memory than the device has, so the attempt
+// fails the way a short HBM makes it fail.
 ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, const SumRanges &rg,
                             bool inject_oom) {
     std::shared_lock<std::shared_mutex> in_use(srs.use_mu);
@@ -1263,8 +1265,8 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
                 ntt_dif_coset_epilogue(c, a, L, true, true, dinv, true);  // icoset, canonical H (bit-reversed)
             }
             }
-            if (inject_oom)
-                throw hip_error(hipErrorOutOfMemory, "hipMalloc failed: out of memory (injected, MI_INJECT_PROVE_OOM)");
+            if (inject_oom) (void)c.scratch[19].get(1ull << 50);  // a real failed growth (1 PiB), as a scratch
+                                                                    // buffer's hipMalloc fails when HBM is short
             const uint64_t h_lo = rg.lo[0], h_cnt = rg.cnt[0], a_lo = rg.lo[2], a_cnt = rg.cnt[2];
             if (need_h)
                 msm_g1(c, srs.h_perm + h_lo, a + h_lo, nullptr, h_cnt, &H, srs.h_hi ? srs.h_hi + h_lo : nullptr,
@@ -1316,7 +1318,8 @@ uint64_t srs_drop_split_tables(Srs &S) {
 }
 
 namespace {
-// the split tables of every key on `device` that no one is using right now, the proving key first
+// the split tables (and trapdoor evaluations) of every key on `device` that no one is using right now, the
+// proving key first
 uint64_t release_device_tables(int device, const Srs *first) {
     std::lock_guard<std::mutex> lk(g_keys_mu);
     std::vector<Srs *> order;
@@ -1325,9 +1328,22 @@ uint64_t release_device_tables(int device, const Srs *first) {
         else if (k->device == device) order.push_back(k);
     uint64_t freed = 0;
     for (Srs *k : order) {
-        if (!k->h_hi && !k->l_hi && !k->a_hi) continue;
+        if (!k->h_hi && !k->l_hi && !k->a_hi && !k->at) continue;
         std::unique_lock<std::shared_mutex> ex(k->use_mu, std::try_to_lock);
-        if (ex.owns_lock()) freed += srs_drop_split_tables(*k);
+        if (!ex.owns_lock()) continue;
+        freed += srs_drop_split_tables(*k);
+        // a generated key's per-variable trapdoor evaluations (3 x 32 B per variable: 12.5 GB at 2^27) serve
+        // only mi_groth16_trapdoor_dlogs, a test aid; they go too, and that call then reports them missing
+        const struct {
+            fr_t **p;
+        } tv[] = {{&k->at}, {&k->bt}, {&k->ct}};
+        for (auto &t : tv)
+            if (*t.p) {
+                (void)hipFree(*t.p);
+                *t.p = nullptr;
+                freed += 32 * k->n_vars;
+            }
+        k->has_trapdoor = false;
     }
     return freed;
 }
@@ -1339,10 +1355,9 @@ uint64_t release_prover_scratch(Ctx &c, const void *keep) {
     auto rel = [&](Ctx &x, int upto) {
         for (int i = 0; i < upto; i++) {
             DevBuf &b = x.scratch[i];
-            if (!b.p) continue;
             const char *lo = (const char *)b.p;
-            if ((const char *)keep >= lo && (const char *)keep < lo + b.cap) continue;
-            freed += b.cap;
+            if (b.p && (const char *)keep >= lo && (const char *)keep < lo + b.cap) continue;
+            freed += b.p ? b.cap : 0;
             b.release();
         }
     };
@@ -1488,7 +1503,9 @@ static fr_t device_dot(Ctx &c, const fr_t *z, const fr_t *e, uint64_t off, uint6
 
 void groth16_trapdoor_dlogs(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, const fr_t &r,
                             const fr_t &s, fr_t out[3]) {
-    if (!srs.has_trapdoor) throw std::invalid_argument("SRS was not generated from known toxic waste");
+    if (!srs.has_trapdoor)
+        throw std::invalid_argument("SRS was not generated from known toxic waste (or its trapdoor evaluations were "
+                                    "released to make room for a proof)");
     uint64_t nv = circ.n_in + circ.n_aux;
     fr_t alpha = to_mont(srs.toxic[1]), beta = to_mont(srs.toxic[2]), delta = to_mont(srs.toxic[4]);
     fr_t u = device_dot(c, z_dev, srs.at, 0, nv);

@@ -45,6 +45,18 @@ class FilGpuError(RuntimeError):
         self.code = code
 
 
+def torch_sync():
+    """Before a device-pointer entry: the library runs on its own streams, so work the caller queued on torch's
+    current stream (the fill or copy that produced an input tensor, or an earlier reader of an output buffer) is
+    finished first.  The C ABI's contract is the same (device inputs complete before the call); this keeps the
+    Python callers, which hand over torch tensors, inside it.  No-op without torch or before CUDA is initialised."""
+    import sys
+
+    t = sys.modules.get("torch")
+    if t is not None and t.cuda.is_initialized():
+        t.cuda.current_stream().synchronize()
+
+
 def build():
     import subprocess
 

@@ -17,7 +17,7 @@ import os
 
 import numpy as np
 
-from ._lib import check, lib
+from ._lib import check, lib, torch_sync
 
 FR_MODULUS = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 PROOF_BYTES = 192
@@ -123,6 +123,7 @@ class Context:
         return buf.raw
 
     def ntt_dev(self, data_ptr: int, log_n: int, inverse=False, coset=False):
+        torch_sync()
         check(lib().mi_ntt_fr_dev(self.h, ctypes.c_void_p(data_ptr), log_n, int(inverse), int(coset)))
 
 
@@ -155,6 +156,7 @@ class Points:
     def msm_dev(self, scalars_ptr: int, n: int) -> bytes:
         out = ctypes.create_string_buffer(192 if self.g2 else 96)
         f = lib().mi_msm_g2_dev if self.g2 else lib().mi_msm_g1_dev
+        torch_sync()
         check(f(self.ctx.h, self.h, ctypes.c_void_p(scalars_ptr), n, out))
         return out.raw
 
@@ -233,6 +235,7 @@ class SrsStream:
 
     def part(self, which: int, first: int, data, n: int, on_device=False):
         if on_device:
+            torch_sync()
             ptr, keep = ctypes.c_void_p(int(data)), None
         else:
             buf = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray)
@@ -313,6 +316,7 @@ class ProvingKey:
     def export_query_dev(self, which: int, first: int, n: int, dev_ptr: int):
         """points [first, first + n) of one query (0 h natural order, 1 l, 2 a, 3 b_g1, 4 b_g2) in the wire
         format, written to device memory"""
+        torch_sync()
         check(lib().mi_srs_export_query_dev(self.ctx.h, self.h, which, first, n, ctypes.c_void_p(dev_ptr)))
 
     def msm_info(self):
@@ -408,6 +412,7 @@ def prove(ctx: Context, pk: ProvingKey, circuit: Circuit, z, r: int = None, s: i
         if want_raw:
             raise ValueError("want_raw needs injected r, s")
         if isinstance(z, int):
+            torch_sync()
             check(lib().mi_groth16_prove_dev_random(ctx.h, pk.h, circuit.h, ctypes.c_void_p(z), int(priority), proof))
         else:
             assert len(z) == 32 * circuit.num_vars, "witness length must be (num_inputs + num_aux) * 32"
@@ -417,6 +422,7 @@ def prove(ctx: Context, pk: ProvingKey, circuit: Circuit, z, r: int = None, s: i
         raise ValueError("give both r and s, or neither")
     raw = ctypes.create_string_buffer(384) if want_raw else None
     if isinstance(z, int):
+        torch_sync()
         check(lib().mi_groth16_prove_dev(ctx.h, pk.h, circuit.h, ctypes.c_void_p(z), fr_bytes(r), fr_bytes(s),
                                          int(priority), proof, raw))
     else:
@@ -501,6 +507,7 @@ def prove_share_ranges(ctx: Context, pk: ProvingKey, circuit: Circuit, z, ranges
     arr = (ctypes.c_uint64 * 8)(*flat)
     out = ctypes.create_string_buffer(SHARE_BYTES)
     if isinstance(z, int):
+        torch_sync()
         check(lib().mi_groth16_prove_share_ranges_dev(ctx.h, pk.h, circuit.h, ctypes.c_void_p(z), arr, int(priority),
                                                       out))
     else:
@@ -514,6 +521,7 @@ def prove_share(ctx: Context, pk: ProvingKey, circuit: Circuit, z, rank: int, wo
     (SHARE_BYTES). z as for ``prove``. The shares of ranks 0..world-1 go to ``assemble``."""
     out = ctypes.create_string_buffer(SHARE_BYTES)
     if isinstance(z, int):
+        torch_sync()
         check(lib().mi_groth16_prove_share_dev(ctx.h, pk.h, circuit.h, ctypes.c_void_p(z), rank, world,
                                                int(priority), out))
     else:
@@ -536,6 +544,7 @@ def assemble(vk: bytes, shares, r: int, s: int, want_raw=False):
 
 def trapdoor_dlogs(ctx: Context, pk: ProvingKey, circuit: Circuit, z_dev_ptr: int, r: int, s: int):
     out = ctypes.create_string_buffer(96)
+    torch_sync()
     check(lib().mi_groth16_trapdoor_dlogs(ctx.h, pk.h, circuit.h, ctypes.c_void_p(z_dev_ptr), fr_bytes(r),
                                           fr_bytes(s), out))
     return [int.from_bytes(out.raw[32 * i:32 * i + 32], "little") for i in range(3)]
