@@ -73,7 +73,10 @@ struct Synth {
     std::vector<fr_t> z;         // canonical
 };
 
-Synth *synth_generate(unsigned log_rows, uint64_t n_in, uint64_t seed) {
+Synth *synth_generate(unsigned log_rows, uint64_t n_in, uint64_t seed, unsigned flags) {
+    // MI_SYNTH_UNIFORM_WITNESS: every BOOL row becomes a PACK row (v random, v * ONE = v), so each aux variable is
+    // a uniform field element or a product of such -- the MSM scalars of a witness without small values
+    const bool uniform = (flags & 1u) != 0;
     if (n_in < 1 || log_rows < 3 || log_rows > 31) throw std::invalid_argument("bad synthetic circuit shape");
     uint64_t d = 1ull << log_rows;
     if (n_in + 8 > d) throw std::invalid_argument("too many inputs for the domain");
@@ -104,7 +107,7 @@ Synth *synth_generate(unsigned log_rows, uint64_t n_in, uint64_t seed) {
     // pass 1: BOOL / PACK values
     parallel_for(n, [&](uint64_t lo, uint64_t hi) {
         for (uint64_t j = lo; j < hi; j++) {
-            if (j % 4 == 0) z[n_in + j] = fr_u32((uint32_t)(h3(seed, j, 1) & 1));
+            if (j % 4 == 0) z[n_in + j] = uniform ? fr_rand(seed ^ 0x5a5a, j) : fr_u32((uint32_t)(h3(seed, j, 1) & 1));
             if (j % 4 == 1) z[n_in + j] = fr_rand(seed, j);
         }
     });
@@ -130,8 +133,10 @@ Synth *synth_generate(unsigned log_rows, uint64_t n_in, uint64_t seed) {
         }
     });
     // CSR: per-row term counts are a function of j mod 4 (A, B, C)
-    static const int cntA[4] = {1, 1, 2, 1}, cntC[4] = {0, 1, 1, 1};
-    auto cntB = [&](uint64_t j) -> int { return j % 4 == 0 ? 2 : (j % 4 == 3 ? (n_in > 1 ? 2 : 1) : 1); };
+    const int cntA[4] = {1, 1, 2, 1}, cntC[4] = {uniform ? 1 : 0, 1, 1, 1};
+    auto cntB = [&](uint64_t j) -> int {
+        return j % 4 == 0 ? (uniform ? 1 : 2) : (j % 4 == 3 ? (n_in > 1 ? 2 : 1) : 1);
+    };
     for (int m = 0; m < 3; m++) S->rp[m].resize(n + 1);
     S->rp[0][0] = S->rp[1][0] = S->rp[2][0] = 0;
     for (uint64_t j = 0; j < n; j++) {
@@ -149,7 +154,7 @@ Synth *synth_generate(unsigned log_rows, uint64_t n_in, uint64_t seed) {
         for (uint64_t j = lo; j < hi; j++) {
             uint64_t ea = S->rp[0][j], eb = S->rp[1][j], ec = S->rp[2][j];
             uint32_t vj = var(j);
-            switch (j % 4) {
+            switch (uniform && j % 4 == 0 ? 1 : j % 4) {
                 case 0:  // BOOL: v * (1 - v) = 0
                     S->col[0][ea] = vj;
                     S->coeff[0][ea] = one;
@@ -213,9 +218,13 @@ struct mi_synth {
 extern "C" {
 
 int mi_synth_generate(unsigned log_rows, uint64_t num_inputs, uint64_t seed, mi_synth **out) {
+    return mi_synth_generate_ex(log_rows, num_inputs, seed, 0, out);
+}
+
+int mi_synth_generate_ex(unsigned log_rows, uint64_t num_inputs, uint64_t seed, unsigned flags, mi_synth **out) {
     if (!out) return MI_ERR_ARG;
     try {
-        *out = new mi_synth{mi::synth_generate(log_rows, num_inputs, seed)};
+        *out = new mi_synth{mi::synth_generate(log_rows, num_inputs, seed, flags)};
         return MI_OK;
     } catch (const std::invalid_argument &) {
         return MI_ERR_ARG;

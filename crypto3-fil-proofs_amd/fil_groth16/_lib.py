@@ -19,7 +19,7 @@ EXPORTS = [
     "mi_points_upload_g1", "mi_points_upload_g2", "mi_points_from_srs", "mi_points_free", "mi_points_count",
     "mi_msm_g1_dev", "mi_msm_g2_dev", "mi_ntt_fr_dev",
     "mi_ctx_get_stats", "mi_ctx_reset_stats", "mi_ctx_get_work", "mi_ctx_get_fallbacks", "mi_msm_window_bits",
-    "mi_synth_generate", "mi_synth_r1cs", "mi_synth_witness", "mi_synth_free",
+    "mi_synth_generate", "mi_synth_generate_ex", "mi_synth_r1cs", "mi_synth_witness", "mi_synth_free",
     "mi_params_inspect", "mi_params_load", "mi_params_write", "mi_vk_write",
     "mi_groth16_verify", "mi_groth16_verify_batch", "mi_pairing",
     "mi_groth16_prove_share", "mi_groth16_prove_share_dev", "mi_groth16_assemble",
@@ -145,6 +145,7 @@ def lib():
         "mi_ctx_get_fallbacks": ([vp, vp], c_int),
         "mi_msm_window_bits": ([u64], ctypes.c_uint),
         "mi_synth_generate": ([ctypes.c_uint, u64, u64, pp], c_int),
+        "mi_synth_generate_ex": ([ctypes.c_uint, u64, u64, ctypes.c_uint, pp], c_int),
         "mi_synth_r1cs": ([vp, vp], c_int),
         "mi_synth_witness": ([vp, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(u64)], c_int),
         "mi_synth_free": ([vp], None),

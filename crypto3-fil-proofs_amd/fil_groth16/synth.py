@@ -11,9 +11,12 @@ from .core import Circuit, _R1CS
 
 
 class SynthCircuit:
-    def __init__(self, log_rows: int, n_in: int = 4, seed: int = 1):
+    def __init__(self, log_rows: int, n_in: int = 4, seed: int = 1, uniform: bool = False):
+        """uniform: no boolean rows, so every witness value is uniform (MI_SYNTH_UNIFORM_WITNESS); the default
+        mixes boolean, random and product rows like a Filecoin witness"""
         self.h = ctypes.c_void_p()
-        check(lib().mi_synth_generate(log_rows, n_in, seed, ctypes.byref(self.h)))
+        check(lib().mi_synth_generate_ex(log_rows, n_in, seed, 1 if uniform else 0, ctypes.byref(self.h)))
+        self.uniform = uniform
         self.s = _R1CS()
         check(lib().mi_synth_r1cs(self.h, ctypes.byref(self.s)))
         zp, nv = ctypes.c_void_p(), ctypes.c_uint64()

@@ -276,6 +276,10 @@ int mi_ntt_fr_dev(mi_ctx *ctx, void *data_dev, unsigned log_n, int inverse, int 
  * the prover boundary.  Pointers returned by mi_synth_r1cs / mi_synth_witness live until mi_synth_free. */
 typedef struct mi_synth mi_synth;
 int mi_synth_generate(unsigned log_rows, uint64_t num_inputs, uint64_t seed, mi_synth **out);
+/* flags: MI_SYNTH_UNIFORM_WITNESS turns the generator's boolean rows into packing rows, so every aux value is
+ * a uniform field element or a product of such (no small MSM scalars: the uniform-witness prove rate) */
+#define MI_SYNTH_UNIFORM_WITNESS 1u
+int mi_synth_generate_ex(unsigned log_rows, uint64_t num_inputs, uint64_t seed, unsigned flags, mi_synth **out);
 int mi_synth_r1cs(const mi_synth *s, mi_r1cs *out);
 int mi_synth_witness(const mi_synth *s, const uint8_t **z, uint64_t *num_vars);
 void mi_synth_free(mi_synth *s);

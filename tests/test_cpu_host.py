@@ -98,6 +98,20 @@ def test_synthetic_circuit_satisfied(oracle, log_rows, n_in):
     assert not oc.satisfied(bytes(bad))
 
 
+@pytest.mark.parametrize("log_rows,n_in", [(6, 1), (12, 4)])
+def test_synthetic_uniform_witness(oracle, log_rows, n_in):
+    """MI_SYNTH_UNIFORM_WITNESS: the same row shapes without boolean rows -- satisfied, same domain, and almost
+    no small aux values (the boolean-heavy default has a quarter of them in {0, 1})."""
+    sc = synth.SynthCircuit(log_rows, n_in, seed=3, uniform=True)
+    assert sc.n + sc.n_in == 1 << log_rows
+    oc = oracle.OracleCircuit(sc.n, sc.n_in, sc.n_aux, sc.csr())
+    assert oc.satisfied(sc.z_bytes())
+    aux = sc.z_array().reshape(-1, 32)[n_in:]
+    small = int((aux[:, 4:] == 0).all(axis=1).sum())  # values below 2^32
+    mixed = synth.SynthCircuit(log_rows, n_in, seed=3).z_array().reshape(-1, 32)[n_in:]
+    assert small <= len(aux) // 64 < int((mixed[:, 4:] == 0).all(axis=1).sum())
+
+
 def test_synthetic_circuit_deterministic():
     a = synth.SynthCircuit(12, 4, seed=5).z_bytes()
     b = synth.SynthCircuit(12, 4, seed=5).z_bytes()
