@@ -652,11 +652,15 @@ inline unsigned grid_for(uint64_t n, unsigned block) { return (unsigned)((n + bl
 #ifndef MI_SORT_RADIX
 #define MI_SORT_RADIX 11
 #endif
+// MergeSortLimit 0: rocPRIM's default sends every sort of <= 2^20 items through block sort + merge passes
+// (~19 launches per sort); below 2^20 items onesweep's 1-2 passes are far faster (the Winning-PoSt proof's
+// 2^19-point MSMs spent 14.6 of 42 ms in merge passes).  Inputs of one block still take the single-block sort.
 using onesweep11_cfg = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
     rocprim::radix_sort_onesweep_config<rocprim::kernel_config<MI_SORT_BLOCK, MI_SORT_IPT>,
                                         rocprim::kernel_config<MI_SORT_BLOCK, MI_SORT_IPT>, MI_SORT_RADIX,
-                                        rocprim::block_radix_rank_algorithm::match>>;
+                                        rocprim::block_radix_rank_algorithm::match>,
+    0>;
 
 inline void sort_pairs_u32(void *tmp, size_t &bytes, const uint32_t *k_in, uint32_t *k_out, const uint32_t *v_in,
                            uint32_t *v_out, uint32_t n, unsigned bits, hipStream_t st) {
@@ -711,9 +715,9 @@ inline bool plan_chunks(Ctx &c, MsmPlan &pl, uint32_t *offA, uint32_t *cntA, uin
     k_chunk_len_keys<<<grid_for(total, 256), 256, 0, st>>>(chunk_bucket, coff, cntA, total, L0, lkeys, lids);
     MI_LAUNCHED(c, "k_chunk_len_keys");
     size_t tb = 0;
-    MI_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, lkeys, lkeys_s, lids, order, total, 0, len_bits, st));
+    sort_pairs_u32(nullptr, tb, lkeys, lkeys_s, lids, order, total, len_bits, st);
     void *tmp2 = c.scratch[4].get(tb);
-    MI_HIP(hipcub::DeviceRadixSort::SortPairs(tmp2, tb, lkeys, lkeys_s, lids, order, total, 0, len_bits, st));
+    sort_pairs_u32(tmp2, tb, lkeys, lkeys_s, lids, order, total, len_bits, st);
     pl.vals_s = vals_s;
     pl.off = offA;
     pl.cnt = cntA;

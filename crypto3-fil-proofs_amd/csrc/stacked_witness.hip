@@ -373,10 +373,101 @@ k_wit_poseidon(const WOp *__restrict__ ops, const uint64_t *__restrict__ idx, ui
     if (i >= n) return;
     pos_op_t<T, EXPAND>(ops[EXPAND ? idx[i] : i], pin, k, z);
 }
+// Phase A's Poseidon ops are a latency chain: each tree level holds a few dozen to a few hundred hashes, and one
+// thread per hash executes a whole permutation alone (0.9 ms per arity-8 level).  Here one hash takes a 16-lane
+// group (4 hashes per wave) and lane j holds state element j:
+//   full rounds  every lane its S-box, then the state is gathered across the group (9-word shuffles) and lane j
+//                forms row j of the MDS product (fr29_row, as the one-thread form);
+//   partial      lane 0 its S-box, s0 broadcast; lane j >= 1 updates s_j += w_j s0 while every lane forms its
+//                term row_j s_j of the new s0, summed by a 4-level butterfly (each level reduced below 2r).
+// The same field values as pos_run (exact arithmetic, lazy representatives < 4r, canonical digest), ~5x
+// shorter per hash.  Phase B keeps one thread per hash: it emits every S-box variable and has thousands of hashes.
+__device__ __forceinline__ fr29_t shfl29(const fr29_t &x, int src) {
+    fr29_t r;
+    MI_UNROLL for (int l = 0; l < 9; l++) r.v[l] = (uint32_t)__shfl((int)x.v[l], src, 16);
+    return r;
+}
+__device__ __forceinline__ fr29_t shfl_xor29(const fr29_t &x, int mask) {
+    fr29_t r;
+    MI_UNROLL for (int l = 0; l < 9; l++) r.v[l] = (uint32_t)__shfl_xor((int)x.v[l], mask, 16);
+    return r;
+}
+__device__ __forceinline__ fr29_t zero29() {
+    fr29_t r;
+    MI_UNROLL for (int l = 0; l < 9; l++) r.v[l] = 0;
+    return r;
+}
+// row . state of lane j's row `m + j * T` over the group's state (gathered from lanes 0 .. T - 1)
+template <int T>
+__device__ __forceinline__ fr29_t group_row(const fr29_t &x, const fr29_t *__restrict__ m, int j) {
+    fr29_t all[T];
+    sfor<T>([&](auto i) { all[i] = shfl29(x, i); });
+    return j < T ? fr29_row<T>(m + j * T, all) : zero29();
+}
+
+template <int T>
+__global__ void __launch_bounds__(64) k_wit_poseidon_lanes(const WOp *__restrict__ ops, uint64_t n,
+                                                           const uint64_t *__restrict__ pin, PosK k,
+                                                           fr_t *__restrict__ z) {
+    static_assert(T <= 16, "one hash per 16-lane group");
+    const uint64_t h = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 4);
+    const int j = (int)(threadIdx.x & 15);
+    if (h >= n) return;  // whole groups only: shuffles stay inside a group
+    const WOp op = ops[h];
+    const fr29_t *img = k.img;
+    fr29_t x = zero29();
+    if (j == 0) {
+        MI_UNROLL for (int l = 0; l < 9; l++) x.v[l] = img[k.off_tag].v[l];
+    } else if (j < T) {
+        x = fr29_mul(fr29_from_fr(zget(z, pin[op.a + j - 1])), img[k.off_tag + 1]);
+    }
+    const fr29_t *mds = img + k.off_mds;
+    const int half = k.rf / 2;
+#pragma unroll 1
+    for (int r = 0; r < half; r++) {
+        if (j < T) x = fr29_sbox(fr29_add(x, img[k.off_rc_first + r * T + j]));
+        x = group_row<T>(x, mds, j);
+    }
+    const fr29_t *sp = img + k.off_sparse;
+#pragma unroll 1
+    for (int q = 0; q < k.rp - 1; q++, sp += 2 * T - 1) {
+        if (j == 0) x = fr29_sbox(fr29_add(x, img[k.off_rc_part + q]));
+        const fr29_t s0 = shfl29(x, 0);
+        fr29_t term = j < T ? fr29_mul(sp[j], x) : zero29();  // row_j s_j (s_0 after its S-box)
+        MI_UNROLL for (int m = 1; m < 16; m <<= 1)
+            term = fr29_sub_if_ge(fr29_add(term, shfl_xor29(term, m)), R2X29);
+        if (j == 0) x = term;
+        else if (j < T) x = fr29_sub_if_ge(fr29_add(x, fr29_mul(sp[T + j - 1], s0)), R2X29);
+    }
+    if (j == 0) x = fr29_sbox(fr29_add(x, img[k.off_rc_part + k.rp - 1]));
+    x = group_row<T>(x, img + k.off_dense, j);
+#pragma unroll 1
+    for (int r = 0; r < half; r++) {
+        if (j < T) x = fr29_sbox(fr29_add(x, img[k.off_rc_last + r * T + j]));
+        x = group_row<T>(x, mds, j);
+    }
+    if (j == 1) zput_fr(z, op.b, fr_from_fr29(fr29_from_mont(x)));
+}
+
 template <bool EXPAND>
 void launch_poseidon(int kind, hipStream_t st, const WOp *ops, const uint64_t *idx, uint64_t n, const uint64_t *pin,
                      const PosKs &pk, fr_t *z) {
     const unsigned g = (unsigned)((n + 63) / 64);
+    // MI_WIT_POS_LANES=0 (read per call, A/B): phase A one thread per hash as phase B
+    static const bool lanes_env = [] {
+        const char *e = getenv("MI_WIT_POS_LANES");
+        return !(e && atoi(e) == 0);
+    }();
+    if (!EXPAND && lanes_env) {
+        const unsigned g4 = (unsigned)((n + 3) / 4);
+        switch (kind) {
+            case 1: k_wit_poseidon_lanes<3><<<g4, 64, 0, st>>>(ops, n, pin, pk.k[0], z); break;
+            case 2: k_wit_poseidon_lanes<5><<<g4, 64, 0, st>>>(ops, n, pin, pk.k[1], z); break;
+            case 3: k_wit_poseidon_lanes<9><<<g4, 64, 0, st>>>(ops, n, pin, pk.k[2], z); break;
+            default: k_wit_poseidon_lanes<12><<<g4, 64, 0, st>>>(ops, n, pin, pk.k[3], z); break;
+        }
+        return;
+    }
     switch (kind) {
         case 1: k_wit_poseidon<3, EXPAND><<<g, 64, 0, st>>>(ops, idx, n, pin, pk.k[0], z); break;
         case 2: k_wit_poseidon<5, EXPAND><<<g, 64, 0, st>>>(ops, idx, n, pin, pk.k[1], z); break;
