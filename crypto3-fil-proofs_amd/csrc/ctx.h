@@ -277,7 +277,7 @@ void msm_g2_planned(Ctx &c, const MsmPlan &plan, const g2_affine_t *bases, g2_xy
 // bases_hi (optional): bases_hi[i] = 2^128 bases[i].  With it, large MSMs run in split mode: scalar
 // k_i = lo_i + 2^128 hi_i becomes two 128-bit scalars over bases[i] and bases_hi[i], which halves the
 // windows (and the bucket reduction) for the same number of mixed additions (MI_MSM_SPLIT: 0 off,
-// 1 default from 2^16 points, 2 always).
+// 1 default above 2^20 points, 2 always).
 // subgroup: every base is known to lie in the prime-order subgroup (a generated key, a checked load, or
 // bases that passed mi_points_check_subgroup); only then may auto mode take the GLV split (glv.h).
 void msm_g1(Ctx &c, const g1_affine_t *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,

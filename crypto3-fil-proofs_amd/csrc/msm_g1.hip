@@ -33,10 +33,20 @@ unsigned msm_window_bits_for(uint64_t n, unsigned sbits, bool glv) {
 }
 
 bool msm_use_split(uint64_t n) {
-    // MI_MSM_SPLIT: 0 off, 1 (default) from 2^16 points, 2 always (tests); read per call
+    // MI_MSM_SPLIT: 0 off, 1 (default) above 2^20 points, 2 always (tests); read per call.  Up to 2^20 points the
+    // plain plan sorts every window in one onesweep call while the split plan sorts window by window: same box,
+    // the 2^20 G1 MSM 6.05 -> 5.39 ms unsplit, the Winning-PoSt proof (2^19-point MSMs) unchanged, the 2^21
+    // proof 40.6 -> 41.4 ms if its 2^21 - 1-point H MSM went unsplit (tools/split_sweep.sh).
+    // MI_MSM_SPLIT_MIN = k splits from 2^k points instead.
     const char *e = getenv("MI_MSM_SPLIT");
     const int mode = e ? atoi(e) : 1;
-    return mode == 2 || (mode == 1 && n >= (1u << 16));
+    if (mode == 2) return true;
+    if (mode != 1) return false;
+    if (const char *m = getenv("MI_MSM_SPLIT_MIN")) {
+        const int lg = atoi(m);
+        return n >= (1ull << (lg < 0 ? 0 : lg > 40 ? 40 : lg));
+    }
+    return n > (1ull << 20);
 }
 
 int msm_glv_mode() {

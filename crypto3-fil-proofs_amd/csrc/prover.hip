@@ -933,7 +933,7 @@ void build_hi_tables(Ctx &c, Srs &S) {
     } qs[] = {{S.h_perm, S.n_h, &S.h_hi}, {S.l, S.n_l, &S.l_hi}, {S.a, S.n_a, &S.a_hi}};
     if (msm_glv_mode() == 2) {  // auto: tables only while they leave the prover its working set
         uint64_t need = 0;
-        for (auto &q : qs) need += q.src ? q.n * sizeof(g1_affine_t) : 0;
+        for (auto &q : qs) need += q.src && msm_use_split(q.n) ? q.n * sizeof(g1_affine_t) : 0;
         size_t free_b = 0, total_b = 0;
         MI_HIP(hipMemGetInfo(&free_b, &total_b));
         // a proof's scratch: the Montgomery witness and the three QAP vectors (32 (m + 3 d) bytes), and per
@@ -951,7 +951,7 @@ void build_hi_tables(Ctx &c, Srs &S) {
     // is fragmented), the key keeps none and its MSMs take the GLV split
     try {
         for (auto &q : qs) {
-            if (!q.src || !q.n) continue;
+            if (!q.src || !q.n || !msm_use_split(q.n)) continue;  // a query its MSM never splits needs no table
             *q.dst = dalloc<g1_affine_t>(q.n);
             g1_shift128(c, q.src, q.n, *q.dst);
         }

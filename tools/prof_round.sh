@@ -7,7 +7,7 @@
 set -e
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
 T=${1:-r2}
-B="python3 bench.py --steps 1 --warmup 1 --msm-reps 1 --no-cpu-baseline --no-device-resident --tree-log-nodes 0 --config4-log-rows 0 --sdr-log-labels 0 --stacked-log-nodes 0 --post-sectors 0"
+B="python3 bench.py --steps 1 --warmup 1 --msm-reps 1 --no-cpu-baseline --no-device-resident --tree-log-nodes 0 --config4-log-rows 0 --sdr-log-labels 0 --stacked-log-nodes 0 --post-sectors 0 --winning-log-nodes 0 --uniform-steps 0"
 mkdir -p gpurun_out
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_trace -o run -- $B > gpurun_out/${T}_trace.json 2> gpurun_out/${T}_trace.err
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${T}_fetch -o run -- $B > gpurun_out/${T}_fetch.json 2> gpurun_out/${T}_fetch.err

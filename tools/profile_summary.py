@@ -81,9 +81,15 @@ def main():
     bench = json.loads(open(args.bench_json).read().strip().splitlines()[-1])
     bench.setdefault("msm_reps", 1)
     out = {"tag": args.tag, "command": "rocprofv3 --kernel-trace --stats / --pmc FETCH_SIZE / --pmc WRITE_SIZE -- "
-                                       "python3 bench.py --steps 1 --warmup 1 --msm-reps 1 --no-cpu-baseline --no-device-resident --tree-log-nodes 0 --config4-log-rows 0 --sdr-log-labels 0 --stacked-log-nodes 0 --post-sectors 0",
+                                       "python3 bench.py --steps 1 --warmup 1 --msm-reps 1 --no-cpu-baseline --no-device-resident --tree-log-nodes 0 --config4-log-rows 0 --sdr-log-labels 0 --stacked-log-nodes 0 --post-sectors 0 --winning-log-nodes 0 --uniform-steps 0",
            "workload": bench["config"]["workload"], "bench_value_under_profiler": bench["value"],
            "kernels": kernel_stats(args.trace)}
+    try:  # the source revision the profiled build came from (bench.py reports it as roofline.traffic_detail)
+        import subprocess
+
+        out["commit"] = subprocess.check_output(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"]).decode().strip()
+    except Exception:
+        out["commit"] = None
     dom = next(k for k in out["kernels"] if args.kernel in k["kernel"])
     out["dominant_kernel"] = {"name": args.kernel, "calls": dom["calls"], "avg_ms": dom["avg_ms"],
                               "total_ms": dom["total_ms"]}
