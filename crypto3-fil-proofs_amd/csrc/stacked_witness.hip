@@ -381,7 +381,7 @@ k_wit_poseidon(const WOp *__restrict__ ops, const uint64_t *__restrict__ idx, ui
 //   partial      lane 0 its S-box, s0 broadcast; lane j >= 1 updates s_j += w_j s0 while every lane forms its
 //                term row_j s_j of the new s0, summed by a 4-level butterfly (each level reduced below 2r).
 // The same field values as pos_run (exact arithmetic, lazy representatives < 4r, canonical digest), ~5x
-// shorter per hash.  Phase B keeps one thread per hash: it emits every S-box variable and has thousands of hashes.
+// shorter per hash.  Phase B (EXPAND) uses the same kernel and writes each S-box's variables from its lane.
 __device__ __forceinline__ fr29_t shfl29(const fr29_t &x, int src) {
     fr29_t r;
     MI_UNROLL for (int l = 0; l < 9; l++) r.v[l] = (uint32_t)__shfl((int)x.v[l], src, 16);
@@ -405,15 +405,22 @@ __device__ __forceinline__ fr29_t group_row(const fr29_t &x, const fr29_t *__res
     return j < T ? fr29_row<T>(m + j * T, all) : zero29();
 }
 
-template <int T>
-__global__ void __launch_bounds__(64) k_wit_poseidon_lanes(const WOp *__restrict__ ops, uint64_t n,
-                                                           const uint64_t *__restrict__ pin, PosK k,
+// EXPAND (phase B): every lane also writes its own S-box variables at their fixed offsets in the gadget's
+// allocation order (pos_run's Sink order: first full rounds element by element -- the first round's inputs
+// without v, the domain tag's first S-box none --, the partial rounds' element 0, the last full rounds, the
+// digest), so the gadget's variables come out as pos_run<ZSink> writes them.
+__device__ __forceinline__ void zput29(fr_t *z, uint64_t k, const fr29_t &x) {
+    zput_fr(z, k, fr_from_fr29(fr29_from_mont(x)));
+}
+template <int T, bool EXPAND>
+__global__ void __launch_bounds__(64) k_wit_poseidon_lanes(const WOp *__restrict__ ops, const uint64_t *__restrict__ idx,
+                                                           uint64_t n, const uint64_t *__restrict__ pin, PosK k,
                                                            fr_t *__restrict__ z) {
     static_assert(T <= 16, "one hash per 16-lane group");
     const uint64_t h = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 4);
     const int j = (int)(threadIdx.x & 15);
     if (h >= n) return;  // whole groups only: shuffles stay inside a group
-    const WOp op = ops[h];
+    const WOp op = ops[EXPAND ? idx[h] : h];
     const fr29_t *img = k.img;
     fr29_t x = zero29();
     if (j == 0) {
@@ -423,15 +430,35 @@ __global__ void __launch_bounds__(64) k_wit_poseidon_lanes(const WOp *__restrict
     }
     const fr29_t *mds = img + k.off_mds;
     const int half = k.rf / 2;
+    // S-box with the gadget's variables written at z[at ..]: (v,) v^2, v^4, v^5
+    auto sbox_emit = [&](const fr29_t &v, uint64_t at, bool with_v) -> fr29_t {
+        const fr29_t v2 = fr29_sqr(v), v4 = fr29_sqr(v2), v5 = fr29_mul(v4, v);
+        if (EXPAND) {
+            if (with_v) zput29(z, at++, v);
+            zput29(z, at++, v2);
+            zput29(z, at++, v4);
+            zput29(z, at, v5);
+        }
+        return v5;
+    };
+    const uint64_t base = op.dst;
+    const uint64_t o_full = 3 * (uint64_t)(T - 1);                      // after round 0's input S-boxes
+    const uint64_t o_part = o_full + 4 * (uint64_t)T * (half - 1);       // partial rounds
+    const uint64_t o_last = o_part + 4 * (uint64_t)k.rp;                 // last full rounds
 #pragma unroll 1
     for (int r = 0; r < half; r++) {
-        if (j < T) x = fr29_sbox(fr29_add(x, img[k.off_rc_first + r * T + j]));
+        if (j < T) {
+            const fr29_t v = fr29_add(x, img[k.off_rc_first + r * T + j]);
+            if (r == 0 && j == 0) x = fr29_sbox(v);  // the domain tag's first S-box: a constant, no variables
+            else if (r == 0) x = sbox_emit(v, base + 3 * (uint64_t)(j - 1), false);
+            else x = sbox_emit(v, base + o_full + 4 * (uint64_t)T * (r - 1) + 4 * (uint64_t)j, true);
+        }
         x = group_row<T>(x, mds, j);
     }
     const fr29_t *sp = img + k.off_sparse;
 #pragma unroll 1
     for (int q = 0; q < k.rp - 1; q++, sp += 2 * T - 1) {
-        if (j == 0) x = fr29_sbox(fr29_add(x, img[k.off_rc_part + q]));
+        if (j == 0) x = sbox_emit(fr29_add(x, img[k.off_rc_part + q]), base + o_part + 4 * (uint64_t)q, true);
         const fr29_t s0 = shfl29(x, 0);
         fr29_t term = j < T ? fr29_mul(sp[j], x) : zero29();  // row_j s_j (s_0 after its S-box)
         MI_UNROLL for (int m = 1; m < 16; m <<= 1)
@@ -439,32 +466,38 @@ __global__ void __launch_bounds__(64) k_wit_poseidon_lanes(const WOp *__restrict
         if (j == 0) x = term;
         else if (j < T) x = fr29_sub_if_ge(fr29_add(x, fr29_mul(sp[T + j - 1], s0)), R2X29);
     }
-    if (j == 0) x = fr29_sbox(fr29_add(x, img[k.off_rc_part + k.rp - 1]));
+    if (j == 0)
+        x = sbox_emit(fr29_add(x, img[k.off_rc_part + k.rp - 1]), base + o_part + 4 * (uint64_t)(k.rp - 1), true);
     x = group_row<T>(x, img + k.off_dense, j);
 #pragma unroll 1
     for (int r = 0; r < half; r++) {
-        if (j < T) x = fr29_sbox(fr29_add(x, img[k.off_rc_last + r * T + j]));
+        if (j < T)
+            x = sbox_emit(fr29_add(x, img[k.off_rc_last + r * T + j]), base + o_last + 4 * (uint64_t)T * r + 4 * (uint64_t)j,
+                          true);
         x = group_row<T>(x, mds, j);
     }
-    if (j == 1) zput_fr(z, op.b, fr_from_fr29(fr29_from_mont(x)));
+    if (j == 1) {
+        if (EXPAND) zput29(z, base + o_last + 4 * (uint64_t)T * half, x);
+        else zput_fr(z, op.b, fr_from_fr29(fr29_from_mont(x)));
+    }
 }
 
 template <bool EXPAND>
 void launch_poseidon(int kind, hipStream_t st, const WOp *ops, const uint64_t *idx, uint64_t n, const uint64_t *pin,
                      const PosKs &pk, fr_t *z) {
     const unsigned g = (unsigned)((n + 63) / 64);
-    // MI_WIT_POS_LANES=0 (read per call, A/B): phase A one thread per hash as phase B
+    // MI_WIT_POS_LANES=0 (read once, A/B): one thread per hash, phase A and phase B
     static const bool lanes_env = [] {
         const char *e = getenv("MI_WIT_POS_LANES");
         return !(e && atoi(e) == 0);
     }();
-    if (!EXPAND && lanes_env) {
+    if (lanes_env) {
         const unsigned g4 = (unsigned)((n + 3) / 4);
         switch (kind) {
-            case 1: k_wit_poseidon_lanes<3><<<g4, 64, 0, st>>>(ops, n, pin, pk.k[0], z); break;
-            case 2: k_wit_poseidon_lanes<5><<<g4, 64, 0, st>>>(ops, n, pin, pk.k[1], z); break;
-            case 3: k_wit_poseidon_lanes<9><<<g4, 64, 0, st>>>(ops, n, pin, pk.k[2], z); break;
-            default: k_wit_poseidon_lanes<12><<<g4, 64, 0, st>>>(ops, n, pin, pk.k[3], z); break;
+            case 1: k_wit_poseidon_lanes<3, EXPAND><<<g4, 64, 0, st>>>(ops, idx, n, pin, pk.k[0], z); break;
+            case 2: k_wit_poseidon_lanes<5, EXPAND><<<g4, 64, 0, st>>>(ops, idx, n, pin, pk.k[1], z); break;
+            case 3: k_wit_poseidon_lanes<9, EXPAND><<<g4, 64, 0, st>>>(ops, idx, n, pin, pk.k[2], z); break;
+            default: k_wit_poseidon_lanes<12, EXPAND><<<g4, 64, 0, st>>>(ops, idx, n, pin, pk.k[3], z); break;
         }
         return;
     }
