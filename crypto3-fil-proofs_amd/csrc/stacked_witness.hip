@@ -486,12 +486,15 @@ template <bool EXPAND>
 void launch_poseidon(int kind, hipStream_t st, const WOp *ops, const uint64_t *idx, uint64_t n, const uint64_t *pin,
                      const PosKs &pk, fr_t *z) {
     const unsigned g = (unsigned)((n + 63) / 64);
-    // MI_WIT_POS_LANES=0 (read once, A/B): one thread per hash, phase A and phase B
-    static const bool lanes_env = [] {
+    // 16 lanes per hash shorten a hash 4-5x but use T of 16 lanes: the form for launches too small to fill the
+    // chip (phase A levels; the stacked partition's 3,151 and the Winning-PoSt proof's 726 phase-B gadgets).
+    // A launch of thousands of waves (the Window-PoSt partition's 237 K phase-B gadgets, 23 K per phase-A level)
+    // keeps one thread per hash.  MI_WIT_POS_LANES (read once): the largest launch on lanes, 0 = never.
+    static const uint64_t lanes_max = [] {
         const char *e = getenv("MI_WIT_POS_LANES");
-        return !(e && atoi(e) == 0);
+        return e ? (uint64_t)atoll(e) : (uint64_t)16384;
     }();
-    if (lanes_env) {
+    if (n <= lanes_max) {
         const unsigned g4 = (unsigned)((n + 3) / 4);
         switch (kind) {
             case 1: k_wit_poseidon_lanes<3, EXPAND><<<g4, 64, 0, st>>>(ops, idx, n, pin, pk.k[0], z); break;
