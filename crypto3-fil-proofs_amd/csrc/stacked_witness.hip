@@ -487,12 +487,13 @@ void launch_poseidon(int kind, hipStream_t st, const WOp *ops, const uint64_t *i
                      const PosKs &pk, fr_t *z) {
     const unsigned g = (unsigned)((n + 63) / 64);
     // 16 lanes per hash shorten a hash 4-5x but use T of 16 lanes: the form for launches too small to fill the
-    // chip (phase A levels; the stacked partition's 3,151 and the Winning-PoSt proof's 726 phase-B gadgets).
-    // A launch of thousands of waves (the Window-PoSt partition's 237 K phase-B gadgets, 23 K per phase-A level)
-    // keeps one thread per hash.  MI_WIT_POS_LANES (read once): the largest launch on lanes, 0 = never.
+    // chip with one thread per hash (phase A levels -- 23 K hashes per level of the Window-PoSt partition are 367
+    // waves for 1,024 SIMDs --, the stacked partition's 3,151 and the Winning-PoSt proof's 726 phase-B gadgets).
+    // The Window-PoSt partition's 237 K phase-B gadgets (3.7 K waves) keep one thread per hash: on lanes they
+    // took 17.5 ms instead of 6.  MI_WIT_POS_LANES (read once): the largest launch on lanes, 0 = never.
     static const uint64_t lanes_max = [] {
         const char *e = getenv("MI_WIT_POS_LANES");
-        return e ? (uint64_t)atoll(e) : (uint64_t)16384;
+        return e ? (uint64_t)atoll(e) : (uint64_t)65536;
     }();
     if (n <= lanes_max) {
         const unsigned g4 = (unsigned)((n + 3) / 4);
