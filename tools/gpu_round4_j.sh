@@ -7,6 +7,3 @@ echo "pytest rc=$rc"; tail -2 gpurun_out/r04_gpu_tests_final.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r04_smoke_final.log 2>&1 || exit 1
 tail -1 gpurun_out/r04_smoke_final.log
-timeout -k 10 900 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r04_bench_default.json 2> gpurun_out/r04_bench_default.err
-echo "bench rc=$?"; grep "^\[bench\]" gpurun_out/r04_bench_default.err | tail -4
-bash tools/lane_prof1.sh r04_lane1

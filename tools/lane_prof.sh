@@ -5,7 +5,7 @@
 set -e
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
 T=${1:-lane}; shift || true
-B="python3 bench.py --steps 3 --warmup 1 --msm-reps 1 --no-cpu-baseline --no-device-resident --tree-log-nodes 0 --config4-log-rows 0 --sdr-log-labels 0 --stacked-log-nodes 0 --post-sectors 0 $*"
+B="python3 bench.py --steps 3 --warmup 1 --msm-reps 1 --no-cpu-baseline --no-device-resident --tree-log-nodes 0 --config4-log-rows 0 --sdr-log-labels 0 --stacked-log-nodes 0 --post-sectors 0 --winning-log-nodes 0 --uniform-steps 0 $*"
 mkdir -p gpurun_out/$T
 timeout -k 10 300 $B > gpurun_out/$T/two_lanes.json 2> gpurun_out/$T/two_lanes.err
 MI_PROVE_LANES=1 timeout -k 10 300 $B > gpurun_out/$T/one_lane.json 2> gpurun_out/$T/one_lane.err
