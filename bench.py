@@ -1206,7 +1206,7 @@ def main():
     ceiling = None
     if os.path.isdir(prof_dir) and grp == "G1":
         for fn in sorted(os.listdir(prof_dir), reverse=True):
-            if fn.startswith("r03_maddloop") and fn.endswith(".jsonl"):
+            if "_maddloop" in fn and fn.endswith(".jsonl"):  # the newest round's microbenchmark with the gather128 form
                 rows = [json.loads(l) for l in open(os.path.join(prof_dir, fn)) if l.strip().startswith("{")]
                 g = [r for r in rows if r.get("form") == "gather128"]
                 if g:
