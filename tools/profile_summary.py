@@ -60,8 +60,8 @@ def step_launch_avg_ms(trace_dir, kernel_substr, bench):
 
 
 def g1_launch_points(bench):
-    """points processed by each k_accum_level0<G1> launch of `bench.py --warmup 1 --steps 1`:
-    per prove H, L, A, B_G1; then the standalone MSM (1 warm + msm_reps)."""
+    """points processed by each k_accum_level0<G1> launch of `bench.py --warmup W --steps K` in submission
+    (dispatch-id) order: per prove H, L, A, B_G1; then the standalone MSM (1 warm + msm_reps)."""
     cfg = bench["config"]
     per_prove = [cfg["domain"] - 1, cfg["num_aux"], cfg["a_query"], cfg["b_query"]]
     proves = bench["warmup"] + bench["steps"]
@@ -77,11 +77,12 @@ def main():
     ap.add_argument("--write")
     ap.add_argument("--bench-json", required=True)
     ap.add_argument("--kernel", default="k_accum_level0<mi::fq_t>")
+    ap.add_argument("--command-file", help="the profiled bench command (tools/prof_round.sh writes <tag>_command.txt)")
     args = ap.parse_args()
     bench = json.loads(open(args.bench_json).read().strip().splitlines()[-1])
     bench.setdefault("msm_reps", 1)
-    out = {"tag": args.tag, "command": "rocprofv3 --kernel-trace --stats / --pmc FETCH_SIZE / --pmc WRITE_SIZE -- "
-                                       "python3 bench.py --steps 1 --warmup 1 --msm-reps 1 --no-cpu-baseline --no-device-resident --tree-log-nodes 0 --config4-log-rows 0 --sdr-log-labels 0 --stacked-log-nodes 0 --post-sectors 0 --winning-log-nodes 0 --uniform-steps 0",
+    cmd = open(args.command_file).read().strip() if args.command_file else "python3 bench.py (see tools/prof_round.sh)"
+    out = {"tag": args.tag, "command": "rocprofv3 --kernel-trace --stats / --pmc FETCH_SIZE / --pmc WRITE_SIZE -- " + cmd,
            "workload": bench["config"]["workload"], "bench_value_under_profiler": bench["value"],
            "kernels": kernel_stats(args.trace)}
     try:  # the source revision the profiled build came from (bench.py reports it as roofline.traffic_detail)
