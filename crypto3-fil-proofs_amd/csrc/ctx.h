@@ -69,6 +69,35 @@ struct DevBuf {
     ~DevBuf() { release(); }
 };
 
+// Page-locked host staging for the small device -> host readbacks of a lane (bucket counts, chunk totals, window
+// sums).  A pageable destination makes HIP stage the copy and hold the host thread inside hipMemcpyAsync until
+// the stream drains, and those staged copies serialise across threads: in a Winning-PoSt proof (four lanes) a
+// lane's synchronisation stalled 2-4 ms behind another lane's pending copy (rocprofv3 HIP runtime trace,
+// DESIGN §5).  Copies into this buffer are plain asynchronous DMA, waited for by the lane's own stream sync.
+struct PinnedBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    void *get(size_t bytes) {
+        if (bytes > cap) {
+            release();
+            const size_t want = bytes < 65536 ? 65536 : bytes;
+            MI_HIP(hipHostMalloc(&p, want, hipHostMallocDefault));
+            cap = want;
+        }
+        return p;
+    }
+    template <class T>
+    T *as(size_t count) {
+        return (T *)get(count * sizeof(T));
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    ~PinnedBuf() { release(); }
+};
+
 // Twiddle tables for every power-of-two domain up to 2^32 (bellman: Fr::ROOT_OF_UNITY with
 // S = 32, multiplicative generator 7).  w^e for e < 2^32 = LO[e & 0xffff] * HI[e >> 16].
 struct NttTables {
@@ -181,10 +210,11 @@ struct Ctx {
                          // 21-22: witness slots (capi.hip uploader; 21 also building-block inputs)
     Stats stats;
     EventTimer timer;
+    PinnedBuf pin;  // small readbacks (msm_impl.h); one lane's, reused call after call
     // Auxiliary lane: a second stream with its own scratch arena and timers, driven from a second
     // host thread inside one prove so MSMs that do not depend on the NTT chain overlap it (the
     // accumulation is VALU-bound, the NTT / sort phases are LDS- / HBM-bound).  Created on first
-    // use; ctx_aux_free releases it.
+    // use; ctx_aux_free releases it.  An auxiliary lane's own `aux` is the next lane (small proofs run three).
     Ctx *aux = nullptr;
     hipStream_t aux_streams[2] = {nullptr, nullptr};  // (in the aux ctx) normal, high priority
 };

@@ -693,7 +693,7 @@ inline bool plan_chunks(Ctx &c, MsmPlan &pl, uint32_t *offA, uint32_t *cntA, uin
     MI_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, ccnt, coff, nb, st));
     void *tmp = c.scratch[4].get(tmp_bytes);
     MI_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, ccnt, coff, nb, st));
-    uint32_t tail[2];
+    uint32_t *tail = c.pin.as<uint32_t>(2);
     MI_HIP(hipMemcpyAsync(&tail[0], coff + nb - 1, 4, hipMemcpyDeviceToHost, st));
     MI_HIP(hipMemcpyAsync(&tail[1], ccnt + nb - 1, 4, hipMemcpyDeviceToHost, st));
     MI_HIP(hipStreamSynchronize(st));
@@ -805,8 +805,10 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
                                                               vals);
                 MI_LAUNCHED(c, "k_digits_c");
             }
-            MI_HIP(hipMemcpyAsync(wn.data(), wcount, sizeof(uint32_t) * nwin, hipMemcpyDeviceToHost, st));
+            uint32_t *wn_pin = c.pin.as<uint32_t>(nwin);
+            MI_HIP(hipMemcpyAsync(wn_pin, wcount, sizeof(uint32_t) * nwin, hipMemcpyDeviceToHost, st));
             MI_HIP(hipStreamSynchronize(st));
+            std::copy(wn_pin, wn_pin + nwin, wn.begin());
             sort_pairs_u32(nullptr, tmp_bytes, keys, keys_s, vals, vals_s, (uint32_t)n, key_bits, st);
             void *tmp = c.scratch[4].get(tmp_bytes);
             for (unsigned w = 0; w < nwin; w++) {
@@ -849,8 +851,10 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
         MI_HIP(hipcub::DeviceReduce::Max(nullptr, tmp_bytes, cntA, dmax, nb, st));
         void *tmp = c.scratch[4].get(tmp_bytes);
         MI_HIP(hipcub::DeviceReduce::Max(tmp, tmp_bytes, cntA, dmax, nb, st));
-        MI_HIP(hipMemcpyAsync(head.data(), dmax, sizeof(uint32_t) * (4 + nwin), hipMemcpyDeviceToHost, st));
+        uint32_t *head_pin = c.pin.as<uint32_t>(4 + nwin);
+        MI_HIP(hipMemcpyAsync(head_pin, dmax, sizeof(uint32_t) * (4 + nwin), hipMemcpyDeviceToHost, st));
         MI_HIP(hipStreamSynchronize(st));
+        std::copy(head_pin, head_pin + 4 + nwin, head.begin());
     }
     pl.maxcnt = head[0];
     pl.entries = 0;  // non-zero digits = mixed additions of the accumulation
@@ -896,9 +900,10 @@ XYZZ<F> *accumulate_chunks(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, co
         MI_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, ids, flag, mlist, dm, nb, st));
         void *tmp = c.scratch[4].get(tb);
         MI_HIP(hipcub::DeviceSelect::Flagged(tmp, tb, ids, flag, mlist, dm, nb, st));
-        uint32_t m = 0;
-        MI_HIP(hipMemcpyAsync(&m, dm, 4, hipMemcpyDeviceToHost, st));
+        uint32_t *m_pin = c.pin.as<uint32_t>(1);
+        MI_HIP(hipMemcpyAsync(m_pin, dm, 4, hipMemcpyDeviceToHost, st));
         MI_HIP(hipStreamSynchronize(st));
+        const uint32_t m = *m_pin;
         uint32_t *qcnt = c.scratch[2].as<uint32_t>(m), *qoff = c.scratch[11].as<uint32_t>(m);
         for (uint64_t stride = 1; stride < maxchunks; stride *= L1) {
             k_tree_count<<<grid_for(m, 256), 256, 0, st>>>(mlist, ccnt, m, (uint32_t)stride, qcnt);
@@ -907,7 +912,7 @@ XYZZ<F> *accumulate_chunks(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, co
             MI_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, qcnt, qoff, m, st));
             tmp = c.scratch[4].get(tb);
             MI_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, qcnt, qoff, m, st));
-            uint32_t tail[2];
+            uint32_t *tail = c.pin.as<uint32_t>(2);
             MI_HIP(hipMemcpyAsync(&tail[0], qoff + m - 1, 4, hipMemcpyDeviceToHost, st));
             MI_HIP(hipMemcpyAsync(&tail[1], qcnt + m - 1, 4, hipMemcpyDeviceToHost, st));
             MI_HIP(hipStreamSynchronize(st));
@@ -977,9 +982,10 @@ void reduce_windows(Ctx &c, const MsmPlan &pl, XYZZ<F> *P0, std::vector<XYZZ<F>>
         cur = bufs[k];
         k ^= 1;
     }
-    std::vector<XYZZ<F>> sums(rows);
-    MI_HIP(hipMemcpyAsync(sums.data(), cur, sizeof(XYZZ<F>) * rows, hipMemcpyDeviceToHost, st));
+    XYZZ<F> *sums_pin = c.pin.as<XYZZ<F>>(rows);
+    MI_HIP(hipMemcpyAsync(sums_pin, cur, sizeof(XYZZ<F>) * rows, hipMemcpyDeviceToHost, st));
     MI_HIP(hipStreamSynchronize(st));
+    std::vector<XYZZ<F>> sums(sums_pin, sums_pin + rows);
     W.assign(nwin, XYZZ<F>::inf());
     for (unsigned w = 0; w < nwin; w++) {  // W = SumA + SA * (V - R)
         const XYZZ<F> &SumA = sums[w], &R = sums[nwin + w], &V = sums[2 * nwin + w];
@@ -1048,7 +1054,7 @@ bool g2_second_level(Ctx &c, const MsmPlan &pl, XYZZ<F> *P0, std::vector<XYZZ<F>
         k_end_to_cnt<<<grid_for(nb2, 256), 256, 0, st>>>(off2, cnt2, nb2);
         MI_LAUNCHED(c, "k_end_to_cnt");
         uint32_t *dm = c.scratch[9].as<uint32_t>(4);
-        uint32_t head[2] = {0, 0};
+        uint32_t *head = c.pin.as<uint32_t>(2);
         tmp_bytes = 0;
         MI_HIP(hipcub::DeviceReduce::Max(nullptr, tmp_bytes, cnt2, dm, nb2, st));
         size_t tb2 = 0;
@@ -1056,7 +1062,7 @@ bool g2_second_level(Ctx &c, const MsmPlan &pl, XYZZ<F> *P0, std::vector<XYZZ<F>
         tmp = c.scratch[4].get(tmp_bytes > tb2 ? tmp_bytes : tb2);
         MI_HIP(hipcub::DeviceReduce::Max(tmp, tmp_bytes, cnt2, dm, nb2, st));
         MI_HIP(hipcub::DeviceReduce::Sum(tmp, tb2, cnt2, dm + 1, nb2, st));
-        MI_HIP(hipMemcpyAsync(head, dm, sizeof(head), hipMemcpyDeviceToHost, st));
+        MI_HIP(hipMemcpyAsync(head, dm, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         MI_HIP(hipStreamSynchronize(st));
         MsmPlan p2;
         p2.n = head[1];

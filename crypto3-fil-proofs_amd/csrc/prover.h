@@ -156,6 +156,15 @@ uint64_t srs_drop_split_tables(Srs &S);
 uint64_t release_for_retry(Ctx &c, const Srs *first, const void *keep);
 // A = alpha + A_sum + r delta, B = beta + B2_sum + s delta, C = H + L + s A + r B1 - r s delta (host)
 ProofPoints groth16_assemble(const AssemblyKey &k, const ProofSums &sums, const fr_t &r, const fr_t &s);
+// The assembly's terms that depend on the blinding and the key only (five of its seven host scalar
+// multiplications): groth16_prove computes them on a host thread while the device runs the MSMs.
+struct BlindTerms {
+    g1_xyzz_t A0;  // alpha + r delta (G1)
+    g2_xyzz_t B0;  // beta + s delta (G2)
+    g1_xyzz_t C0;  // r s delta + s alpha + r beta (G1)
+};
+BlindTerms groth16_blind_terms(const AssemblyKey &k, const fr_t &r, const fr_t &s);
+ProofPoints groth16_finish(const BlindTerms &t, const ProofSums &sums, const fr_t &r, const fr_t &s);
 AssemblyKey assembly_key(const Srs &srs);
 // share wire format (MI_SHARE_BYTES = 576): H | L | A | B_G1 (96 B each) | B_G2 (192 B), zcash uncompressed
 void sums_encode(const ProofSums &sums, uint8_t out[576]);

@@ -24,6 +24,7 @@
 #include <unordered_map>
 
 #include "prover.h"
+#include <future>
 
 namespace mi {
 
@@ -1136,8 +1137,8 @@ Srs *srs_generate_once(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5
         // 32 GiB partition): key generation is one-time, so give them back before the table decision and
         // the first proof
         for (auto &b : c.scratch) b.release();
-        if (c.aux)  // and the auxiliary lane's arena (earlier proofs' B / L plans)
-            for (auto &b : c.aux->scratch) b.release();
+        for (Ctx *x = c.aux; x; x = x->aux)  // and the auxiliary lanes' arenas (earlier proofs' B / L / A plans)
+            for (auto &b : x->scratch) b.release();
         // verifying key
         S->alpha_g1 = host_mul_affine(g1, toxic_canonical[1]);
         S->beta_g1 = host_mul_affine(g1, toxic_canonical[2]);
@@ -1201,40 +1202,81 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
             const char *e = getenv("MI_PROVE_LANES");
             return e && atoi(e) == 1;
         }();
-        Ctx &x = one_lane ? c : ctx_aux(c);
-        hipEvent_t ready = x.timer.get(), done = x.timer.get();
+        // Small proofs (domain <= 2^MI_PROVE_WIDE_LOG, default 2^21: Winning PoSt, 2^19) are latency-bound: their
+        // MSMs' bucket reductions, sorts and host round trips leave most CUs idle, so B, L and A each get a lane
+        // of their own (three auxiliary streams and host threads beside the main lane's witness map, NTT chain
+        // and H).  Large proofs keep two lanes: their accumulation fills the chip and every lane holds a scratch
+        // arena sized to its MSMs.  Read per call (tests compare the two layouts).
+        const char *we = getenv("MI_PROVE_WIDE_LOG");
+        const unsigned wide_log = we ? (unsigned)atoi(we) : 21u;
+        const bool wide = !one_lane && L <= wide_log;
+        const unsigned nlanes = wide ? 3 : 1;
+        Ctx *lane_ctx[3] = {one_lane ? &c : &ctx_aux(c), nullptr, nullptr};
+        for (unsigned k = 1; k < nlanes; k++) lane_ctx[k] = &ctx_aux(*lane_ctx[k - 1]);
+        hipEvent_t ready = c.timer.get(), done[3] = {nullptr, nullptr, nullptr};
         MI_HIP(hipEventRecord(ready, st));  // z_dev and everything queued before this prove
-        MI_HIP(hipStreamWaitEvent(x.stream, ready, 0));
-        std::exception_ptr err;
-        auto aux_work = [&] {
+        for (unsigned k = 0; k < nlanes; k++) {
+            done[k] = lane_ctx[k]->timer.get();
+            MI_HIP(hipStreamWaitEvent(lane_ctx[k]->stream, ready, 0));
+        }
+        std::exception_ptr err[3];
+        // B_G1 and B_G2 share the scalars (z over the B-density): sort them once.  MI_PROVE_B1_LANE = 1 / 2 (small
+        // proofs only) moves B_G1 after L / after A on that lane, which sorts the scalars again for itself (no
+        // plan is shared between lanes: the G2 second level reuses its plan's scratch)
+        const char *b1e = getenv("MI_PROVE_B1_LANE");
+        const unsigned b1_lane = wide && b1e ? (unsigned)atoi(b1e) : 0u;
+        auto run_b = [&](Ctx &x) {
+            const uint64_t lo = rg.lo[3], cnt = rg.cnt[3];
+            MsmPlan pb;
+            msm_prepare(x, z_dev, circ.idx_b + lo, cnt, pb);
+            if (b1_lane == 0) msm_g1_planned(x, pb, srs.b_g1 + lo, &B1);
+            msm_g2_planned(x, pb, srs.b_g2 + lo, &B2);
+        };
+        auto run_b1 = [&](Ctx &x) {
+            const uint64_t lo = rg.lo[3], cnt = rg.cnt[3];
+            msm_g1(x, srs.b_g1 + lo, z_dev, circ.idx_b + lo, cnt, &B1, nullptr, srs.in_subgroup);
+        };
+        auto run_l = [&](Ctx &x) {
+            const uint64_t l_lo = rg.lo[1], l_cnt = rg.cnt[1];
+            msm_g1(x, srs.l + l_lo, z_dev + circ.n_in + l_lo, nullptr, l_cnt, &Lq, srs.l_hi ? srs.l_hi + l_lo : nullptr,
+                   srs.in_subgroup);
+        };
+        auto run_a = [&](Ctx &x) {
+            const uint64_t a_lo = rg.lo[2], a_cnt = rg.cnt[2];
+            msm_g1(x, srs.a + a_lo, z_dev, circ.idx_a + a_lo, a_cnt, &As, srs.a_hi ? srs.a_hi + a_lo : nullptr,
+                   srs.in_subgroup);
+        };
+        // aux-lane order: B before L (same-box A/B at 2^26: -2 ms per proof; MI_AUX_ORDER=l_first
+        // restores L first)
+        static const bool b_first = [] {
+            const char *e = getenv("MI_AUX_ORDER");
+            return !(e && strcmp(e, "l_first") == 0);
+        }();
+        auto lane_work = [&](unsigned k) {
             try {
+                Ctx &x = *lane_ctx[k];
                 MI_HIP(hipSetDevice(c.device));
-                // B_G1 and B_G2 share the scalars (z over the B-density): sort them once
-                auto run_b = [&] {
-                    const uint64_t lo = rg.lo[3], cnt = rg.cnt[3];
-                    MsmPlan pb;
-                    msm_prepare(x, z_dev, circ.idx_b + lo, cnt, pb);
-                    msm_g1_planned(x, pb, srs.b_g1 + lo, &B1);
-                    msm_g2_planned(x, pb, srs.b_g2 + lo, &B2);
-                };
-                // aux-lane order: B before L (same-box A/B at 2^26: -2 ms per proof; MI_AUX_ORDER=l_first
-                // restores L first)
-                static const bool b_first = [] {
-                    const char *e = getenv("MI_AUX_ORDER");
-                    return !(e && strcmp(e, "l_first") == 0);
-                }();
-                if (b_first) run_b();
-                const uint64_t l_lo = rg.lo[1], l_cnt = rg.cnt[1];
-                msm_g1(x, srs.l + l_lo, z_dev + circ.n_in + l_lo, nullptr, l_cnt, &Lq,
-                       srs.l_hi ? srs.l_hi + l_lo : nullptr, srs.in_subgroup);
-                if (!b_first) run_b();
-                MI_HIP(hipEventRecord(done, x.stream));
+                if (!wide) {
+                    if (b_first) run_b(x);
+                    run_l(x);
+                    if (!b_first) run_b(x);
+                } else if (k == 0) {
+                    run_b(x);
+                } else if (k == 1) {
+                    run_l(x);
+                    if (b1_lane == 1) run_b1(x);
+                } else {
+                    run_a(x);
+                    if (b1_lane == 2) run_b1(x);
+                }
+                MI_HIP(hipEventRecord(done[k], x.stream));
             } catch (...) {
-                err = std::current_exception();
+                err[k] = std::current_exception();
             }
         };
-        std::thread lane;
-        if (!one_lane) lane = std::thread(aux_work);
+        std::thread lanes[3];
+        if (!one_lane)
+            for (unsigned k = 0; k < nlanes; k++) lanes[k] = std::thread(lane_work, k);
         std::exception_ptr err_main;
         try {
             fr_t *a = nullptr;
@@ -1267,31 +1309,36 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
             }
             if (inject_oom) (void)c.scratch[19].get(1ull << 50);  // a real failed growth (1 PiB), as a scratch
                                                                     // buffer's hipMalloc fails when HBM is short
-            const uint64_t h_lo = rg.lo[0], h_cnt = rg.cnt[0], a_lo = rg.lo[2], a_cnt = rg.cnt[2];
+            const uint64_t h_lo = rg.lo[0], h_cnt = rg.cnt[0];
             if (need_h)
                 msm_g1(c, srs.h_perm + h_lo, a + h_lo, nullptr, h_cnt, &H, srs.h_hi ? srs.h_hi + h_lo : nullptr,
                        srs.in_subgroup);
             else
                 H = g1_xyzz_t::inf();
-            msm_g1(c, srs.a + a_lo, z_dev, circ.idx_a + a_lo, a_cnt, &As, srs.a_hi ? srs.a_hi + a_lo : nullptr,
-                   srs.in_subgroup);
+            if (!wide) run_a(c);
         } catch (...) {
             err_main = std::current_exception();
         }
         if (one_lane) {
-            if (!err_main) aux_work();
+            if (!err_main) lane_work(0);
         } else {
-            lane.join();
+            for (unsigned k = 0; k < nlanes; k++) lanes[k].join();
         }
         if (err_main) std::rethrow_exception(err_main);
-        if (err) std::rethrow_exception(err);
-        MI_HIP(hipStreamWaitEvent(st, done, 0));  // the prove timer ends after both lanes
-        x.timer.pool.push_back(ready);
-        x.timer.pool.push_back(done);
+        for (unsigned k = 0; k < nlanes; k++)
+            if (err[k]) std::rethrow_exception(err[k]);
+        for (unsigned k = 0; k < nlanes; k++) {
+            MI_HIP(hipStreamWaitEvent(st, done[k], 0));  // the prove timer ends after every lane
+            lane_ctx[k]->timer.pool.push_back(done[k]);
+        }
+        c.timer.pool.push_back(ready);
         if (!one_lane) {
-            x.timer.resolve();
-            c.stats.merge(x.stats);
-            x.stats = Stats();
+            for (unsigned k = 0; k < nlanes; k++) {
+                Ctx &x = *lane_ctx[k];
+                x.timer.resolve();
+                c.stats.merge(x.stats);
+                x.stats = Stats();
+            }
         }
     }
     }
@@ -1348,7 +1395,7 @@ uint64_t release_device_tables(int device, const Srs *first) {
     return freed;
 }
 
-// releases a context's grow-only scratch (both lanes), except the witness slots of the batch uploader (21, 22:
+// releases a context's grow-only scratch (every lane), except the witness slots of the batch uploader (21, 22:
 // the next partition may be uploading into the other one) and any buffer holding `keep` (the proof's witness)
 uint64_t release_prover_scratch(Ctx &c, const void *keep) {
     uint64_t freed = 0;
@@ -1362,14 +1409,14 @@ uint64_t release_prover_scratch(Ctx &c, const void *keep) {
         }
     };
     rel(c, 21);
-    if (c.aux) rel(*c.aux, 24);
+    for (Ctx *x = c.aux; x; x = x->aux) rel(*x, 24);
     return freed;
 }
 }  // namespace
 
 uint64_t release_for_retry(Ctx &c, const Srs *first, const void *keep) {
     (void)hipStreamSynchronize(c.stream);
-    if (c.aux) (void)hipStreamSynchronize(c.aux->stream);
+    for (Ctx *x = c.aux; x; x = x->aux) (void)hipStreamSynchronize(x->stream);
     (void)hipGetLastError();  // the failed allocation's error, so the retry's launch checks start clean
     return release_device_tables(c.device, first) + release_prover_scratch(c, keep);
 }
@@ -1414,30 +1461,47 @@ AssemblyKey assembly_key(const Srs &srs) {
 }
 
 // libsnark r1cs_gg_ppzksnark_prover / bellman create_proof: the blinded proof from the five MSM sums
-ProofPoints groth16_assemble(const AssemblyKey &k, const ProofSums &m, const fr_t &r, const fr_t &s) {
-    fr_t rs = from_mont(to_mont(r) * to_mont(s));
-    // A = alpha + sum z_i A_i + r delta;  B = beta + sum z_i B_i + s delta (G2), B1 likewise in G1
-    g1_xyzz_t A = xyzz_add(xyzz_add_affine(m.A, k.alpha_g1), xyzz_mul(xyzz_from_affine(k.delta_g1), r.v, 8));
-    g2_xyzz_t B = xyzz_add(xyzz_add_affine(m.B2, k.beta_g2), xyzz_mul(xyzz_from_affine(k.delta_g2), s.v, 8));
-    // C = H + L + s A + r B1 - r s delta, expanded so that A and B1 enter without their blinding:
-    //   s (alpha + A_sum + r delta) + r (beta + B1_sum + s delta) - r s delta = s alpha + r beta + s A_sum + r B1_sum + r s delta
+//   A = alpha + sum z_i A_i + r delta;  B = beta + sum z_i B_i + s delta (G2), B1 likewise in G1
+//   C = H + L + s A + r B1 - r s delta, expanded so that A and B1 enter without their blinding:
+//   s (alpha + A_sum + r delta) + r (beta + B1_sum + s delta) - r s delta = s alpha + r beta + s A_sum + r B1_sum + r s delta
+BlindTerms groth16_blind_terms(const AssemblyKey &k, const fr_t &r, const fr_t &s) {
+    const fr_t rs = from_mont(to_mont(r) * to_mont(s));
+    BlindTerms t;
+    t.A0 = xyzz_add_affine(xyzz_mul(xyzz_from_affine(k.delta_g1), r.v, 8), k.alpha_g1);
+    t.B0 = xyzz_add_affine(xyzz_mul(xyzz_from_affine(k.delta_g2), s.v, 8), k.beta_g2);
     g1_xyzz_t C = xyzz_mul(xyzz_from_affine(k.delta_g1), rs.v, 8);
     C = xyzz_add(C, xyzz_mul(xyzz_from_affine(k.alpha_g1), s.v, 8));
-    C = xyzz_add(C, xyzz_mul(xyzz_from_affine(k.beta_g1), r.v, 8));
-    C = xyzz_add(C, xyzz_mul(m.A, s.v, 8));
-    C = xyzz_add(C, xyzz_mul(m.B1, r.v, 8));
+    t.C0 = xyzz_add(C, xyzz_mul(xyzz_from_affine(k.beta_g1), r.v, 8));
+    return t;
+}
+
+ProofPoints groth16_finish(const BlindTerms &t, const ProofSums &m, const fr_t &r, const fr_t &s) {
+    // the two multiplications by MSM sums run side by side (one on a helper thread)
+    auto sA = std::async(std::launch::async, [&] { return xyzz_mul(m.A, s.v, 8); });
+    const g1_xyzz_t rB1 = xyzz_mul(m.B1, r.v, 8);
+    g1_xyzz_t C = xyzz_add(t.C0, sA.get());
+    C = xyzz_add(C, rB1);
     C = xyzz_add(C, m.H);
     C = xyzz_add(C, m.L);
     ProofPoints out;
-    out.A = xyzz_to_affine(A);
-    out.B = xyzz_to_affine(B);
+    out.A = xyzz_to_affine(xyzz_add(m.A, t.A0));
+    out.B = xyzz_to_affine(xyzz_add(m.B2, t.B0));
     out.C = xyzz_to_affine(C);
     return out;
 }
 
+ProofPoints groth16_assemble(const AssemblyKey &k, const ProofSums &m, const fr_t &r, const fr_t &s) {
+    return groth16_finish(groth16_blind_terms(k, r, s), m, r, s);
+}
+
 ProofPoints groth16_prove(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, const fr_t &r,
                           const fr_t &s) {
-    return groth16_assemble(assembly_key(srs), groth16_sums(c, srs, circ, z_dev), r, s);
+    // the blinding-only terms on a host thread while the device works (Winning PoSt: ~4 ms of host scalar
+    // multiplications off a ~25 ms proof)
+    const AssemblyKey key = assembly_key(srs);
+    auto terms = std::async(std::launch::async, [&] { return groth16_blind_terms(key, r, s); });
+    const ProofSums m = groth16_sums(c, srs, circ, z_dev);
+    return groth16_finish(terms.get(), m, r, s);
 }
 
 void sums_encode(const ProofSums &m, uint8_t out[576]) {
@@ -1480,6 +1544,7 @@ Ctx &ctx_aux(Ctx &c) {
 
 void ctx_aux_free(Ctx &c) {
     if (!c.aux) return;
+    ctx_aux_free(*c.aux);  // the lanes after it (small proofs use a chain of three)
     for (auto &b : c.aux->scratch) b.release();
     for (auto s : c.aux->aux_streams)
         if (s) hipStreamDestroy(s);

@@ -180,6 +180,23 @@ def test_prove_batch_and_priority(ctx, oracle):
     assert fg.MultiProof.from_bytes(mp.to_bytes()).circuit_proofs == proofs
 
 
+def test_prove_lane_layouts_identical(ctx, oracle, monkeypatch):
+    """Small proofs (domain <= 2^MI_PROVE_WIDE_LOG, default 2^21) run B, L and A on three auxiliary lanes of their
+    own; large ones keep the two-lane layout (prover.hip groth16_sums_once).  Both layouts give the oracle's
+    proof, for several witnesses in a row on the same context (the lanes' scratch arenas are reused)."""
+    n_in, n_aux, rws, z = circuits.random_circuit(43, 5000)
+    oc, gc = _load(ctx, oracle, n_in, n_aux, rws, z)
+    pk = fg.generate_random_parameters(ctx, gc, circuits.toxic())
+    op = oracle.OracleParams(oc, circuits.toxic())
+    zb = circuits.z_bytes(z)
+    want = [op.prove(zb, r, s)[0] for r, s in [(7, 8), (9, 10)]]
+    for wide_log, b1_lane in (("0", "0"), ("21", "0"), ("21", "1"), ("21", "2")):
+        monkeypatch.setenv("MI_PROVE_WIDE_LOG", wide_log)
+        monkeypatch.setenv("MI_PROVE_B1_LANE", b1_lane)
+        got = [fg.prove(ctx, pk, gc, zb, r, s) for r, s in [(7, 8), (9, 10)]]
+        assert got == want, f"MI_PROVE_WIDE_LOG={wide_log} MI_PROVE_B1_LANE={b1_lane}"
+
+
 def test_prove_rejects_mismatched_srs(ctx):
     n_in, n_aux, rws, z = circuits.random_circuit(51, 30)
     gc = fg.Circuit(ctx, len(rws), n_in, n_aux, circuits.to_csr(rws))

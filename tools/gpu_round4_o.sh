@@ -1,0 +1,9 @@
+# round-4: Winning-PoSt latency across lane layouts after the pinned-readback change
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out/lanes3
+B="python3 bench.py --steps 1 --warmup 0 --log-rows 12 --msm-reps 1 --no-cpu-baseline --no-device-resident --tree-log-nodes 0 --sdr-log-labels 0 --config4-log-rows 0 --stacked-log-nodes 0 --post-sectors 0 --uniform-steps 0 --winning-reps 30"
+for r in 1 2; do for v in 0:0 21:0 21:1 21:2; do
+    w=${v%:*}; b1=${v#*:}; f=gpurun_out/lanes3/w${w}_b${b1}_$r
+    MI_PROVE_WIDE_LOG=$w MI_PROVE_B1_LANE=$b1 timeout -k 10 180 $B > $f.json 2> $f.err || exit 1
+    python3 -c "import json; d=json.loads(open('$f.json').read().strip().splitlines()[-1])['winning_post_32gib']; print('wide_log=$w b1_lane=$b1', round(d['latency_ms_median'],2), round(d['latency_ms_min'],2), d['verified'])"
+done; done
