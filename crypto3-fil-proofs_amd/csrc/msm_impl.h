@@ -956,7 +956,17 @@ void reduce_windows(Ctx &c, const MsmPlan &pl, XYZZ<F> *P0, std::vector<XYZZ<F>>
     unsigned SA = 1;
     while (SA < nbk && (uint64_t)nb / (SA * 2) >= segA_target) SA *= 2;
     const uint32_t nsegA = nbk / SA, totA = nwin * nsegA;
-    const uint32_t nsegB = nsegA < 8192 ? nsegA : 8192, SB = nsegA / nsegB, totB = nwin * nsegB;
+    // second-level segments per window: 8192 for large MSMs.  Small ones (<= 2^19 first-level segments in all,
+    // Winning PoSt's 2^18-2^19-point MSMs) take 2048: k_seg_fold's double-and-add over ~14-bit offsets per
+    // segment was the largest reduction kernel there (thousands of full additions per window for a weighted
+    // sum the running sums of k_bucket_reduce_dense do with 2 per segment).  MI_MSM_SEGB_LOG = k forces 2^k.
+    static const int segb_env = [] {
+        const char *e = getenv("MI_MSM_SEGB_LOG");
+        return e ? atoi(e) : 0;
+    }();
+    const uint32_t segB_cap = segb_env > 0 ? (1u << (segb_env > 13 ? 13 : segb_env))
+                                           : totA <= (1u << 19) ? 2048u : 8192u;
+    const uint32_t nsegB = nsegA < segB_cap ? nsegA : segB_cap, SB = nsegA / nsegB, totB = nwin * nsegB;
     XYZZ<F> *accA = c.scratch[12].as<XYZZ<F>>(2 * (uint64_t)totA), *runA = accA + totA;
     // [sumAccB | runB | foldB] contiguous (one stacked tree sum over 3 * nwin rows), then accB
     XYZZ<F> *sumB = c.scratch[14].as<XYZZ<F>>(4 * (uint64_t)totB), *runB = sumB + totB, *foldB = runB + totB,

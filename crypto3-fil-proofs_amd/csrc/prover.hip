@@ -1203,9 +1203,9 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
             return e && atoi(e) == 1;
         }();
         // Small proofs (domain <= 2^MI_PROVE_WIDE_LOG, default 2^21: Winning PoSt, 2^19) are latency-bound: their
-        // MSMs' bucket reductions, sorts and host round trips leave most CUs idle, so B, L and A each get a lane
-        // of their own (three auxiliary streams and host threads beside the main lane's witness map, NTT chain
-        // and H).  Large proofs keep two lanes: their accumulation fills the chip and every lane holds a scratch
+        // MSMs' bucket reductions, sorts and host round trips leave most CUs idle, so B_G2, L and A + B_G1 each get
+        // a lane of their own (three auxiliary streams and host threads beside the main lane's witness map, NTT
+        // chain and H).  Large proofs keep two lanes: their accumulation fills the chip and every lane holds a scratch
         // arena sized to its MSMs.  Read per call (tests compare the two layouts).
         const char *we = getenv("MI_PROVE_WIDE_LOG");
         const unsigned wide_log = we ? (unsigned)atoi(we) : 21u;
@@ -1220,11 +1220,12 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
             MI_HIP(hipStreamWaitEvent(lane_ctx[k]->stream, ready, 0));
         }
         std::exception_ptr err[3];
-        // B_G1 and B_G2 share the scalars (z over the B-density): sort them once.  MI_PROVE_B1_LANE = 1 / 2 (small
-        // proofs only) moves B_G1 after L / after A on that lane, which sorts the scalars again for itself (no
-        // plan is shared between lanes: the G2 second level reuses its plan's scratch)
+        // B_G1 and B_G2 share the scalars (z over the B-density): sort them once on large proofs.  Small proofs run
+        // B_G1 after A on A's lane (MI_PROVE_B1_LANE: 2 default, 1 after L, 0 with B_G2), which sorts the scalars
+        // again for itself (no plan is shared between lanes: the G2 second level reuses its plan's scratch).
+        // Same box, Winning PoSt: 23.1 ms with B_G1 beside B_G2, 20.5 ms after A.
         const char *b1e = getenv("MI_PROVE_B1_LANE");
-        const unsigned b1_lane = wide && b1e ? (unsigned)atoi(b1e) : 0u;
+        const unsigned b1_lane = wide ? (b1e ? (unsigned)atoi(b1e) : 2u) : 0u;
         auto run_b = [&](Ctx &x) {
             const uint64_t lo = rg.lo[3], cnt = rg.cnt[3];
             MsmPlan pb;
