@@ -9,7 +9,8 @@ timeout -k 10 300 python3 -u -m pytest -x -v --timeout 200 --timeout-method thre
     -k "winning" > gpurun_out/lanes/post.log 2>&1 || { tail -30 gpurun_out/lanes/post.log; exit 1; }
 tail -3 gpurun_out/lanes/post.log
 B="python3 bench.py --steps 1 --warmup 0 --log-rows 12 --msm-reps 1 --no-cpu-baseline --no-device-resident --tree-log-nodes 0 --sdr-log-labels 0 --config4-log-rows 0 --stacked-log-nodes 0 --post-sectors 0 --uniform-steps 0 --winning-reps 20"
-for v in 21 0 21 0; do
-    MI_PROVE_WIDE_LOG=$v timeout -k 10 180 $B > gpurun_out/lanes/w$v.json 2> gpurun_out/lanes/w$v.err || exit 1
-    python3 -c "import json; d=json.loads(open('gpurun_out/lanes/w$v.json').read().strip().splitlines()[-1])['winning_post_32gib']; print('wide_log=$v', round(d['latency_ms_median'],2), round(d['latency_ms_min'],2), d['verified'], d['device_ms_per_proof'])"
-done
+for r in 1 2; do for v in 21:0 0:0 21:1 21:2; do
+    w=${v%:*}; b1=${v#*:}; f=gpurun_out/lanes/w${w}_b${b1}_$r
+    MI_PROVE_WIDE_LOG=$w MI_PROVE_B1_LANE=$b1 timeout -k 10 180 $B > $f.json 2> $f.err || exit 1
+    python3 -c "import json; d=json.loads(open('$f.json').read().strip().splitlines()[-1])['winning_post_32gib']; print('wide_log=$w b1_lane=$b1', round(d['latency_ms_median'],2), round(d['latency_ms_min'],2), d['verified'])"
+done; done
