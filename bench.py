@@ -528,7 +528,8 @@ def window_post_leg(args, fg, ctx, device, rank, world, gdev, dist):
 
     from fil_groth16 import stacked
     from fil_groth16.compound import shard_partitions
-    from fil_groth16.distributed import (agree_float, balanced_schedule, calibrate_lead_share, latency_ranges,
+    from fil_groth16.distributed import (agree_float, balanced_schedule, calibrate_hsplit, calibrate_lead_share,
+                                         hsplit_fractions, hsplit_shares, latency_ranges, latency_ranges_hsplit,
                                          lead_share_from_times, prove_partitions, prove_partitions_balanced)
 
     S, C, nodes = args.post_sectors, args.post_challenges, 1 << args.post_log_nodes
@@ -601,31 +602,53 @@ def window_post_leg(args, fg, ctx, device, rank, world, gdev, dist):
 
     vk, ic = pk.verifying_key()
 
-    # latency-mode groups compute H once (MI_C5_LATENCY=h_once, default): the group's lead rank runs the witness
-    # map, the NTT chain and the whole H MSM plus a calibrated fraction of L, A, B; the others split the rest
-    # (distributed.latency_ranges).  MI_C5_LATENCY=slices: every rank repeats H and takes equal slices.
-    latency = os.environ.get("MI_C5_LATENCY", "h_once")
+    # latency-mode groups compute H once and split it (MI_C5_LATENCY=h_split, default): the group's
+    # lead rank runs the witness map and the NTT chain (mi_groth16_h_coeffs_dev), broadcasts the d H coefficients
+    # over the group (RCCL, asynchronous) and takes a calibrated slice of H; the others prove their L / A / B
+    # slices first, then their H slices from the broadcast (distributed.hsplit_shares).  MI_C5_LATENCY=h_once: the
+    # lead keeps the whole H MSM (round 4); slices: every rank repeats H and takes equal slices.
+    latency = os.environ.get("MI_C5_LATENCY", "h_split")
     sizes = (pk.n_h, pk.n_l, pk.n_a, pk.n_b)
     calib = {}
+    hbuf = torch.zeros(32 * circ.d, dtype=torch.uint8, device=device) if latency == "h_split" else None
 
-    def share_fn(p, k, g):
+    def share_fn(p, k, g, bcast=None):
         pc.witness_dev(ctx, sdev[p].data_ptr(), z.data_ptr())
         if latency == "slices":
             return fg.prove_share(ctx, pk, circ, z.data_ptr(), k, g)
-        rg = latency_ranges(sizes, g, lead_share_from_times(calib["t_h_ms"], calib["t_lab_ms"], g))
-        return fg.prove_share_ranges(ctx, pk, circ, z.data_ptr(), rg[k])
+        if latency == "h_once":
+            rg = latency_ranges(sizes, g, lead_share_from_times(calib["t_h_ms"], calib["t_lab_ms"], g))
+            return fg.prove_share_ranges(ctx, pk, circ, z.data_ptr(), rg[k])
+        rg = latency_ranges_hsplit(sizes, g, *hsplit_fractions(calib["t_qap_ms"], calib["t_hmsm_ms"],
+                                                               calib["t_lab_ms"], g))
+
+        def h_coeffs(*arg):
+            if not arg:  # the lead: witness map + NTT chain into hbuf
+                fg.h_coeffs_dev(ctx, circ, z.data_ptr(), hbuf.data_ptr())
+            return hbuf
+
+        def one(ranges, h):
+            return fg.prove_share_ranges(ctx, pk, circ, z.data_ptr(), ranges,
+                                         h_dev=h.data_ptr() if h is not None else None)
+
+        return hsplit_shares(k, rg, h_coeffs, one, bcast or (lambda t: (lambda: t)))
 
     def assemble_fn(p, shares):  # the same blinding on every rank of the group
         return fg.assemble(vk, shares, *splitmix_frs(9500 + p, 2))
 
     if latency != "slices" and (tail or (world == 1 and args.post_share_groups)):
-        # one GPU's times of the two halves of a proof (H part; L, A, B part), rank 0's agreed by every rank
+        # one GPU's times of the parts of a proof (h_once: H part; L, A, B part -- h_split: NTT chain; H MSM; L, A,
+        # B), rank 0's agreed by every rank
+        keys = ("t_qap_ms", "t_hmsm_ms", "t_lab_ms") if latency == "h_split" else ("t_h_ms", "t_lab_ms")
         if mine:
             pc.witness_dev(ctx, sdev[mine[0]].data_ptr(), z.data_ptr())
-            _, t = calibrate_lead_share(ctx, pk, circ, z.data_ptr(), 2)
+            if latency == "h_split":
+                t = calibrate_hsplit(ctx, pk, circ, z.data_ptr(), hbuf.data_ptr())
+            else:
+                _, t = calibrate_lead_share(ctx, pk, circ, z.data_ptr(), 2)
         else:
-            t = {"t_h_ms": 0.0, "t_lab_ms": 0.0}
-        calib = {k: agree_float(v, rank, gdev) if dist else v for k, v in t.items()}
+            t = {k: 0.0 for k in keys}
+        calib = {k: agree_float(t[k], rank, gdev) if dist else t[k] for k in keys}
     if mine:  # warm-up (program upload, plans)
         pc.witness_dev(ctx, sdev[mine[0]].data_ptr(), z.data_ptr())
         if whole[rank]:
@@ -643,7 +666,8 @@ def window_post_leg(args, fg, ctx, device, rank, world, gdev, dist):
     multi = []
     for _ in range(steps):
         if world > 1:
-            multi.append(prove_partitions_balanced(prove_ids, share_fn, assemble_fn, P, rank, world, gdev)
+            multi.append(prove_partitions_balanced(prove_ids, share_fn, assemble_fn, P, rank, world, gdev,
+                                                   group_bcast=latency == "h_split")
                          if tail else prove_partitions(prove_ids, P, rank, world, gdev))
         else:
             multi.append(b"".join(prove_ids(mine)))
@@ -667,16 +691,26 @@ def window_post_leg(args, fg, ctx, device, rank, world, gdev, dist):
             share_fn(p0, 0, g)  # warm (slice plans)
             ctx.synchronize()
             ts, shs = [], []
-            for k in range(g):
+            for k in range(g):  # rank k's shares in turn (h_split: rank 0's H coefficients stay in hbuf)
                 t2 = time.perf_counter()
-                shs.append(share_fn(p0, k, g))
+                got = share_fn(p0, k, g)
                 ctx.synchronize()
                 ts.append(time.perf_counter() - t2)
+                shs += [got] if isinstance(got, (bytes, bytearray)) else list(got)
+            mean = sum(ts) / len(ts)
             shares_res[str(g)] = {"share_ms": [1e3 * x for x in ts], "slowest_ms": 1e3 * max(ts),
+                                  "mean_ms": 1e3 * mean, "slowest_over_mean": max(ts) / mean,
                                   "assembled_equals_whole_proof": fg.assemble(vk, shs, *rs0) == ref,
                                   "mode": latency}
-            if latency != "slices":
+            if latency == "h_once":
                 shares_res[str(g)]["lead_share"] = lead_share_from_times(calib["t_h_ms"], calib["t_lab_ms"], g)
+            elif latency == "h_split":
+                hl, fl = hsplit_fractions(calib["t_qap_ms"], calib["t_hmsm_ms"], calib["t_lab_ms"], g)
+                # the lead's broadcast of d x 32 B runs beside its own share (asynchronous); the others need H only
+                # after their L / A / B slices: estimated at one xGMI link (~64 GB/s effective), a projection
+                bc_ms = 32 * circ.d / 64e9 * 1e3
+                shares_res[str(g)].update(h_lead=hl, lab_lead=fl, h_bcast_ms_estimate=bc_ms,
+                                          h_needed_after_ms=1e3 * min(ts[1:]) if g > 1 else None)
     if dist:
         tt = torch.tensor([dt], dtype=torch.float64, device=gdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -710,8 +744,10 @@ def window_post_leg(args, fg, ctx, device, rank, world, gdev, dist):
                 "note": "projected from this GPU's times (witness + share per rank, ranks independent): 10 "
                         "partitions; balanced = P - P % W whole partitions round-robin, then each of the P % W "
                         "tail partitions over W / (P % W) GPUs in latency mode (" + latency + ": " +
-                        ("the group's lead rank alone computes H" if latency != "slices" else
-                         "every rank repeats H, equal slices") + ")",
+                        {"h_split": "the group's lead rank alone computes H and broadcasts it, every rank proves a "
+                                    "slice of H, L, A and B",
+                         "h_once": "the group's lead rank alone computes H and proves the whole H MSM"}.get(
+                            latency, "every rank repeats H, equal slices") + "); a PROJECTION, not a measurement",
                 "w8_roundrobin_makespan_ms": 2 * tp1,
                 "w8_balanced_makespan_ms": tp1 + shares_res["4"]["slowest_ms"] if "4" in shares_res else None,
                 "w4_roundrobin_makespan_ms": 3 * tp1,
@@ -1027,6 +1063,22 @@ def main():
                     "note": "witness resident in HBM before the timer (no H2D): the round-1 definition"}
         del zdev
 
+    # the dominant kernel measured alone: one proof with MI_PROVE_LANES=1 (the auxiliary lane's MSMs run after the
+    # main lane's, on the same stream), so k_accum_level0's launch times are the kernel's own and not stretched by
+    # the other lane's sorts and NTTs (the timed proofs' two-lane figure is reported beside it)
+    one_lane = None
+    if rank == 0:
+        os.environ["MI_PROVE_LANES"] = "1"
+        try:
+            ctx.reset_stats()
+            fg.prove_batch(ctx, pk, circ, [zhost], [blinding(0, 0)], priority=prio)
+            ctx.synchronize()
+            one_lane = ctx.stats()
+        except Exception as e:  # reported, never fatal
+            one_lane = {"error": str(e)}
+        finally:
+            del os.environ["MI_PROVE_LANES"]
+
     # secondary metric: standalone G1 MSM over the resident 2^log_rows - 1 h-query points
     msm_n = pk.n_h
     pts = pk.points(0)
@@ -1214,6 +1266,19 @@ def main():
                                "gmadd_per_s": max(r["gmadd_per_s"] for r in g),
                                "clock_ghz": max(r["clock_ghz_median"] for r in g)}
                     break
+    one_lane_res = None
+    if one_lane and "accum_g1" in one_lane and grp == "G1" and one_lane["accum_g1"]["launches"]:
+        o = one_lane["accum_g1"]
+        o_ms = o["ms"] / o["launches"]
+        o_madds = o.get("madds", 0) / o["launches"]
+        o_rate = o_madds / (o_ms * 1e-3) / 1e9 if o_ms > 0 else None
+        one_lane_res = {
+            "mode": "one lane (MI_PROVE_LANES=1, one proof): the kernel alone on the chip",
+            "avg_launch_ms": o_ms, "launches": o["launches"], "madds_per_launch": o_madds, "gmadd_per_s": o_rate,
+            "hbm_frac": (bytes_per_unit * o["units"] / o["launches"] / (o_ms * 1e-3) / 1e9) / HBM_PEAK_GBS
+            if o_ms > 0 else None,
+            "group_law_ceiling_frac": o_rate / ceiling["gmadd_per_s"] if ceiling and o_rate else None,
+            "proof_ms": one_lane["prove"]["ms"] / max(one_lane["prove"]["launches"], 1)}
     fq_muls = madds_per_launch * FQ_MUL_PER_MIXED_ADD[grp]
     valu_ach = fq_muls / (avg_ms * 1e-3) if avg_ms > 0 and fq_muls else None
     valu_peak = MAD_RATE / FQ_MUL_MADS
@@ -1272,8 +1337,11 @@ def main():
             "unit": "Fq-mul/s",
             "frac": valu_ach / valu_peak if valu_ach else None,
             "madds_per_launch": madds_per_launch,
-            "group_law_ceiling": dict(ceiling, frac=(madds_per_launch / (avg_ms * 1e-3) / 1e9) / ceiling["gmadd_per_s"])
+            "group_law_ceiling": dict(ceiling, frac=(madds_per_launch / (avg_ms * 1e-3) / 1e9) / ceiling["gmadd_per_s"],
+                                      frac_is="two lanes: the timed proofs' launches, stretched by the other lane's "
+                                              "sorts and NTTs sharing the CUs")
             if ceiling and avg_ms > 0 and madds_per_launch else None,
+            "one_lane": one_lane_res,
             "spec_issue": {"peak_lane_instr_per_s": SPEC_VALU_LANE_INSTR,
                            "instr_per_mixed_add": G1_MADD_VALU_INSTR if grp == "G1" else None,
                            "frac": (madds_per_launch * G1_MADD_VALU_INSTR / (avg_ms * 1e-3) / SPEC_VALU_LANE_INSTR)

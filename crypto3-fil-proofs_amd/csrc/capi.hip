@@ -54,6 +54,11 @@ struct mi_ctx {
     mi::Ctx c;
     hipStream_t normal = nullptr, high = nullptr;
     WitnessUploader up;
+    // Stream-ordering contract of the entries that touch caller device memory (include/mi355x_groth16.h
+    // "Device pointers"): their first device access waits, on the device, for everything queued on `caller`
+    // before the call.  nullptr = the legacy default stream, which also waits for every blocking stream.
+    hipStream_t caller = nullptr;
+    hipEvent_t fence = nullptr;
 };
 struct mi_circuit {
     mi::Circuit *p;
@@ -125,6 +130,7 @@ void need(bool cond, const std::string &msg) {
 void need(bool cond, const char *msg) {
     if (!cond) throw std::invalid_argument(msg);
 }
+void check_dev_canonical(mi::Ctx &c, const mi::fr_t *d, uint64_t n, const char *what);  // below
 
 // ---- bellman / filecoin Groth16 parameter files (v28-*.params, *.vk) ----------------------
 // Parameters::write: vk (MI_VK_BYTES) | u32 BE n_ic | ic (96 B each) | then for h, l, a, b_g1
@@ -212,12 +218,24 @@ struct DeviceScope {
     }
 };
 
+// Orders the context's current stream after the caller's prior work (event recorded on the caller stream, waited
+// for on the device: no host synchronisation).  The aux lanes and the copy stream fork from the context stream,
+// so ordering it orders every library stream of the call.
+void caller_fence(mi_ctx *ctx) {
+    if (!ctx->fence) MI_HIP(hipEventCreateWithFlags(&ctx->fence, hipEventDisableTiming));
+    MI_HIP(hipEventRecord(ctx->fence, ctx->caller));
+    MI_HIP(hipStreamWaitEvent(ctx->c.stream, ctx->fence, 0));
+}
+
+enum { NO_FENCE = 0, FENCE = 1 };  // FENCE: the entry reads or writes caller device memory
+
 struct CtxLock {
     mi_ctx *ctx;
     std::lock_guard<std::recursive_mutex> lk;
     DeviceScope dev;
-    CtxLock(mi_ctx *c, int priority = 0) : ctx(c), lk(c->c.mu), dev(c->c.device) {
+    CtxLock(mi_ctx *c, int priority = 0, int fence = NO_FENCE) : ctx(c), lk(c->c.mu), dev(c->c.device) {
         c->c.stream = priority ? c->high : c->normal;
+        if (fence == FENCE) caller_fence(c);
     }
 };
 
@@ -364,6 +382,10 @@ struct DevWitnessCheck {
 
 }  // namespace
 
+namespace mi {
+void set_last_error(const std::string &msg) { g_err = msg; }
+}  // namespace mi
+
 extern "C" {
 
 const char *mi_last_error(void) { return g_err.c_str(); }
@@ -411,12 +433,14 @@ void mi_ctx_destroy(mi_ctx *ctx) {
     DeviceScope dev(ctx->c.device, false);
     hipDeviceSynchronize();
     ctx->up.release();
+    for (mi::Ctx *x = &ctx->c; x; x = x->aux) mi::stacked::forget_ctx(x->uid);
     mi::ntt_free_tables(ctx->c);
     mi::ctx_aux_free(ctx->c);
     mi::poseidon_free(ctx->c);
     for (auto &b : ctx->c.scratch) b.release();
     if (ctx->normal) hipStreamDestroy(ctx->normal);
     if (ctx->high) hipStreamDestroy(ctx->high);
+    if (ctx->fence) hipEventDestroy(ctx->fence);
     delete ctx;
 }
 
@@ -424,6 +448,14 @@ int mi_ctx_stream(mi_ctx *ctx, void **stream_out) {
     return guard([&] {
         need(ctx && stream_out, "null argument");
         *stream_out = (void *)ctx->normal;
+    });
+}
+
+int mi_ctx_set_caller_stream(mi_ctx *ctx, void *stream) {
+    return guard([&] {
+        need(ctx != nullptr, "null ctx");
+        CtxLock l(ctx);
+        ctx->caller = (hipStream_t)stream;
     });
 }
 
@@ -533,7 +565,7 @@ int mi_srs_stream_part(mi_srs_stream *st, int which, uint64_t first, const void 
                        int on_device) {
     return guard([&] {
         need(st && st->p && (bytes || !n_points), "null argument");
-        CtxLock l(st->ctx);
+        CtxLock l(st->ctx, 0, on_device ? FENCE : NO_FENCE);
         mi::srs_stream_part(st->ctx->c, *st->p, which, first, (const uint8_t *)bytes, n_points, on_device != 0);
     });
 }
@@ -606,10 +638,39 @@ int mi_srs_msm_info(const mi_srs *srs, uint64_t out[2]) {
     });
 }
 
+int mi_srs_table_state(const mi_srs *srs, uint64_t out[3]) {
+    return guard([&] {
+        need(srs && out, "null argument");
+        const mi::Srs &s = *srs->p;
+        std::shared_lock<std::shared_mutex> in_use(s.use_mu);
+        out[0] = (s.h_hi || s.l_hi || s.a_hi) ? 1 : 0;
+        out[1] = s.tables_dropped;
+        out[2] = s.in_subgroup ? 1 : 0;
+    });
+}
+
+int mi_srs_readmit(mi_ctx *ctx, mi_srs *srs, uint64_t *rebuilt_bytes) {
+    return guard([&] {
+        need(ctx && srs, "null argument");
+        need(srs->device == ctx->c.device, "key and context on different devices");
+        CtxLock l(ctx);
+        const uint64_t got = mi::srs_readmit(ctx->c, *srs->p);
+        if (rebuilt_bytes) *rebuilt_bytes = got;
+    });
+}
+
+int mi_ctx_inject_oom(mi_ctx *ctx, int64_t count) {
+    return guard([&] {
+        need(ctx != nullptr, "null ctx");
+        CtxLock l(ctx);
+        ctx->c.inject_oom = count;
+    });
+}
+
 int mi_srs_export_query_dev(mi_ctx *ctx, const mi_srs *srs, int which, uint64_t first, uint64_t n, void *dev_out) {
     return guard([&] {
         need(ctx && srs && (dev_out || !n), "null argument");
-        CtxLock l(ctx);
+        CtxLock l(ctx, 0, FENCE);
         const mi::Srs &s = *srs->p;
         uint64_t total = 0;
         switch (which) {
@@ -705,7 +766,7 @@ int mi_groth16_prove_dev(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circ,
                          const uint8_t r[32], const uint8_t s[32], int priority, uint8_t *proof, uint8_t *raw) {
     return guard([&] {
         need(ctx && srs && circ && z_dev && r && s && proof, "null argument");
-        CtxLock l(ctx, priority);
+        CtxLock l(ctx, priority, FENCE);
         uint64_t nv = circ->p->n_in + circ->p->n_aux;
         DevWitnessCheck chk(ctx, (const mi::fr_t *)z_dev, nv);
         uint8_t p[MI_PROOF_BYTES], w[384];
@@ -835,7 +896,7 @@ int mi_groth16_prove_share_dev(mi_ctx *ctx, const mi_srs *srs, const mi_circuit 
                                uint32_t rank, uint32_t world, int priority, uint8_t *share) {
     return guard([&] {
         need(ctx && srs && circ && z_dev && share, "null argument");
-        CtxLock l(ctx, priority);
+        CtxLock l(ctx, priority, FENCE);
         uint64_t nv = circ->p->n_in + circ->p->n_aux;
         DevWitnessCheck chk(ctx, (const mi::fr_t *)z_dev, nv);
         uint8_t sh[MI_SHARE_BYTES];
@@ -870,11 +931,40 @@ int mi_groth16_prove_share_ranges_dev(mi_ctx *ctx, const mi_srs *srs, const mi_c
                                       const uint64_t ranges[8], int priority, uint8_t *share) {
     return guard([&] {
         need(ctx && srs && circ && z_dev && ranges && share, "null argument");
-        CtxLock l(ctx, priority);
+        CtxLock l(ctx, priority, FENCE);
         uint64_t nv = circ->p->n_in + circ->p->n_aux;
         DevWitnessCheck chk(ctx, (const mi::fr_t *)z_dev, nv);
         uint8_t sh[MI_SHARE_BYTES];
         mi::sums_encode(mi::groth16_sums_ranges(ctx->c, *srs->p, *circ->p, (const mi::fr_t *)z_dev, ranges_of(ranges)),
+                        sh);
+        chk.verdict(nv);
+        memcpy(share, sh, MI_SHARE_BYTES);
+    });
+}
+
+int mi_groth16_h_coeffs_dev(mi_ctx *ctx, const mi_circuit *circ, const void *z_dev, void *h_out_dev) {
+    return guard([&] {
+        need(ctx && circ && z_dev && h_out_dev, "null argument");
+        CtxLock l(ctx, 0, FENCE);
+        uint64_t nv = circ->p->n_in + circ->p->n_aux;
+        DevWitnessCheck chk(ctx, (const mi::fr_t *)z_dev, nv);
+        mi::groth16_h_coeffs(ctx->c, *circ->p, (const mi::fr_t *)z_dev, (mi::fr_t *)h_out_dev);
+        chk.verdict(nv);
+    });
+}
+
+int mi_groth16_prove_share_ranges_h_dev(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circ, const void *z_dev,
+                                        const void *h_dev, const uint64_t ranges[8], int priority, uint8_t *share) {
+    return guard([&] {
+        need(ctx && srs && circ && z_dev && ranges && share, "null argument");
+        CtxLock l(ctx, priority, FENCE);
+        uint64_t nv = circ->p->n_in + circ->p->n_aux;
+        // received H coefficients are scalars like the witness: canonical Fr or refused
+        if (h_dev) check_dev_canonical(ctx->c, (const mi::fr_t *)h_dev, circ->p->d, "H coefficient");
+        DevWitnessCheck chk(ctx, (const mi::fr_t *)z_dev, nv);
+        uint8_t sh[MI_SHARE_BYTES];
+        mi::sums_encode(mi::groth16_sums_ranges(ctx->c, *srs->p, *circ->p, (const mi::fr_t *)z_dev, ranges_of(ranges),
+                                                (const mi::fr_t *)h_dev),
                         sh);
         chk.verdict(nv);
         memcpy(share, sh, MI_SHARE_BYTES);
@@ -894,7 +984,7 @@ int mi_groth16_trapdoor_dlogs(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *
                               const uint8_t r[32], const uint8_t s[32], uint8_t out[96]) {
     return guard([&] {
         need(ctx && srs && circ && z_dev && r && s && out, "null argument");
-        CtxLock l(ctx);
+        CtxLock l(ctx, 0, FENCE);
         mi::fr_t d[3];
         mi::groth16_trapdoor_dlogs(ctx->c, *srs->p, *circ->p, (const mi::fr_t *)z_dev, fr_checked(r), fr_checked(s),
                                    d);
@@ -1001,7 +1091,7 @@ int mi_msm_g1_dev(mi_ctx *ctx, const mi_points *bases, const void *scalars_dev, 
         need(ctx && bases && scalars_dev && out96, "null argument");
         need(!bases->is_g2, "G2 bases passed to mi_msm_g1_dev");
         need(n <= bases->n, "n exceeds the number of bases");
-        CtxLock l(ctx);
+        CtxLock l(ctx, 0, FENCE);
         std::shared_lock<std::shared_mutex> in_use;  // a key's query: its split table stays while this MSM runs
         if (bases->srs) in_use = std::shared_lock<std::shared_mutex>(bases->srs->use_mu);
         mi::g1_xyzz_t r;
@@ -1015,7 +1105,7 @@ int mi_msm_g2_dev(mi_ctx *ctx, const mi_points *bases, const void *scalars_dev, 
         need(ctx && bases && scalars_dev && out192, "null argument");
         need(bases->is_g2, "G1 bases passed to mi_msm_g2_dev");
         need(n <= bases->n, "n exceeds the number of bases");
-        CtxLock l(ctx);
+        CtxLock l(ctx, 0, FENCE);
         mi::g2_xyzz_t r;
         mi::msm_g2(ctx->c, (const mi::g2_affine_t *)bases->dev, (const mi::fr_t *)scalars_dev, nullptr, n, &r);
         mi::g2_encode(mi::xyzz_to_affine(r), out192);
@@ -1080,9 +1170,10 @@ int mi_ntt_fr_dev(mi_ctx *ctx, void *data_dev, unsigned log_n, int inverse, int 
     return guard([&] {
         need(ctx && data_dev, "null argument");
         need(log_n <= 32, "log_n > 32 (Fr 2-adicity)");
-        CtxLock l(ctx);
+        CtxLock l(ctx, 0, FENCE);
         mi::fr_canonicalize(ctx->c, (mi::fr_t *)data_dev, 1ull << log_n);
         ntt_impl(ctx->c, (mi::fr_t *)data_dev, log_n, inverse, coset);
+        MI_HIP(hipStreamSynchronize(ctx->c.stream));  // data_dev complete on return (the _dev contract)
     });
 }
 
@@ -1213,12 +1304,13 @@ int mi_stacked_public_inputs(const mi_stacked *s, const uint8_t *slots, uint8_t 
 int mi_stacked_witness_dev(mi_ctx *ctx, mi_stacked *s, const void *slots_dev, void *z_dev) {
     return guard([&] {
         need(ctx && s && slots_dev && z_dev, "null argument");
-        CtxLock l(ctx);
+        CtxLock l(ctx, 0, FENCE);
         std::vector<uint8_t> host(32 * s->b->lay.slots);
         MI_HIP(hipMemcpyAsync(host.data(), slots_dev, host.size(), hipMemcpyDeviceToHost, ctx->c.stream));
         MI_HIP(hipStreamSynchronize(ctx->c.stream));
         stacked_check_slots(*s->b, host.data());
         mi::stacked::witness_dev(ctx->c, *s->b, (const uint8_t *)slots_dev, (mi::fr_t *)z_dev);
+        MI_HIP(hipStreamSynchronize(ctx->c.stream));
     });
 }
 int mi_stacked_witness(mi_ctx *ctx, mi_stacked *s, const uint8_t *slots, uint8_t *z_out) {
@@ -1244,7 +1336,7 @@ void mi_stacked_free(mi_stacked *s) {
 int mi_circuit_check_dev(mi_ctx *ctx, const mi_circuit *circ, const void *z_dev, uint64_t out[2]) {
     return guard([&] {
         need(ctx && circ && z_dev && out, "null argument");
-        CtxLock l(ctx);
+        CtxLock l(ctx, 0, FENCE);
         uint64_t first = ~0ull;
         out[0] = mi::circuit_check(ctx->c, *circ->p, (const mi::fr_t *)z_dev, &first);
         out[1] = first;
@@ -1535,10 +1627,11 @@ int mi_poseidon_hash_dev(mi_ctx *ctx, unsigned arity, const void *preimages_dev,
     return guard([&] {
         need(ctx && (count == 0 || (preimages_dev && digests_dev)), "null argument");
         need_tree_arity(arity);
-        CtxLock l(ctx);
+        CtxLock l(ctx, 0, FENCE);
         check_dev_canonical(ctx->c, (const mi::fr_t *)preimages_dev, count * arity, "poseidon preimage");
         mi::poseidon_hash_dev(ctx->c, arity, (const mi::fr_t *)preimages_dev, count, arity, 1,
                               (mi::fr_t *)digests_dev);
+        MI_HIP(hipStreamSynchronize(ctx->c.stream));
     });
 }
 
@@ -1570,7 +1663,7 @@ int mi_tree_build_dev(mi_ctx *ctx, unsigned arity, const void *leaves_dev, uint6
     return guard([&] {
         need(ctx && leaves_dev && tree_dev, "null argument");
         need_tree_arity(arity);
-        CtxLock l(ctx);
+        CtxLock l(ctx, 0, FENCE);
         mi::tree_rows_size(leaves, arity, rows_to_discard);
         check_dev_canonical(ctx->c, (const mi::fr_t *)leaves_dev, leaves, "tree leaf");
         mi::fr_t *tmp = ctx->c.scratch[22].as<mi::fr_t>(2 * (leaves / arity) + 1);
@@ -1616,7 +1709,7 @@ int mi_tree_c_build_dev(mi_ctx *ctx, unsigned layers, uint64_t nodes, const void
         need(ctx && labels_dev && base_dev && tree_dev, "null argument");
         need_tree_arity(layers);
         need_tree_arity(tree_arity);
-        CtxLock l(ctx);
+        CtxLock l(ctx, 0, FENCE);
         mi::Ctx &c = ctx->c;
         mi::tree_rows_size(nodes, tree_arity, 0);
         check_dev_canonical(c, (const mi::fr_t *)labels_dev, nodes * layers, "layer label");
@@ -1664,7 +1757,7 @@ int mi_tree_r_last_build_dev(mi_ctx *ctx, uint64_t nodes, const void *labels_dev
     return guard([&] {
         need(ctx && labels_dev && data_dev && tree_dev, "null argument");
         need_tree_arity(tree_arity);
-        CtxLock l(ctx);
+        CtxLock l(ctx, 0, FENCE);
         mi::Ctx &c = ctx->c;
         mi::tree_rows_size(nodes, tree_arity, rows_to_discard);
         check_dev_canonical(c, (const mi::fr_t *)labels_dev, nodes, "last-layer label");
@@ -1730,7 +1823,7 @@ int mi_sdr_labels_dev(mi_ctx *ctx, const uint8_t replica_id[32], uint64_t count,
         need(ctx && replica_id && (count == 0 || (layers_dev && nodes_dev && labels_dev)), "null argument");
         need(n_parents <= 37, "n_parents must be <= 37");
         need(count == 0 || n_parents == 0 || parents_dev, "null parents");
-        CtxLock l(ctx);
+        CtxLock l(ctx, 0, FENCE);
         mi::sdr_labels_dev(ctx->c, mi::sdr_replica(replica_id), (const uint32_t *)layers_dev,
                            (const uint64_t *)nodes_dev, parents_dev, n_parents, count, labels_dev);
         MI_HIP(hipStreamSynchronize(ctx->c.stream));  // labels_dev complete on return, like the other _dev calls
@@ -1770,7 +1863,7 @@ int mi_sdr_labeling_proofs_dev(mi_ctx *ctx, const uint8_t replica_id[32], unsign
         need(n_base >= 1 && n_base + n_exp <= 37, "need 1 <= n_base and n_base + n_exp <= 37");
         need(n_layers >= 1 && nodes_per_layer >= 1, "need at least one layer and one node");
         need(nodes_per_layer <= (1ull << 32), "nodes_per_layer must fit the u32 parent indices");
-        CtxLock l(ctx);
+        CtxLock l(ctx, 0, FENCE);
         if (!count) return;
         mi::Ctx &c = ctx->c;
         // every layer and parent index is checked on the device before the gather reads through them
@@ -1807,7 +1900,7 @@ int mi_tree_inclusion_paths_dev(mi_ctx *ctx, unsigned arity, const void *leaves_
         need(ctx && leaves_dev && tree_dev && (count == 0 || (challenges_dev && leaf_out_dev && siblings_out_dev)),
              "null argument");
         need_tree_arity(arity);
-        CtxLock l(ctx);
+        CtxLock l(ctx, 0, FENCE);
         mi::tree_rows_size(leaf_count, arity, rows_to_discard);
         if (!count) return;
         mi::Ctx &c = ctx->c;
@@ -1842,7 +1935,7 @@ int mi_tree_d_build_dev(mi_ctx *ctx, const void *leaves_dev, uint64_t leaf_count
     return guard([&] {
         need(ctx && leaves_dev && tree_dev, "null argument");
         need(leaf_count >= 2 && (leaf_count & (leaf_count - 1)) == 0, "tree D: leaf count must be a power of two >= 2");
-        CtxLock l(ctx);
+        CtxLock l(ctx, 0, FENCE);
         mi::tree_d_build_dev(ctx->c, leaves_dev, leaf_count, tree_dev);
         MI_HIP(hipStreamSynchronize(ctx->c.stream));
     });

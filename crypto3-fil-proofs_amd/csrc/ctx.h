@@ -211,6 +211,9 @@ struct Ctx {
     Stats stats;
     EventTimer timer;
     PinnedBuf pin;  // small readbacks (msm_impl.h); one lane's, reused call after call
+    // test hook (mi_ctx_inject_oom): the next inject_oom proofs' first attempts fail with a real out-of-memory
+    // error after the NTT chain (-1: every proof), exercising the release-and-retry path of groth16_sums
+    int64_t inject_oom = 0;
     // Auxiliary lane: a second stream with its own scratch arena and timers, driven from a second
     // host thread inside one prove so MSMs that do not depend on the NTT chain overlap it (the
     // accumulation is VALU-bound, the NTT / sort phases are LDS- / HBM-bound).  Created on first

@@ -2,15 +2,15 @@
 //
 // Restates crypto3's multiprecision Montgomery backend ([NOT IN TREE]: libs/crypto/multiprecision,
 // used via algebra::curves::bls12<381>, core/crypto/scheme_params.hpp:39-43) for CDNA4:
-//   * Fq (the MSM hot loop) uses 14 limbs of 29 bits, Montgomery radix R = 2^406, product-scanning
-//     (FIPS) Montgomery multiplication: a column holds <= 28 products < 2^58, so every limb product
-//     is ONE v_mad_u64_u32 accumulating into a 64-bit register pair and carries move once per
-//     column -- 544 instructions per multiplication vs 1453 for 32-bit CIOS, measured 79 vs 39
-//     G Fq-mul/s on MI355X (microbench/fieldmul.hip).  Values are kept lazily in [0, 2p): the
-//     product of two such values is again < 2p because R > 4p, so there is no final subtraction.
+//   * Fq (the MSM hot loop) uses 13 balanced signed limbs of 30 bits, Montgomery radix R = 2^390,
+//     product-scanning (FIPS) Montgomery multiplication: a column holds <= 26 products of magnitude
+//     <= 2^58, so every limb product is ONE v_mad_i64_i32 accumulating into a signed 64-bit register
+//     pair and carries move once per column (338 MADs; 84 G Fq-mul/s on MI355X against 79 for the
+//     rounds 1-4 form over 14 x 29-bit unsigned limbs and 38 for 32-bit CIOS, microbench/fieldmul.hip).
+//     Values are any representative (no range reduction); see "Fq" below.
 //   * Fr (NTT, scalars) uses 8 limbs of 32 bits with "no-carry" CIOS (top limb < 2^31 - 1); its
 //     memory image is the canonical 32-byte little-endian encoding.
-//   * everything is fully unrolled so elements live in VGPRs (Fq = 14, Fr = 8 registers).
+//   * everything is fully unrolled so elements live in VGPRs (Fq = 13, Fr = 8 registers).
 // The same code compiles for the host (final window combination, proof assembly).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -277,33 +277,46 @@ typedef Fp<FqDesc> fq32_t;  // canonical 12 x 32-bit container (wire format conv
 typedef Fp<FrDesc> fr_t;
 
 // ---------------------------------------------------------------------------------------------
-// Fq: 14 x 29-bit limbs, Montgomery form with R = 2^406, values in [0, 2p)
+// Fq: 13 x 30-bit BALANCED SIGNED limbs, Montgomery form with R = 2^390
 // ---------------------------------------------------------------------------------------------
-struct Fq29 {
-    static constexpr int L = 14;
-    static constexpr uint32_t M = (1u << 29) - 1;
-    static constexpr uint32_t INV = 0x1ffcfffdu;  // -p^-1 mod 2^29
-    static constexpr uint32_t P[14] = {0x1fffaaabu, 0x0ff7ffffu, 0x14ffffeeu, 0x17fffd62u, 0x0f6241eau,
-                                       0x09507b58u, 0x0afd9cc3u, 0x109e70a2u, 0x1764774bu, 0x121a5d66u,
-                                       0x12c6e9edu, 0x12ffcd34u, 0x00111ea3u, 0x0000000du};
-    static constexpr uint32_t P2[14] = {0x1fff5556u, 0x1fefffffu, 0x09ffffdcu, 0x0ffffac5u, 0x1ec483d5u,
-                                        0x12a0f6b0u, 0x15fb3986u, 0x013ce144u, 0x0ec8ee97u, 0x0434bacdu,
-                                        0x058dd3dbu, 0x05ff9a69u, 0x00223d47u, 0x0000001au};
-    static constexpr uint32_t ONE[14] = {0x03a9fb84u, 0x0ba00690u, 0x071288f1u, 0x0f59bcc5u, 0x126cb614u,
-                                         0x0585bf36u, 0x1b85ac3du, 0x1cf856fau, 0x1891ecbdu, 0x1a7eec05u,
-                                         0x155a88f0u, 0x0741ac6du, 0x1317c30fu, 0x00000009u};
-    static constexpr uint32_t R2[14] = {0x15bef7aeu, 0x1031cd0eu, 0x02dd93e8u, 0x09226323u, 0x0e6e2cd2u,
-                                        0x11684daau, 0x1170e5dbu, 0x088e25b1u, 0x1b366399u, 0x1c536f47u,
-                                        0x0d1f9cbcu, 0x0278b67fu, 0x1ea66a2bu, 0x0000000cu};
+// A value is V = sum_i v_i 2^(30 i) with limbs 0..11 normalised to [-2^29, 2^29] and a small signed top
+// limb; V is any representative of its residue (no range reduction in add / sub / neg), |V| < 2^388.
+// Why balanced 30-bit limbs (round 5, microbench/fieldmul.hip): a limb product is at most 2^58 in
+// magnitude, so a product-scanning column of 13 a*b + 13 m*p products stays inside a signed 64-bit
+// accumulator (26 * 2^58 = 2^62.7) and every limb product is ONE v_mad_i64_i32: 338 per Montgomery
+// product instead of the 392 v_mad_u64_u32 of 14 x 29-bit unsigned limbs (84.3 vs 79.0 G Fq-mul/s on
+// MI355X, same box).  Unsigned 30-bit limbs would overflow the column (26 * 2^60).  Signed limbs also make
+// negation free (limb-wise) and let add / sub skip the conditional subtraction of 2p: they only carry-
+// normalise.  The Montgomery output satisfies |out| <= |a b| / R + p / 2 (m has balanced digits too), so
+// products pull every magnitude back below ~0.52 p for operands below 3 p, the group law's range.
+// Equality and is_zero work modulo p for any representative (quotient estimate from the top limb, then an
+// exact limb check), so no caller depends on a reduced range.
+struct Fq30 {
+    static constexpr int L = 13;
+    static constexpr uint32_t M = (1u << 30) - 1;
+    static constexpr uint32_t INV = 0x3ffcfffdu;  // -p^-1 mod 2^30
+    static constexpr int32_t P[13] = {-21845,     -402915328, 356515836, -352321620, -252304353, 55215067, 288093811,
+                                      316751073,  -321428361, 517541167, -375082566, -91332614,  1704210};
+    static constexpr int32_t ONE[13] = {13762350,   433586176, -192935228, -301937177, 37952645, -425753694, -36732706,
+                                        162803105,  -437337492, 366579475, 78814996,   -442511456, 89578};
+    static constexpr int32_t R2[13] = {84936463,   -82245875, 20063291,   -375672600, -184045713, -75371400, -508475920,
+                                       172522421,  -150322876, 98350284,  415856896,  -132992156, 1010031};
+    // round(2^52 / (p / 2^360)): quotient estimate k = round(V / p) from the top limb alone (exact for V = k p)
+    static constexpr int64_t QINV = 2642631983ll;
     // p - 2 as 32-bit words (Fermat inversion exponent)
     static constexpr uint32_t PM2[12] = {0xffffaaa9u, 0xb9feffffu, 0xb153ffffu, 0x1eabfffeu,
                                          0xf6b0f624u, 0x6730d2a0u, 0xf38512bfu, 0x64774b84u,
                                          0x434bacd7u, 0x4b1ba7b6u, 0x397fe69au, 0x1a0111eau};
 };
 
+MI_HD int32_t fq_sext30(uint32_t x) { return ((int32_t)(x << 2)) >> 2; }
+
+struct fq_t;
+MI_HD bool fq_is_zero(const fq_t &a);
+
 struct alignas(8) fq_t {
-    static constexpr int L = 14;
-    uint32_t v[14];
+    static constexpr int L = 13;
+    int32_t v[13];
     MI_HD static fq_t zero() {
         fq_t r;
         MI_UNROLL for (int i = 0; i < L; i++) r.v[i] = 0;
@@ -311,268 +324,235 @@ struct alignas(8) fq_t {
     }
     MI_HD static fq_t one() {
         fq_t r;
-        MI_UNROLL for (int i = 0; i < L; i++) r.v[i] = Fq29::ONE[i];
+        MI_UNROLL for (int i = 0; i < L; i++) r.v[i] = Fq30::ONE[i];
         return r;
     }
-    // value == 0 mod p (representatives 0 and p)
-    MI_HD bool is_zero() const {
-        uint32_t z = 0, q = 0;
-        MI_UNROLL for (int i = 0; i < L; i++) {
-            z |= v[i];
-            q |= v[i] ^ Fq29::P[i];
-        }
-        return z == 0 || q == 0;
-    }
+    // value == 0 mod p, for any representative
+    MI_HD bool is_zero() const { return fq_is_zero(*this); }
     MI_HD bool operator==(const fq_t &o) const;
     MI_HD bool operator!=(const fq_t &o) const { return !(*this == o); }
 };
 
-// s - 2p if s >= 2p else s;  s normalised, s < 4p
-MI_HD fq_t fq_sub_2p_if_ge(const uint32_t *s) {
-    fq_t d;
-    int32_t bw = 0;
-    MI_UNROLL for (int i = 0; i < 13; i++) {
-        int32_t t = (int32_t)s[i] - (int32_t)Fq29::P2[i] + bw;
-        d.v[i] = (uint32_t)t & Fq29::M;
-        bw = t >> 29;
+// round(V / p) from the top limb (|V| < 2^388): the other limbs move V / p by < 2^-21, so the estimate is
+// exact whenever V is a multiple of p and within 1 of V / p otherwise
+MI_HD int32_t fq_quot(const fq_t &a) { return (int32_t)(((int64_t)a.v[12] * Fq30::QINV + (1ll << 51)) >> 52); }
+
+// V - k p, carry-normalised (limbs 0..11 in [-2^29, 2^29))
+MI_HD fq_t fq_sub_kp(const fq_t &a, int32_t k) {
+    fq_t r;
+    int64_t c = 0;
+    MI_UNROLL for (int i = 0; i < 12; i++) {
+        const int64_t t = (int64_t)a.v[i] - (int64_t)k * Fq30::P[i] + c;
+        r.v[i] = fq_sext30((uint32_t)t);
+        c = (t + (1 << 29)) >> 30;
     }
-    int32_t top = (int32_t)s[13] - (int32_t)Fq29::P2[13] + bw;
-    d.v[13] = (uint32_t)top;
-    if (top < 0) {
-        MI_UNROLL for (int i = 0; i < 14; i++) d.v[i] = s[i];
+    r.v[12] = (int32_t)((int64_t)a.v[12] - (int64_t)k * Fq30::P[12] + c);
+    return r;
+}
+
+// V == 0 mod p: with k = round(V / p), V is a multiple of p iff V = k p, which first needs the low limb to
+// match (one 32-bit check, the hot path); only then (never, for random data) are all limbs compared
+MI_HD bool fq_is_zero(const fq_t &a) {
+    const int32_t k = fq_quot(a);
+    if ((((uint32_t)a.v[0] - (uint32_t)k * (uint32_t)Fq30::P[0]) & Fq30::M) != 0) return false;
+    const fq_t d = fq_sub_kp(a, k);
+    uint32_t z = 0;
+    MI_UNROLL for (int i = 0; i < 13; i++) z |= (uint32_t)d.v[i];
+    return z == 0;
+}
+
+// carry-normalise limb sums t_i of two normalised operands (|t_i| <= 2^30, so t_i + carry + 2^29 < 2^31):
+// limbs 0..11 into [-2^29, 2^29), the carry into the top
+MI_HD fq_t fq_norm(const int32_t *t) {
+    fq_t r;
+    int32_t c = 0;
+    MI_UNROLL for (int i = 0; i < 12; i++) {
+        const int32_t x = t[i] + c;
+        c = (x + (1 << 29)) >> 30;
+        r.v[i] = x - (int32_t)((uint32_t)c << 30);
     }
-    return d;
+    r.v[12] = t[12] + c;
+    // Magnitude control: products come out below ~0.7 p whatever their inputs, but a value rebuilt from sums alone
+    // (the Miller loop's affine x3 = lambda^2 - 2 x, iterated) would double each time.  Past |V| ~ 2^384 (top limb
+    // 2^24, ~9.8 p) subtract round(V / p) p.  The group law's sums stay below 3 p, so the MSM kernels never take
+    // this branch.
+    const int32_t top = r.v[12] < 0 ? -r.v[12] : r.v[12];
+    if (__builtin_expect(top > (1 << 24), 0)) r = fq_sub_kp(r, fq_quot(r));
+    return r;
 }
 
 MI_HD fq_t operator+(const fq_t &a, const fq_t &b) {
-    uint32_t s[14];
-    uint32_t c = 0;
-    MI_UNROLL for (int i = 0; i < 13; i++) {
-        uint32_t t = a.v[i] + b.v[i] + c;
-        s[i] = t & Fq29::M;
-        c = t >> 29;
-    }
-    s[13] = a.v[13] + b.v[13] + c;
-    return fq_sub_2p_if_ge(s);
+    int32_t t[13];
+    MI_UNROLL for (int i = 0; i < 13; i++) t[i] = a.v[i] + b.v[i];
+    return fq_norm(t);
 }
-
-MI_HD fq_t operator-(const fq_t &a, const fq_t &b) {  // a - b + 2p, then reduce below 2p
-    uint32_t s[14];
-    int32_t c = 0;
-    MI_UNROLL for (int i = 0; i < 13; i++) {
-        int32_t t = (int32_t)a.v[i] - (int32_t)b.v[i] + (int32_t)Fq29::P2[i] + c;
-        s[i] = (uint32_t)t & Fq29::M;
-        c = t >> 29;
-    }
-    s[13] = (uint32_t)((int32_t)a.v[13] - (int32_t)b.v[13] + (int32_t)Fq29::P2[13] + c);
-    return fq_sub_2p_if_ge(s);
+MI_HD fq_t operator-(const fq_t &a, const fq_t &b) {
+    int32_t t[13];
+    MI_UNROLL for (int i = 0; i < 13; i++) t[i] = a.v[i] - b.v[i];
+    return fq_norm(t);
 }
-
-MI_HD fq_t operator-(const fq_t &a) { return fq_t::zero() - a; }
+MI_HD fq_t operator-(const fq_t &a) {  // limb-wise: |-v_i| <= 2^29 stays normalised, and -0 = 0
+    fq_t r;
+    MI_UNROLL for (int i = 0; i < 13; i++) r.v[i] = -a.v[i];
+    return r;
+}
 MI_HD fq_t dbl(const fq_t &a) { return a + a; }
 
-// ---- lazy forms: values that only feed multiplications skip the conditional subtraction ----
-// REDC(a b) = (a b + m p) / R < a b / R + p, so a product is < 2p whenever a b < p R; with
-// R = 2^406 > 2^25 p that holds for operands up to ~2^12 p each.  The column-sum bound of operator*
-// and mul_add (<= 42 products per column) needs carry-normalised 29-bit limbs, not values < 2p, so
-// an unreduced but normalised operand in [0, 4p) costs nothing.  (The group law keeps every value it
-// tests with is_zero or stores reduced to [0, 2p).)
-struct Fq29L {
-    static constexpr uint32_t P4[14] = {0x1ffeaaacu, 0x1fdfffffu, 0x13ffffb9u, 0x1ffff58au, 0x1d8907aau,
-                                        0x0541ed61u, 0x0bf6730du, 0x0279c289u, 0x1d91dd2eu, 0x0869759au,
-                                        0x0b1ba7b6u, 0x0bff34d2u, 0x00447a8eu, 0x00000034u};
-    static constexpr uint32_t P6[14] = {0x1ffe0002u, 0x1fcfffffu, 0x1dffff96u, 0x0ffff04fu, 0x1c4d8b80u,
-                                        0x17e2e412u, 0x01f1ac93u, 0x03b6a3ceu, 0x0c5acbc5u, 0x0c9e3068u,
-                                        0x10a97b91u, 0x11fecf3bu, 0x0066b7d5u, 0x0000004eu};
-};
+// The group law's former lazy forms (values feeding only multiplications skipped the conditional
+// subtraction of the unsigned representation): with signed limbs every add / sub is already "lazy".
+MI_HD fq_t fq_sub_lazy(const fq_t &a, const fq_t &b) { return a - b; }
+MI_HD fq_t fq_neg_lazy(const fq_t &y) { return -y; }
+// X3 = R^2 - PPP - 2Q (three two-operand passes: a three-operand limb sum plus the rounding bias of fq_norm
+// could reach 2^31)
+MI_HD fq_t fq_x3(const fq_t &r2, const fq_t &ppp, const fq_t &q) { return (r2 - ppp) - dbl(q); }
 
-// a - b + 2p for b <= 2p: normalised limbs, value in [0, a + 2p) (not reduced)
-MI_HD fq_t fq_sub_lazy(const fq_t &a, const fq_t &b) {
-    fq_t s;
-    int32_t c = 0;
-    MI_UNROLL for (int i = 0; i < 13; i++) {
-        int32_t t = (int32_t)a.v[i] - (int32_t)b.v[i] + (int32_t)Fq29::P2[i] + c;
-        s.v[i] = (uint32_t)t & Fq29::M;
-        c = t >> 29;
-    }
-    s.v[13] = (uint32_t)((int32_t)a.v[13] - (int32_t)b.v[13] + (int32_t)Fq29::P2[13] + c);
+// sign of the value (-1, 0, 1): the sign of the most significant non-zero limb
+MI_HD int fq_sign(const fq_t &a) {
+    int s = 0;
+    MI_UNROLL for (int i = 0; i < 13; i++) s = a.v[i] > 0 ? 1 : (a.v[i] < 0 ? -1 : s);
     return s;
 }
-
-// -y of an affine coordinate y in [0, 2p] as 2p - y (in [0, 2p]); the raw zero stays zero so the
-// (0, 0) infinity encoding survives negation
-MI_HD fq_t fq_neg_lazy(const fq_t &y) {
-    uint32_t z = 0;
-    MI_UNROLL for (int i = 0; i < 14; i++) z |= y.v[i];
-    const fq_t s = fq_sub_lazy(fq_t::zero(), y);
-    fq_t r;
-    MI_UNROLL for (int i = 0; i < 14; i++) r.v[i] = z ? s.v[i] : 0u;
-    return r;
-}
-
-// X3 = R^2 - PPP - 2Q of the XYZZ additions, reduced to [0, 2p): one signed limb pass computes
-// R^2 + 6p - PPP - 2Q in [0, 8p) (all three inputs < 2p), then 4p and 2p are conditionally subtracted
-// (instead of three add/sub passes with a conditional subtraction each).
-MI_HD fq_t fq_x3(const fq_t &r2, const fq_t &ppp, const fq_t &q) {
-    uint32_t s[14];
-    int32_t c = 0;
-    MI_UNROLL for (int i = 0; i < 13; i++) {
-        int32_t t = (int32_t)r2.v[i] + (int32_t)Fq29L::P6[i] - (int32_t)ppp.v[i] - 2 * (int32_t)q.v[i] + c;
-        s[i] = (uint32_t)t & Fq29::M;
-        c = t >> 29;
-    }
-    s[13] = (uint32_t)((int32_t)r2.v[13] + (int32_t)Fq29L::P6[13] - (int32_t)ppp.v[13] - 2 * (int32_t)q.v[13] + c);
-    uint32_t d[14];
-    int32_t bw = 0;
-    MI_UNROLL for (int i = 0; i < 13; i++) {
-        int32_t t = (int32_t)s[i] - (int32_t)Fq29L::P4[i] + bw;
-        d[i] = (uint32_t)t & Fq29::M;
-        bw = t >> 29;
-    }
-    const int32_t top = (int32_t)s[13] - (int32_t)Fq29L::P4[13] + bw;
-    d[13] = (uint32_t)top;
-    if (top < 0) {
-        MI_UNROLL for (int i = 0; i < 14; i++) d[i] = s[i];
-    }
-    return fq_sub_2p_if_ge(d);
-}
-
-// canonical representative in [0, p)
+// canonical representative in [0, p), normalised limbs (cold paths: encodings, equality of host values)
 MI_HD fq_t fq_canon(const fq_t &a) {
-    fq_t d;
-    int32_t bw = 0;
-    MI_UNROLL for (int i = 0; i < 13; i++) {
-        int32_t t = (int32_t)a.v[i] - (int32_t)Fq29::P[i] + bw;
-        d.v[i] = (uint32_t)t & Fq29::M;
-        bw = t >> 29;
-    }
-    int32_t top = (int32_t)a.v[13] - (int32_t)Fq29::P[13] + bw;
-    d.v[13] = (uint32_t)top;
-    return top < 0 ? a : d;
+    fq_t d = fq_sub_kp(a, fq_quot(a));  // |d| < p
+    if (fq_sign(d) < 0) d = fq_sub_kp(d, -1);
+    const fq_t e = fq_sub_kp(d, 1);
+    return fq_sign(e) >= 0 ? e : d;
 }
 
-MI_HD bool fq_t::operator==(const fq_t &o) const {
-    fq_t a = fq_canon(*this), b = fq_canon(o);
-    uint32_t x = 0;
-    MI_UNROLL for (int i = 0; i < L; i++) x |= a.v[i] ^ b.v[i];
-    return x == 0;
-}
+MI_HD bool fq_t::operator==(const fq_t &o) const { return fq_is_zero(*this - o); }
 
-// Product-scanning Montgomery multiplication, a, b < 2p -> a b R^-1 mod p in [0, 2p).
+// Product-scanning Montgomery multiplication: a b R^-1 mod p, |out| <= |a b| / R + p / 2.
+// Column k <= 12 holds <= 13 a*b and 13 m*p products (|.| <= 2^58) plus a carry: < 2^62.71.
 MI_HD fq_t operator*(const fq_t &a, const fq_t &b) {
-    constexpr int L = 14;
-    uint32_t m[L];
+    constexpr int L = 13;
+    int32_t m[L];
     fq_t r;
-    uint64_t acc = 0;
+    int64_t acc = 0;
     MI_UNROLL for (int k = 0; k < L; k++) {
         MI_UNROLL for (int i = 0; i < k; i++) {
-            acc += (uint64_t)a.v[i] * b.v[k - i];
-            acc += (uint64_t)m[i] * Fq29::P[k - i];
+            acc += (int64_t)a.v[i] * b.v[k - i];
+            acc += (int64_t)m[i] * Fq30::P[k - i];
         }
-        acc += (uint64_t)a.v[k] * b.v[0];
-        m[k] = ((uint32_t)acc * Fq29::INV) & Fq29::M;
-        acc += (uint64_t)m[k] * Fq29::P[0];
-        acc >>= 29;
+        acc += (int64_t)a.v[k] * b.v[0];
+        m[k] = fq_sext30((uint32_t)acc * Fq30::INV);
+        acc += (int64_t)m[k] * Fq30::P[0];
+        acc >>= 30;  // exact: the low 30 bits are zero
     }
     MI_UNROLL for (int k = L; k < 2 * L - 1; k++) {
         MI_UNROLL for (int i = k - L + 1; i < L; i++) {
-            acc += (uint64_t)a.v[i] * b.v[k - i];
-            acc += (uint64_t)m[i] * Fq29::P[k - i];
+            acc += (int64_t)a.v[i] * b.v[k - i];
+            acc += (int64_t)m[i] * Fq30::P[k - i];
         }
-        r.v[k - L] = (uint32_t)acc & Fq29::M;
-        acc >>= 29;
+        r.v[k - L] = fq_sext30((uint32_t)acc);
+        acc = (acc + (1 << 29)) >> 30;  // == (acc - sext30(acc)) >> 30
     }
-    r.v[L - 1] = (uint32_t)acc;
+    r.v[L - 1] = (int32_t)acc;
     return r;
 }
-// Squaring: the same product scanning over the symmetric products only -- column k takes
-// (2 a_i) a_(k-i) for i < k - i and a_(k/2)^2 -- so the product half costs 105 MADs instead of 196
-// (301 instead of 392 in all).  2 a_i < 2^30 for the normalised limbs 0..12 and for a top limb below
-// 2^16 (operands < 2^12 p), so each column stays within operator*'s bound (pair products < 2^59, at most
-// 7 of them, plus 14 reduction products < 2^58).
+// Squaring over the symmetric products: column k takes (2 a_i) a_(k-i) for i < k - i (|.| <= 2^59, at most
+// 6 of them) and a_(k/2)^2, so the product half costs 91 MADs instead of 169 (260 in all); column bound
+// 6 * 2^59 + 14 * 2^58 = 26 * 2^58.
 MI_HD fq_t sqr(const fq_t &a) {
-    constexpr int L = 14;
-    uint32_t a2[L];
-    MI_UNROLL for (int i = 0; i < L; i++) a2[i] = a.v[i] << 1;
-    uint32_t m[L];
+    constexpr int L = 13;
+    int32_t a2[L];
+    MI_UNROLL for (int i = 0; i < L; i++) a2[i] = a.v[i] * 2;
+    int32_t m[L];
     fq_t r;
-    uint64_t acc = 0;
+    int64_t acc = 0;
     MI_UNROLL for (int k = 0; k < L; k++) {
-        MI_UNROLL for (int i = 0; i < k - i; i++) acc += (uint64_t)a2[i] * a.v[k - i];
-        if ((k & 1) == 0) acc += (uint64_t)a.v[k >> 1] * a.v[k >> 1];
-        MI_UNROLL for (int i = 0; i < k; i++) acc += (uint64_t)m[i] * Fq29::P[k - i];
-        m[k] = ((uint32_t)acc * Fq29::INV) & Fq29::M;
-        acc += (uint64_t)m[k] * Fq29::P[0];
-        acc >>= 29;
+        MI_UNROLL for (int i = 0; i < k - i; i++) acc += (int64_t)a2[i] * a.v[k - i];
+        if ((k & 1) == 0) acc += (int64_t)a.v[k >> 1] * a.v[k >> 1];
+        MI_UNROLL for (int i = 0; i < k; i++) acc += (int64_t)m[i] * Fq30::P[k - i];
+        m[k] = fq_sext30((uint32_t)acc * Fq30::INV);
+        acc += (int64_t)m[k] * Fq30::P[0];
+        acc >>= 30;
     }
     MI_UNROLL for (int k = L; k < 2 * L - 1; k++) {
-        MI_UNROLL for (int i = k - L + 1; i < k - i; i++) acc += (uint64_t)a2[i] * a.v[k - i];
-        if ((k & 1) == 0) acc += (uint64_t)a.v[k >> 1] * a.v[k >> 1];
-        MI_UNROLL for (int i = k - L + 1; i < L; i++) acc += (uint64_t)m[i] * Fq29::P[k - i];
-        r.v[k - L] = (uint32_t)acc & Fq29::M;
-        acc >>= 29;
+        MI_UNROLL for (int i = k - L + 1; i < k - i; i++) acc += (int64_t)a2[i] * a.v[k - i];
+        if ((k & 1) == 0) acc += (int64_t)a.v[k >> 1] * a.v[k >> 1];
+        MI_UNROLL for (int i = k - L + 1; i < L; i++) acc += (int64_t)m[i] * Fq30::P[k - i];
+        r.v[k - L] = fq_sext30((uint32_t)acc);
+        acc = (acc + (1 << 29)) >> 30;
     }
-    r.v[L - 1] = (uint32_t)acc;
+    r.v[L - 1] = (int32_t)acc;
     return r;
 }
 
-// a*b + c*d with ONE Montgomery reduction (the group law's "X * Y - Z * W" with c = -Z in lazy
-// form): 392 + 196 MADs instead of 2 x 392 plus a subtraction.  Column sums stay below 2^64:
-// <= 28 products < 2^58 + 14 reduction products < 2^58 + a carry < 2^35 (42 * 2^58 < 2^63.4).
-// Output < (8p^2 + R p) / R < 2p for inputs in [0, 2p) since 8p < R = 2^406.
+// a*b + c*d with ONE Montgomery reduction (the group law's Y3 and the G2 lane-pair product): 507 MADs
+// instead of 2 x 338.  A column can hold 3 x 13 products, more than the accumulator takes, so in columns
+// 10..14 (the only ones with more than 31 products of magnitude 2^58; p_0 and p_12 are small) the a*b and
+// m*p part is split into its high part (kept aside) and its low 30 bits before the c*d products go in.
+// |out| <= (|a b| + |c d|) / R + p / 2.
 MI_HD fq_t mul_add(const fq_t &a, const fq_t &b, const fq_t &c, const fq_t &d) {
-    constexpr int L = 14;
-    uint32_t m[L];
+    constexpr int L = 13;
+    int32_t m[L];
     fq_t r;
-    uint64_t acc = 0;
+    int64_t acc = 0;
     MI_UNROLL for (int k = 0; k < L; k++) {
         MI_UNROLL for (int i = 0; i < k; i++) {
-            acc += (uint64_t)a.v[i] * b.v[k - i];
-            acc += (uint64_t)c.v[i] * d.v[k - i];
-            acc += (uint64_t)m[i] * Fq29::P[k - i];
+            acc += (int64_t)a.v[i] * b.v[k - i];
+            acc += (int64_t)m[i] * Fq30::P[k - i];
         }
-        acc += (uint64_t)a.v[k] * b.v[0];
-        acc += (uint64_t)c.v[k] * d.v[0];
-        m[k] = ((uint32_t)acc * Fq29::INV) & Fq29::M;
-        acc += (uint64_t)m[k] * Fq29::P[0];
-        acc >>= 29;
+        acc += (int64_t)a.v[k] * b.v[0];
+        int64_t hi = 0;
+        if (k >= 10) {
+            hi = acc >> 30;
+            acc &= Fq30::M;
+        }
+        MI_UNROLL for (int i = 0; i <= k; i++) acc += (int64_t)c.v[i] * d.v[k - i];
+        m[k] = fq_sext30((uint32_t)acc * Fq30::INV);
+        acc += (int64_t)m[k] * Fq30::P[0];
+        acc = (acc >> 30) + hi;
     }
     MI_UNROLL for (int k = L; k < 2 * L - 1; k++) {
         MI_UNROLL for (int i = k - L + 1; i < L; i++) {
-            acc += (uint64_t)a.v[i] * b.v[k - i];
-            acc += (uint64_t)c.v[i] * d.v[k - i];
-            acc += (uint64_t)m[i] * Fq29::P[k - i];
+            acc += (int64_t)a.v[i] * b.v[k - i];
+            acc += (int64_t)m[i] * Fq30::P[k - i];
         }
-        r.v[k - L] = (uint32_t)acc & Fq29::M;
-        acc >>= 29;
+        int64_t hi = 0;
+        if (k <= 14) {
+            hi = acc >> 30;
+            acc &= Fq30::M;
+        }
+        MI_UNROLL for (int i = k - L + 1; i < L; i++) acc += (int64_t)c.v[i] * d.v[k - i];
+        r.v[k - L] = fq_sext30((uint32_t)acc);
+        acc = ((acc + (1 << 29)) >> 30) + hi;
     }
-    r.v[L - 1] = (uint32_t)acc;
+    r.v[L - 1] = (int32_t)acc;
     return r;
 }
 
 // canonical 12 x 32-bit integer (< p) -> Montgomery
 MI_HD fq_t fq_from_raw(const fq32_t &raw) {
-    fq_t t;
-    MI_UNROLL for (int i = 0; i < 14; i++) {
-        const int bit = 29 * i, w = bit >> 5, s = bit & 31;
+    int32_t t[13];
+    MI_UNROLL for (int i = 0; i < 13; i++) {
+        const int bit = 30 * i, w = bit >> 5, s = bit & 31;
         uint64_t x = raw.v[w];
         if (w + 1 < 12) x |= (uint64_t)raw.v[w + 1] << 32;
-        t.v[i] = (uint32_t)(x >> s) & Fq29::M;
+        t[i] = (int32_t)((uint32_t)(x >> s) & Fq30::M);  // unsigned 30-bit digits, normalised below
     }
     fq_t r2;
-    MI_UNROLL for (int i = 0; i < 14; i++) r2.v[i] = Fq29::R2[i];
-    return t * r2;
+    MI_UNROLL for (int i = 0; i < 13; i++) r2.v[i] = Fq30::R2[i];
+    return fq_norm(t) * r2;
 }
 // Montgomery -> canonical 12 x 32-bit integer (< p)
 MI_HD fq32_t fq_to_raw(const fq_t &a) {
     fq_t one = fq_t::zero();
     one.v[0] = 1;
-    fq_t c = fq_canon(a * one);
+    const fq_t c = fq_canon(a * one);
+    uint32_t u[13];  // unsigned 30-bit digits of the canonical value
+    int32_t cy = 0;
+    MI_UNROLL for (int i = 0; i < 13; i++) {
+        const int32_t x = c.v[i] + cy;
+        u[i] = (uint32_t)x & Fq30::M;
+        cy = x >> 30;  // floor
+    }
     fq32_t r = fq32_t::zero();
-    MI_UNROLL for (int i = 0; i < 14; i++) {
-        const int bit = 29 * i, w = bit >> 5, s = bit & 31;
-        r.v[w] |= c.v[i] << s;
-        if (s > 3 && w + 1 < 12) r.v[w + 1] |= c.v[i] >> (32 - s);
+    MI_UNROLL for (int i = 0; i < 13; i++) {
+        const int bit = 30 * i, w = bit >> 5, s = bit & 31;
+        r.v[w] |= u[i] << s;
+        if (s > 2 && w + 1 < 12) r.v[w + 1] |= u[i] >> (32 - s);
     }
     return r;
 }
@@ -590,7 +570,7 @@ MI_HD fq_t inverse_inl(const fq_t &a) {
 #pragma unroll 1
         for (int b = 31; b >= 0; b--) {
             r = sqr(r);
-            if ((Fq29::PM2[i] >> b) & 1) r = r * a;
+            if ((Fq30::PM2[i] >> b) & 1) r = r * a;
         }
     return r;
 }

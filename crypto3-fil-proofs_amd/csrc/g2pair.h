@@ -5,9 +5,9 @@
 // scratch spills (2 waves per SIMD at best).  Here lane 2k holds the c0 halves and lane 2k + 1 the c1
 // halves of every Fq2 value of one chunk, so each lane carries Fq-sized state and the pair exchanges
 // halves with one DPP quad_perm move per register:
-//   mul: c0 = a0 b0 + a1 (2p - b1) (even lane), c1 = a0 b1 + a1 b0 (odd lane), each ONE fused
-//        product-scanning Montgomery pass over two products: 2 x 588 lane-MADs, the same MAD count
-//        as a 3-multiplication Karatsuba on one lane;
+//   mul: c0 = a0 b0 + a1 (-b1) (even lane), c1 = a0 b1 + a1 b0 (odd lane), each ONE fused
+//        product-scanning Montgomery pass over two products: 2 x 507 lane-MADs, fewer than a
+//        3-multiplication Karatsuba on one lane (3 x 338);
 //   sqr: c0 = (a0 + a1)(a0 - a1), c1 = 2 a1 a0: one Fq multiplication per lane;
 //   add / sub / neg: component-wise, no exchange;  is_zero: both halves (one exchanged flag).
 // Every branch of the group law depends only on pair-combined predicates, so both lanes of a pair
@@ -23,7 +23,7 @@ __device__ __forceinline__ uint32_t pair_swap(uint32_t x) {
 }
 __device__ __forceinline__ fq_t pair_swap(const fq_t &a) {
     fq_t r;
-    MI_UNROLL for (int i = 0; i < 14; i++) r.v[i] = pair_swap(a.v[i]);
+    MI_UNROLL for (int i = 0; i < fq_t::L; i++) r.v[i] = pair_swap(a.v[i]);
     return r;
 }
 __device__ __forceinline__ bool pair_odd() { return threadIdx.x & 1; }
@@ -42,19 +42,18 @@ __device__ __forceinline__ fq2h_t operator-(const fq2h_t &a, const fq2h_t &b) { 
 __device__ __forceinline__ fq2h_t operator-(const fq2h_t &a) { return {-a.v}; }
 __device__ __forceinline__ fq2h_t dbl(const fq2h_t &a) { return {a.v + a.v}; }
 __device__ __forceinline__ fq2h_t operator*(const fq2h_t &a, const fq2h_t &b) {
-    // even: a0 b0 + a1 (2p - b1)     odd: a0 b1 + a1 b0
-    // The odd lane sends 2p - b1 instead of b1 (sender-side negation), so the received halves are
-    // pa = a_partner, psb = (odd ? b0 : -b1) and both lanes run mul_add(X1, b, X3, psb) with
-    // (X1, X3) = (a, pa) on even lanes and (pa, a) on odd lanes: one unsigned fused REDC
-    // (field.h mul_add: column sums < 2^63.4, result < 2p).
+    // even: a0 b0 + a1 (-b1)     odd: a0 b1 + a1 b0
+    // The odd lane sends -b1 instead of b1 (sender-side negation, limb-wise with signed limbs), so the
+    // received halves are pa = a_partner, psb = (odd ? b0 : -b1) and both lanes run mul_add(X1, b, X3, psb)
+    // with (X1, X3) = (a, pa) on even lanes and (pa, a) on odd lanes: one fused REDC (field.h mul_add).
     __builtin_amdgcn_sched_barrier(0);  // one pair multiplication at a time (register pressure)
     const bool odd = pair_odd();
     const fq_t nb = -b.v;
     fq_t sb;
-    MI_UNROLL for (int i = 0; i < 14; i++) sb.v[i] = odd ? nb.v[i] : b.v.v[i];
+    MI_UNROLL for (int i = 0; i < fq_t::L; i++) sb.v[i] = odd ? nb.v[i] : b.v.v[i];
     const fq_t pa = pair_swap(a.v), psb = pair_swap(sb);
     fq_t x1, x3;
-    MI_UNROLL for (int i = 0; i < 14; i++) {
+    MI_UNROLL for (int i = 0; i < fq_t::L; i++) {
         x1.v[i] = odd ? pa.v[i] : a.v.v[i];
         x3.v[i] = odd ? a.v.v[i] : pa.v[i];
     }

@@ -59,6 +59,8 @@ struct Srs {
     // shared; releasing another key's tables takes it exclusive, and only when no one is using that key.
     int device = -1;
     mutable std::shared_mutex use_mu;
+    // out-of-memory releases that took this key's split tables since they were last built (mi_srs_readmit)
+    uint64_t tables_dropped = 0;
     explicit Srs(int dev);
     Srs(const Srs &) = delete;
     Srs &operator=(const Srs &) = delete;
@@ -121,9 +123,9 @@ struct ProofPoints {
 // sum_i z_i B2_i (G2).  With world > 1 each is one rank's share: the sum over the rank's contiguous slice
 // of every query (h in its bit-reversed device order; single-proof latency mode); the shares of
 // all ranks add up to the full sums.
-struct ProofSums {
-    g1_xyzz_t H, L, A, B1;
-    g2_xyzz_t B2;
+struct ProofSums {  // every sum starts as the identity: a lane that never runs leaves a valid (if wrong) point
+    g1_xyzz_t H = g1_xyzz_t::inf(), L = g1_xyzz_t::inf(), A = g1_xyzz_t::inf(), B1 = g1_xyzz_t::inf();
+    g2_xyzz_t B2 = g2_xyzz_t::inf();
 };
 // The verifying-key points the assembly adds (scheme_params vk: alpha_g1, beta_g1, beta_g2, delta_g1, delta_g2).
 struct AssemblyKey {
@@ -145,7 +147,12 @@ ProofSums groth16_sums(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *
 struct SumRanges {
     uint64_t lo[4] = {0, 0, 0, 0}, cnt[4] = {0, 0, 0, 0};
 };
-ProofSums groth16_sums_ranges(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, const SumRanges &rg);
+// h_in (optional): the d H coefficients of mi_groth16_h_coeffs_dev (canonical, bit-reversed); the share then skips
+// the witness map and the NTT chain
+ProofSums groth16_sums_ranges(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, const SumRanges &rg,
+                               const fr_t *h_in = nullptr);
+// the witness map + NTT chain alone: out = d canonical H coefficients in the key's bit-reversed h order
+void groth16_h_coeffs(Ctx &c, const Circuit &circ, const fr_t *z_dev, fr_t *out);
 SumRanges share_ranges(const Circuit &circ, unsigned rank, unsigned world);
 // releases the 2^128 split tables of a key (its G1 MSMs then take the GLV split); returns the bytes freed.  The
 // caller holds the key exclusively (use_mu) or owns it outright.
@@ -154,6 +161,9 @@ uint64_t srs_drop_split_tables(Srs &S);
 // device that no one is using (`first` before the others; may be null) and the context's idle scratch, except a
 // buffer holding `keep`.  Returns the bytes freed.
 uint64_t release_for_retry(Ctx &c, const Srs *first, const void *keep);
+// rebuilds a key's split tables after an out-of-memory release took them, when they fit under the key-load rule;
+// returns the table bytes rebuilt (0: nothing dropped, or still no room)
+uint64_t srs_readmit(Ctx &c, Srs &S);
 // A = alpha + A_sum + r delta, B = beta + B2_sum + s delta, C = H + L + s A + r B1 - r s delta (host)
 ProofPoints groth16_assemble(const AssemblyKey &k, const ProofSums &sums, const fr_t &r, const fr_t &s);
 // The assembly's terms that depend on the blinding and the key only (five of its seven host scalar

@@ -469,9 +469,14 @@ std::mutex g_keys_mu;
 std::vector<Srs *> g_keys;  // every live proving key (Srs::device says where it lives)
 }  // namespace
 
-Srs::Srs(int dev) : device(dev) {
+Srs::Srs(int dev) : device(dev) {}
+
+// A key joins the registry (and becomes visible to another context's out-of-memory release) only once it is
+// complete: generation and stream loads build their queries and tables with no lock held, so a half-built key in
+// the registry could have its tables freed under the kernels still filling them.
+void srs_publish(Srs *S) {
     std::lock_guard<std::mutex> lk(g_keys_mu);
-    g_keys.push_back(this);
+    g_keys.push_back(S);
 }
 
 Srs::~Srs() {
@@ -834,6 +839,7 @@ Srs *srs_stream_end(Ctx &c, SrsStream *st) {
     }
     st->S = nullptr;
     srs_stream_abort(st);
+    srs_publish(S);
     return S;
 }
 
@@ -1152,6 +1158,7 @@ Srs *srs_generate_once(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5
         delete S;
         throw;
     }
+    srs_publish(S);
     return S;
 }
 }  // namespace
@@ -1171,11 +1178,47 @@ Srs *srs_generate(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5]) {
 
 // ================================================================================ prove
 namespace {
-// One attempt at a proof's MSM sums.  inject_oom (tests, MI_INJECT_PROVE_OOM): after the NTT chain, while the
+// One attempt at a proof's MSM sums.  inject_oom (tests, mi_ctx_inject_oom): after the NTT chain, while the
 // auxiliary lane runs, the main lane asks a scratch buffer for more memory than the device has, so the attempt
 // fails the way a short HBM makes it fail.
+// The witness map and the QAP's NTT chain: A z, B z, C z, three coset round trips and (a b - c) / Z, then the
+// inverse coset transform -> the d canonical H coefficients in bit-reversed order (the key's h_perm order),
+// in the context's prover scratch (slot 20, after the Montgomery witness).
+fr_t *compute_h(Ctx &c, const Circuit &circ, const fr_t *z_dev) {
+    hipStream_t st = c.stream;
+    const uint64_t d = circ.d, nv = circ.n_in + circ.n_aux;
+    const unsigned L = circ.log_d;
+    fr_t *zm = c.scratch[20].as<fr_t>(nv + 3 * d);
+    fr_t *a = zm + nv, *b = a + d, *cc = b + d;
+    k_copy_to_mont<<<grid1(nv), 256, 0, st>>>(z_dev, zm, nv);
+    eval_witness_map(c, circ, zm, a, b, cc);
+    fr_t dd = fr_t::zero();
+    dd.v[0] = (uint32_t)d;
+    dd.v[1] = (uint32_t)(d >> 32);
+    fr_t dinv = inverse(to_mont(dd));
+    fr_t g = fr_small_mont(7);
+    fr_t zinv = inverse(pow_u64(g, d) - fr_t::one());
+    // ifft, * g^i / d, fft on the coset (natural order) for a and b; c's last pass also forms
+    // (a b - c) / Z and starts the inverse coset transform (ntt_coset_qap); MI_QAP_FUSED=0 runs
+    // the separate division pass (A/B)
+    static const bool qap_fused = [] {
+        const char *e = getenv("MI_QAP_FUSED");
+        return !(e && atoi(e) == 0);
+    }();
+    ntt_coset_roundtrip(c, a, L, dinv);
+    ntt_coset_roundtrip(c, b, L, dinv);
+    if (!qap_fused || !ntt_coset_qap(c, a, b, cc, L, dinv, zinv)) {
+        ntt_coset_roundtrip(c, cc, L, dinv);
+        k_qap_divide<<<grid1(d), 256, 0, st>>>(a, b, cc, d, zinv);
+        ntt_dif_coset_epilogue(c, a, L, true, true, dinv, true);  // icoset, canonical H (bit-reversed)
+    }
+    return a;
+}
+
+// h_in (optional): the H coefficients computed elsewhere (mi_groth16_h_coeffs_dev on a latency group's lead rank,
+// broadcast to the group), so this share runs its H slice without the witness map and the NTT chain.
 ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, const SumRanges &rg,
-                            bool inject_oom) {
+                            bool inject_oom, const fr_t *h_in) {
     std::shared_lock<std::shared_mutex> in_use(srs.use_mu);
     if (srs.d != circ.d || srs.n_l != circ.n_aux || srs.n_a != circ.n_a || srs.n_b != circ.n_b)
         throw std::invalid_argument("SRS does not match circuit");
@@ -1198,10 +1241,8 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
         // second host thread) while this stream runs the witness map, the NTT chain, H and A.
         // MI_PROVE_LANES=1 runs the auxiliary work after the main lane on the same stream (measurement
         // only: every phase's device time without the other lane's kernels beside it)
-        static const bool one_lane = [] {
-            const char *e = getenv("MI_PROVE_LANES");
-            return e && atoi(e) == 1;
-        }();
+        const char *ole = getenv("MI_PROVE_LANES");  // read per call: bench.py times a one-lane proof beside the default
+        const bool one_lane = ole && atoi(ole) == 1;
         // Small proofs (domain <= 2^MI_PROVE_WIDE_LOG, default 2^21: Winning PoSt, 2^19) are latency-bound: their
         // MSMs' bucket reductions, sorts and host round trips leave most CUs idle, so B_G2, L and A + B_G1 each get
         // a lane of their own (three auxiliary streams and host threads beside the main lane's witness map, NTT
@@ -1225,7 +1266,8 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
         // again for itself (no plan is shared between lanes: the G2 second level reuses its plan's scratch).
         // Same box, Winning PoSt: 23.1 ms with B_G1 beside B_G2, 20.5 ms after A.
         const char *b1e = getenv("MI_PROVE_B1_LANE");
-        const unsigned b1_lane = wide ? (b1e ? (unsigned)atoi(b1e) : 2u) : 0u;
+        unsigned b1_lane = wide ? (b1e ? (unsigned)atoi(b1e) : 2u) : 0u;
+        if (b1_lane > 2) b1_lane = 2;  // every value names a lane that computes B_G1
         auto run_b = [&](Ctx &x) {
             const uint64_t lo = rg.lo[3], cnt = rg.cnt[3];
             MsmPlan pb;
@@ -1280,34 +1322,8 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
             for (unsigned k = 0; k < nlanes; k++) lanes[k] = std::thread(lane_work, k);
         std::exception_ptr err_main;
         try {
-            fr_t *a = nullptr;
-            if (need_h) {
-            fr_t *zm = c.scratch[20].as<fr_t>(nv + 3 * d);
-            a = zm + nv;
-            fr_t *b = a + d, *cc = b + d;
-            k_copy_to_mont<<<grid1(nv), 256, 0, st>>>(z_dev, zm, nv);
-            eval_witness_map(c, circ, zm, a, b, cc);
-            fr_t dd = fr_t::zero();
-            dd.v[0] = (uint32_t)d;
-            dd.v[1] = (uint32_t)(d >> 32);
-            fr_t dinv = inverse(to_mont(dd));
-            fr_t g = fr_small_mont(7);
-            fr_t zinv = inverse(pow_u64(g, d) - fr_t::one());
-            // ifft, * g^i / d, fft on the coset (natural order) for a and b; c's last pass also forms
-            // (a b - c) / Z and starts the inverse coset transform (ntt_coset_qap); MI_QAP_FUSED=0 runs
-            // the separate division pass (A/B)
-            static const bool qap_fused = [] {
-                const char *e = getenv("MI_QAP_FUSED");
-                return !(e && atoi(e) == 0);
-            }();
-            ntt_coset_roundtrip(c, a, L, dinv);
-            ntt_coset_roundtrip(c, b, L, dinv);
-            if (!qap_fused || !ntt_coset_qap(c, a, b, cc, L, dinv, zinv)) {
-                ntt_coset_roundtrip(c, cc, L, dinv);
-                k_qap_divide<<<grid1(d), 256, 0, st>>>(a, b, cc, d, zinv);
-                ntt_dif_coset_epilogue(c, a, L, true, true, dinv, true);  // icoset, canonical H (bit-reversed)
-            }
-            }
+            const fr_t *a = h_in;
+            if (need_h && !a) a = compute_h(c, circ, z_dev);
             if (inject_oom) (void)c.scratch[19].get(1ull << 50);  // a real failed growth (1 PiB), as a scratch
                                                                     // buffer's hipMalloc fails when HBM is short
             const uint64_t h_lo = rg.lo[0], h_cnt = rg.cnt[0];
@@ -1379,7 +1395,9 @@ uint64_t release_device_tables(int device, const Srs *first) {
         if (!k->h_hi && !k->l_hi && !k->a_hi && !k->at) continue;
         std::unique_lock<std::shared_mutex> ex(k->use_mu, std::try_to_lock);
         if (!ex.owns_lock()) continue;
-        freed += srs_drop_split_tables(*k);
+        const uint64_t t = srs_drop_split_tables(*k);
+        if (t) k->tables_dropped += 1;  // mi_srs_readmit rebuilds them once memory allows
+        freed += t;
         // a generated key's per-variable trapdoor evaluations (3 x 32 B per variable: 12.5 GB at 2^27) serve
         // only mi_groth16_trapdoor_dlogs, a test aid; they go too, and that call then reports them missing
         const struct {
@@ -1415,6 +1433,22 @@ uint64_t release_prover_scratch(Ctx &c, const void *keep) {
 }
 }  // namespace
 
+// Rebuilds the split tables an out-of-memory release took from a key, under the key-load admission rule
+// (build_hi_tables: only while they leave a proof its working set).  Returns the bytes of tables rebuilt.
+uint64_t srs_readmit(Ctx &c, Srs &S) {
+    std::unique_lock<std::shared_mutex> ex(S.use_mu);  // no proof or MSM over the key while its tables change
+    if (!S.tables_dropped || S.h_hi || S.l_hi || S.a_hi) return 0;
+    release_prover_scratch(c, nullptr);  // this context's idle arenas would count against the admission
+    build_hi_tables(c, S);
+    MI_HIP(hipStreamSynchronize(c.stream));
+    uint64_t got = 0;
+    if (S.h_hi) got += S.n_h * sizeof(g1_affine_t);
+    if (S.l_hi) got += S.n_l * sizeof(g1_affine_t);
+    if (S.a_hi) got += S.n_a * sizeof(g1_affine_t);
+    if (got) S.tables_dropped = 0;
+    return got;
+}
+
 uint64_t release_for_retry(Ctx &c, const Srs *first, const void *keep) {
     (void)hipStreamSynchronize(c.stream);
     for (Ctx *x = c.aux; x; x = x->aux) (void)hipStreamSynchronize(x->stream);
@@ -1429,16 +1463,28 @@ uint64_t release_for_retry(Ctx &c, const Srs *first, const void *keep) {
 // released, and the proof runs again; its G1 MSMs take the GLV split, which needs no table (glv.h).  The MSM
 // sums are unique group elements, so the retried proof is byte-identical.  A second out-of-memory error
 // propagates.
-ProofSums groth16_sums_ranges(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, const SumRanges &rg) {
-    const bool inject = getenv("MI_INJECT_PROVE_OOM") != nullptr;
+ProofSums groth16_sums_ranges(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, const SumRanges &rg,
+                               const fr_t *h_in) {
+    // test hook (mi_ctx_inject_oom): a counter on the context, not an environment lookup in the production path
+    bool inject = false;
+    if (c.inject_oom != 0) {
+        inject = true;
+        if (c.inject_oom > 0) c.inject_oom -= 1;
+    }
     try {
-        return groth16_sums_once(c, srs, circ, z_dev, rg, inject);
+        return groth16_sums_once(c, srs, circ, z_dev, rg, inject, h_in);
     } catch (const hip_error &e) {
         if (e.code != hipErrorOutOfMemory) throw;
         c.stats.oom_retries += 1;
-        c.stats.oom_freed_bytes += release_for_retry(c, &srs, z_dev);
-        return groth16_sums_once(c, srs, circ, z_dev, rg, false);
+        c.stats.oom_freed_bytes += release_for_retry(c, &srs, h_in ? (const void *)h_in : (const void *)z_dev);
+        return groth16_sums_once(c, srs, circ, z_dev, rg, false, h_in);
     }
+}
+
+void groth16_h_coeffs(Ctx &c, const Circuit &circ, const fr_t *z_dev, fr_t *out) {
+    const fr_t *a = compute_h(c, circ, z_dev);
+    MI_HIP(hipMemcpyAsync(out, a, 32 * circ.d, hipMemcpyDeviceToDevice, c.stream));
+    MI_HIP(hipStreamSynchronize(c.stream));
 }
 
 SumRanges share_ranges(const Circuit &circ, unsigned rank, unsigned world) {
@@ -1569,6 +1615,8 @@ static fr_t device_dot(Ctx &c, const fr_t *z, const fr_t *e, uint64_t off, uint6
 
 void groth16_trapdoor_dlogs(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *z_dev, const fr_t &r,
                             const fr_t &s, fr_t out[3]) {
+    // another context's out-of-memory release may free at / bt / ct and clear has_trapdoor: hold the key
+    std::shared_lock<std::shared_mutex> in_use(srs.use_mu);
     if (!srs.has_trapdoor)
         throw std::invalid_argument("SRS was not generated from known toxic waste (or its trapdoor evaluations were "
                                     "released to make room for a proof)");

@@ -149,6 +149,8 @@ void public_inputs(const Built &b, const uint8_t *slots, std::vector<fr_t> &out)
 // written completely (z[0] = ONE, the public inputs, every aux variable), canonical little-endian.
 // Returns after the last kernel finished (on the context stream).  Phase timings go to c.stats.
 void witness_dev(Ctx &c, Built &b, const uint8_t *slots_dev, fr_t *z_dev);
+// drops the device programs a context (Ctx::uid) uploaded into every circuit (mi_ctx_destroy)
+void forget_ctx(uint64_t uid);
 
 // Poseidon circuit constraint count for one hash (3 per first-round S-box of an input, 4 per later S-box,
 // 1 for the digest): 311 / 377 / 505 / 598 for arity 2 / 4 / 8 / 11

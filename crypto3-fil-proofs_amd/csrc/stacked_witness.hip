@@ -521,10 +521,18 @@ T *upload(const std::vector<T> &v) {
     return d;
 }
 
+// every Built holding device programs, so a context's programs go when the context does (forget_ctx)
+std::mutex g_built_mu;
+std::vector<Built *> g_built;
+
 DevProg *prog_for(Ctx &c, Built &b) {
     std::lock_guard<std::mutex> lk(b.dev_mu);
     for (auto &e : b.dev_progs)
         if (e.first == c.uid) return (DevProg *)e.second;
+    if (b.dev_progs.empty()) {
+        std::lock_guard<std::mutex> g(g_built_mu);
+        g_built.push_back(&b);
+    }
     DevProg *p = new DevProg();
     try {
         p->device = c.device;
@@ -555,7 +563,35 @@ unsigned grid64(uint64_t n) { return (unsigned)((n + 63) / 64); }
 }  // namespace
 
 Built::~Built() {
+    {
+        std::lock_guard<std::mutex> g(g_built_mu);
+        for (size_t i = 0; i < g_built.size(); i++)
+            if (g_built[i] == this) {
+                g_built.erase(g_built.begin() + i);
+                break;
+            }
+    }
     for (auto &e : dev_progs) delete (DevProg *)e.second;
+}
+
+// A destroyed context's device programs (their ops, pin lists and SHA state scratch, and the views of its
+// Poseidon tables, which poseidon_free releases) are dropped from every circuit (long-lived circuits
+// with many short-lived contexts used to keep them all).
+void forget_ctx(uint64_t uid) {
+    std::lock_guard<std::mutex> g(g_built_mu);
+    for (size_t i = 0; i < g_built.size();) {
+        Built *b = g_built[i];
+        std::lock_guard<std::mutex> lk(b->dev_mu);
+        for (size_t j = 0; j < b->dev_progs.size();)
+            if (b->dev_progs[j].first == uid) {
+                delete (DevProg *)b->dev_progs[j].second;
+                b->dev_progs.erase(b->dev_progs.begin() + j);
+            } else {
+                j++;
+            }
+        if (b->dev_progs.empty()) g_built.erase(g_built.begin() + i);
+        else i++;
+    }
 }
 
 void witness_dev(Ctx &c, Built &b, const uint8_t *slots_dev, fr_t *z_dev) {

@@ -7,7 +7,8 @@ reference-side binding.
 from ._lib import EXPORTS, LIB_PATH, FilGpuError, build, lib  # noqa: F401
 from .core import (FR_MODULUS, PROOF_BYTES, SHARE_BYTES, VK_BYTES, Circuit, Context, HostBuffer, Points,  # noqa: F401
                    ProvingKey, assemble, device_count, fr_bytes, generate_random_parameters, msm_window_bits,
-                   params_inspect, pairing, prove, prove_batch, prove_share, prove_share_ranges, trapdoor_dlogs, verify, verify_batch)
+                   params_inspect, pairing, prove, param_cache_id, param_cache_path, param_cache_metadata,
+                   get_groth_params, PARAMS, META, VK, prove_batch, prove_share, prove_share_ranges, h_coeffs_dev, trapdoor_dlogs, verify, verify_batch)
 from .compound import (MultiProof, partition_count, get_partitions_for_window_post,  # noqa: F401
                        circuit_proofs, seal_commit_phase2_proofs, generate_window_post_proofs,
                        generate_winning_post_proof)

@@ -12,6 +12,7 @@ LIB_PATH = os.environ.get("FILGPU_LIB", os.path.join(_PKG_ROOT, "build", "libfil
 # Every symbol declared in include/mi355x_groth16.h (checked by tests/test_abi.py)
 EXPORTS = [
     "mi_device_count", "mi_ctx_create", "mi_ctx_destroy", "mi_last_error", "mi_ctx_stream", "mi_ctx_synchronize",
+    "mi_ctx_set_caller_stream",
     "mi_circuit_load", "mi_circuit_info", "mi_circuit_free",
     "mi_srs_load", "mi_srs_generate", "mi_srs_export_vk", "mi_srs_export_query", "mi_srs_info", "mi_srs_free",
     "mi_groth16_prove", "mi_groth16_prove_dev", "mi_groth16_prove_batch", "mi_groth16_trapdoor_dlogs",
@@ -29,7 +30,9 @@ EXPORTS = [
     "mi_tree_build", "mi_tree_build_dev", "mi_tree_c_build", "mi_tree_c_build_dev",
     "mi_tree_r_last_build", "mi_tree_r_last_build_dev",
     "mi_sdr_labels", "mi_sdr_labels_dev", "mi_sdr_labeling_proofs_dev", "mi_tree_inclusion_paths_dev", "mi_tree_d_inclusion_paths_dev",
-    "mi_tree_d_build_dev", "mi_srs_msm_info", "mi_points_check_subgroup", "mi_points_info",
+    "mi_tree_d_build_dev", "mi_srs_msm_info", "mi_srs_table_state", "mi_srs_readmit", "mi_ctx_inject_oom",
+    "mi_param_cache_id", "mi_param_cache_path", "mi_param_cache_metadata", "mi_get_groth_params",
+    "mi_groth16_h_coeffs_dev", "mi_groth16_prove_share_ranges_h_dev", "mi_points_check_subgroup", "mi_points_info",
     "mi_groth16_prove_random", "mi_groth16_prove_dev_random", "mi_groth16_prove_batch_random",
     "mi_srs_stream_begin", "mi_srs_stream_part", "mi_srs_stream_end", "mi_srs_stream_abort", "mi_srs_export_query_dev",
     "mi_stacked_build", "mi_post_build", "mi_stacked_info", "mi_stacked_r1cs", "mi_stacked_load", "mi_stacked_public_inputs", "mi_stacked_witness_dev",
@@ -45,16 +48,22 @@ class FilGpuError(RuntimeError):
         self.code = code
 
 
-def torch_sync():
-    """Before a device-pointer entry: the library runs on its own streams, so work the caller queued on torch's
-    current stream (the fill or copy that produced an input tensor, or an earlier reader of an output buffer) is
-    finished first.  The C ABI's contract is the same (device inputs complete before the call); this keeps the
-    Python callers, which hand over torch tensors, inside it.  No-op without torch or before CUDA is initialised."""
+def torch_sync(ctx):
+    """Before a device-pointer entry: name torch's current stream on ctx's device as the library's caller stream
+    (mi_ctx_set_caller_stream).  The C ABI then orders its first device access after the work queued there --
+    the fill or copy that produced an input tensor, or an earlier reader of an output buffer -- with an event
+    waited for on the device, not a host synchronisation (include/mi355x_groth16.h, "device pointers").  The
+    entries return with their outputs written.  No-op without torch or before CUDA is initialised (the library's
+    default caller stream, the legacy NULL stream, then covers every blocking stream)."""
     import sys
 
     t = sys.modules.get("torch")
     if t is not None and t.cuda.is_initialized():
-        t.cuda.current_stream().synchronize()
+        dev = getattr(ctx, "device", 0)
+        if "mi_ctx_set_caller_stream" in lib().missing_symbols:  # a pre-round-5 library: host synchronisation
+            t.cuda.current_stream(dev).synchronize()
+            return
+        check(lib().mi_ctx_set_caller_stream(ctx.h, ctypes.c_void_p(t.cuda.current_stream(dev).cuda_stream or None)))
 
 
 def build():
@@ -89,6 +98,7 @@ def lib():
         "mi_last_error": ([], ctypes.c_char_p),
         "mi_ctx_stream": ([vp, pp], c_int),
         "mi_ctx_synchronize": ([vp], c_int),
+        "mi_ctx_set_caller_stream": ([vp, vp], c_int),
         "mi_circuit_load": ([vp, vp, pp], c_int),
         "mi_circuit_info": ([vp, vp], c_int),
         "mi_circuit_free": ([vp], None),
@@ -99,6 +109,15 @@ def lib():
         "mi_srs_info": ([vp, vp], c_int),
         "mi_srs_free": ([vp], None),
         "mi_srs_msm_info": ([vp, vp], c_int),
+        "mi_srs_table_state": ([vp, vp], c_int),
+        "mi_srs_readmit": ([vp, vp, vp], c_int),
+        "mi_ctx_inject_oom": ([vp, ctypes.c_int64], c_int),
+        "mi_param_cache_id": ([u8p, u8p, vp, ctypes.c_size_t], c_int),
+        "mi_param_cache_path": ([u8p, c_int, vp, ctypes.c_size_t], c_int),
+        "mi_param_cache_metadata": ([u8p, u64, vp], c_int),
+        "mi_get_groth_params": ([vp, vp, u8p, vp, c_int, pp, ctypes.POINTER(c_int)], c_int),
+        "mi_groth16_h_coeffs_dev": ([vp, vp, vp, vp], c_int),
+        "mi_groth16_prove_share_ranges_h_dev": ([vp, vp, vp, vp, vp, vp, c_int, vp], c_int),
         "mi_stacked_build": ([vp, c_int, pp], c_int),
         "mi_post_build": ([vp, c_int, pp], c_int),
         "mi_stacked_load": ([vp, vp, pp], c_int),
@@ -177,10 +196,16 @@ def lib():
         "mi_sdr_labeling_proofs_dev": ([vp, vp, ctypes.c_uint, u64, vp, u64, vp, vp, vp, ctypes.c_uint,
                                         ctypes.c_uint, vp, vp], c_int),
     }
+    missing = []
     for name, (args, res) in sig.items():
-        f = getattr(L, name)
+        try:
+            f = getattr(L, name)
+        except AttributeError:  # an older build (same-box A/B of library variants): fails when called
+            missing.append(name)
+            continue
         f.argtypes = args
         f.restype = res
+    L.missing_symbols = missing
     _lib = L
     return L
 

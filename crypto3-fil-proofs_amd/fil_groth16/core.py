@@ -101,6 +101,11 @@ class Context:
         check(lib().mi_ctx_get_fallbacks(self.h, w))
         return {"oom_retries": int(w[0]), "freed_bytes": int(w[1])}
 
+    def inject_oom(self, count: int):
+        """TEST ONLY (mi_ctx_inject_oom): the first attempt of each of the next ``count`` proofs fails with a real
+        out-of-memory error after the NTT chain (-1: every proof, 0: off)"""
+        check(lib().mi_ctx_inject_oom(self.h, int(count)))
+
     # ---- building blocks ----
     def msm_g1(self, bases96: bytes, scalars32: bytes) -> bytes:
         n = len(scalars32) // 32
@@ -123,7 +128,7 @@ class Context:
         return buf.raw
 
     def ntt_dev(self, data_ptr: int, log_n: int, inverse=False, coset=False):
-        torch_sync()
+        torch_sync(self)
         check(lib().mi_ntt_fr_dev(self.h, ctypes.c_void_p(data_ptr), log_n, int(inverse), int(coset)))
 
 
@@ -156,7 +161,7 @@ class Points:
     def msm_dev(self, scalars_ptr: int, n: int) -> bytes:
         out = ctypes.create_string_buffer(192 if self.g2 else 96)
         f = lib().mi_msm_g2_dev if self.g2 else lib().mi_msm_g1_dev
-        torch_sync()
+        torch_sync(self.ctx)
         check(f(self.ctx.h, self.h, ctypes.c_void_p(scalars_ptr), n, out))
         return out.raw
 
@@ -235,7 +240,7 @@ class SrsStream:
 
     def part(self, which: int, first: int, data, n: int, on_device=False):
         if on_device:
-            torch_sync()
+            torch_sync(self.ctx)
             ptr, keep = ctypes.c_void_p(int(data)), None
         else:
             buf = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray)
@@ -316,7 +321,7 @@ class ProvingKey:
     def export_query_dev(self, which: int, first: int, n: int, dev_ptr: int):
         """points [first, first + n) of one query (0 h natural order, 1 l, 2 a, 3 b_g1, 4 b_g2) in the wire
         format, written to device memory"""
-        torch_sync()
+        torch_sync(self.ctx)
         check(lib().mi_srs_export_query_dev(self.ctx.h, self.h, which, first, n, ctypes.c_void_p(dev_ptr)))
 
     def msm_info(self):
@@ -325,6 +330,19 @@ class ProvingKey:
         out = (ctypes.c_uint64 * 2)()
         check(lib().mi_srs_msm_info(self.h, out))
         return {"split_tables": bool(out[0]), "subgroup": bool(out[1])}
+
+    def table_state(self):
+        """{"split_tables", "dropped": out-of-memory releases since the tables were last built, "subgroup"}"""
+        out = (ctypes.c_uint64 * 3)()
+        check(lib().mi_srs_table_state(self.h, out))
+        return {"split_tables": bool(out[0]), "dropped": int(out[1]), "subgroup": bool(out[2])}
+
+    def readmit(self) -> int:
+        """rebuilds split tables an out-of-memory release took, once they fit again (mi_srs_readmit); returns the
+        table bytes rebuilt"""
+        got = ctypes.c_uint64()
+        check(lib().mi_srs_readmit(self.ctx.h, self.h, ctypes.byref(got)))
+        return int(got.value)
 
     def verifying_key(self):
         vk = ctypes.create_string_buffer(VK_BYTES)
@@ -394,6 +412,44 @@ def params_inspect(path: str) -> dict:
     return dict(zip(("ic", "h", "l", "a", "b_g1", "b_g2"), list(out)))
 
 
+# ---- parameter cache (core/parameter_cache.hpp:50-219; mi_param_cache_* / mi_get_groth_params) ----
+PARAMS_VERSION = 28
+PARAMS, META, VK = 0, 1, 2  # parameter_cache_{params,metadata,verifying_key}_path
+
+
+def _cstr(f, *args) -> str:
+    buf = ctypes.create_string_buffer(4096)
+    check(f(*args, buf, len(buf)))
+    return buf.value.decode()
+
+
+def param_cache_id(cache_prefix: str, identifier: str) -> str:
+    """cacheable_parameters::cache_identifier: "<cache_prefix>-<hex sha256(identifier)>" """
+    return _cstr(lib().mi_param_cache_id, cache_prefix.encode(), identifier.encode())
+
+
+def param_cache_path(cache_id: str, kind: int = PARAMS) -> str:
+    """$FIL_PROOFS_PARAMETER_CACHE/v28-<id>.params / .meta / .vk"""
+    return _cstr(lib().mi_param_cache_path, cache_id.encode(), int(kind))
+
+
+def param_cache_metadata(cache_id: str, sector_size: int) -> int:
+    """get_param_metadata: the cached sector size, written on first use"""
+    out = ctypes.c_uint64()
+    check(lib().mi_param_cache_metadata(cache_id.encode(), int(sector_size), ctypes.byref(out)))
+    return int(out.value)
+
+
+def get_groth_params(ctx: Context, circuit: Circuit, cache_id: str, toxic=None, checked=False):
+    """get_groth_params: the cached key when <id>.params exists and parses, else a generated one (from ``toxic``,
+    or OS randomness when None), written to the cache together with <id>.vk.  Returns (ProvingKey, generated)."""
+    hd, gen = ctypes.c_void_p(), ctypes.c_int()
+    tb = b"".join(fr_bytes(t) for t in toxic) if toxic is not None else None
+    check(lib().mi_get_groth_params(ctx.h, circuit.h, cache_id.encode(), tb, int(checked), ctypes.byref(hd),
+                                    ctypes.byref(gen)))
+    return ProvingKey(ctx, hd), bool(gen.value)
+
+
 def generate_random_parameters(ctx: Context, circuit: Circuit, toxic) -> ProvingKey:
     """GPU groth16::generate_random_parameters with known toxic waste (tau, alpha, beta, gamma, delta)."""
     tb = b"".join(fr_bytes(t) for t in toxic)
@@ -412,7 +468,7 @@ def prove(ctx: Context, pk: ProvingKey, circuit: Circuit, z, r: int = None, s: i
         if want_raw:
             raise ValueError("want_raw needs injected r, s")
         if isinstance(z, int):
-            torch_sync()
+            torch_sync(ctx)
             check(lib().mi_groth16_prove_dev_random(ctx.h, pk.h, circuit.h, ctypes.c_void_p(z), int(priority), proof))
         else:
             assert len(z) == 32 * circuit.num_vars, "witness length must be (num_inputs + num_aux) * 32"
@@ -422,7 +478,7 @@ def prove(ctx: Context, pk: ProvingKey, circuit: Circuit, z, r: int = None, s: i
         raise ValueError("give both r and s, or neither")
     raw = ctypes.create_string_buffer(384) if want_raw else None
     if isinstance(z, int):
-        torch_sync()
+        torch_sync(ctx)
         check(lib().mi_groth16_prove_dev(ctx.h, pk.h, circuit.h, ctypes.c_void_p(z), fr_bytes(r), fr_bytes(s),
                                          int(priority), proof, raw))
     else:
@@ -497,17 +553,32 @@ def prove_batch(ctx: Context, pk: ProvingKey, circuit: Circuit, zs, rs=None, pri
     return [out.raw[i * PROOF_BYTES:(i + 1) * PROOF_BYTES] for i in range(count)]
 
 
-def prove_share_ranges(ctx: Context, pk: ProvingKey, circuit: Circuit, z, ranges, priority=False) -> bytes:
+def h_coeffs_dev(ctx: Context, circuit: Circuit, z_dev_ptr: int, h_out_ptr: int):
+    """mi_groth16_h_coeffs_dev: the witness map + NTT chain alone; writes d x 32 B canonical H coefficients (the
+    key's bit-reversed h order) to device memory (a latency group's lead broadcasts them)"""
+    torch_sync(ctx)
+    check(lib().mi_groth16_h_coeffs_dev(ctx.h, circuit.h, ctypes.c_void_p(z_dev_ptr), ctypes.c_void_p(h_out_ptr)))
+
+
+def prove_share_ranges(ctx: Context, pk: ProvingKey, circuit: Circuit, z, ranges, priority=False, h_dev=None) -> bytes:
     """A latency-mode share over explicit query ranges: ranges = [(first, count)] for H (d - 1 points, h order),
-    L, A and B (B_G1 and B_G2); H is computed (witness map + NTT chain) only when its count is non-zero.
-    z as for ``prove``.  Shares whose ranges partition every query go to ``assemble``."""
+    L, A and B (B_G1 and B_G2); H is computed (witness map + NTT chain) only when its count is non-zero and no
+    ``h_dev`` (device pointer to h_coeffs_dev's output) is given.  z as for ``prove`` (a device pointer when h_dev
+    is given).  Shares whose ranges partition every query go to ``assemble`` (a rank may contribute several)."""
     flat = [int(v) for fc in ranges for v in fc]
     if len(flat) != 8:
         raise ValueError("four (first, count) ranges: H, L, A, B")
     arr = (ctypes.c_uint64 * 8)(*flat)
     out = ctypes.create_string_buffer(SHARE_BYTES)
+    if h_dev is not None:
+        if not isinstance(z, int):
+            raise ValueError("h_dev needs a device witness pointer")
+        torch_sync(ctx)
+        check(lib().mi_groth16_prove_share_ranges_h_dev(ctx.h, pk.h, circuit.h, ctypes.c_void_p(z),
+                                                        ctypes.c_void_p(h_dev), arr, int(priority), out))
+        return out.raw
     if isinstance(z, int):
-        torch_sync()
+        torch_sync(ctx)
         check(lib().mi_groth16_prove_share_ranges_dev(ctx.h, pk.h, circuit.h, ctypes.c_void_p(z), arr, int(priority),
                                                       out))
     else:
@@ -521,7 +592,7 @@ def prove_share(ctx: Context, pk: ProvingKey, circuit: Circuit, z, rank: int, wo
     (SHARE_BYTES). z as for ``prove``. The shares of ranks 0..world-1 go to ``assemble``."""
     out = ctypes.create_string_buffer(SHARE_BYTES)
     if isinstance(z, int):
-        torch_sync()
+        torch_sync(ctx)
         check(lib().mi_groth16_prove_share_dev(ctx.h, pk.h, circuit.h, ctypes.c_void_p(z), rank, world,
                                                int(priority), out))
     else:
@@ -544,7 +615,7 @@ def assemble(vk: bytes, shares, r: int, s: int, want_raw=False):
 
 def trapdoor_dlogs(ctx: Context, pk: ProvingKey, circuit: Circuit, z_dev_ptr: int, r: int, s: int):
     out = ctypes.create_string_buffer(96)
-    torch_sync()
+    torch_sync(ctx)
     check(lib().mi_groth16_trapdoor_dlogs(ctx.h, pk.h, circuit.h, ctypes.c_void_p(z_dev_ptr), fr_bytes(r),
                                           fr_bytes(s), out))
     return [int.from_bytes(out.raw[32 * i:32 * i + 32], "little") for i in range(3)]

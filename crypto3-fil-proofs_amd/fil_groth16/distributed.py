@@ -118,37 +118,74 @@ def agree_blinding(count: int, rank: int, device="cpu"):
     return [(ints[2 * i], ints[2 * i + 1]) for i in range(count)]
 
 
+MAX_SHARES = 2  # shares one rank contributes to a tail proof (H-split groups: its L/A/B slice, then its H slice)
+
+
+def group_broadcaster(ranks, device="cpu"):
+    """bcast(tensor) over the process subgroup ``ranks`` from its first rank (the group's lead), in place; every
+    process must create the subgroups of a schedule in the same order (torch.distributed.new_group).  Without a
+    process group (one rank) it is the identity."""
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()):
+        return lambda t: (lambda: t)
+    pg = dist.new_group(ranks)
+
+    def bcast(t):
+        """starts the broadcast of t (asynchronous: RCCL on its own stream); returns done() -> t, which waits for
+        it (and orders torch's current stream after it, so the library's caller-stream fence covers the data)"""
+        work = dist.broadcast(t, ranks[0], group=pg, async_op=True)
+
+        def done():
+            work.wait()
+            return t
+
+        return done
+
+    return bcast
+
+
 def prove_partitions_balanced(prove_fn, share_fn, assemble_fn, num_partitions: int, rank: int, world: int,
-                              device="cpu"):
+                              device="cpu", group_bcast=False):
     """prove_partitions with the balanced_schedule: ``prove_fn(ids) -> [192-byte proofs]`` for this rank's
-    whole partitions, ``share_fn(partition, k, g) -> 576-byte share`` for its slice k of g of a tail
-    partition, ``assemble_fn(partition, shares) -> 192-byte proof`` (fg.assemble with that partition's
-    blinding, identical on every rank).  One all-gather carries every rank's whole proofs and its share;
-    each rank then assembles the tail proofs itself.  Returns the P x 192-byte multi-proof (partition
-    order) on every rank, byte-identical to prove_partitions' for the same blinding."""
+    whole partitions, ``share_fn(partition, k, g) -> 576-byte share`` (or a list of up to MAX_SHARES of them)
+    for its slice k of g of a tail partition, ``assemble_fn(partition, shares) -> 192-byte proof`` (fg.assemble
+    with that partition's blinding, identical on every rank).  group_bcast: share_fn gets a fourth argument, the
+    tail group's broadcaster (group_broadcaster: H coefficients from the lead, hsplit_shares).  One all-gather
+    carries every rank's whole proofs and its shares; each rank then assembles the tail proofs itself.  Returns
+    the P x 192-byte multi-proof (partition order) on every rank, byte-identical to prove_partitions' for the
+    same blinding."""
     import torch
 
     whole, tail = balanced_schedule(num_partitions, world)
+    bcasts = {p: group_broadcaster(ranks, device) for p, ranks in tail} if group_bcast else {}
     kmax = max((len(w) for w in whole), default=0)
     local = list(prove_fn(whole[rank])) if whole[rank] else []
     if len(local) != len(whole[rank]) or any(len(p) != PROOF_BYTES for p in local):
         raise ValueError(f"rank {rank}: prove_fn returned {len(local)} proofs for {len(whole[rank])} partitions")
-    rec = np.zeros(kmax * PROOF_BYTES + SHARE_BYTES, dtype=np.uint8)
+    base = kmax * PROOF_BYTES
+    rec = np.zeros(base + 1 + MAX_SHARES * SHARE_BYTES, dtype=np.uint8)
     for i, p in enumerate(local):
         rec[i * PROOF_BYTES:(i + 1) * PROOF_BYTES] = np.frombuffer(p, dtype=np.uint8)
     for p, ranks in tail:
         if rank in ranks:
-            share = share_fn(p, ranks.index(rank), len(ranks))
-            if len(share) != SHARE_BYTES:
-                raise ValueError(f"shares are {SHARE_BYTES} bytes")
-            rec[kmax * PROOF_BYTES:] = np.frombuffer(share, dtype=np.uint8)
+            args = (p, ranks.index(rank), len(ranks)) + ((bcasts[p],) if group_bcast else ())
+            got = share_fn(*args)
+            shares = [got] if isinstance(got, (bytes, bytearray)) else list(got)
+            if not 1 <= len(shares) <= MAX_SHARES or any(len(sh) != SHARE_BYTES for sh in shares):
+                raise ValueError(f"one to {MAX_SHARES} shares of {SHARE_BYTES} bytes per rank")
+            rec[base] = len(shares)
+            for j, sh in enumerate(shares):
+                rec[base + 1 + j * SHARE_BYTES:base + 1 + (j + 1) * SHARE_BYTES] = np.frombuffer(sh, dtype=np.uint8)
     allr = _all_gather(torch.from_numpy(rec).to(device), world)
     out = {}
     for r in range(world):
         for i, p in enumerate(whole[r]):
             out[p] = allr[r][i * PROOF_BYTES:(i + 1) * PROOF_BYTES].tobytes()
     for p, ranks in tail:
-        out[p] = assemble_fn(p, [allr[r][kmax * PROOF_BYTES:].tobytes() for r in ranks])
+        sh = [allr[r][base + 1 + j * SHARE_BYTES:base + 1 + (j + 1) * SHARE_BYTES].tobytes()
+              for r in ranks for j in range(int(allr[r][base]))]
+        out[p] = assemble_fn(p, sh)
     return b"".join(out[p] for p in range(num_partitions))
 
 
@@ -177,6 +214,93 @@ def latency_ranges(sizes, group: int, lead_share: float = 0.0):
             hi = n0 + rest * k // (group - 1)
             out[k][q] = (lo, hi - lo)
     return out
+
+
+def latency_ranges_hsplit(sizes, group: int, h_lead: float, lab_lead: float = 0.0):
+    """Query ranges of a latency group that computes H ONCE and SPLITS it: the lead (rank 0 of the
+    group) runs the witness map and the NTT chain (mi_groth16_h_coeffs_dev), broadcasts the d H coefficients over
+    the group, and takes the fraction ``h_lead`` of the H query plus ``lab_lead`` of L, A and B; ranks 1 .. g - 1
+    split the rest of every query into equal contiguous slices.  One [(first, count)] x 4 (H, L, A, B) list per
+    rank; together they partition every query (the assembled proof equals the one-GPU proof)."""
+    if group < 1:
+        raise ValueError("a group has at least one rank")
+    if not (0.0 <= h_lead <= 1.0 and 0.0 <= lab_lead <= 1.0):
+        raise ValueError("lead fractions are in [0, 1]")
+    n = [int(x) for x in sizes]
+    if group == 1:
+        return [[(0, n[0]), (0, n[1]), (0, n[2]), (0, n[3])]]
+    out = [[None] * 4 for _ in range(group)]
+    for q in range(4):
+        n0 = int(round(n[q] * (h_lead if q == 0 else lab_lead)))
+        out[0][q] = (0, n0)
+        rest = n[q] - n0
+        for k in range(1, group):
+            lo = n0 + rest * (k - 1) // (group - 1)
+            hi = n0 + rest * k // (group - 1)
+            out[k][q] = (lo, hi - lo)
+    return out
+
+
+def hsplit_fractions(t_qap: float, t_hmsm: float, t_lab: float, group: int):
+    """(h_lead, lab_lead) that even out an H-split group: t_qap = witness map + NTT chain (the lead alone), t_hmsm =
+    the whole H MSM, t_lab = L, A and B, all on one GPU.  The lead runs t_qap + h t_hmsm + f t_lab, every other rank
+    ((1 - h) t_hmsm + (1 - f) t_lab) / (g - 1).  With f = 0: h = (t_lab + t_hmsm - (g - 1) t_qap) / (g t_hmsm); if
+    that exceeds 1 the lead takes all of H and f = (t_lab - (g - 1)(t_qap + t_hmsm)) / (g t_lab); if it is negative
+    the NTT chain alone outweighs a share (h = f = 0).  Clamped to [0, 1]."""
+    if group <= 1:
+        return 1.0, 1.0
+    h = (t_lab + t_hmsm - (group - 1) * t_qap) / (group * t_hmsm) if t_hmsm > 0 else 1.0
+    if h <= 1.0:
+        return max(0.0, h), 0.0
+    f = (t_lab - (group - 1) * (t_qap + t_hmsm)) / (group * t_lab) if t_lab > 0 else 0.0
+    return 1.0, min(1.0, max(0.0, f))
+
+
+def hsplit_shares(k: int, ranges, h_coeffs_fn, share_fn, bcast):
+    """This rank's shares of an H-split tail proof (latency_ranges_hsplit): ``h_coeffs_fn() -> H tensor`` on the
+    lead (witness map + NTT chain), ``bcast(tensor) -> done()`` the group broadcaster (group_broadcaster) -- the
+    lead's tensor goes out, the others receive into ``h_coeffs_fn(None)``'s buffer -- and ``share_fn(ranges, h) ->
+    576 bytes``.  The lead starts the broadcast and proves all its ranges with the H it computed while the
+    broadcast is in flight; every other rank first proves its L / A / B slice (no H needed: it runs while the
+    lead's NTT chain and the broadcast are under way), then waits for H and proves its H slice.  Returns a list of
+    one or two shares (prove_partitions_balanced carries both)."""
+    if k == 0:
+        h = h_coeffs_fn()
+        done = bcast(h)
+        share = share_fn(ranges[0], h)
+        done()
+        return [share]
+    rg = ranges[k]
+    lab_only = [(rg[0][0], 0), rg[1], rg[2], rg[3]]
+    h_only = [rg[0], (rg[1][0], 0), (rg[2][0], 0), (rg[3][0], 0)]
+    first = share_fn(lab_only, None)
+    h = bcast(h_coeffs_fn(None))()
+    return [first, share_fn(h_only, h)]
+
+
+def calibrate_hsplit(ctx, pk, circuit, z_dev: int, h_dev: int, reps: int = 1):
+    """One GPU's times of the three parts of an H-split proof (after a warm call each): t_qap_ms (witness map + NTT
+    chain, mi_groth16_h_coeffs_dev into h_dev), t_hmsm_ms (the whole H MSM from h_dev), t_lab_ms (L, A, B)."""
+    import time
+
+    from .core import h_coeffs_dev, prove_share_ranges
+
+    sizes = (pk.n_h, pk.n_l, pk.n_a, pk.n_b)
+    parts = {"t_qap_ms": lambda: h_coeffs_dev(ctx, circuit, z_dev, h_dev),
+             "t_hmsm_ms": lambda: prove_share_ranges(ctx, pk, circuit, z_dev, [(0, sizes[0]), (0, 0), (0, 0), (0, 0)],
+                                                     h_dev=h_dev),
+             "t_lab_ms": lambda: prove_share_ranges(ctx, pk, circuit, z_dev,
+                                                    [(0, 0), (0, sizes[1]), (0, sizes[2]), (0, sizes[3])])}
+    t = {}
+    for name, fn in parts.items():
+        fn()
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        ctx.synchronize()
+        t[name] = 1e3 * (time.perf_counter() - t0) / reps
+    return t
 
 
 def lead_share_from_times(t_h: float, t_lab: float, group: int) -> float:

@@ -58,7 +58,7 @@ def create_labels_dev(ctx, replica_id: bytes, count: int, layers_dev: int, nodes
                       n_parents: int, labels_dev: int) -> None:
     """Device-resident form of create_labels (raw device pointers, e.g. torch tensor data_ptr())."""
     rp, k = _ptr(bytes(replica_id))
-    torch_sync()
+    torch_sync(ctx)
     check(lib().mi_sdr_labels_dev(ctx.h, rp, count, ctypes.c_void_p(layers_dev), ctypes.c_void_p(nodes_dev),
                                   ctypes.c_void_p(parents_dev), n_parents, ctypes.c_void_p(labels_dev)))
 
@@ -72,7 +72,7 @@ def labeling_proofs_dev(ctx, replica_id: bytes, n_layers: int, nodes_per_layer: 
     indices raise FilGpuError (MI_ERR_ARG) before any gather."""
     rp, k = _ptr(bytes(replica_id))
     vp = ctypes.c_void_p
-    torch_sync()
+    torch_sync(ctx)
     check(lib().mi_sdr_labeling_proofs_dev(ctx.h, rp, n_layers, nodes_per_layer, vp(layer_labels_dev), count,
                                            vp(layers_dev), vp(challenges_dev), vp(parent_idx_dev), n_base, n_exp,
                                            vp(labels_dev), vp(parents_out_dev or None)))
@@ -118,7 +118,7 @@ class EncodingProof:
 def build_tree_d_dev(ctx, leaves_ptr: int, leafs: int, tree_ptr: int) -> None:
     """tree D over 32-byte data nodes on the device (node = SHA256(left || right), byte 31 &= 0x3f): every row
     above the leaves, bottom-up, leafs - 1 entries.  Openings: tree_d_proofs_dev."""
-    torch_sync()
+    torch_sync(ctx)
     check(lib().mi_tree_d_build_dev(ctx.h, ctypes.c_void_p(leaves_ptr), leafs, ctypes.c_void_p(tree_ptr)))
 
 
@@ -128,6 +128,6 @@ def tree_d_proofs_dev(ctx, leaves_ptr: int, leafs: int, tree_ptr: int, count: in
     the layouts of tree.gen_proofs_dev at arity 2; every row is cached, so nothing is rebuilt (a rebuild would
     need SHA-256, and tree.gen_proofs_dev rebuilds discarded rows with Poseidon)."""
     vp = ctypes.c_void_p
-    torch_sync()
+    torch_sync(ctx)
     check(lib().mi_tree_d_inclusion_paths_dev(ctx.h, vp(leaves_ptr), leafs, vp(tree_ptr), count, vp(challenges_ptr),
                                               vp(leaf_out_ptr), vp(siblings_out_ptr)))

@@ -111,7 +111,7 @@ class _BuiltCircuit:
         return out.raw
 
     def witness_dev(self, ctx, slots_dev_ptr: int, z_dev_ptr: int):
-        torch_sync()
+        torch_sync(ctx)
         check(lib().mi_stacked_witness_dev(ctx.h, self.h, ctypes.c_void_p(slots_dev_ptr), ctypes.c_void_p(z_dev_ptr)))
 
     def __del__(self):
@@ -305,7 +305,7 @@ def synthetic_winning_post_instance(ctx, circuit: WinningPoStCircuit, seed: int 
 def circuit_check_dev(ctx, circuit: Circuit, z_dev_ptr: int):
     """(unsatisfied rows, first unsatisfied row or None) of A z * B z = C z on the device"""
     out = (ctypes.c_uint64 * 2)()
-    torch_sync()
+    torch_sync(ctx)
     check(lib().mi_circuit_check_dev(ctx.h, circuit.h, ctypes.c_void_p(z_dev_ptr), out))
     return int(out[0]), (None if out[1] == 2 ** 64 - 1 else int(out[1]))
 

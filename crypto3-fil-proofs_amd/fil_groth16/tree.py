@@ -80,7 +80,7 @@ def poseidon_hash(ctx, arity: int, preimages) -> bytes:
 
 
 def poseidon_hash_dev(ctx, arity: int, in_ptr: int, count: int, out_ptr: int):
-    torch_sync()
+    torch_sync(ctx)
     check(lib().mi_poseidon_hash_dev(ctx.h, arity, ctypes.c_void_p(in_ptr), count, ctypes.c_void_p(out_ptr)))
 
 
@@ -131,7 +131,7 @@ class ColumnTreeBuilder:
 
     def add_final_columns_dev(self, labels_ptr: int, nodes: int, base_ptr: int, tree_ptr: int):
         """device variant: labels layer-major at labels_ptr (layer l at entry l * nodes)."""
-        torch_sync()
+        torch_sync(self.ctx)
         check(lib().mi_tree_c_build_dev(self.ctx.h, self.column_arity, nodes, ctypes.c_void_p(labels_ptr),
                                         self.tree_arity, ctypes.c_void_p(base_ptr), ctypes.c_void_p(tree_ptr)))
 
@@ -153,7 +153,7 @@ def generate_tree_r_last(ctx, last_layer_labels, data, arity: int = 8, rows_to_d
 
 def generate_tree_r_last_dev(ctx, nodes: int, labels_ptr: int, data_ptr: int, tree_ptr: int, arity: int = 8,
                              rows_to_discard: int = 0):
-    torch_sync()
+    torch_sync(ctx)
     check(lib().mi_tree_r_last_build_dev(ctx.h, nodes, ctypes.c_void_p(labels_ptr), ctypes.c_void_p(data_ptr),
                                          arity, rows_to_discard, ctypes.c_void_p(tree_ptr)))
 
@@ -177,7 +177,7 @@ def gen_proofs_dev(ctx, arity: int, leaves_ptr: int, leafs: int, rows_to_discard
     j = 0 .. height-1 the arity - 1 siblings in position order skipping the path's own slot (digit j of the
     challenge in base arity).  tree_ptr holds the cached rows built with the same rows_to_discard."""
     vp = ctypes.c_void_p
-    torch_sync()
+    torch_sync(ctx)
     check(lib().mi_tree_inclusion_paths_dev(ctx.h, arity, vp(leaves_ptr), leafs, rows_to_discard, vp(tree_ptr), count,
                                             vp(challenges_ptr), vp(leaf_out_ptr), vp(siblings_out_ptr)))
 

@@ -76,7 +76,7 @@ __device__ __forceinline__ void mac(Acc96 &a, uint32_t x, uint32_t y) {
         : "v"(x), "v"(y)
         : "vcc");
 }
-__device__ __forceinline__ fq_t mul_v1(const fq_t &a, const fq_t &b) {
+__device__ __forceinline__ fq32_t mul_v1(const fq32_t &a, const fq32_t &b) {
     constexpr int N = 12;
     uint32_t m[N], t[N];
     Acc96 acc = {0, 0};
@@ -101,7 +101,7 @@ __device__ __forceinline__ fq_t mul_v1(const fq_t &a, const fq_t &b) {
         acc.c2 = 0;
     }
     t[N - 1] = (uint32_t)acc.lo;
-    fq_t r;
+    fq32_t r;
     MI_UNROLL for (int i = 0; i < N; i++) r.v[i] = t[i];
     return reduce_once(r);
 }
@@ -144,7 +144,7 @@ __device__ __forceinline__ fq29 mul_v2(const fq29 &a, const fq29 &b) {
     r.v[L29 - 1] = (uint32_t)acc;
     return r;
 }
-__device__ fq29 to29(const fq_t &raw) {  // 12x32 -> 14x29 (raw integer)
+__device__ fq29 to29(const fq32_t &raw) {  // 12x32 -> 14x29 (raw integer)
     fq29 r;
     MI_UNROLL for (int i = 0; i < L29; i++) {
         int bit = 29 * i, w = bit >> 5, s = bit & 31;
@@ -154,8 +154,8 @@ __device__ fq29 to29(const fq_t &raw) {  // 12x32 -> 14x29 (raw integer)
     }
     return r;
 }
-__device__ fq_t from29(const fq29 &a) {  // 14x29 -> 12x32 (assumes normalized, < 2^384)
-    fq_t r = fq_t::zero();
+__device__ fq32_t from29(const fq29 &a) {  // 14x29 -> 12x32 (assumes normalized, < 2^384)
+    fq32_t r = fq32_t::zero();
     MI_UNROLL for (int i = 0; i < L29; i++) {
         int bit = 29 * i, w = bit >> 5, s = bit & 31;
         r.v[w] |= a.v[i] << s;
@@ -164,16 +164,112 @@ __device__ fq_t from29(const fq29 &a) {  // 14x29 -> 12x32 (assumes normalized, 
     return r;
 }
 
-// ------------------------------------------------------------------------------ throughput kernels
-__global__ void __launch_bounds__(256) k_v0(fq_t *d, int iters) {
+// ------------------------------------------------------------------------------ v3: 13 x 30-bit balanced
+// Signed limbs in [-2^29, 2^29): every limb product is at most 2^58 in magnitude, so a column of 13 a*b plus
+// 13 m*p products (plus a carry) stays inside a signed 64-bit accumulator (26 * 2^58 = 2^62.7) -- one
+// v_mad_i64_i32 per limb product, 338 per multiplication instead of 392 over 14 x 29-bit limbs.
+constexpr int L30 = 13;
+constexpr int32_t P30[L30] = {-21845, -402915328, 356515836, -352321620, -252304353, 55215067, 288093811,
+                              316751073, -321428361, 517541167, -375082566, -91332614, 1704210};
+constexpr int32_t R2_30[L30] = {84936463, -82245875, 20063291, -375672600, -184045713, -75371400, -508475920,
+                                172522421, -150322876, 98350284, 415856896, -132992156, 1010031};
+constexpr uint32_t INV30 = 0x3ffcfffdu;  // -p^-1 mod 2^30
+struct fqs {
+    int32_t v[L30];
+};
+__device__ __forceinline__ int32_t sext30(uint32_t x) { return ((int32_t)(x << 2)) >> 2; }
+__device__ __forceinline__ fqs mul_v3(const fqs &a, const fqs &b) {
+    int32_t m[L30];
+    fqs r;
+    int64_t acc = 0;
+    MI_UNROLL for (int k = 0; k < L30; k++) {
+        MI_UNROLL for (int i = 0; i < k; i++) {
+            acc += (int64_t)a.v[i] * b.v[k - i];
+            acc += (int64_t)m[i] * P30[k - i];
+        }
+        acc += (int64_t)a.v[k] * b.v[0];
+        m[k] = sext30((uint32_t)acc * INV30);
+        acc += (int64_t)m[k] * P30[0];
+        acc >>= 30;
+    }
+    MI_UNROLL for (int k = L30; k < 2 * L30 - 1; k++) {
+        MI_UNROLL for (int i = k - L30 + 1; i < L30; i++) {
+            acc += (int64_t)a.v[i] * b.v[k - i];
+            acc += (int64_t)m[i] * P30[k - i];
+        }
+        r.v[k - L30] = sext30((uint32_t)acc);
+        acc = (acc + (1 << 29)) >> 30;  // == (acc - sext30(acc)) >> 30
+    }
+    r.v[L30 - 1] = (int32_t)acc;
+    return r;
+}
+__device__ fqs to30(const fq32_t &raw) {  // 12x32 canonical -> balanced 13x30
+    fqs r;
+    int32_t c = 0;
+    MI_UNROLL for (int i = 0; i < L30; i++) {
+        int bit = 30 * i, w = bit >> 5, s = bit & 31;
+        uint64_t x = raw.v[w];
+        if (w + 1 < 12) x |= (uint64_t)raw.v[w + 1] << 32;
+        int32_t d = (int32_t)((uint32_t)(x >> s) & ((1u << 30) - 1)) + c;
+        if (i < L30 - 1) {
+            c = d >= (1 << 29) ? 1 : 0;
+            d -= c << 30;
+        }
+        r.v[i] = d;
+    }
+    return r;
+}
+__device__ fq32_t from30(const fqs &a0) {  // balanced, |value| < p -> canonical 12x32
+    fqs a = a0;
+    int top = 0;
+    for (int i = L30 - 1; i >= 0; i--)
+        if (a.v[i] != 0) { top = a.v[i] < 0 ? -1 : 1; break; }
+    if (top < 0)
+        for (int i = 0; i < L30; i++) a.v[i] += P30[i];
+    uint32_t u[L30];
+    int64_t c = 0;
+    for (int i = 0; i < L30; i++) {
+        int64_t t = (int64_t)a.v[i] + c;
+        u[i] = (uint32_t)(t & ((1 << 30) - 1));
+        c = t >> 30;
+    }
+    fq32_t r = fq32_t::zero();
+    for (int i = 0; i < L30; i++) {
+        int bit = 30 * i, w = bit >> 5, s = bit & 31;
+        r.v[w] |= u[i] << s;
+        if (s > 2 && w + 1 < 12) r.v[w + 1] |= u[i] >> (32 - s);
+    }
+    return r;
+}
+__global__ void __launch_bounds__(256) k_v3(fqs *d, int iters) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    fq_t x = d[i], y = d[i ^ 1];
+    fqs x = d[i], y = d[i ^ 1];
+    for (int it = 0; it < iters; it++) x = mul_v3(x, y);
+    d[i] = x;
+}
+__global__ void k_check3(const fq32_t *xs, const fq32_t *ys, int n, int *bad) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fq32_t x = xs[i], y = ys[i];
+    fq32_t ref = from_mont(to_mont(x) * to_mont(y));
+    fqs R2v, one = {};
+    MI_UNROLL for (int k = 0; k < L30; k++) R2v.v[k] = R2_30[k];
+    one.v[0] = 1;
+    fqs a = mul_v3(to30(x), R2v), b = mul_v3(to30(y), R2v);
+    fq32_t v3 = from30(mul_v3(mul_v3(a, b), one));
+    if (!(v3 == ref)) atomicAdd(bad + 2, 1);
+}
+
+// ------------------------------------------------------------------------------ throughput kernels
+__global__ void __launch_bounds__(256) k_v0(fq32_t *d, int iters) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    fq32_t x = d[i], y = d[i ^ 1];
     for (int it = 0; it < iters; it++) x = x * y;
     d[i] = x;
 }
-__global__ void __launch_bounds__(256) k_v1(fq_t *d, int iters) {
+__global__ void __launch_bounds__(256) k_v1(fq32_t *d, int iters) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    fq_t x = d[i], y = d[i ^ 1];
+    fq32_t x = d[i], y = d[i ^ 1];
     for (int it = 0; it < iters; it++) x = mul_v1(x, y);
     d[i] = x;
 }
@@ -185,22 +281,22 @@ __global__ void __launch_bounds__(256) k_v2(fq29 *d, int iters) {
 }
 
 // correctness: x*y for random canonical x, y through each variant, compared canonically
-__global__ void k_check(const fq_t *xs, const fq_t *ys, int n, int *bad) {
+__global__ void k_check(const fq32_t *xs, const fq32_t *ys, int n, int *bad) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    fq_t x = xs[i], y = ys[i];
-    fq_t ref = from_mont(to_mont(x) * to_mont(y));
-    fq_t r2;
+    fq32_t x = xs[i], y = ys[i];
+    fq32_t ref = from_mont(to_mont(x) * to_mont(y));
+    fq32_t r2;
     MI_UNROLL for (int k = 0; k < 12; k++) r2.v[k] = FqDesc::R2[k];
-    fq_t one = fq_t::zero();
+    fq32_t one = fq32_t::zero();
     one.v[0] = 1;
-    fq_t v1 = mul_v1(mul_v1(mul_v1(x, r2), mul_v1(y, r2)), one);
+    fq32_t v1 = mul_v1(mul_v1(mul_v1(x, r2), mul_v1(y, r2)), one);
     fq29 R2v, one29 = {};
     MI_UNROLL for (int k = 0; k < L29; k++) R2v.v[k] = R2_29[k];
     one29.v[0] = 1;
     fq29 a = mul_v2(to29(x), R2v), b = mul_v2(to29(y), R2v);
     fq29 c = mul_v2(mul_v2(a, b), one29);
-    fq_t v2 = reduce_once(from29(c));
+    fq32_t v2 = reduce_once(from29(c));
     if (!(v1 == ref)) atomicAdd(bad, 1);
     if (!(v2 == ref)) atomicAdd(bad + 1, 1);
 }
@@ -240,7 +336,7 @@ int main() {
 
     // correctness
     const int nc = 1 << 16;
-    fq_t *hx = (fq_t *)malloc(sizeof(fq_t) * nc * 2);
+    fq32_t *hx = (fq32_t *)malloc(sizeof(fq32_t) * nc * 2);
     srand(1);
     for (int i = 0; i < 2 * nc; i++) {
         for (int k = 0; k < 12; k++) hx[i].v[k] = ((uint32_t)rand() << 16) ^ (uint32_t)rand();
@@ -254,22 +350,24 @@ int main() {
     }
     hx[1].v[0] -= 1;
     hx[nc].v[0] -= 1;
-    fq_t *dx;
+    fq32_t *dx;
     int *bad;
-    CHECK(hipMalloc(&dx, sizeof(fq_t) * nc * 2));
-    CHECK(hipMalloc(&bad, 8));
-    CHECK(hipMemset(bad, 0, 8));
-    CHECK(hipMemcpy(dx, hx, sizeof(fq_t) * nc * 2, hipMemcpyHostToDevice));
+    CHECK(hipMalloc(&dx, sizeof(fq32_t) * nc * 2));
+    CHECK(hipMalloc(&bad, 12));
+    CHECK(hipMemset(bad, 0, 12));
+    CHECK(hipMemcpy(dx, hx, sizeof(fq32_t) * nc * 2, hipMemcpyHostToDevice));
     hipLaunchKernelGGL(k_check, dim3(nc / 256), dim3(256), 0, 0, dx, dx + nc, nc, bad);
-    int hb[2];
-    CHECK(hipMemcpy(hb, bad, 8, hipMemcpyDeviceToHost));
-    printf("correctness vs v0 over %d random products: v1 mismatches %d, v2 mismatches %d\n", nc, hb[0], hb[1]);
+    hipLaunchKernelGGL(k_check3, dim3(nc / 256), dim3(256), 0, 0, dx, dx + nc, nc, bad);
+    int hb[3];
+    CHECK(hipMemcpy(hb, bad, 12, hipMemcpyDeviceToHost));
+    printf("correctness vs v0 over %d random products: v1 mismatches %d, v2 mismatches %d, v3 mismatches %d\n", nc,
+           hb[0], hb[1], hb[2]);
 
     // throughput
     it = 200;
-    fq_t *d0;
-    CHECK(hipMalloc(&d0, sizeof(fq_t) * nt));
-    CHECK(hipMemset(d0, 1, sizeof(fq_t) * nt));
+    fq32_t *d0;
+    CHECK(hipMalloc(&d0, sizeof(fq32_t) * nt));
+    CHECK(hipMemset(d0, 1, sizeof(fq32_t) * nt));
     double muls = (double)nt * it;
     ms = timeit(k_v0, dim3(blocks), dim3(threads), d0, it);
     printf("v0 CIOS (compiler)     : %.2f G Fq-mul/s\n", muls / ms / 1e6);
@@ -280,5 +378,14 @@ int main() {
     CHECK(hipMemset(d2, 1, sizeof(fq29) * nt));
     ms = timeit(k_v2, dim3(blocks), dim3(threads), d2, it);
     printf("v2 FIPS 29-bit limbs   : %.2f G Fq-mul/s\n", muls / ms / 1e6);
+    fqs *d3;
+    CHECK(hipMalloc(&d3, sizeof(fqs) * nt));
+    CHECK(hipMemset(d3, 1, sizeof(fqs) * nt));
+    for (int rep = 0; rep < 3; rep++) {
+        ms = timeit(k_v2, dim3(blocks), dim3(threads), d2, it);
+        printf("v2 FIPS 29-bit limbs   : %.2f G Fq-mul/s\n", muls / ms / 1e6);
+        ms = timeit(k_v3, dim3(blocks), dim3(threads), d3, it);
+        printf("v3 13x30 balanced      : %.2f G Fq-mul/s\n", muls / ms / 1e6);
+    }
     return 0;
 }

@@ -49,7 +49,7 @@ __device__ __forceinline__ uint64_t stamp_real() {
 
 // point record layouts for the gather form: the earlier library's 112-byte record (7 x 16 B, straddling a
 // 128-byte line for 7 of 8 records), the same padded to an aligned 128-byte line, and 96 bytes of packed
-// 32-bit words (the canonical width) unpacked to 14 x 29-bit limbs in registers
+// 32-bit words (the canonical width) unpacked to 13 balanced 30-bit limbs in registers
 struct alignas(16) Rec112 {  // the round-2 / round-3 library record (curve.h Affine before the padding)
     fq_t x, y;
 };
@@ -61,15 +61,15 @@ struct alignas(32) Rec96 {
     uint32_t w[24];
 };
 __device__ __forceinline__ fq_t unpack29(const uint32_t *w) {
-    fq_t r;
+    int32_t t[13];
 #pragma unroll
-    for (int i = 0; i < 14; i++) {
-        const int bit = 29 * i, k = bit >> 5, sh = bit & 31;
+    for (int i = 0; i < 13; i++) {
+        const int bit = 30 * i, k = bit >> 5, sh = bit & 31;
         uint64_t x = w[k];
         if (k + 1 < 12) x |= (uint64_t)w[k + 1] << 32;
-        r.v[i] = (uint32_t)(x >> sh) & Fq29::M;
+        t[i] = (int32_t)((uint32_t)(x >> sh) & Fq30::M);
     }
-    return r;
+    return fq_norm(t);
 }
 template <class T>
 __device__ __forceinline__ Affine<fq_t> ld(const T *t, uint32_t i) {
@@ -299,7 +299,7 @@ __global__ void __launch_bounds__(256) k_ba_g2(const T *__restrict__ table, uint
     }
 }
 
-// random field elements (14 limbs below 2^381, not reduced) as batch-affine accumulator starts, on the device
+// random field elements (balanced 30-bit limbs, small top limb) as batch-affine accumulator starts, on the device
 template <class F>
 __global__ void k_fill(F *__restrict__ out, uint64_t n, uint32_t seed) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -308,7 +308,7 @@ __global__ void k_fill(F *__restrict__ out, uint64_t n, uint32_t seed) {
     constexpr int L = sizeof(F) / 4;
     for (int q = 0; q < L; q++) {
         uint32_t h = hidx((uint32_t)i, seed, q) ^ (uint32_t)(i >> 32);
-        w[q] = (q % 14 == 13) ? (h & 0xf) : (h & Fq29::M);
+        w[q] = (q % 14 == 13) ? 0u : (q % 14 == 12) ? (h & 0xfffff) : (h & Fq30::M) - (1u << 29);
     }
 }
 
@@ -378,12 +378,12 @@ int main(int argc, char **argv) {
     std::vector<Rec112> h(tn);
     uint64_t s = 12345;
     for (uint32_t i = 0; i < tn; i++) {
-        for (int k = 0; k < 14; k++) {
-            h[i].x.v[k] = rng32(s) & Fq29::M;
-            h[i].y.v[k] = rng32(s) & Fq29::M;
+        for (int k = 0; k < 13; k++) {
+            h[i].x.v[k] = (int32_t)(rng32(s) & Fq30::M) - (1 << 29);
+            h[i].y.v[k] = (int32_t)(rng32(s) & Fq30::M) - (1 << 29);
         }
-        h[i].x.v[13] &= 0xf;  // below 2^381 < 2p
-        h[i].y.v[13] &= 0xf;
+        h[i].x.v[12] >>= 9;  // |value| below p
+        h[i].y.v[12] >>= 9;
     }
     Rec112 *dt;
     XYZZ<fq_t> *dout;
@@ -408,13 +408,8 @@ int main(int argc, char **argv) {
         h128[i].y = h[i].y;
         for (int c = 0; c < 2; c++) {
             const fq_t &f = c ? h[i].y : h[i].x;
-            uint32_t w[12] = {0};
-            for (int k = 0; k < 14; k++) {
-                const int bit = 29 * k, j = bit >> 5, sh = bit & 31;
-                w[j] |= f.v[k] << sh;
-                if (sh > 3 && j + 1 < 12) w[j + 1] |= f.v[k] >> (32 - sh);
-            }
-            for (int j = 0; j < 12; j++) h96[i].w[12 * c + j] = w[j];
+            const fq32_t w = fq_to_raw(f);  // some canonical value (timing only)
+            for (int j = 0; j < 12; j++) h96[i].w[12 * c + j] = w.v[j];
         }
     }
     Rec128 *d128;

@@ -37,6 +37,19 @@
  *                     reference's assert/throw style (compound_proof.hpp:94).
  *   threading       : a context is internally serialised (one mutex); drive one context per GPU
  *                     from one host thread each for multi-GPU.
+ *   device pointers : the entries that take or fill caller device memory (every *_dev entry,
+ *                     mi_groth16_trapdoor_dlogs, mi_srs_stream_part with on_device != 0) follow one
+ *                     stream-ordering rule, so the caller needs no host synchronisation around them:
+ *                     (1) on entry, the library's first device access waits ON THE DEVICE for all work
+ *                         queued before the call on the context's caller stream (mi_ctx_set_caller_stream;
+ *                         default NULL = the legacy default stream, which by HIP semantics also covers
+ *                         every blocking stream -- e.g. torch's default stream).  A producer that fills an
+ *                         input or clears an output on its own non-blocking stream names that stream;
+ *                     (2) on return, every device output is fully written and no input is read any more,
+ *                         so the caller may consume or overwrite them from any stream.
+ *                     The library's own streams are non-blocking; they never wait for the NULL stream
+ *                     implicitly (the round-4 tree-C race: a torch.zeros fill of the output landed after
+ *                     the kernel's writes), which is why rule (1) records an event on the caller stream.
  */
 #ifndef MI355X_GROTH16_H
 #define MI355X_GROTH16_H
@@ -99,6 +112,9 @@ void mi_ctx_destroy(mi_ctx *ctx);
 const char *mi_last_error(void);
 /* stream handle (hipStream_t) the context launches on; external work may be ordered against it */
 int mi_ctx_stream(mi_ctx *ctx, void **stream_out);
+/* the caller stream of the "device pointers" rule above (a hipStream_t on this context's device; NULL = legacy
+ * default stream); it stays set for every later call on the context */
+int mi_ctx_set_caller_stream(mi_ctx *ctx, void *stream);
 int mi_ctx_synchronize(mi_ctx *ctx);
 /* Page-locked host memory for witnesses.  The reference hands the prover host-side assignments
  * (api/seal.hpp:298-301); a synthesiser that writes z into such a buffer lets the prover's H2D copy
@@ -147,6 +163,14 @@ int mi_srs_info(const mi_srs *srs, uint64_t out[6]);
  * known to be in the prime-order subgroup (generated key or checked load).  Without tables, the G1
  * MSMs of a subgroup-known key take the GLV split; otherwise they run the plain 256-bit path. */
 int mi_srs_msm_info(const mi_srs *srs, uint64_t out[2]);
+/* Split tables after memory pressure: a proof, key generation or key load that runs out of HBM releases the 2^128
+ * tables of the device's idle keys and retries (mi_ctx_get_fallbacks); the key then proves through the GLV split,
+ * byte-identical.  mi_srs_table_state: out[0] = tables resident, out[1] = releases since they were last built,
+ * out[2] = subgroup-known.  mi_srs_readmit rebuilds released tables once they fit again under the key-load rule
+ * (e.g. after another key was freed); *rebuilt_bytes (may be NULL) = table bytes rebuilt, 0 when nothing was
+ * released or there is still no room.  Waits for proofs running on the key. */
+int mi_srs_table_state(const mi_srs *srs, uint64_t out[3]);
+int mi_srs_readmit(mi_ctx *ctx, mi_srs *srs, uint64_t *rebuilt_bytes);
 void mi_srs_free(mi_srs *srs);
 
 /* ---- verification (host CPU; no device needed) ----
@@ -187,6 +211,27 @@ int mi_params_load(mi_ctx *ctx, const mi_circuit *circuit_or_null, const char *p
                    mi_srs **out);
 int mi_params_write(mi_ctx *ctx, const mi_srs *srs, const char *path);
 int mi_vk_write(const mi_srs *srs, const char *path);
+
+/* ---- parameter cache (core/parameter_cache.hpp:50-219) ----
+ *   mi_param_cache_id       <- cacheable_parameters::cache_identifier (:166-171): "<cache_prefix>-<hex sha256(identifier)>",
+ *                              identifier = pub_params.identifier() (e.g. stacked/vanilla/params.hpp:80-85)
+ *   mi_param_cache_path     <- parameter_cache_{params,metadata,verifying_key}_path (:78-94): kind 0 / 1 / 2 ->
+ *                              $FIL_PROOFS_PARAMETER_CACHE/v28-<id>.params / .meta / .vk (PARAMETER_CACHE_DIR,
+ *                              "/var/tmp/filecoin-proof-parameters/", when the variable is unset)
+ *   mi_param_cache_metadata <- get_param_metadata (:173-183): reads <id>.meta, else writes {"sector_size":N};
+ *                              *sector_size_out = the cached value
+ *   mi_get_groth_params     <- get_groth_params (:185-200) + get_verifying_key (:202-219): loads <id>.params when it
+ *                              exists and parses, else generates the key (toxic waste as for mi_srs_generate, or drawn
+ *                              from getrandom() when toxic_or_null is NULL), writes <id>.params (atomically, via a
+ *                              rename) and <id>.vk when missing; *generated = 1 on that branch.  The cache
+ *                              directory must exist (ensure_ancestor_dirs_exist, :96-103): MI_ERR_ARG otherwise.
+ * These need no device except mi_get_groth_params. */
+#define MI_PARAMS_VERSION 28
+int mi_param_cache_id(const char *cache_prefix, const char *identifier, char *out, size_t cap);
+int mi_param_cache_path(const char *id, int kind, char *out, size_t cap);
+int mi_param_cache_metadata(const char *id, uint64_t sector_size, uint64_t *sector_size_out);
+int mi_get_groth_params(mi_ctx *ctx, const mi_circuit *circuit, const char *id, const uint8_t *toxic_or_null,
+                        int checked, mi_srs **out, int *generated);
 
 /* ---- Groth16 ---- */
 /* z: (num_inputs + num_aux) x 32 B, z[0] = ONE.  Every entry must be canonical (< r): a witness holding
@@ -237,6 +282,15 @@ int mi_groth16_prove_share_ranges(mi_ctx *ctx, const mi_srs *srs, const mi_circu
                                   const uint64_t ranges[8], int priority, uint8_t share_out[MI_SHARE_BYTES]);
 int mi_groth16_prove_share_ranges_dev(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circuit, const void *z_dev,
                                       const uint64_t ranges[8], int priority, uint8_t share_out[MI_SHARE_BYTES]);
+/* H computed once and SPLIT over a latency group: mi_groth16_h_coeffs_dev runs the witness map and the QAP's NTT chain
+ * alone and writes the d canonical H coefficients (32 B LE each, in the key's bit-reversed h order) to h_out_dev;
+ * the group broadcasts them (RCCL), and every rank's mi_groth16_prove_share_ranges_h_dev then runs its H slice from
+ * h_dev (NULL: computed in place, as mi_groth16_prove_share_ranges_dev) beside its L, A, B slices.  A rank may make
+ * several shares (e.g. L/A/B while H is still on its way, then its H slice); mi_groth16_assemble adds them all. */
+int mi_groth16_h_coeffs_dev(mi_ctx *ctx, const mi_circuit *circuit, const void *z_dev, void *h_out_dev);
+int mi_groth16_prove_share_ranges_h_dev(mi_ctx *ctx, const mi_srs *srs, const mi_circuit *circuit, const void *z_dev,
+                                        const void *h_dev, const uint64_t ranges[8], int priority,
+                                        uint8_t share_out[MI_SHARE_BYTES]);
 /* host only (no device): vk = MI_VK_BYTES uncompressed, shares = count x MI_SHARE_BYTES (any order) */
 int mi_groth16_assemble(const uint8_t *vk, const uint8_t *shares, uint64_t count, const uint8_t r[32],
                         const uint8_t s[32], uint8_t proof_out[MI_PROOF_BYTES], uint8_t *raw_out);
@@ -320,8 +374,8 @@ int mi_stacked_r1cs(const mi_stacked *s, mi_r1cs *out);
 int mi_stacked_load(mi_ctx *ctx, const mi_stacked *s, mi_circuit **out);
 /* (inputs - 1) x 32 B: the public inputs in generate_public_inputs order (without ONE) */
 int mi_stacked_public_inputs(const mi_stacked *s, const uint8_t *slots, uint8_t *out);
-/* z_dev: (inputs + aux) x 32 B on this context's GPU, fully written; slots refused if not canonical or an
- * index >= nodes (MI_ERR_ARG) */
+/* z_dev: (inputs + aux) x 32 B on this context's GPU, fully written on return; slots refused if not canonical or
+ * an index >= nodes (MI_ERR_ARG) */
 int mi_stacked_witness_dev(mi_ctx *ctx, mi_stacked *s, const void *slots_dev, void *z_dev);
 int mi_stacked_witness(mi_ctx *ctx, mi_stacked *s, const uint8_t *slots, uint8_t *z_out);
 void mi_stacked_free(mi_stacked *s);
@@ -368,6 +422,10 @@ int mi_ctx_get_work(mi_ctx *ctx, uint64_t out[2]);
  * Replaces failing outright when several keys share one GPU, as GROTH_PARAM_MEMORY_CACHE keeps them
  * (libs/filecoin/include/nil/filecoin/proofs/caches.hpp:48-116). */
 int mi_ctx_get_fallbacks(mi_ctx *ctx, uint64_t out[2]);
+/* TEST ONLY: the first attempt of each of the next `count` proofs on this context fails with a real out-of-memory
+ * error after its NTT chain (count < 0: every proof until reset to 0), so the release-and-retry path runs at any
+ * size.  Production code never calls it; nothing in the prove path reads the environment for it. */
+int mi_ctx_inject_oom(mi_ctx *ctx, int64_t count);
 /* msm window size chosen for n points (exposed for tests / reports) */
 unsigned mi_msm_window_bits(uint64_t n);
 

@@ -51,6 +51,11 @@ public:
     context &operator=(const context &) = delete;
     mi_ctx *get() const { return h_; }
     void synchronize() { check(mi_ctx_synchronize(h_)); }
+    // The stream that produces this context's device inputs and consumes its device outputs (a hipStream_t;
+    // nullptr = the legacy default stream).  Every entry taking a device pointer then waits, on the device,
+    // for the work queued there before the call, and returns with its outputs written -- see "Device pointers"
+    // in mi355x_groth16.h.  No host synchronisation is needed around the calls.
+    void set_caller_stream(void *hip_stream) { check(mi_ctx_set_caller_stream(h_, hip_stream)); }
 
 private:
     mi_ctx *h_ = nullptr;
@@ -137,6 +142,17 @@ inline proof_bytes prove(context &ctx, const proving_key &pk, const circuit &c, 
     if (z.size() != c.num_variables()) throw error(MI_ERR_ARG, "assignment length != number of variables");
     proof_bytes out;
     check(mi_groth16_prove_random(ctx.get(), pk.get(), c.get(), z.front().data(), priority ? 1 : 0, out.data()));
+    return out;
+}
+
+// A witness already in device memory (a GPU synthesiser's output, e.g. mi_stacked_witness_dev): the call waits on
+// the device for the work queued on the context's caller stream before it (context::set_caller_stream), so the
+// producer's kernels and copies need no host synchronisation in between.
+inline proof_bytes prove_dev(context &ctx, const proving_key &pk, const circuit &c, const void *z_dev, const fr32 &r,
+                             const fr32 &s, bool priority = false) {
+    proof_bytes out;
+    check(mi_groth16_prove_dev(ctx.get(), pk.get(), c.get(), z_dev, r.data(), s.data(), priority ? 1 : 0, out.data(),
+                               nullptr));
     return out;
 }
 

@@ -1,12 +1,13 @@
 // grouplaw_check.cpp -- TEST INFRASTRUCTURE: the device group law (csrc/field.h, csrc/curve.h) compiled
 // for the host, checked against the CPU oracle (oracle/, linked) under ASan/UBSan.
 //
-// The XYZZ additions the MSM kernels inline use lazily reduced intermediates (field.h "lazy forms":
-// unreduced subtractions feeding multiplications, one-pass X3).  This program runs exactly that code
-// on the host over sequences that hit every branch -- distinct points with random signs, P + P
-// (doubling), P + (-P) (infinity), infinity operands, non-canonical representatives v + p of every
-// coordinate -- and compares each result with the oracle's affine group law.  It also checks the lazy
-// field forms against the reduced operators on random and extreme (near 2p) values.
+// The Fq arithmetic the MSM kernels inline works on balanced signed 30-bit limbs with no range reduction
+// (field.h "Fq").  This program runs exactly that code on the host over sequences that hit every branch
+// of the group law -- distinct points with random signs, P + P (doubling), P + (-P) (infinity), infinity
+// operands, other representatives v + k p of every coordinate -- and compares each result with the
+// oracle's affine group law.  It also checks every field operation against plain integers mod p (an
+// independent reference over 32-bit words with reduced additions only), on random values and on limb
+// patterns at the column-sum bound (every low limb +-2^29).
 // Build/run: tests/test_cpu_grouplaw.py (hipcc host-only, ASan + UBSan, host code only).
 #include <cstdio>
 #include <cstdlib>
@@ -48,23 +49,84 @@ static void fq_to_be(const fq_t &a, uint8_t *p) {
         q[0] = w >> 24, q[1] = w >> 16, q[2] = w >> 8, q[3] = w;
     }
 }
-// the other representative of the same residue: v + p when v < p (limbs stay normalised)
-static fq_t alt_rep(const fq_t &a) {
-    fq_t c = fq_canon(a), r;
-    uint32_t carry = 0;
-    for (int i = 0; i < 14; i++) {
-        uint32_t t = c.v[i] + Fq29::P[i] + carry;
-        r.v[i] = i < 13 ? (t & Fq29::M) : t;
-        carry = i < 13 ? t >> 29 : 0;
-    }
-    return r;
-}
-static fq_t rand_fq() {  // uniform-ish value in [0, 2p) (random residue, random representative)
+// another representative of the same residue: v + k p for a random k in [-2, 2] (limbs stay normalised)
+static fq_t alt_rep(const fq_t &a) { return fq_sub_kp(fq_canon(a), (int32_t)(rng() % 5) - 2); }
+static fq_t rand_fq() {  // random residue, random representative in (-2p, 3p)
     uint8_t b[48];
     for (int i = 0; i < 48; i++) b[i] = (uint8_t)rng();
     b[0] &= 0x0f;  // < 2^380 < p
     fq_t a = fq_from_be(b);
     return (rng() & 1) ? alt_rep(a) : fq_canon(a);
+}
+
+// ---- an independent reference for the field checks: values mod p over fq32_t (12 x 32-bit, reduced
+// additions only, no Montgomery code), so the signed-limb forms are checked against plain integers ----
+static fq32_t ref_add(const fq32_t &a, const fq32_t &b) { return a + b; }  // Fp<FqDesc>: reduced a + b
+static fq32_t ref_sub(const fq32_t &a, const fq32_t &b) { return a - b; }
+static fq32_t ref_small(uint32_t v) {
+    fq32_t r = fq32_t::zero();
+    r.v[0] = v;
+    return reduce_once(r);
+}
+// value of a limb vector mod p: Horner over the signed limbs, base 2^30 by doublings
+static fq32_t ref_val(const fq_t &a) {
+    fq32_t acc = fq32_t::zero();
+    for (int i = 12; i >= 0; i--) {
+        for (int j = 0; j < 30; j++) acc = ref_add(acc, acc);
+        const int32_t v = a.v[i];
+        const uint32_t mag = v < 0 ? (uint32_t)(-(int64_t)v) : (uint32_t)v;
+        // |v| may exceed p's low word range only as an integer < 2^31, so add it in two halves
+        fq32_t m = ref_add(ref_small(mag >> 16), fq32_t::zero());
+        for (int j = 0; j < 16; j++) m = ref_add(m, m);
+        m = ref_add(m, ref_small(mag & 0xffff));
+        acc = v < 0 ? ref_sub(acc, m) : ref_add(acc, m);
+    }
+    return acc;
+}
+static fq32_t ref_mul(const fq32_t &a, const fq32_t &b) {  // double-and-add over b's bits
+    fq32_t acc = fq32_t::zero();
+    for (int i = 11; i >= 0; i--)
+        for (int j = 31; j >= 0; j--) {
+            acc = ref_add(acc, acc);
+            if ((b.v[i] >> j) & 1) acc = ref_add(acc, a);
+        }
+    return acc;
+}
+static fq32_t ref_rinv() {  // 2^-390 mod p by 390 halvings of 1
+    static const fq32_t P = fq32_t::modulus_raw();
+    fq32_t x = ref_small(1);
+    for (int k = 0; k < 390; k++) {
+        if (x.v[0] & 1) {  // (x + p) / 2 over 13 words
+            uint64_t c = 0;
+            uint32_t w[13];
+            for (int i = 0; i < 12; i++) {
+                c += (uint64_t)x.v[i] + P.v[i];
+                w[i] = (uint32_t)c;
+                c >>= 32;
+            }
+            w[12] = (uint32_t)c;
+            for (int i = 0; i < 12; i++) x.v[i] = (w[i] >> 1) | (w[i + 1] << 31);
+        } else {
+            for (int i = 0; i < 12; i++) x.v[i] = (x.v[i] >> 1) | (i < 11 ? x.v[i + 1] << 31 : 0);
+        }
+    }
+    return x;
+}
+static bool ref_eq(const fq32_t &a, const fq32_t &b) { return std::memcmp(a.v, b.v, sizeof a.v) == 0; }
+static bool normalised(const fq_t &a) {
+    for (int i = 0; i < 12; i++)
+        if (a.v[i] < -(1 << 29) || a.v[i] > (1 << 29)) return false;
+    return a.v[12] >= -(1 << 29) && a.v[12] <= (1 << 29);
+}
+// limb patterns at the column-sum bound: every low limb +-2^29 (or random extremes), moderate top limb
+static fq_t extreme_fq(int kind) {
+    fq_t a;
+    for (int i = 0; i < 12; i++) {
+        const int sgn = kind == 0 ? 1 : kind == 1 ? -1 : ((rng() & 1) ? 1 : -1);
+        a.v[i] = sgn * (1 << 29);
+    }
+    a.v[12] = (int32_t)(rng() % 4000001) - 2000000;  // |V| up to ~1.2 p
+    return a;
 }
 
 static void g1_to_bytes(const g1_affine_t &a, uint8_t out[96]) {
@@ -106,39 +168,59 @@ static bool same_point(const g1_xyzz_t &acc, const uint8_t expect[96]) {
 }
 
 static void check_fields() {
-    for (int it = 0; it < 20000; it++) {
+    const fq32_t rinv = ref_rinv();
+    for (int it = 0; it < 4000; it++) {
         fq_t a = rand_fq(), b = rand_fq(), c = rand_fq(), d = rand_fq();
-        if (it < 64) {  // extremes: 2p - 1 - small, 0, p
-            fq_t two_p_m1;
-            for (int i = 0; i < 14; i++) two_p_m1.v[i] = Fq29::P2[i];
-            two_p_m1.v[0] -= 1 + (it & 7);
-            if (it & 8) a = two_p_m1;
-            if (it & 16) b = two_p_m1;
-            if (it & 32) c = fq_t::zero();
+        if (it < 96) {  // limb extremes (the column-sum bound) and zero
+            if (it & 1) a = extreme_fq(it % 3);
+            if (it & 2) b = extreme_fq((it / 3) % 3);
+            if (it & 4) c = extreme_fq((it / 7) % 3);
+            if (it & 8) d = extreme_fq((it / 11) % 3);
+            if (it & 64) c = fq_t::zero();
         }
-        // lazy subtraction / negation feed a multiplication exactly like the reduced forms
-        CHECK(fq_canon(fq_sub_lazy(a, b) * c) == fq_canon((a - b) * c), "sub_lazy it=%d", it);
-        CHECK(fq_canon(fq_neg_lazy(a) * c) == fq_canon((-a) * c), "neg_lazy it=%d", it);
-        CHECK(fq_canon(mul_add(a, fq_sub_lazy(b, c), fq_neg_lazy(d), a)) ==
-                  fq_canon(a * (b - c) - d * a), "mul_add lazy it=%d", it);
-        // symmetric-product squaring equals the general product, also on lazy operands in [0, 4p)
-        CHECK(fq_canon(sqr(a)) == fq_canon(a * a), "sqr it=%d", it);
-        const fq_t lz = fq_sub_lazy(a, b);
-        CHECK(fq_canon(sqr(lz)) == fq_canon(lz * lz), "sqr lazy it=%d", it);
-        // one-pass X3 equals the three reduced operations, and stays in [0, 2p)
-        fq_t x3 = fq_x3(a, b, c);
-        CHECK(x3 == a - b - dbl(c), "x3 it=%d", it);
-        fq_t lim;
-        for (int i = 0; i < 14; i++) lim.v[i] = Fq29::P2[i];
-        bool below = false;
-        for (int i = 13; i >= 0; i--)
-            if (x3.v[i] != lim.v[i]) {
-                below = x3.v[i] < lim.v[i];
-                break;
-            }
-        CHECK(below, "x3 not reduced it=%d", it);
-        for (int i = 0; i < 13; i++) CHECK(x3.v[i] <= Fq29::M, "x3 limb it=%d", it);
+        const fq32_t va = ref_val(a), vb = ref_val(b), vc = ref_val(c), vd = ref_val(d);
+        // Montgomery product / square / fused a b + c d against the plain integers, outputs normalised
+        const fq_t ab = a * b, aa = sqr(a), ma = mul_add(a, b, c, d);
+        CHECK(ref_eq(ref_val(ab), ref_mul(ref_mul(va, vb), rinv)), "mul it=%d", it);
+        CHECK(ref_eq(ref_val(aa), ref_mul(ref_mul(va, va), rinv)), "sqr it=%d", it);
+        CHECK(ref_eq(ref_val(ma), ref_mul(ref_add(ref_mul(va, vb), ref_mul(vc, vd)), rinv)), "mul_add it=%d", it);
+        CHECK(normalised(ab) && normalised(aa) && normalised(ma), "product limbs not normalised it=%d", it);
+        // output magnitude: |a b| / R + p / 2 < 0.6 p for operands below 3 p, so round(V / p) is -1, 0 or 1
+        CHECK(fq_quot(ab) >= -1 && fq_quot(ab) <= 1 && fq_quot(ma) >= -1 && fq_quot(ma) <= 1, "product range it=%d", it);
+        // add / sub / neg / x3 and the former lazy names
+        CHECK(ref_eq(ref_val(a + b), ref_add(va, vb)) && normalised(a + b), "add it=%d", it);
+        CHECK(ref_eq(ref_val(a - b), ref_sub(va, vb)) && normalised(a - b), "sub it=%d", it);
+        CHECK(ref_eq(ref_val(-a), ref_sub(fq32_t::zero(), va)) && normalised(-a), "neg it=%d", it);
+        CHECK(ref_eq(ref_val(fq_sub_lazy(a, b)), ref_sub(va, vb)), "sub_lazy it=%d", it);
+        CHECK(ref_eq(ref_val(fq_neg_lazy(a)), ref_sub(fq32_t::zero(), va)), "neg_lazy it=%d", it);
+        const fq_t x3 = fq_x3(a, b, c);
+        CHECK(ref_eq(ref_val(x3), ref_sub(ref_sub(va, vb), ref_add(vc, vc))) && normalised(x3), "x3 it=%d", it);
+        // is_zero / == modulo p for every representative; canonical form in [0, p)
+        CHECK((a - a).is_zero() && fq_sub_kp(fq_t::zero(), (int32_t)(rng() % 9) - 4).is_zero(), "is_zero it=%d", it);
+        CHECK(a.is_zero() == ref_eq(va, fq32_t::zero()), "is_zero value it=%d", it);
+        CHECK(alt_rep(a) == a && !(a == a + fq_t::one()), "eq it=%d", it);
+        const fq_t ca = fq_canon(a);
+        CHECK(ref_eq(ref_val(ca), va) && fq_sign(ca) >= 0 && fq_sign(fq_sub_kp(ca, 1)) < 0, "canon it=%d", it);
+        // the wire conversions round-trip
+        CHECK(fq_from_raw(fq_to_raw(a)) == a, "raw round trip it=%d", it);
     }
+}
+
+// sums alone never grow without bound (the Miller loop's x3 = lambda^2 - 2 x): 400 doublings by addition and
+// 400 x = x - 3 x steps stay normalised, bounded and equal to the integers mod p
+static void check_growth() {
+    fq_t a = rand_fq(), b = rand_fq();
+    fq32_t va = ref_val(a), vb = ref_val(b);
+    for (int it = 0; it < 400; it++) {
+        a = a + a;
+        va = ref_add(va, va);
+        b = b - dbl(b) - b;
+        vb = ref_sub(ref_sub(vb, ref_add(vb, vb)), vb);
+        CHECK(normalised(a) && normalised(b) && a.v[12] <= (1 << 25) && a.v[12] >= -(1 << 25) &&
+                  b.v[12] <= (1 << 25) && b.v[12] >= -(1 << 25), "growth not bounded it=%d", it);
+    }
+    CHECK(ref_eq(ref_val(a), va) && ref_eq(ref_val(b), vb), "growth values");
+    CHECK(ref_eq(ref_val(a * b), ref_mul(ref_mul(va, vb), ref_rinv())), "growth product");
 }
 
 static void check_g1_sequences() {
@@ -343,6 +425,7 @@ static void check_glv() {
 
 int main() {
     check_fields();
+    check_growth();
     check_g1_sequences();
     check_g2();
     check_glv();

@@ -62,9 +62,22 @@ def shares(oracle, params, n_in, n_aux, mats, z: bytes, world: int):
     return out
 
 
-def shares_ranges(oracle, params, n_in, n_aux, mats, z: bytes, ranges_list):
+def h_coeffs_perm(params, z: bytes) -> bytes:
+    """The d H coefficients in the device's bit-reversed h order (what mi_groth16_h_coeffs_dev writes): the d - 1
+    coefficients bellman keeps at positions bitrev(i), the last position (coefficient d - 1) zero."""
+    _, _, hb = params.prove(z, 0, 0, want_h=True)
+    log_d = params.d.bit_length() - 1
+    hc = np.frombuffer(hb, dtype=np.uint8).reshape(-1, 32)
+    out = np.zeros((params.d, 32), dtype=np.uint8)
+    for i in range(params.d - 1):
+        out[int(format(i, f"0{log_d}b")[::-1], 2) if log_d else 0] = hc[i]
+    return out.tobytes()
+
+
+def shares_ranges(oracle, params, n_in, n_aux, mats, z: bytes, ranges_list, h_perm_coeffs: bytes = None):
     """Oracle shares over explicit query ranges (what mi_groth16_prove_share_ranges computes): one
-    [(first, count)] x 4 list (H in the bit-reversed h order, L, A, B) per share."""
+    [(first, count)] x 4 list (H in the bit-reversed h order, L, A, B) per share.  h_perm_coeffs: H coefficients
+    received from elsewhere (h_coeffs_perm's layout), used instead of the oracle's own (the H-split protocol)."""
     ex = params.export()
     _, _, hb = params.prove(z, 0, 0, want_h=True)
     idx_a, idx_b = densities(n_in, n_aux, mats)
@@ -82,6 +95,8 @@ def shares_ranges(oracle, params, n_in, n_aux, mats, z: bytes, ranges_list):
     hq = np.frombuffer(ex["h"], dtype=np.uint8).reshape(-1, 96)
     hc = np.frombuffer(hb, dtype=np.uint8).reshape(-1, 32)
     h_perm, hb_perm = hq[rev].tobytes(), hc[rev].tobytes()
+    if h_perm_coeffs is not None:
+        hb_perm = h_perm_coeffs[:32 * (params.d - 1)]
     out = []
     for (h, l, a, b) in ranges_list:
         rec = msm(h_perm, 96, hb_perm, *h) + msm(ex["l"], 96, zaux, *l) + msm(ex["a"], 96, za, *a)

@@ -385,3 +385,120 @@ def test_gloo_balanced_runner_h_once(tmp_path, oracle):
     zb = circuits.z_bytes(z)
     serial = b"".join(P.prove(zb, 300 + p, 400 + p)[0] for p in range(5)) + repr(0.3).encode()
     assert all(open(tmp_path / f"r{r}.bin", "rb").read() == serial for r in range(3))
+
+
+# ------------------------------------------------------------------ latency groups that compute H once and split it
+@pytest.mark.parametrize("g", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("h_lead,lab_lead", [(0.0, 0.0), (0.69, 0.0), (1.0, 0.3), (1.0, 1.0)])
+def test_latency_ranges_hsplit_partition_every_query(g, h_lead, lab_lead):
+    from fil_groth16.distributed import latency_ranges_hsplit
+
+    sizes = (1023, 1000, 977, 501)
+    rg = latency_ranges_hsplit(sizes, g, h_lead, lab_lead)
+    assert len(rg) == g
+    for q, n in enumerate(sizes):
+        pos = 0
+        for k in range(g):
+            lo, cnt = rg[k][q]
+            assert lo == pos and cnt >= 0
+            pos += cnt
+        assert pos == n
+        if g > 1:
+            counts = [rg[k][q][1] for k in range(1, g)]
+            assert max(counts) - min(counts) <= 1
+
+
+def test_hsplit_fractions_even_the_group():
+    """Window-PoSt numbers of round 4 (t_qap 202 ms, H MSM 283 ms, L/A/B 1,104 ms): four ranks finish together at
+    ~(t_qap + t_hmsm + t_lab) / 4 instead of the lead's 571 ms with H unsplit."""
+    from fil_groth16.distributed import hsplit_fractions
+
+    t_qap, t_h, t_lab = 202.0, 283.0, 1104.0
+    for g in (2, 3, 4, 8):
+        h, f = hsplit_fractions(t_qap, t_h, t_lab, g)
+        lead = t_qap + h * t_h + f * t_lab
+        other = ((1 - h) * t_h + (1 - f) * t_lab) / (g - 1)
+        if 0.0 < h < 1.0 or 0.0 < f < 1.0:
+            assert abs(lead - other) < 1e-6
+        assert max(lead, other) <= 1.0001 * max(t_qap, (t_qap + t_h + t_lab) / g)
+    h, f = hsplit_fractions(t_qap, t_h, t_lab, 4)
+    assert 0.68 < h < 0.70 and f == 0.0
+    assert hsplit_fractions(500.0, 10.0, 100.0, 4) == (0.0, 0.0)  # the NTT chain alone outweighs a share
+    assert hsplit_fractions(1.0, 10.0, 1000.0, 2)[0] == 1.0  # small H: the lead also takes L/A/B
+    assert hsplit_fractions(1.0, 1.0, 1.0, 1) == (1.0, 1.0)
+
+
+def _hsplit_worker(rank, world, port, num_partitions, outdir):
+    """The balanced runner with H-split tail groups: the lead's H coefficients (oracle, device order) are broadcast
+    over the group's subgroup; the others prove L/A/B first, then their H slice from the received coefficients."""
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "crypto3-fil-proofs_amd"), os.path.join(root, "oracle"),
+              os.path.join(root, "tests", "golden"), os.path.join(root, "tests")):
+        sys.path.insert(0, p)
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import circuits
+    import fil_groth16 as fg
+    import oracle_py
+    import split_oracle
+    from fil_groth16.distributed import hsplit_fractions, hsplit_shares, latency_ranges_hsplit, \
+        prove_partitions_balanced
+
+    oracle_py.set_threads(1)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n_in, n_aux, rows, z = circuits.random_circuit(64, 40)
+    mats = circuits.to_csr(rows)
+    P = oracle_py.OracleParams(oracle_py.OracleCircuit(len(rows), n_in, n_aux, mats), circuits.toxic())
+    zb = circuits.z_bytes(z)
+    ex = P.export()
+    idx_a, idx_b = split_oracle.densities(n_in, n_aux, mats)
+    sizes = (P.d - 1, n_aux, len(idx_a), len(idx_b))
+    used = {"h_from_bcast": 0}
+
+    def share_fn(p, k, g, bcast):
+        h_lead, lab_lead = hsplit_fractions(20.0, 30.0, 100.0, g)
+        rg = latency_ranges_hsplit(sizes, g, h_lead, lab_lead)
+
+        def h_coeffs(*arg):
+            if arg and arg[0] is None:  # a receiver's buffer
+                return torch.zeros(32 * P.d, dtype=torch.uint8)
+            return torch.from_numpy(np.frombuffer(split_oracle.h_coeffs_perm(P, zb), dtype=np.uint8).copy())
+
+        def one(ranges, h):
+            if h is not None and k > 0:
+                used["h_from_bcast"] += 1
+            hp = h.numpy().tobytes() if h is not None else None
+            return split_oracle.shares_ranges(oracle_py, P, n_in, n_aux, mats, zb, [ranges], hp)[0]
+
+        return hsplit_shares(k, rg, h_coeffs, one, bcast)
+
+    buf = prove_partitions_balanced(lambda ids: [P.prove(zb, 300 + p, 400 + p)[0] for p in ids], share_fn,
+                                    lambda p, sh: fg.assemble(ex["vk"], sh, 300 + p, 400 + p), num_partitions, rank,
+                                    world, group_bcast=True)
+    with open(os.path.join(outdir, f"r{rank}.bin"), "wb") as f:
+        f.write(buf + repr(used["h_from_bcast"]).encode())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,num_partitions", [(4, 5), (3, 4)])
+def test_gloo_balanced_runner_h_split(tmp_path, oracle, world, num_partitions):
+    """One tail partition over a group of every rank, H computed once by the lead, broadcast over the group and
+    split: the multi-proof equals the serial one on every rank, and every non-lead rank proved an H slice from the
+    broadcast coefficients."""
+    import circuits
+
+    mp.spawn(_hsplit_worker, args=(world, _free_port(), num_partitions, str(tmp_path)), nprocs=world, join=True)
+    n_in, n_aux, rows, z = circuits.random_circuit(64, 40)
+    P = oracle.OracleParams(oracle.OracleCircuit(len(rows), n_in, n_aux, circuits.to_csr(rows)), circuits.toxic())
+    zb = circuits.z_bytes(z)
+    serial = b"".join(P.prove(zb, 300 + p, 400 + p)[0] for p in range(num_partitions))
+    for r in range(world):
+        got = open(tmp_path / f"r{r}.bin", "rb").read()
+        assert got[:len(serial)] == serial
+        assert int(got[len(serial):]) == (0 if r == 0 else 1)

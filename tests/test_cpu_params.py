@@ -42,3 +42,43 @@ def test_inspect_rejects_trailing_and_missing(tmp_path, exported):
         fg.params_inspect(str(p))
     with pytest.raises(fg.FilGpuError, match="cannot open"):
         fg.params_inspect(str(tmp_path / "missing.params"))
+
+
+# ---- parameter-cache naming (core/parameter_cache.hpp:50-219) ----
+def test_param_cache_identifier_and_paths(tmp_path, monkeypatch):
+    """cache_identifier = <cache_prefix>-<hex sha256(identifier)> (:166-171), paths <dir>/v28-<id>.<ext> under
+    FIL_PROOFS_PARAMETER_CACHE (:50-56, :78-94), and the reference's PARAMETER_CACHE_DIR when it is unset."""
+    import hashlib
+
+    ident = "layered_drgporep::PublicParams{ graph: stacked_graph::StackedGraph{expansion_degree: 8 base_graph: ...}"
+    cid = fg.param_cache_id("stacked-proof-of-replication-merkletree-poseidon_hasher-8-8-0-sha256_hasher", ident)
+    want = "stacked-proof-of-replication-merkletree-poseidon_hasher-8-8-0-sha256_hasher-" + \
+        hashlib.sha256(ident.encode()).hexdigest()
+    assert cid == want
+    for msg in ["", "a", "x" * 55, "y" * 56, "z" * 64, "w" * 200]:  # SHA-256 padding edges
+        assert fg.param_cache_id("p", msg) == "p-" + hashlib.sha256(msg.encode()).hexdigest()
+    monkeypatch.setenv("FIL_PROOFS_PARAMETER_CACHE", str(tmp_path))
+    assert fg.param_cache_path(cid, fg.PARAMS) == f"{tmp_path}/v28-{cid}.params"
+    assert fg.param_cache_path(cid, fg.META) == f"{tmp_path}/v28-{cid}.meta"
+    assert fg.param_cache_path(cid, fg.VK) == f"{tmp_path}/v28-{cid}.vk"
+    monkeypatch.delenv("FIL_PROOFS_PARAMETER_CACHE")
+    assert fg.param_cache_path("x", fg.VK) == "/var/tmp/filecoin-proof-parameters//v28-x.vk"
+    with pytest.raises(fg.FilGpuError):
+        fg.param_cache_path("x", 3)
+
+
+def test_param_cache_metadata_read_or_write(tmp_path, monkeypatch):
+    """get_param_metadata (:173-183): the first call writes {"sector_size":N}, later calls read it back; a cache
+    directory that does not exist is refused (ensure_ancestor_dirs_exist, :96-103)."""
+    monkeypatch.setenv("FIL_PROOFS_PARAMETER_CACHE", str(tmp_path))
+    cid = fg.param_cache_id("post", "fallback::PublicParams{...}")
+    assert fg.param_cache_metadata(cid, 34359738368) == 34359738368
+    meta = tmp_path / f"v28-{cid}.meta"
+    assert meta.read_text() == '{"sector_size":34359738368}'
+    assert fg.param_cache_metadata(cid, 2048) == 34359738368  # cached value wins
+    meta.write_text("not json")
+    assert fg.param_cache_metadata(cid, 2048) == 2048  # unreadable -> rewritten
+    monkeypatch.setenv("FIL_PROOFS_PARAMETER_CACHE", str(tmp_path / "missing"))
+    with pytest.raises(fg.FilGpuError) as e:
+        fg.param_cache_metadata(cid, 1)
+    assert e.value.code == -1 and "no parent directory" in str(e.value)

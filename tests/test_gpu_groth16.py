@@ -133,10 +133,11 @@ def test_groth16_split_msm_vs_oracle(ctx, oracle, monkeypatch, split):
 
 
 def test_prove_out_of_memory_degrades_to_glv(ctx, oracle, monkeypatch):
-    """A proof whose scratch allocation fails (MI_INJECT_PROVE_OOM: the main lane raises hipMalloc's
-    out-of-memory error after the NTT chain while the auxiliary lane runs) is re-run in-process after the key's
-    2^128 split tables are released: the bytes equal the oracle's, the key reports no tables afterwards, and
-    the context counts the retry.  Every prove entry (host / device witness, batch, share) recovers alike."""
+    """A proof whose scratch allocation fails (mi_ctx_inject_oom, a test-only entry: the main lane raises
+    hipMalloc's out-of-memory error after the NTT chain while the auxiliary lane runs) is re-run in-process after
+    the key's 2^128 split tables are released: the bytes equal the oracle's, the key reports no tables afterwards,
+    and the context counts the retry.  Every prove entry (host / device witness, batch, share) recovers alike.
+    mi_srs_readmit then rebuilds the tables (the release is not one-way) and the proof is unchanged."""
     monkeypatch.setenv("MI_MSM_SPLIT", "2")  # split mode at this size, so the tables are in use
     n_in, n_aux, rws, z = circuits.random_circuit(36, 5000, n_in=6, n_free=32)
     oc, gc = _load(ctx, oracle, n_in, n_aux, rws, z)
@@ -148,11 +149,13 @@ def test_prove_out_of_memory_degrades_to_glv(ctx, oracle, monkeypatch):
     want = [op.prove(zb, 10 + k, 20 + k)[0] for k in range(3)]
     assert fg.prove(ctx, pk, gc, zb, 10, 20) == want[0]
     ctx.reset_stats()
-    monkeypatch.setenv("MI_INJECT_PROVE_OOM", "1")
+    ctx.inject_oom(1)
     assert fg.prove(ctx, pk, gc, zb, 10, 20) == want[0]
     fb = ctx.fallbacks()
     assert fb["oom_retries"] == 1 and fb["freed_bytes"] > 0
     assert pk.msm_info() == {"split_tables": False, "subgroup": True}
+    assert pk.table_state() == {"split_tables": False, "dropped": 1, "subgroup": True}
+    ctx.inject_oom(-1)
     import torch
 
     zd = torch.from_numpy(np.frombuffer(zb, dtype=np.uint8).copy()).cuda()
@@ -161,9 +164,14 @@ def test_prove_out_of_memory_degrades_to_glv(ctx, oracle, monkeypatch):
     vk, _ = pk.verifying_key()
     assert fg.assemble(vk, [fg.prove_share(ctx, pk, gc, zb, k, 2) for k in range(2)], 10, 20) == want[0]
     assert ctx.fallbacks()["oom_retries"] == 6
-    monkeypatch.delenv("MI_INJECT_PROVE_OOM")
+    ctx.inject_oom(0)
     ctx.reset_stats()
     assert fg.prove(ctx, pk, gc, zb, 12, 22) == want[2] and ctx.fallbacks()["oom_retries"] == 0
+    # re-admission: the tables come back once they fit, and the proofs keep their bytes
+    assert pk.readmit() > 0
+    assert pk.table_state() == {"split_tables": True, "dropped": 0, "subgroup": True}
+    assert pk.readmit() == 0  # nothing to rebuild
+    assert fg.prove(ctx, pk, gc, zb, 11, 21) == want[1] and ctx.fallbacks()["oom_retries"] == 0
 
 
 def test_prove_batch_and_priority(ctx, oracle):
@@ -549,3 +557,92 @@ def test_production_random_blinding_entries(ctx, oracle):
     assert fg.circuit_proofs(ctx, pk, gc, [zb] * 3, blind) == [op.prove(zb, r, s)[0] for r, s in blind]
     buf = fg.seal_commit_phase2_proofs(ctx, pk, gc, [zb] * 2)
     assert all(fg.verify(vk, ic, zb[32:32 * n_in], buf[192 * k:192 * k + 192]) for k in range(2))
+
+
+def test_get_groth_params_read_or_generate(ctx, oracle, golden, tmp_path, monkeypatch):
+    """get_groth_params / get_verifying_key (core/parameter_cache.hpp:185-219) through mi_get_groth_params: the
+    first call finds no v28-<id>.params under FIL_PROOFS_PARAMETER_CACHE, generates the key and writes the params
+    and vk files (byte-identical to the oracle key's bellman layout); the second call loads the file instead and
+    proves the golden bytes; a corrupt file is regenerated, as the reference's catch-all does."""
+    import params_io
+
+    monkeypatch.setenv("FIL_PROOFS_PARAMETER_CACHE", str(tmp_path))
+    g = golden["groth16"]["random_11_24"]
+    n_in, n_aux, rows, z = _circuit_from_name("random_11_24")
+    oc, gc = _load(ctx, oracle, n_in, n_aux, rows, z)
+    ex = oracle.OracleParams(oc, circuits.toxic()).export()
+    cid = fg.param_cache_id("test-circuit", "random_11_24{n_in: %d, n_aux: %d}" % (n_in, n_aux))
+    r, s = circuits.blinding()
+    pk1, gen1 = fg.get_groth_params(ctx, gc, cid, toxic=circuits.toxic())
+    assert gen1
+    assert (tmp_path / f"v28-{cid}.params").read_bytes() == params_io.params_bytes(ex)
+    assert (tmp_path / f"v28-{cid}.vk").read_bytes() == params_io.vk_bytes(ex)
+    pk2, gen2 = fg.get_groth_params(ctx, gc, cid, toxic=[1, 2, 3, 4, 5])  # toxic unused: the file is read
+    assert not gen2
+    assert fg.prove(ctx, pk1, gc, circuits.z_bytes(z), r, s).hex() == g["proof"]
+    assert fg.prove(ctx, pk2, gc, circuits.z_bytes(z), r, s).hex() == g["proof"]
+    p = tmp_path / f"v28-{cid}.params"
+    p.write_bytes(p.read_bytes()[:-5])
+    pk3, gen3 = fg.get_groth_params(ctx, gc, cid)  # corrupt -> regenerated from OS randomness, valid proof
+    assert gen3 and fg.params_inspect(str(p))["h"] == len(ex["h"]) // 96
+    vk, ic = pk3.verifying_key()
+    raw = fg.prove(ctx, pk3, gc, circuits.z_bytes(z), r, s, want_raw=True)[1]
+    assert oracle.groth16_verify(vk, ic, circuits.z_bytes(z)[:32 * n_in], raw)
+
+
+@pytest.mark.parametrize("rows,seed", [(700, 91), (5000, 92)])
+def test_h_split_shares_vs_oracle(ctx, oracle, rows, seed):
+    """H computed once and split (mi_groth16_h_coeffs_dev + mi_groth16_prove_share_ranges_h_dev): the exported H
+    coefficients equal the oracle's in the device's bit-reversed order; H-only, L/A/B-only and mixed shares from the
+    received coefficients equal the oracle's range sums byte for byte; the shares of hsplit_shares over 2-4 ranks
+    assemble into the one-GPU proof; non-canonical coefficients are refused."""
+    import torch
+
+    import split_oracle
+    from fil_groth16.distributed import hsplit_fractions, hsplit_shares, latency_ranges_hsplit
+
+    n_in, n_aux, rws, z = circuits.random_circuit(seed, rows, n_in=6, n_free=32)
+    mats = circuits.to_csr(rws)
+    oc, gc = _load(ctx, oracle, n_in, n_aux, rws, z)
+    tox = circuits.toxic(seed)
+    pk = fg.generate_random_parameters(ctx, gc, tox)
+    op = oracle.OracleParams(oc, tox)
+    zb = circuits.z_bytes(z)
+    r, s = circuits.blinding(seed)
+    vk, _ = pk.verifying_key()
+    one = fg.prove(ctx, pk, gc, zb, r, s)
+    zd = torch.from_numpy(np.frombuffer(zb, dtype=np.uint8).copy()).cuda()
+    hbuf = torch.zeros(32 * gc.d, dtype=torch.uint8, device="cuda")
+    fg.h_coeffs_dev(ctx, gc, zd.data_ptr(), hbuf.data_ptr())
+    want_h = split_oracle.h_coeffs_perm(op, zb)
+    assert hbuf.cpu().numpy().tobytes() == want_h
+    sizes = (pk.n_h, pk.n_l, pk.n_a, pk.n_b)
+    h, l, a, b = sizes
+    rg = [[(0, h // 3), (0, 0), (0, 0), (0, 0)], [(h // 3, h - h // 3), (0, l // 2), (0, a), (0, 0)],
+          [(0, 0), (l // 2, l - l // 2), (a, 0), (0, b)]]
+    got = [fg.prove_share_ranges(ctx, pk, gc, zd.data_ptr(), x, h_dev=hbuf.data_ptr()) for x in rg]
+    assert got == split_oracle.shares_ranges(oracle, op, n_in, n_aux, mats, zb, rg)
+    assert fg.assemble(vk, got, r, s) == one
+    for g in (2, 3, 4):
+        hl, fl = hsplit_fractions(10.0, 20.0, 50.0, g)
+        ranges = latency_ranges_hsplit(sizes, g, hl, fl)
+        hbuf.zero_()
+        shs = []
+        for k in range(g):  # rank 0 first, as the group runs it (its coefficients stay in hbuf)
+
+            def h_coeffs(*arg):
+                if not arg:
+                    fg.h_coeffs_dev(ctx, gc, zd.data_ptr(), hbuf.data_ptr())
+                return hbuf
+
+            shs += hsplit_shares(k, ranges, h_coeffs,
+                                 lambda x, hh: fg.prove_share_ranges(ctx, pk, gc, zd.data_ptr(), x,
+                                                                     h_dev=hh.data_ptr() if hh is not None else None),
+                                 lambda t: (lambda: t))
+        assert len(shs) == 2 * g - 1
+        assert fg.assemble(vk, shs, r, s) == one, g
+    bad = hbuf.clone()
+    bad[32 * 5:32 * 6] = 0xFF  # coefficient 5 >= r
+    with pytest.raises(fg.FilGpuError) as e:
+        fg.prove_share_ranges(ctx, pk, gc, zd.data_ptr(), rg[0], h_dev=bad.data_ptr())
+    assert e.value.code == -1

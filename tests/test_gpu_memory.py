@@ -8,7 +8,7 @@ generation and the Window-PoSt proof's working set (~109 GB) do not fit beside t
 an allocation that fails makes the library release the split tables of the keys on the device that no one is
 using (and the context's idle scratch) and run the step again (prover.hip srs_generate / groth16_sums).  Both circuits prove and pairing-verify, and the stacked proof made after its tables
 were released (GLV split) is byte-identical to the one made with them.  The same is checked once more with the
-failure forced (MI_INJECT_PROVE_OOM), so the equality holds whether or not the natural failure happened.
+failure forced (mi_ctx_inject_oom), so the equality holds whether or not the natural failure happened.
 """
 import json
 import os
@@ -80,12 +80,12 @@ def test_two_32gib_keys_in_one_context(monkeypatch):
         p1b = fg.prove(c, k1, g1, z1.data_ptr(), 5, 6)
         assert p1b == p1
         note(f"stacked proof again (tables {k1.msm_info()['split_tables']}): byte-identical")
-        monkeypatch.setenv("MI_INJECT_PROVE_OOM", "1")
+        c.inject_oom(-1)
         c.reset_stats()
         p1c = fg.prove(c, k1, g1, z1.data_ptr(), 5, 6)
         p2c = fg.prove(c, k2, g2, z2.data_ptr(), 7, 8)
         assert c.fallbacks()["oom_retries"] == 2
-        monkeypatch.delenv("MI_INJECT_PROVE_OOM")
+        c.inject_oom(0)
         assert p1c == p1 and p2c == p2
         assert not k1.msm_info()["split_tables"]
         note("forced prove-time fallback: both proofs byte-identical")
