@@ -34,23 +34,23 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "crypto3-fil-proofs_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# VALU bound of the accumulation kernel: v_mad_u64_u32 issue.  One wave64 MAD occupies its SIMD
+# VALU bound of the accumulation kernel: v_mad_i64_i32 issue.  One wave64 MAD occupies its SIMD
 # for 4 cycles: 1024 SIMDs x 64 lanes / 4 x 2.4 GHz = 39.3e12 lane-MADs/s.  (The dependent-chain
 # microbench crypto3-fil-proofs_amd/microbench/madrate.hip sustains only 30.9e12 = 5.1 cycles,
-# because each chain waits on its own previous MAD; the accumulation kernel's ISA -- 3920 MADs
-# + ~1700 other VALU per mixed add, 14x29-bit limbs -- and its measured time imply the 4-cycle
-# rate.)  One Fq multiplication = 392 MADs -> 100.3e9 Fq-mul/s of pure MAD issue; the remaining
-# gap to it is the non-MAD instructions (carries, subtractions, selects).
+# because each chain waits on its own previous MAD; the accumulation kernel's ISA and its measured
+# time imply the 4-cycle rate.)  One Fq multiplication over 13 balanced 30-bit limbs = 338 MADs
+# (field.h) -> 116.3e9 Fq-mul/s of pure MAD issue; the remaining gap to it is the non-MAD
+# instructions (column carries, the quotient-digit selects of the exact zero test).
 MAD_RATE = 1024 * 64 / 4 * 2.4e9
-FQ_MUL_MADS = 392
+FQ_MUL_MADS = 338
 FQ_MUL_PER_MIXED_ADD = {"G1": 10, "G2": 28}
 # The chip's spec VALU issue rate (MI355X_MICROARCH.md "Wave scheduling": a wave64 VALU instruction issues
 # over 2 cycles, 32 lanes/cycle per SIMD): 1024 SIMDs x 32 x 2.4 GHz lane-instructions/s.  Reported next to
 # the measured-rate peaks so that a fraction of a measured instruction rate is not read as "done".
 SPEC_VALU_LANE_INSTR = 1024 * 32 * 2.4e9
-# ISA VALU instructions per G1 mixed addition in k_accum_level0 (3,546 v_mad_u64_u32 +
-# ~1,550 other after the lazy reduction)
-G1_MADD_VALU_INSTR = 3546 + 1550  # madd-2008-s: 8M + 2S over Fq / Fq2 (Karatsuba 3M, 2M per sqr)
+# ISA VALU instructions per G1 mixed addition (microbench/maddloop.hip's register form over
+# the 13 x 30-bit field, 3,081 v_mad_i64_i32 + 1,915 other)
+G1_MADD_VALU_INSTR = 3081 + 1915  # madd-2008-s: 8M + 2S over Fq
 TOXIC_SEED = 0x5EED
 
 
@@ -221,7 +221,7 @@ def tree_c_leg(args, fg, ctx, device, world):
     out = {"workload": f"tree C of one sub-tree: 2^{args.tree_log_nodes} columns x 11 layers -> Poseidon-11 "
                        f"column hashes -> arity-8 Poseidon tree (device-resident labels)",
            "columns_per_s": n / dt, "ms_per_tree": dt * 1e3, "kernel_ms_per_tree": kern_s * 1e3,
-           "valu_roofline": {"kernel": "k_poseidon<12> + k_poseidon<9>", "bound": "valu (v_mad_u64_u32 issue)",
+           "valu_roofline": {"kernel": "k_poseidon<12> + k_poseidon<9>", "bound": "valu (v_mad_i64_i32 issue)",
                              "mads_per_tree": mads, "achieved_mads_per_s": mads / kern_s,
                              "peak_mads_per_s": TREE_MAD_RATE, "frac": mads / kern_s / TREE_MAD_RATE,
                              "spec_issue": {"peak_lane_instr_per_s": SPEC_VALU_LANE_INSTR,
@@ -1330,7 +1330,7 @@ def main():
                     "per BASELINE.json north_star; the binding roofline is 'valu_roofline'",
         },
         "valu_roofline": {
-            "bound": "valu (v_mad_u64_u32 issue)",
+            "bound": "valu (v_mad_i64_i32 issue)",
             "kernel": dom_name,
             "achieved": valu_ach,
             "peak": valu_peak,
@@ -1348,10 +1348,10 @@ def main():
                            if grp == "G1" and avg_ms > 0 and madds_per_launch else None,
                            "note": "ISA VALU instructions per mixed add x mixed adds issued / launch time, against "
                                    "the spec issue rate (MI355X_MICROARCH.md: 32 lanes/cycle/SIMD); the gap to "
-                                   "1 is v_mad_u64_u32's 4-cycle issue (measured, DESIGN.md §5) and DVFS"},
+                                   "1 is the MAD's 4-cycle issue (measured, DESIGN.md §5) and DVFS"},
             "model": f"{FQ_MUL_PER_MIXED_ADD[grp]} Fq-mul per mixed add x mixed adds issued (non-zero signed digits "
                      f"counted by the library; split-mode MSMs: 2n half-scalar points over 6 windows); "
-                     f"peak = v_mad_u64_u32 issue rate / {FQ_MUL_MADS} MADs",
+                     f"peak = v_mad_i64_i32 issue rate / {FQ_MUL_MADS} MADs",
         },
         "cpu_baseline": cpu,
         "tree_c": tree,

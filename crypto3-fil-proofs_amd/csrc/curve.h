@@ -27,10 +27,17 @@ struct AffineAlign<fq_t> {
     static constexpr size_t value = 128;
 };
 
+// Infinity tests.  An affine infinity is stored as raw (0, 0) and an XYZZ infinity has ZZ = 0; Fq coordinates
+// that are zero mod p are zero as limbs there (every ZZ is a Montgomery product, |product| < p, or a constant),
+// so Fq tests the limbs (no modular check); other coordinate types use their is_zero.
+template <class F>
+MI_HD bool coord_zero(const F &a) { return a.is_zero(); }
+MI_HD bool coord_zero(const fq_t &a) { return a.is_raw_zero(); }
+
 template <class F>
 struct alignas(AffineAlign<F>::value) Affine {
     F x, y;
-    MI_HD bool is_inf() const { return x.is_zero() && y.is_zero(); }
+    MI_HD bool is_inf() const { return coord_zero(x) && coord_zero(y); }
     MI_HD static Affine inf() { return {F::zero(), F::zero()}; }
 };
 
@@ -38,7 +45,7 @@ template <class F>
 struct alignas(16) XYZZ {
     F X, Y, ZZ, ZZZ;
     MI_HD static XYZZ inf() { return {F::one(), F::one(), F::zero(), F::zero()}; }
-    MI_HD bool is_inf() const { return ZZ.is_zero(); }
+    MI_HD bool is_inf() const { return coord_zero(ZZ); }
 };
 
 template <class F>

@@ -301,8 +301,8 @@ struct Fq30 {
                                         162803105,  -437337492, 366579475, 78814996,   -442511456, 89578};
     static constexpr int32_t R2[13] = {84936463,   -82245875, 20063291,   -375672600, -184045713, -75371400, -508475920,
                                        172522421,  -150322876, 98350284,  415856896,  -132992156, 1010031};
-    // round(2^52 / (p / 2^360)): quotient estimate k = round(V / p) from the top limb alone (exact for V = k p)
-    static constexpr int64_t QINV = 2642631983ll;
+    // round(2^51 / (p / 2^360)) < 2^31: quotient estimate k = round(V / p) from the top limb alone (exact for V = k p)
+    static constexpr int32_t QINV = 1321315992;
     // p - 2 as 32-bit words (Fermat inversion exponent)
     static constexpr uint32_t PM2[12] = {0xffffaaa9u, 0xb9feffffu, 0xb153ffffu, 0x1eabfffeu,
                                          0xf6b0f624u, 0x6730d2a0u, 0xf38512bfu, 0x64774b84u,
@@ -310,6 +310,20 @@ struct Fq30 {
 };
 
 MI_HD int32_t fq_sext30(uint32_t x) { return ((int32_t)(x << 2)) >> 2; }
+
+// The operands of the limb products as plain 32-bit registers.  Inside the inlined group law LLVM widens limbs that
+// live across loop iterations to 64-bit values and then no longer sees that (int64) a_i * b_j is a product of two
+// sign-extended 32-bit values: it emits a 64 x 64 multiply (v_mad_u64_u32 + 2 v_mul_lo_u32 + v_add3) instead of one
+// v_mad_i64_i32.  An empty asm on each 32-bit limb (device only) pins the value at 32 bits.
+MI_HD void fq_pin(int32_t *x, const int32_t *a) {
+#pragma unroll
+    for (int i = 0; i < 13; i++) {
+        x[i] = a[i];
+#if defined(__HIP_DEVICE_COMPILE__)
+        asm("" : "+v"(x[i]));
+#endif
+    }
+}
 
 struct fq_t;
 MI_HD bool fq_is_zero(const fq_t &a);
@@ -329,13 +343,19 @@ struct alignas(8) fq_t {
     }
     // value == 0 mod p, for any representative
     MI_HD bool is_zero() const { return fq_is_zero(*this); }
+    // all limbs zero: the exact test for values that are zero only as the raw 0 (products, stored coordinates)
+    MI_HD bool is_raw_zero() const {
+        uint32_t z = 0;
+        MI_UNROLL for (int i = 0; i < L; i++) z |= (uint32_t)v[i];
+        return z == 0;
+    }
     MI_HD bool operator==(const fq_t &o) const;
     MI_HD bool operator!=(const fq_t &o) const { return !(*this == o); }
 };
 
 // round(V / p) from the top limb (|V| < 2^388): the other limbs move V / p by < 2^-21, so the estimate is
 // exact whenever V is a multiple of p and within 1 of V / p otherwise
-MI_HD int32_t fq_quot(const fq_t &a) { return (int32_t)(((int64_t)a.v[12] * Fq30::QINV + (1ll << 51)) >> 52); }
+MI_HD int32_t fq_quot(const fq_t &a) { return (int32_t)(((int64_t)a.v[12] * Fq30::QINV + (1ll << 50)) >> 51); }
 
 // V - k p, carry-normalised (limbs 0..11 in [-2^29, 2^29))
 MI_HD fq_t fq_sub_kp(const fq_t &a, int32_t k) {
@@ -350,15 +370,50 @@ MI_HD fq_t fq_sub_kp(const fq_t &a, int32_t k) {
     return r;
 }
 
+// V - j p for |j| <= 3 in 32-bit arithmetic (|v_i - j p_i + c| < 2^29 + 1.56e9 + 2 < 2^31), carry-normalised
+MI_HD fq_t fq_sub_small(const fq_t &a, int32_t j) {
+    fq_t r;
+    int32_t c = 0;
+    MI_UNROLL for (int i = 0; i < 12; i++) {
+        const int32_t t = a.v[i] - j * Fq30::P[i] + c;
+        r.v[i] = fq_sext30((uint32_t)t);
+        c = ((t >> 29) + 1) >> 1;  // round(t / 2^30) = (t - r_i) / 2^30 without forming t - r_i (up to 2^31)
+    }
+    r.v[12] = a.v[12] - j * Fq30::P[12] + c;
+    return r;
+}
+// a == k p exactly, |k| <= 3: the balanced digits of k p are formed on the fly (32-bit) and compared limb by limb.
+// Exact because no canonical digit of k p (|k| <= 3) is -2^29, so k p has one representation with digits in
+// [-2^29, 2^29] (checked when the constants were derived) and any normalised a equal to it has those digits.
+MI_HD bool fq_is_kp(const fq_t &a, int32_t k) {
+    int32_t c = 0;
+    uint32_t diff = 0;
+    MI_UNROLL for (int i = 0; i < 12; i++) {
+        const int32_t t = k * Fq30::P[i] + c;
+        const int32_t d = fq_sext30((uint32_t)t);
+        c = (t - d) >> 30;
+        diff |= (uint32_t)(a.v[i] - d);
+    }
+    diff |= (uint32_t)(a.v[12] - (k * Fq30::P[12] + c));
+    return diff == 0;
+}
+
 // V == 0 mod p: with k = round(V / p), V is a multiple of p iff V = k p, which first needs the low limb to
-// match (one 32-bit check, the hot path); only then (never, for random data) are all limbs compared
+// match (one 32-bit check, the hot path); only then (never, for random data) are all limbs compared, in 32-bit
+// register-light steps (an inlined 64-bit V - k p here cost the accumulation kernel 50 registers)
 MI_HD bool fq_is_zero(const fq_t &a) {
-    const int32_t k = fq_quot(a);
+    int32_t k = fq_quot(a);
     if ((((uint32_t)a.v[0] - (uint32_t)k * (uint32_t)Fq30::P[0]) & Fq30::M) != 0) return false;
-    const fq_t d = fq_sub_kp(a, k);
-    uint32_t z = 0;
-    MI_UNROLL for (int i = 0; i < 13; i++) z |= (uint32_t)d.v[i];
-    return z == 0;
+    fq_t x = a;
+    while (k > 3) {  // only far-out representatives (never in the group law, whose values stay below 3 p)
+        x = fq_sub_small(x, 3);
+        k -= 3;
+    }
+    while (k < -3) {
+        x = fq_sub_small(x, -3);
+        k += 3;
+    }
+    return fq_is_kp(x, k);
 }
 
 // carry-normalise limb sums t_i of two normalised operands (|t_i| <= 2^30, so t_i + carry + 2^29 < 2^31):
@@ -376,8 +431,10 @@ MI_HD fq_t fq_norm(const int32_t *t) {
     // (the Miller loop's affine x3 = lambda^2 - 2 x, iterated) would double each time.  Past |V| ~ 2^384 (top limb
     // 2^24, ~9.8 p) subtract round(V / p) p.  The group law's sums stay below 3 p, so the MSM kernels never take
     // this branch.
+#if !defined(__HIP_DEVICE_COMPILE__)
     const int32_t top = r.v[12] < 0 ? -r.v[12] : r.v[12];
     if (__builtin_expect(top > (1 << 24), 0)) r = fq_sub_kp(r, fq_quot(r));
+#endif
     return r;
 }
 
@@ -424,8 +481,13 @@ MI_HD bool fq_t::operator==(const fq_t &o) const { return fq_is_zero(*this - o);
 
 // Product-scanning Montgomery multiplication: a b R^-1 mod p, |out| <= |a b| / R + p / 2.
 // Column k <= 12 holds <= 13 a*b and 13 m*p products (|.| <= 2^58) plus a carry: < 2^62.71.
-MI_HD fq_t operator*(const fq_t &a, const fq_t &b) {
+MI_HD fq_t operator*(const fq_t &a_, const fq_t &b_) {
     constexpr int L = 13;
+    struct {
+        int32_t v[13];
+    } a, b;
+    fq_pin(a.v, a_.v);
+    fq_pin(b.v, b_.v);
     int32_t m[L];
     fq_t r;
     int64_t acc = 0;
@@ -453,8 +515,12 @@ MI_HD fq_t operator*(const fq_t &a, const fq_t &b) {
 // Squaring over the symmetric products: column k takes (2 a_i) a_(k-i) for i < k - i (|.| <= 2^59, at most
 // 6 of them) and a_(k/2)^2, so the product half costs 91 MADs instead of 169 (260 in all); column bound
 // 6 * 2^59 + 14 * 2^58 = 26 * 2^58.
-MI_HD fq_t sqr(const fq_t &a) {
+MI_HD fq_t sqr(const fq_t &a_) {
     constexpr int L = 13;
+    struct {
+        int32_t v[13];
+    } a;
+    fq_pin(a.v, a_.v);
     int32_t a2[L];
     MI_UNROLL for (int i = 0; i < L; i++) a2[i] = a.v[i] * 2;
     int32_t m[L];
@@ -484,8 +550,15 @@ MI_HD fq_t sqr(const fq_t &a) {
 // 10..14 (the only ones with more than 31 products of magnitude 2^58; p_0 and p_12 are small) the a*b and
 // m*p part is split into its high part (kept aside) and its low 30 bits before the c*d products go in.
 // |out| <= (|a b| + |c d|) / R + p / 2.
-MI_HD fq_t mul_add(const fq_t &a, const fq_t &b, const fq_t &c, const fq_t &d) {
+MI_HD fq_t mul_add(const fq_t &a_, const fq_t &b_, const fq_t &c_, const fq_t &d_) {
     constexpr int L = 13;
+    struct {
+        int32_t v[13];
+    } a, b, c, d;
+    fq_pin(a.v, a_.v);
+    fq_pin(b.v, b_.v);
+    fq_pin(c.v, c_.v);
+    fq_pin(d.v, d_.v);
     int32_t m[L];
     fq_t r;
     int64_t acc = 0;

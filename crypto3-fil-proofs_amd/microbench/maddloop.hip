@@ -9,7 +9,8 @@
 // Both run at the kernel's occupancy cap (amdgpu_waves_per_eu(2)).  A diagnostic build stamps s_memtime /
 // s_memrealtime around the loop once per wave: the in-kernel clock is delta(memtime) / delta(realtime) x
 // 100 MHz (MI355X_MICROARCH.md, DVFS item 6), so the cycles per wave-madd per SIMD can be compared with
-// the ISA issue model (3,546 v_mad_u64_u32 at 4 cycles + 1,824 other VALU at 2 cycles = 17.8 k cycles).
+// the ISA issue model (3,081 v_mad_i64_i32 at 4 cycles + 1,915 other VALU at 2 cycles = 16.2 k cycles; the
+// 14 x 29-bit field before round 5: 3,546 + 1,824 = 17.8 k).
 // Inputs are random field elements (not curve points): the formula's instruction stream is the same, and
 // P = U2 - X1 is never zero, so every addition takes the general branch.
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 maddloop.hip -o maddloop && ./maddloop
@@ -421,7 +422,7 @@ int main(int argc, char **argv) {
     auto g1 = [&](const char *name, auto gather, auto *table) {
         using T = std::remove_pointer_t<decltype(table)>;
         run_with(name, [&] { k_madd<decltype(gather)::value, T><<<blocks, 256>>>(table, tn - 1, didx, iters, dout, dst); },
-                 iters, blocks, 1, 17832.0, dst, warm_s);
+                 iters, blocks, 1, 16154.0, dst, warm_s);
     };
     g1("gather128", std::true_type{}, d128);
     if (!only_ba) {

@@ -4,7 +4,8 @@
 // The Fq arithmetic the MSM kernels inline works on balanced signed 30-bit limbs with no range reduction
 // (field.h "Fq").  This program runs exactly that code on the host over sequences that hit every branch
 // of the group law -- distinct points with random signs, P + P (doubling), P + (-P) (infinity), infinity
-// operands, other representatives v + k p of every coordinate -- and compares each result with the
+// operands (the raw (0, 0) encoding), other representatives v + k p of every finite coordinate -- and compares
+// each result with the
 // oracle's affine group law.  It also checks every field operation against plain integers mod p (an
 // independent reference over 32-bit words with reduced additions only), on random values and on limb
 // patterns at the column-sum bound (every low limb +-2^29).
@@ -17,6 +18,7 @@
 
 #include "curve.h"
 #include "glv.h"
+#include "hostfield.h"
 #include "oracle.h"
 
 using namespace mi;
@@ -223,6 +225,45 @@ static void check_growth() {
     CHECK(ref_eq(ref_val(a * b), ref_mul(ref_mul(va, vb), ref_rinv())), "growth product");
 }
 
+// the host-only 64-bit field (hostfield.h) against the device field: products, sums, inverses, and the host chains
+// (scalar multiplication, window combination) against the generic group law over fq_t
+static void check_host_field() {
+    for (int it = 0; it < 2000; it++) {
+        const fq_t a = rand_fq(), b = rand_fq();
+        const host::hfq ha = host::to_h(a), hb = host::to_h(b);
+        CHECK(host::from_h(ha * hb) == a * b && host::from_h(ha + hb) == a + b && host::from_h(ha - hb) == a - b,
+              "hfq ops it=%d", it);
+        CHECK(host::from_h(-ha) == -a && host::from_h(sqr(ha)) == sqr(a), "hfq neg/sqr it=%d", it);
+        if (it < 20 && !a.is_zero()) CHECK(host::from_h(host::inverse_inl(ha)) * a == fq_t::one(), "hfq inverse it=%d", it);
+    }
+    uint8_t gen[96], gen2[192];
+    or_g1_generator(gen);
+    or_g2_generator(gen2);
+    const g1_xyzz_t P = xyzz_dbl(xyzz_from_affine(g1_from_bytes(gen)));
+    auto from2 = [](const uint8_t *p) -> g2_affine_t {
+        return {{fq_from_be(p + 48), fq_from_be(p)}, {fq_from_be(p + 144), fq_from_be(p + 96)}};
+    };
+    const g2_xyzz_t Q = xyzz_dbl(xyzz_from_affine(from2(gen2)));
+    for (int it = 0; it < 6; it++) {
+        uint32_t k[8];
+        for (auto &w : k) w = (uint32_t)rng();
+        k[7] &= 0x3fffffff;
+        const g1_affine_t a1 = xyzz_to_affine(host::xyzz_mul(P, k, 8)), b1 = xyzz_to_affine(xyzz_mul(P, k, 8));
+        CHECK(a1.x == b1.x && a1.y == b1.y, "host g1 mul it=%d", it);
+        const g2_affine_t a2 = xyzz_to_affine(host::xyzz_mul(Q, k, 8)), b2 = xyzz_to_affine(xyzz_mul(Q, k, 8));
+        CHECK(a2.x == b2.x && a2.y == b2.y, "host g2 mul it=%d", it);
+        std::vector<g1_xyzz_t> W;
+        for (int w = 0; w < 5; w++) W.push_back(w == 2 ? g1_xyzz_t::inf() : xyzz_mul(P, k + w, 1));
+        g1_xyzz_t ref = W.back();
+        for (int w = 3; w >= 0; w--) {
+            for (int i = 0; i < 13; i++) ref = xyzz_dbl(ref);
+            ref = xyzz_add(ref, W[w]);
+        }
+        const g1_affine_t c1 = xyzz_to_affine(host::combine_windows(W, 13)), d1 = xyzz_to_affine(ref);
+        CHECK(c1.x == d1.x && c1.y == d1.y, "host combine it=%d", it);
+    }
+}
+
 static void check_g1_sequences() {
     uint8_t gen[96];
     or_g1_generator(gen);
@@ -250,7 +291,9 @@ static void check_g1_sequences() {
                 or_g1_mul(gen, s, pt);
             }
             g1_affine_t q = g1_from_bytes(pt);
-            if (rng() & 1) q.x = alt_rep(q.x);
+            // other representatives of the coordinates of a point (an infinity stays the raw (0, 0) encoding:
+            // curve.h coord_zero tests Fq infinity coordinates by their limbs)
+            if (rng() & 1 && !q.is_inf()) q.x = alt_rep(q.x);
             if (rng() & 1 && !q.is_inf()) q.y = alt_rep(q.y);
             if (neg) q.y = lazy_neg(q.y);  // what k_accum_level0 does for a negative digit
             acc = xyzz_add_affine_inl(acc, q);
@@ -426,6 +469,7 @@ static void check_glv() {
 int main() {
     check_fields();
     check_growth();
+    check_host_field();
     check_g1_sequences();
     check_g2();
     check_glv();
