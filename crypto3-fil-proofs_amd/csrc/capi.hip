@@ -87,6 +87,13 @@ struct mi_points {
     // out of memory may release the key's tables (prover.hip groth16_sums)
     const mi::Srs *srs = nullptr;
     int which = -1;
+    // fixed-base window table (mi_points_precompute) of caller-owned points; a key query's is the key's (Srs::wt)
+    void *wt_own = nullptr;
+    mi::WinTable wt_user;
+    mi::WinTable wtab() const {
+        if (wt_own || !srs) return wt_user;  // a table built on this point set first
+        return srs->wt_of(which);
+    }
     const void *table() const {
         if (!srs) return hi;
         return which == 0 ? (const void *)srs->h_hi : which == 1 ? (const void *)srs->l_hi
@@ -649,6 +656,19 @@ int mi_srs_table_state(const mi_srs *srs, uint64_t out[3]) {
     });
 }
 
+int mi_srs_window_tables(const mi_srs *srs, uint64_t out[3]) {
+    return guard([&] {
+        need(srs && out, "null argument");
+        const mi::Srs &s = *srs->p;
+        std::shared_lock<std::shared_mutex> in_use(s.use_mu);
+        uint64_t q = 0;
+        for (int i = 0; i < 5; i++) q += s.wt[i] ? 1 : 0;
+        out[0] = q ? s.wt_c : 0;
+        out[1] = q ? (256 + s.wt_c - 1) / s.wt_c : 0;
+        out[2] = q;
+    });
+}
+
 int mi_srs_readmit(mi_ctx *ctx, mi_srs *srs, uint64_t *rebuilt_bytes) {
     return guard([&] {
         need(ctx && srs, "null argument");
@@ -1082,7 +1102,45 @@ int mi_points_info(const mi_points *p, uint64_t out[3]) {
 void mi_points_free(mi_points *p) {
     if (!p) return;
     if (p->owns && p->dev) hipFree(p->dev);
+    if (p->wt_own) hipFree(p->wt_own);
     delete p;
+}
+int mi_points_precompute(mi_ctx *ctx, mi_points *p, unsigned window_bits, uint64_t n_points) {
+    return guard([&] {
+        need(ctx && p, "null argument");
+        need(n_points >= 1 && n_points <= p->n, "n_points must be in [1, number of bases]");
+        need(window_bits == 0 || (window_bits >= 8 && window_bits <= 22), "window_bits must be 0 or 8..22");
+        CtxLock l(ctx);
+        const unsigned wc = window_bits ? window_bits : mi::msm_wt_window_bits(n_points);
+        const unsigned nwin = (256 + wc - 1) / wc;
+        need(n_points * nwin < 0x80000000ull, "table too large for 31-bit point indices");
+        void *t = nullptr;
+        MI_HIP(hipMalloc(&t, (p->is_g2 ? sizeof(mi::g2_affine_t) : sizeof(mi::g1_affine_t)) * n_points * nwin));
+        try {
+            if (p->is_g2)
+                mi::g2_window_table(ctx->c, (const mi::g2_affine_t *)p->dev, n_points, wc, (mi::g2_affine_t *)t);
+            else
+                mi::g1_window_table(ctx->c, (const mi::g1_affine_t *)p->dev, n_points, wc, (mi::g1_affine_t *)t);
+        } catch (...) {
+            (void)hipFree(t);
+            throw;
+        }
+        if (p->wt_own) (void)hipFree(p->wt_own);
+        p->wt_own = t;
+        p->wt_user.p = t;
+        p->wt_user.stride = n_points;
+        p->wt_user.c = wc;
+        p->wt_user.nwin = nwin;
+    });
+}
+int mi_points_table_info(const mi_points *p, uint64_t out[3]) {
+    return guard([&] {
+        need(p && out, "null argument");
+        const mi::WinTable t = p->wtab();
+        out[0] = t.p ? t.c : 0;
+        out[1] = t.p ? t.nwin : 0;
+        out[2] = t.p ? t.stride : 0;
+    });
 }
 uint64_t mi_points_count(const mi_points *p) { return p ? p->n : 0; }
 
@@ -1095,8 +1153,9 @@ int mi_msm_g1_dev(mi_ctx *ctx, const mi_points *bases, const void *scalars_dev, 
         std::shared_lock<std::shared_mutex> in_use;  // a key's query: its split table stays while this MSM runs
         if (bases->srs) in_use = std::shared_lock<std::shared_mutex>(bases->srs->use_mu);
         mi::g1_xyzz_t r;
+        const mi::WinTable wt = bases->wtab();  // used when it covers the n points
         mi::msm_g1(ctx->c, (const mi::g1_affine_t *)bases->dev, (const mi::fr_t *)scalars_dev, nullptr, n, &r,
-                   (const mi::g1_affine_t *)bases->table(), bases->subgroup != 0);
+                   (const mi::g1_affine_t *)bases->table(), bases->subgroup != 0, n <= wt.stride ? &wt : nullptr);
         mi::g1_encode(mi::xyzz_to_affine(r), out96);
     });
 }
@@ -1106,8 +1165,12 @@ int mi_msm_g2_dev(mi_ctx *ctx, const mi_points *bases, const void *scalars_dev, 
         need(bases->is_g2, "G1 bases passed to mi_msm_g2_dev");
         need(n <= bases->n, "n exceeds the number of bases");
         CtxLock l(ctx, 0, FENCE);
+        std::shared_lock<std::shared_mutex> in_use;  // a key's query: its window table stays while this MSM runs
+        if (bases->srs) in_use = std::shared_lock<std::shared_mutex>(bases->srs->use_mu);
         mi::g2_xyzz_t r;
-        mi::msm_g2(ctx->c, (const mi::g2_affine_t *)bases->dev, (const mi::fr_t *)scalars_dev, nullptr, n, &r);
+        const mi::WinTable wt = bases->wtab();
+        mi::msm_g2(ctx->c, (const mi::g2_affine_t *)bases->dev, (const mi::fr_t *)scalars_dev, nullptr, n, &r,
+                   n <= wt.stride ? &wt : nullptr);
         mi::g2_encode(mi::xyzz_to_affine(r), out192);
     });
 }
@@ -1378,6 +1441,14 @@ int mi_ctx_get_work(mi_ctx *ctx, uint64_t out[2]) {
         CtxLock l(ctx);
         out[0] = ctx->c.stats.madds_g1;
         out[1] = ctx->c.stats.madds_g2;
+    });
+}
+int mi_ctx_get_table_msms(mi_ctx *ctx, uint64_t out[2]) {
+    return guard([&] {
+        need(ctx && out, "null argument");
+        CtxLock l(ctx);
+        out[0] = ctx->c.stats.wt_msms;
+        out[1] = ctx->c.stats.wt_msms_g2;
     });
 }
 int mi_ctx_get_fallbacks(mi_ctx *ctx, uint64_t out[2]) {

@@ -133,9 +133,12 @@ struct Stats {
     uint64_t madds_g1 = 0, madds_g2 = 0;  // mixed additions issued by k_accum_level0 (non-zero digits)
     uint64_t oom_retries = 0;      // proofs re-run after an out-of-memory error (prover.hip groth16_sums)
     uint64_t oom_freed_bytes = 0;  // split tables + scratch released for those retries
+    uint64_t wt_msms = 0, wt_msms_g2 = 0;  // G1 / G2 MSMs that ran over a window table (msm_run_wt)
     static constexpr int NK = 13;
     void merge(const Stats &o) {
         madds_g1 += o.madds_g1;
+        wt_msms += o.wt_msms;
+        wt_msms_g2 += o.wt_msms_g2;
         madds_g2 += o.madds_g2;
         KStat *d[] = {&accum_g1, &accum_g2, &msm_g1, &msm_g2, &sort, &ntt, &prove, &h2d, &poseidon, &tree_h2d,
                       &wit_a, &wit_sha, &wit_pos};
@@ -206,8 +209,9 @@ struct Ctx {
     hipStream_t stream = nullptr;
     std::recursive_mutex mu;
     NttTables tw;
-    DevBuf scratch[24];  // 0-19: MSM / NTT / upload temporaries (18-19: G2 second level), 20: prover vectors,
-                         // 21-22: witness slots (capi.hip uploader; 21 also building-block inputs)
+    DevBuf scratch[26];  // 0-19: MSM / NTT / upload temporaries (18-19: G2 second level), 20: prover vectors,
+                         // 21-22: witness slots (capi.hip uploader; 21 also building-block inputs),
+                         // 24-25: an MSM plan's multi-chunk bucket list and first chunk-tree level (msm_impl.h)
     Stats stats;
     EventTimer timer;
     PinnedBuf pin;  // small readbacks (msm_impl.h); one lane's, reused call after call
@@ -299,6 +303,10 @@ struct MsmPlan {
     bool glv = false;      // split through the GLV endomorphism: nbk / nb count sub-buckets (2 per bucket)
     const uint32_t *vals_s = nullptr, *off = nullptr, *cnt = nullptr, *coff = nullptr, *ccnt = nullptr,
                    *chunk_bucket = nullptr, *order = nullptr;
+    // buckets with more than one level-0 chunk (mlist[0, m)) and the first in-place tree level over them (per-bucket
+    // partial counts qcnt / offsets qoff, l1_total partials), counted before the plan's one readback
+    uint32_t m = 0, l1_total = 0;
+    uint32_t *mlist = nullptr, *qcnt = nullptr, *qoff = nullptr;
 };
 // false when every scalar is zero (the MSM is the identity).  split: plan the 2n half-scalar points of
 // the 2^128-shifted base table (msm_g1 with bases_hi); the plan then needs bases_hi too.
@@ -306,6 +314,20 @@ bool msm_prepare(Ctx &c, const fr_t *scalars, const uint32_t *idx, uint64_t n, M
 void msm_g1_planned(Ctx &c, const MsmPlan &plan, const g1_affine_t *bases, g1_xyzz_t *result_host,
                     const g1_affine_t *bases_hi = nullptr);
 void msm_g2_planned(Ctx &c, const MsmPlan &plan, const g2_affine_t *bases, g2_xyzz_t *result_host);
+// Fixed-base window table of a G1 / G2 base set P_0 .. P_{stride-1}: p[w * stride + i] = 2^(c w) P_i for w < nwin =
+// ceil(256 / c).  An MSM over it (msm_g1 with wt) puts every window's digits into ONE set of 2^(c - 1) buckets: the
+// same mixed additions as a c-bit Pippenger, the bucket reduction of one window instead of nwin, and no window
+// combination.  Memory: nwin x the base set.
+struct WinTable {
+    const void *p = nullptr;  // g1_affine_t or g2_affine_t
+    uint64_t stride = 0;
+    unsigned c = 0, nwin = 0;
+};
+// window bits of the tables built for n-point base sets (MI_MSM_WT_C overrides; read per call)
+unsigned msm_wt_window_bits(uint64_t n);
+// builds the table of `n` bases into dst (nwin * n points); synchronises c's stream
+void g1_window_table(Ctx &c, const g1_affine_t *bases, uint64_t n, unsigned wbits, g1_affine_t *dst);
+void g2_window_table(Ctx &c, const g2_affine_t *bases, uint64_t n, unsigned wbits, g2_affine_t *dst);
 // result = sum_i scalar[idx ? idx[i] : i] * bases[i]; scalars canonical (raw) Fr.
 // bases_hi (optional): bases_hi[i] = 2^128 bases[i].  With it, large MSMs run in split mode: scalar
 // k_i = lo_i + 2^128 hi_i becomes two 128-bit scalars over bases[i] and bases_hi[i], which halves the
@@ -313,8 +335,11 @@ void msm_g2_planned(Ctx &c, const MsmPlan &plan, const g2_affine_t *bases, g2_xy
 // 1 default above 2^20 points, 2 always).
 // subgroup: every base is known to lie in the prime-order subgroup (a generated key, a checked load, or
 // bases that passed mi_points_check_subgroup); only then may auto mode take the GLV split (glv.h).
+// wt (optional): the window table of the base set `bases` belongs to, `bases` being its point wt_lo; the MSM then
+// runs over the table (msm_run_wt) instead.
 void msm_g1(Ctx &c, const g1_affine_t *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,
-            g1_xyzz_t *result_host, const g1_affine_t *bases_hi = nullptr, bool subgroup = false);
+            g1_xyzz_t *result_host, const g1_affine_t *bases_hi = nullptr, bool subgroup = false,
+            const WinTable *wt = nullptr, uint64_t wt_lo = 0);
 // whether msm_g1 with a bases_hi table takes the split path for n points
 bool msm_use_split(uint64_t n);
 // G1 split mode through the GLV endomorphism (glv.h) instead of the 2^128 tables: MI_MSM_GLV unset -> 2
@@ -326,7 +351,8 @@ int msm_glv_mode();
 // bases_hi table: out[i] = 2^128 in[i] (128 doublings, batch-normalised to affine); scratch slots 10, 11
 void g1_shift128(Ctx &c, const g1_affine_t *in, uint64_t n, g1_affine_t *out);
 void msm_g2(Ctx &c, const g2_affine_t *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,
-            g2_xyzz_t *result_host);
+            g2_xyzz_t *result_host,
+            const WinTable *wt = nullptr, uint64_t wt_lo = 0);
 // host-side window-size heuristic (exposed for tests)
 unsigned msm_window_bits(uint64_t n);
 // same for `n` points with scalars of `sbits` bits including the signed-digit carry (256 plain, 129 split)

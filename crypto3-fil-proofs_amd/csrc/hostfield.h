@@ -54,9 +54,8 @@ inline hfq hfq_sub_p_if_ge(const uint64_t t[6], uint64_t hi) {  // t (+ hi 2^384
         r.v[i] = (uint64_t)d;
         bw = (uint64_t)(d >> 64) & 1;
     }
-    if (bw > hi) {  // t < p
-        for (int i = 0; i < 6; i++) r.v[i] = t[i];
-    }
+    const uint64_t keep = (uint64_t)0 - (uint64_t)(bw > hi);  // t < p: keep t
+    for (int i = 0; i < 6; i++) r.v[i] = (t[i] & keep) | (r.v[i] & ~keep);
     return r;
 }
 
@@ -90,31 +89,27 @@ inline hfq operator-(const hfq &a, const hfq &b) {
 inline hfq operator-(const hfq &a) { return hfq::zero() - a; }
 inline hfq dbl(const hfq &a) { return a + a; }
 
-// CIOS Montgomery product a b 2^-384 mod p (p < 2^382: the running total fits 7 words)
+// CIOS Montgomery product a b 2^-384 mod p.  p < 2^382 leaves the top word two spare bits, so the running
+// total never needs a seventh word (the "no-carry" CIOS form: the product and the reduction of each outer
+// step share one inner loop); the result is < 2p and one branchless subtraction makes it canonical.
 inline hfq operator*(const hfq &a, const hfq &b) {
-    uint64_t t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t t[6] = {0, 0, 0, 0, 0, 0};
     for (int i = 0; i < 6; i++) {
-        uint64_t c = 0;
-        for (int j = 0; j < 6; j++) {
-            const u128 s = (u128)a.v[j] * b.v[i] + t[j] + c;
-            t[j] = (uint64_t)s;
-            c = (uint64_t)(s >> 64);
-        }
-        u128 s = (u128)t[6] + c;
-        t[6] = (uint64_t)s;
-        t[7] = (uint64_t)(s >> 64);
-        const uint64_t m = t[0] * HP::INV;
-        c = (uint64_t)(((u128)m * HP::P[0] + t[0]) >> 64);
+        u128 s = (u128)a.v[0] * b.v[i] + t[0];
+        uint64_t A = (uint64_t)(s >> 64);
+        const uint64_t m = (uint64_t)s * HP::INV;
+        u128 q = (u128)m * HP::P[0] + (uint64_t)s;
+        uint64_t C = (uint64_t)(q >> 64);
         for (int j = 1; j < 6; j++) {
-            const u128 q = (u128)m * HP::P[j] + t[j] + c;
+            s = (u128)a.v[j] * b.v[i] + t[j] + A;
+            A = (uint64_t)(s >> 64);
+            q = (u128)m * HP::P[j] + (uint64_t)s + C;
+            C = (uint64_t)(q >> 64);
             t[j - 1] = (uint64_t)q;
-            c = (uint64_t)(q >> 64);
         }
-        s = (u128)t[6] + c;
-        t[5] = (uint64_t)s;
-        t[6] = t[7] + (uint64_t)(s >> 64);
+        t[5] = A + C;
     }
-    return hfq_sub_p_if_ge(t, t[6]);
+    return hfq_sub_p_if_ge(t, 0);
 }
 inline hfq sqr(const hfq &a) { return a * a; }
 inline hfq mul_add(const hfq &a, const hfq &b, const hfq &c, const hfq &d) { return a * b + c * d; }
@@ -210,6 +205,25 @@ XYZZ<F> xyzz_mul(const XYZZ<F> &p, const uint32_t *k, int nwords) {
 template <class F>
 XYZZ<F> xyzz_add(const XYZZ<F> &p, const XYZZ<F> &q) {
     return from_h<F>(mi::xyzz_add_inl(to_h(p), to_h(q)));
+}
+template <class F>
+XYZZ<F> xyzz_add_affine(const XYZZ<F> &p, const Affine<F> &q) {
+    if (q.is_inf()) return p;
+    return from_h<F>(mi::xyzz_add_inl(to_h(p), to_h(xyzz_from_affine(q))));
+}
+template <class F>
+Affine<F> xyzz_to_affine(const XYZZ<F> &p) {
+    if (p.is_inf()) return Affine<F>::inf();
+    const auto a = mi::xyzz_to_affine_inl(to_h(p));
+    return {from_h(a.x), from_h(a.y)};
+}
+// 2^n p
+template <class F>
+XYZZ<F> xyzz_dbl_n(const XYZZ<F> &p, unsigned n) {
+    if (n == 0 || p.is_inf()) return p;
+    auto t = to_h(p);
+    for (unsigned i = 0; i < n; i++) t = mi::xyzz_dbl_inl(t);
+    return from_h<F>(t);
 }
 // sum_w 2^(c w) W[w] by Horner over the windows (c doublings per window): the MSM's final combination
 template <class F>

@@ -57,8 +57,38 @@ int msm_glv_mode() {
 }
 
 void msm_g1(Ctx &c, const g1_affine_t *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,
-            g1_xyzz_t *result_host, const g1_affine_t *bases_hi, bool subgroup) {
+            g1_xyzz_t *result_host, const g1_affine_t *bases_hi, bool subgroup, const WinTable *wt, uint64_t wt_lo) {
+    // MI_MSM_WT=0 ignores the window tables (A/B; read per call)
+    const char *e = getenv("MI_MSM_WT");
+    if (wt && wt->p && n && !(e && atoi(e) == 0)) {
+        msm_run_wt<fq_t>(c, *wt, wt_lo, scalars, idx, n, result_host);
+        return;
+    }
     msm_run<fq_t>(c, bases, scalars, idx, n, result_host, bases_hi, subgroup);
+}
+
+unsigned msm_wt_window_bits(uint64_t n) {
+    if (const char *e = getenv("MI_MSM_WT_C")) {
+        const int cf = atoi(e);
+        if (cf > 0) return (unsigned)(cf < 8 ? 8 : cf > 22 ? 22 : cf);
+    }
+    // One bucket set for every window.  Per entry (n ceil(256 / c) of them): a mixed add (1 / 6.6e9 s, measured at
+    // 2^20) and its sort (~0.03 ns); per bucket: the first reduction level's two full adds (~3e9 / s); plus the
+    // latency-bound bit-row tree (~0.4 ms).  The top window of a 255-bit scalar holds 255 - (nwin - 1) c bits: a c
+    // that leaves it a few bits piles the entries of every point into its few buckets (deep chunk trees: measured
+    // 5.0 ms at c = 18 against 3.9 at c = 20), so c needs >= 2^(log2 n - 8) top-window buckets.
+    unsigned lg = 0;
+    while ((1ull << lg) < n) lg++;
+    unsigned best = 16;
+    double best_cost = 1e300;
+    for (unsigned c = 8; c <= 22; c++) {
+        const unsigned nwin = (256 + c - 1) / c;
+        const int top = 255 - (int)((nwin - 1) * c);
+        if (top < (int)lg - 8 && top < (int)c - 1) continue;
+        const double cost = (double)n * nwin * (1.0 / 6.6e9 + 0.03e-9) + 2.0 * (double)(1u << (c - 1)) / 3e9 + 0.4e-3;
+        if (cost < best_cost) best_cost = cost, best = c;
+    }
+    return best;
 }
 
 bool msm_prepare(Ctx &c, const fr_t *scalars, const uint32_t *idx, uint64_t n, MsmPlan &plan, bool split) {

@@ -28,6 +28,7 @@
 #include "ctx.h"
 #include "g2pair.h"
 #include "glv.h"
+#include "hostfield.h"
 
 namespace mi {
 
@@ -86,6 +87,40 @@ __global__ void k_digits(const fr_t *__restrict__ scalars, const uint32_t *__res
         // bucket within the window (+ w * wk when all windows are sorted in one call)
         keys[o] = (d ? d - 1 : invalid) + w * wk;
         vals[o] = i | (neg << 31);
+    }
+}
+
+// Window-table plans (fixed-base precomputation, msm_run_wt): table point w * stride + i is 2^(c w) P_i, so the
+// window-w digit of scalar i goes into the ONE bucket set of the plan as an entry over that point.  Entries are
+// laid out [window][scalar] like k_digits'; zero digits take the key `invalid` and sort last.
+__global__ void k_digits_wt(const fr_t *__restrict__ scalars, const uint32_t *__restrict__ idx, uint32_t n, unsigned c,
+                            unsigned nwin, uint32_t stride, uint32_t invalid, uint32_t *__restrict__ keys,
+                            uint32_t *__restrict__ vals) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const fr_t s = scalars[idx ? idx[i] : i];
+    const uint32_t nbk = 1u << (c - 1);
+    const uint32_t mask = (1u << c) - 1;
+    uint32_t carry = 0;
+    for (unsigned w = 0; w < nwin; w++) {
+        unsigned bit = w * c, word = bit >> 5, sh = bit & 31;
+        uint32_t d = 0;
+        if (word < 8) {
+            d = word_of(s, word) >> sh;
+            if (sh + c > 32 && word + 1 < 8) d |= word_of(s, word + 1) << (32 - sh);
+        }
+        d = (d & mask) + carry;
+        uint32_t neg = 0;
+        if (d > nbk) {
+            d = (1u << c) - d;
+            neg = 1;
+            carry = 1;
+        } else {
+            carry = 0;
+        }
+        const uint64_t o = (uint64_t)w * n + i;
+        keys[o] = d ? d - 1 : invalid;
+        vals[o] = (w * stride + i) | (neg << 31);
     }
 }
 
@@ -430,6 +465,14 @@ __global__ void k_tree_count(const uint32_t *__restrict__ mlist, const uint32_t 
     qcnt[i] = (parts + L1 - 1) / L1;
 }
 
+// the first tree level's quotas before m is known on the host: over all nb slots, zero from *m_dev on
+__global__ void k_tree_count_l1(const uint32_t *__restrict__ mlist, const uint32_t *__restrict__ ccnt,
+                                const uint32_t *__restrict__ m_dev, uint32_t nb, uint32_t *__restrict__ qcnt) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nb) return;
+    qcnt[i] = i < *m_dev ? (ccnt[mlist[i]] + L1 - 1) / L1 : 0u;
+}
+
 __global__ void k_tree_heads(const uint32_t *__restrict__ qcnt, const uint32_t *__restrict__ qoff, uint32_t m,
                              uint32_t *__restrict__ heads) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -575,6 +618,56 @@ __global__ void __launch_bounds__(256) MI_WAVES_RED k_sum_groups(const XYZZ<F> *
     LP::st(out + t, acc);
 }
 
+// ---- low-depth bucket reduction of one-window plans (reduce_bitsum) ----
+// From the first level's segment sums (acc_s = sum_j (j + 1) B_{s SA + j}, run_s = sum_j B_{s SA + j}, s < nseg
+// = 2^lseg per window): W = sum_s acc_s + SA sum_s s run_s, and sum_s s run_s = sum_k 2^k T_k with
+// T_k = sum of run_s over the s whose bit k is set.  Row 0 of a window sums acc, row 1 + k gives T_k: plain sums,
+// so the device part is a tree of depth ~log2(nseg) instead of running sums over the segments (depth ~2 nseg /
+// parallelism) -- the reduction of a one-window plan is latency-bound, not work-bound.  Thread (row, g) sums G
+// items of its row; bit rows hold nseg / 2 items, so their upper half of partials is the identity.
+template <class F>
+__global__ void __launch_bounds__(256) MI_WAVES_RED k_bitsum_first(const XYZZ<F> *__restrict__ acc,
+                                                      const XYZZ<F> *__restrict__ run, uint32_t nwin, uint32_t nseg,
+                                                      unsigned lseg, unsigned G, XYZZ<F> *__restrict__ out) {
+    using LP = LaneRed<F>;  // a lane pair per element for G2 (g2pair.h)
+    using R = typename LP::R;
+    // rows of a window: 0 / 1 = the two halves of acc, 2 + k = T_k; every row holds nseg / 2 items
+    const uint32_t half = nseg >> 1, per = half / G, rpw = 2 + lseg;
+    const uint64_t t = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / LP::K;
+    if (t >= (uint64_t)nwin * rpw * per) return;
+    const uint32_t g = (uint32_t)(t % per), r = (uint32_t)((t / per) % rpw), w = (uint32_t)(t / ((uint64_t)per * rpw));
+    XYZZ<R> s = XYZZ<R>::inf();
+    if (r < 2) {
+        const XYZZ<F> *p = acc + (uint64_t)w * nseg + (uint64_t)r * half + (uint64_t)g * G;
+        for (unsigned j = 0; j < G; j++) s = xyzz_add_inl(s, LP::ld(p + j));
+    } else {
+        const unsigned k = r - 2;
+        const XYZZ<F> *p = run + (uint64_t)w * nseg;
+        for (unsigned j = 0; j < G; j++) {
+            const uint32_t i = g * G + j;
+            s = xyzz_add_inl(s, LP::ld(p + (((i >> k) << (k + 1)) | (1u << k) | (i & ((1u << k) - 1)))));
+        }
+    }
+    LP::st(out + t, s);
+}
+
+// out[b] = sum of in[b m, b m + m) (m <= 256 / K, a power of two): one block per output, pairwise tree in LDS
+template <class F>
+__global__ void __launch_bounds__(256) MI_WAVES_RED k_sum_lds(const XYZZ<F> *__restrict__ in, uint32_t m,
+                                                 XYZZ<F> *__restrict__ out) {
+    using LP = LaneRed<F>;
+    __shared__ __align__(16) unsigned char raw[256 / LP::K * sizeof(XYZZ<F>)];
+    XYZZ<F> *sh = reinterpret_cast<XYZZ<F> *>(raw);
+    const uint32_t b = blockIdx.x, e = threadIdx.x / LP::K;  // element of this thread (both lanes of a pair)
+    if (e < m) LP::st(sh + e, LP::ld(in + (uint64_t)b * m + e));
+    __syncthreads();
+    for (uint32_t h = m >> 1; h; h >>= 1) {
+        if (e < h) LP::st(sh + e, xyzz_add_inl(LP::ld(sh + e), LP::ld(sh + e + h)));
+        __syncthreads();
+    }
+    if (e == 0) LP::st(out + b, LP::ld(sh));
+}
+
 // ---- G2 second-level bucket reduction (g2_second_level) ----
 // Bucket sums -> affine by Montgomery's trick over K consecutive buckets per thread (empty or
 // infinite buckets become the affine infinity (0, 0)).
@@ -671,11 +764,14 @@ inline void sort_pairs_u32(void *tmp, size_t &bytes, const uint32_t *k_in, uint3
 
 // ---- phase 1 (scalars only, shared by every MSM over the same scalars: B_G1 and B_G2) ----
 // digits -> per-window sort -> bucket bounds -> level-0 chunking -> length-sorted chunk order.
-// Level-0 chunking of a bucketed entry list (bucket b: entries [off[b], off[b] + cnt[b]) of vals_s;
-// pl.maxcnt set): chunk counts/offsets per bucket, chunk -> bucket map, length-sorted chunk order.
-// Fills the rest of the plan; false when there is no entry at all.
-inline bool plan_chunks(Ctx &c, MsmPlan &pl, uint32_t *offA, uint32_t *cntA, uint32_t *offB, uint32_t *cntB,
-                        uint32_t nb, const uint32_t *vals_s) {
+// Level-0 chunking of a bucketed entry list (bucket b: entries [off[b], off[b] + cnt[b]) of vals_s).
+// plan_counts queues everything that needs no host-side count -- chunk counts and offsets, the multi-chunk bucket
+// list and the first chunk-tree level's quotas -- and the readback of those counts into pin[0, PLAN_PIN); the
+// caller reads them after ITS one synchronisation (with its own bucket maxima) and plan_finish completes the plan:
+// chunk -> bucket map, length-sorted chunk order.  false when there is no entry at all.
+constexpr unsigned PLAN_PIN = 5;
+inline void plan_counts(Ctx &c, MsmPlan &pl, const uint32_t *cntA, uint32_t *offB, uint32_t *cntB, uint32_t nb,
+                        uint32_t *pin) {
     hipStream_t st = c.stream;
     static const uint32_t L0 = [] {
         const char *e = getenv("MI_MSM_L0");
@@ -683,8 +779,6 @@ inline bool plan_chunks(Ctx &c, MsmPlan &pl, uint32_t *offA, uint32_t *cntA, uin
         return v >= 2 && v <= 1024 ? v : L0_DEFAULT;
     }();
     pl.L0 = L0;
-    unsigned len_bits = 1;
-    while ((1u << len_bits) <= L0) len_bits++;
     uint32_t *coff = offB, *ccnt = cntB;
     // level 0: buckets cut into chunks of <= L0 sorted entries; one mixed-add chain per chunk
     k_chunk_count<<<grid_for(nb, 256), 256, 0, st>>>(cntA, nb, L0, ccnt);
@@ -693,21 +787,55 @@ inline bool plan_chunks(Ctx &c, MsmPlan &pl, uint32_t *offA, uint32_t *cntA, uin
     MI_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, ccnt, coff, nb, st));
     void *tmp = c.scratch[4].get(tmp_bytes);
     MI_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, ccnt, coff, nb, st));
-    uint32_t *tail = c.pin.as<uint32_t>(2);
-    MI_HIP(hipMemcpyAsync(&tail[0], coff + nb - 1, 4, hipMemcpyDeviceToHost, st));
-    MI_HIP(hipMemcpyAsync(&tail[1], ccnt + nb - 1, 4, hipMemcpyDeviceToHost, st));
-    MI_HIP(hipStreamSynchronize(st));
-    uint32_t total = tail[0] + tail[1];
+    MI_HIP(hipMemcpyAsync(&pin[0], coff + nb - 1, 4, hipMemcpyDeviceToHost, st));
+    MI_HIP(hipMemcpyAsync(&pin[1], ccnt + nb - 1, 4, hipMemcpyDeviceToHost, st));
+    // buckets of several chunks, and the first in-place tree level over their partials
+    uint32_t *mlist = c.scratch[24].as<uint32_t>(3 * (uint64_t)nb + 1), *m_dev = mlist + nb;
+    uint32_t *qcnt = m_dev + 1, *qoff = qcnt + nb;
+    uint8_t *flag = c.scratch[25].as<uint8_t>(nb);
+    k_flag_multi<<<grid_for(nb, 256), 256, 0, st>>>(ccnt, nb, flag);
+    MI_LAUNCHED(c, "k_flag_multi");
+    size_t tb = 0;
+    hipcub::CountingInputIterator<uint32_t> ids(0);
+    MI_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, ids, flag, mlist, m_dev, nb, st));
+    tmp = c.scratch[4].get(tb);
+    MI_HIP(hipcub::DeviceSelect::Flagged(tmp, tb, ids, flag, mlist, m_dev, nb, st));
+    k_tree_count_l1<<<grid_for(nb, 256), 256, 0, st>>>(mlist, ccnt, m_dev, nb, qcnt);
+    MI_LAUNCHED(c, "k_tree_count_l1");
+    tb = 0;
+    MI_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, qcnt, qoff, nb, st));
+    tmp = c.scratch[4].get(tb);
+    MI_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, qcnt, qoff, nb, st));
+    MI_HIP(hipMemcpyAsync(&pin[2], m_dev, 4, hipMemcpyDeviceToHost, st));
+    MI_HIP(hipMemcpyAsync(&pin[3], qoff + nb - 1, 4, hipMemcpyDeviceToHost, st));
+    MI_HIP(hipMemcpyAsync(&pin[4], qcnt + nb - 1, 4, hipMemcpyDeviceToHost, st));
+    pl.coff = coff;
+    pl.ccnt = ccnt;
+    pl.mlist = mlist;
+    pl.qcnt = qcnt;
+    pl.qoff = qoff;
+}
+
+inline bool plan_finish(Ctx &c, MsmPlan &pl, const uint32_t *offA, const uint32_t *cntA, uint32_t nb,
+                        const uint32_t *vals_s, const uint32_t *pin) {
+    hipStream_t st = c.stream;
+    const uint32_t L0 = pl.L0;
+    unsigned len_bits = 1;
+    while ((1u << len_bits) <= L0) len_bits++;
+    const uint32_t total = pin[0] + pin[1];
     pl.total = total;
+    pl.m = pin[2];
+    pl.l1_total = pin[3] + pin[4];
     if (total == 0) return false;  // every scalar is zero
+    const uint32_t *coff = pl.coff, *ccnt = pl.ccnt;
     uint32_t *heads = c.scratch[15].as<uint32_t>(total + 1);
     uint32_t *chunk_bucket = c.scratch[17].as<uint32_t>(total + 1);
     MI_HIP(hipMemsetAsync(heads, 0, sizeof(uint32_t) * (total + 1), st));
     k_chunk_heads<<<grid_for(nb, 256), 256, 0, st>>>(ccnt, coff, nb, heads);
     MI_LAUNCHED(c, "k_chunk_heads");
-    tmp_bytes = 0;
+    size_t tmp_bytes = 0;
     MI_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tmp_bytes, heads, chunk_bucket, MaxOp(), total, st));
-    tmp = c.scratch[4].get(tmp_bytes);
+    void *tmp = c.scratch[4].get(tmp_bytes);
     MI_HIP(hipcub::DeviceScan::InclusiveScan(tmp, tmp_bytes, heads, chunk_bucket, MaxOp(), total, st));
     // length-sorted chunk order (keys/vals scratch of the main sort are free by now)
     uint32_t *lkeys = c.scratch[0].as<uint32_t>(total), *lids = c.scratch[1].as<uint32_t>(total);
@@ -721,8 +849,6 @@ inline bool plan_chunks(Ctx &c, MsmPlan &pl, uint32_t *offA, uint32_t *cntA, uin
     pl.vals_s = vals_s;
     pl.off = offA;
     pl.cnt = cntA;
-    pl.coff = coff;
-    pl.ccnt = ccnt;
     pl.chunk_bucket = chunk_bucket;
     pl.order = order;
     return true;
@@ -844,24 +970,82 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
         MI_LAUNCHED(c, "k_end_to_cnt");
     }
 
-    // largest bucket decides the number of accumulation levels
-    std::vector<uint32_t> head(4 + nwin);
+    // largest bucket (the number of chunk-tree levels), each window's zero-digit start and the plan's counts: one
+    // readback
+    uint32_t *pin = c.pin.as<uint32_t>(4 + nwin + PLAN_PIN);
     {
         size_t tmp_bytes = 0;
         MI_HIP(hipcub::DeviceReduce::Max(nullptr, tmp_bytes, cntA, dmax, nb, st));
         void *tmp = c.scratch[4].get(tmp_bytes);
         MI_HIP(hipcub::DeviceReduce::Max(tmp, tmp_bytes, cntA, dmax, nb, st));
-        uint32_t *head_pin = c.pin.as<uint32_t>(4 + nwin);
-        MI_HIP(hipMemcpyAsync(head_pin, dmax, sizeof(uint32_t) * (4 + nwin), hipMemcpyDeviceToHost, st));
+        MI_HIP(hipMemcpyAsync(pin, dmax, sizeof(uint32_t) * (4 + nwin), hipMemcpyDeviceToHost, st));
+        plan_counts(c, pl, cntA, offB, cntB, nb, pin + 4 + nwin);
         MI_HIP(hipStreamSynchronize(st));
-        std::copy(head_pin, head_pin + 4 + nwin, head.begin());
     }
-    pl.maxcnt = head[0];
+    pl.maxcnt = pin[0];
     pl.entries = 0;  // non-zero digits = mixed additions of the accumulation
     for (unsigned w = 0; w < nwin; w++)
-        pl.entries += compact ? wn[w] : head[4 + w] == 0xffffffffu ? n : head[4 + w] - (uint64_t)w * n;
+        pl.entries += compact ? wn[w] : pin[4 + w] == 0xffffffffu ? n : pin[4 + w] - (uint64_t)w * n;
 
-    return plan_chunks(c, pl, offA, cntA, offB, cntB, nb, vals_s);
+    return plan_finish(c, pl, offA, cntA, nb, vals_s, pin + 4 + nwin);
+}
+
+// MI_MSM_BITSUM=0 sends one-window plans through reduce_windows (A/B); read per call
+inline bool bitsum_enabled() {
+    const char *e = getenv("MI_MSM_BITSUM");
+    return !(e && atoi(e) == 0);
+}
+
+// Window-table plan (msm_run_wt): nscal scalars, nwin windows of cb bits, over the table whose window w starts at
+// point w * stride (relative to the bases pointer the accumulation gets).  Every window's digits share one set of
+// 2^(cb - 1) buckets, so the plan has ONE window (pl.nwin = 1) of nwin * nscal entries.
+inline bool msm_prepare_wt_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, uint64_t nscal, unsigned cb,
+                                unsigned nwin, uint64_t stride, MsmPlan &pl) {
+    pl = MsmPlan();
+    if (nscal == 0) return false;
+    const uint64_t np64 = (uint64_t)nwin * nscal;
+    if (np64 >= 0xffffffffull || (uint64_t)nwin * stride >= 0x80000000ull || cb < 2 || cb > 24)
+        throw std::runtime_error("msm: window-table instance too large for 32-bit sort indices");
+    hipStream_t st = c.stream;
+    const uint32_t nbk = 1u << (cb - 1), np = (uint32_t)np64, invalid = nbk;
+    pl.n = np;
+    pl.cb = cb;
+    pl.nwin = 1;
+    pl.nbk = nbk;
+    pl.nb = nbk;
+    uint32_t *keys = c.scratch[0].as<uint32_t>(np), *vals = c.scratch[1].as<uint32_t>(np);
+    uint32_t *keys_s = c.scratch[2].as<uint32_t>(np), *vals_s = c.scratch[3].as<uint32_t>(np);
+    uint32_t *offA = c.scratch[5].as<uint32_t>(nbk), *cntA = c.scratch[6].as<uint32_t>(nbk);
+    uint32_t *offB = c.scratch[7].as<uint32_t>(nbk), *cntB = c.scratch[8].as<uint32_t>(nbk);
+    uint32_t *dmax = c.scratch[9].as<uint32_t>(8), *zstart = dmax + 4;
+    {
+        ScopedTimer tsort(c, &c.stats.sort, nscal);
+        k_digits_wt<<<grid_for(nscal, 256), 256, 0, st>>>(scalars, idx, (uint32_t)nscal, cb, nwin, (uint32_t)stride,
+                                                          invalid, keys, vals);
+        MI_LAUNCHED(c, "k_digits_wt");
+        size_t tmp_bytes = 0;
+        sort_pairs_u32(nullptr, tmp_bytes, keys, keys_s, vals, vals_s, np, cb, st);
+        void *tmp = c.scratch[4].get(tmp_bytes);
+        sort_pairs_u32(tmp, tmp_bytes, keys, keys_s, vals, vals_s, np, cb, st);
+        MI_HIP(hipMemsetAsync(offA, 0, sizeof(uint32_t) * nbk, st));
+        MI_HIP(hipMemsetAsync(cntA, 0, sizeof(uint32_t) * nbk, st));
+        MI_HIP(hipMemsetAsync(zstart, 0xff, sizeof(uint32_t), st));
+        k_bounds4<<<grid_for((np + 3) / 4, 256), 256, 0, st>>>(keys_s, np, np, nbk, 0, nullptr, offA, cntA, zstart);
+        MI_LAUNCHED(c, "k_bounds4");
+        k_end_to_cnt<<<grid_for(nbk, 256), 256, 0, st>>>(offA, cntA, nbk);
+        MI_LAUNCHED(c, "k_end_to_cnt");
+        size_t tb = 0;
+        MI_HIP(hipcub::DeviceReduce::Max(nullptr, tb, cntA, dmax, nbk, st));
+        tmp = c.scratch[4].get(tb);
+        MI_HIP(hipcub::DeviceReduce::Max(tmp, tb, cntA, dmax, nbk, st));
+    }
+    uint32_t *pin = c.pin.as<uint32_t>(5 + PLAN_PIN);  // one readback: bucket maximum, zero-digit start, plan counts
+    MI_HIP(hipMemcpyAsync(pin, dmax, sizeof(uint32_t) * 5, hipMemcpyDeviceToHost, st));
+    plan_counts(c, pl, cntA, offB, cntB, nbk, pin + 5);
+    MI_HIP(hipStreamSynchronize(st));
+    pl.maxcnt = pin[0];
+    pl.entries = pin[4] == 0xffffffffu ? np : pin[4];
+    return plan_finish(c, pl, offA, cntA, nbk, vals_s, pin + 5);
 }
 
 // ---- phase 2 (per base set): accumulation, chunk tree, bucket reduction, window combination ----
@@ -890,40 +1074,34 @@ XYZZ<F> *accumulate_chunks(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, co
 
     const uint32_t maxchunks = (pl.maxcnt + L0 - 1) / L0;
     if (maxchunks > 1) {  // in-place strided tree over the chunk partials of multi-chunk buckets only
-        uint8_t *flag = c.scratch[1].as<uint8_t>(nb);
-        uint32_t *mlist = c.scratch[0].as<uint32_t>(nb);
-        uint32_t *dm = c.scratch[9].as<uint32_t>(4);
-        k_flag_multi<<<grid_for(nb, 256), 256, 0, st>>>(ccnt, nb, flag);
-        MI_LAUNCHED(c, "k_flag_multi");
-        size_t tb = 0;
-        hipcub::CountingInputIterator<uint32_t> ids(0);
-        MI_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, ids, flag, mlist, dm, nb, st));
-        void *tmp = c.scratch[4].get(tb);
-        MI_HIP(hipcub::DeviceSelect::Flagged(tmp, tb, ids, flag, mlist, dm, nb, st));
-        uint32_t *m_pin = c.pin.as<uint32_t>(1);
-        MI_HIP(hipMemcpyAsync(m_pin, dm, 4, hipMemcpyDeviceToHost, st));
-        MI_HIP(hipStreamSynchronize(st));
-        const uint32_t m = *m_pin;
-        uint32_t *qcnt = c.scratch[2].as<uint32_t>(m), *qoff = c.scratch[11].as<uint32_t>(m);
+        const uint32_t m = pl.m, *mlist = pl.mlist;
         for (uint64_t stride = 1; stride < maxchunks; stride *= L1) {
-            k_tree_count<<<grid_for(m, 256), 256, 0, st>>>(mlist, ccnt, m, (uint32_t)stride, qcnt);
-            MI_LAUNCHED(c, "k_tree_count");
-            tb = 0;
-            MI_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, qcnt, qoff, m, st));
-            tmp = c.scratch[4].get(tb);
-            MI_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, qcnt, qoff, m, st));
-            uint32_t *tail = c.pin.as<uint32_t>(2);
-            MI_HIP(hipMemcpyAsync(&tail[0], qoff + m - 1, 4, hipMemcpyDeviceToHost, st));
-            MI_HIP(hipMemcpyAsync(&tail[1], qcnt + m - 1, 4, hipMemcpyDeviceToHost, st));
-            MI_HIP(hipStreamSynchronize(st));
-            uint32_t total = tail[0] + tail[1];
+            // the first level's quotas were counted with the plan; deeper levels (buckets of more than L0 L1
+            // entries) are counted here, into this accumulation's own scratch: a plan serves B_G1 and B_G2 alike,
+            // so its arrays stay as they are
+            uint32_t total = pl.l1_total, *qcnt = pl.qcnt, *qoff = pl.qoff;
+            if (stride > 1) {
+                qcnt = c.scratch[2].as<uint32_t>(m);
+                qoff = c.scratch[11].as<uint32_t>(m);
+                k_tree_count<<<grid_for(m, 256), 256, 0, st>>>(mlist, ccnt, m, (uint32_t)stride, qcnt);
+                MI_LAUNCHED(c, "k_tree_count");
+                size_t tb = 0;
+                MI_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, qcnt, qoff, m, st));
+                void *tmp = c.scratch[4].get(tb);
+                MI_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, qcnt, qoff, m, st));
+                uint32_t *tail = c.pin.as<uint32_t>(2);
+                MI_HIP(hipMemcpyAsync(&tail[0], qoff + m - 1, 4, hipMemcpyDeviceToHost, st));
+                MI_HIP(hipMemcpyAsync(&tail[1], qcnt + m - 1, 4, hipMemcpyDeviceToHost, st));
+                MI_HIP(hipStreamSynchronize(st));
+                total = tail[0] + tail[1];
+            }
             uint32_t *heads = c.scratch[15].as<uint32_t>(total + 1), *map = c.scratch[13].as<uint32_t>(total + 1);
             MI_HIP(hipMemsetAsync(heads, 0, sizeof(uint32_t) * (total + 1), st));
             k_tree_heads<<<grid_for(m, 256), 256, 0, st>>>(qcnt, qoff, m, heads);
             MI_LAUNCHED(c, "k_tree_heads");
-            tb = 0;
+            size_t tb = 0;
             MI_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, heads, map, MaxOp(), total, st));
-            tmp = c.scratch[4].get(tb);
+            void *tmp = c.scratch[4].get(tb);
             MI_HIP(hipcub::DeviceScan::InclusiveScan(tmp, tb, heads, map, MaxOp(), total, st));
             k_tree_level<F><<<grid_for((uint64_t)total * KR, 256), 256, 0, st>>>(map, qoff, mlist, coff, ccnt, total,
                                                                    (uint32_t)stride, P0);
@@ -1002,11 +1180,71 @@ void reduce_windows(Ctx &c, const MsmPlan &pl, XYZZ<F> *P0, std::vector<XYZZ<F>>
     MI_HIP(hipStreamSynchronize(st));
     std::vector<XYZZ<F>> sums(sums_pin, sums_pin + rows);
     W.assign(nwin, XYZZ<F>::inf());
-    for (unsigned w = 0; w < nwin; w++) {  // W = SumA + SA * (V - R)
-        const XYZZ<F> &SumA = sums[w], &R = sums[nwin + w], &V = sums[2 * nwin + w];
-        XYZZ<F> t = xyzz_add(V, xyzz_neg(R));
-        for (unsigned sa = SA; sa > 1; sa >>= 1) t = xyzz_dbl(t);
-        W[w] = xyzz_add(SumA, t);
+    unsigned log_sa = 0;
+    while ((1u << log_sa) < SA) log_sa++;
+    for (unsigned w = 0; w < nwin; w++)  // W = SumA + SA * (V - R), in the host field (hostfield.h)
+        W[w] = host::window_from_sums(sums[w], sums[nwin + w], sums[2 * nwin + w], log_sa);
+}
+
+// Bucket reduction of a plan with few windows (window-table plans: one) through k_bitsum_first / k_sum_lds; the host
+// folds each window's rows: W = row0 + SA sum_k 2^k row(1 + k) (hostfield.h).
+template <class F>
+void reduce_bitsum(Ctx &c, const MsmPlan &pl, XYZZ<F> *P0, std::vector<XYZZ<F>> &W) {
+    hipStream_t st = c.stream;
+    const unsigned nwin = pl.nwin;
+    const uint32_t nbk = pl.nbk;
+    // first-level segments in all (threads of k_bucket_reduce): >= 2^MI_MSM_BS_SEG_LOG (default 2^16) while a
+    // segment holds more than one bucket; read per call (tuning)
+    const char *e = getenv("MI_MSM_BS_SEG_LOG");
+    const unsigned seg_log = e && atoi(e) > 0 ? (unsigned)atoi(e) : 16u;
+    unsigned SA = 1, log_sa = 0;
+    while (SA < nbk && (uint64_t)nbk * nwin / (SA * 2) >= (1ull << seg_log)) SA *= 2, log_sa++;
+    const uint32_t nseg = nbk / SA, totA = nwin * nseg;
+    unsigned lseg = 0;
+    while ((1u << lseg) < nseg) lseg++;
+    XYZZ<F> *accA = c.scratch[12].as<XYZZ<F>>(2 * (uint64_t)totA), *runA = accA + totA;
+    const unsigned KR = LaneRed<F>::K;
+    k_bucket_reduce<F><<<grid_for((uint64_t)totA * KR, 256), 256, 0, st>>>(pl.coff, pl.cnt, P0, totA, SA, accA, runA);
+    MI_LAUNCHED(c, "k_bucket_reduce");
+    // rows per window: the two halves of sum acc, then T_k; nseg / 2 items each.  Items per thread of the first
+    // level: enough that <= 2^15 threads run it (the LDS tree passes after it are latency-bound: fewer, shallower
+    // blocks; 2^20 over a c = 20 table, same box: 3.29 / 3.26 / 3.24 ms at 4 / 8 / 16 items), MI_MSM_BS_G0 overrides
+    const uint32_t rows = nwin * (2 + lseg), half = nseg / 2 ? nseg / 2 : 1;
+    const char *ge = getenv("MI_MSM_BS_G0");
+    unsigned G = 1;
+    if (ge && atoi(ge) > 0) {
+        G = (unsigned)atoi(ge);
+    } else {
+        while ((uint64_t)rows * half / (G * 2) >= (1u << 15) && G < 64) G *= 2;
+    }
+    while (G > 1 && G > half) G /= 2;
+    uint32_t per = nseg >= 2 ? half / G : 1;
+    XYZZ<F> *bufs[2] = {c.scratch[11].as<XYZZ<F>>((uint64_t)rows * per), c.scratch[14].as<XYZZ<F>>((uint64_t)rows * per)};
+    if (nseg >= 2) {
+        k_bitsum_first<F><<<grid_for((uint64_t)rows * per * KR, 256), 256, 0, st>>>(accA, runA, nwin, nseg, lseg, G,
+                                                                                 bufs[0]);
+        MI_LAUNCHED(c, "k_bitsum_first");
+    } else {  // one segment per window: its acc is row 0, row 1 the identity (all-zero coordinates), no bit rows
+        MI_HIP(hipMemsetAsync(bufs[0], 0, sizeof(XYZZ<F>) * rows, st));
+        for (unsigned w = 0; w < nwin; w++)
+            MI_HIP(hipMemcpyAsync(bufs[0] + 2 * (uint64_t)w, accA + w, sizeof(XYZZ<F>), hipMemcpyDeviceToDevice, st));
+    }
+    int k = 0;
+    while (per > 1) {
+        const uint32_t m = per < 256 / KR ? per : 256 / KR;
+        k_sum_lds<F><<<rows * (per / m), 256, 0, st>>>(bufs[k], m, bufs[k ^ 1]);
+        MI_LAUNCHED(c, "k_sum_lds");
+        per /= m;
+        k ^= 1;
+    }
+    XYZZ<F> *sums_pin = c.pin.as<XYZZ<F>>(rows);
+    MI_HIP(hipMemcpyAsync(sums_pin, bufs[k], sizeof(XYZZ<F>) * rows, hipMemcpyDeviceToHost, st));
+    MI_HIP(hipStreamSynchronize(st));
+    W.assign(nwin, XYZZ<F>::inf());
+    for (unsigned w = 0; w < nwin; w++) {
+        const XYZZ<F> *r = sums_pin + (uint64_t)w * (2 + lseg);
+        const std::vector<XYZZ<F>> bits(r + 2, r + 2 + lseg);
+        W[w] = host::xyzz_add(host::xyzz_add(r[0], r[1]), host::xyzz_dbl_n(host::combine_windows(bits, 1), log_sa));
     }
 }
 
@@ -1069,7 +1307,7 @@ bool g2_second_level(Ctx &c, const MsmPlan &pl, XYZZ<F> *P0, std::vector<XYZZ<F>
         k_end_to_cnt<<<grid_for(nb2, 256), 256, 0, st>>>(off2, cnt2, nb2);
         MI_LAUNCHED(c, "k_end_to_cnt");
         uint32_t *dm = c.scratch[9].as<uint32_t>(4);
-        uint32_t *head = c.pin.as<uint32_t>(2);
+        uint32_t *head = c.pin.as<uint32_t>(2 + PLAN_PIN);
         tmp_bytes = 0;
         MI_HIP(hipcub::DeviceReduce::Max(nullptr, tmp_bytes, cnt2, dm, nb2, st));
         size_t tb2 = 0;
@@ -1078,8 +1316,9 @@ bool g2_second_level(Ctx &c, const MsmPlan &pl, XYZZ<F> *P0, std::vector<XYZZ<F>
         MI_HIP(hipcub::DeviceReduce::Max(tmp, tmp_bytes, cnt2, dm, nb2, st));
         MI_HIP(hipcub::DeviceReduce::Sum(tmp, tb2, cnt2, dm + 1, nb2, st));
         MI_HIP(hipMemcpyAsync(head, dm, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-        MI_HIP(hipStreamSynchronize(st));
         MsmPlan p2;
+        plan_counts(c, p2, cnt2, c.scratch[7].as<uint32_t>(nb2), c.scratch[8].as<uint32_t>(nb2), nb2, head + 2);
+        MI_HIP(hipStreamSynchronize(st));
         p2.n = head[1];
         p2.cb = c2;
         p2.nwin = nwin2;
@@ -1088,18 +1327,12 @@ bool g2_second_level(Ctx &c, const MsmPlan &pl, XYZZ<F> *P0, std::vector<XYZZ<F>
         p2.maxcnt = head[0];
         p2.entries = head[1];
         W.assign(nwin, XYZZ<F>::inf());
-        if (!plan_chunks(c, p2, off2, cnt2, c.scratch[7].as<uint32_t>(nb2), c.scratch[8].as<uint32_t>(nb2), nb2,
-                         vals_s))
-            return true;  // every bucket empty
+        if (!plan_finish(c, p2, off2, cnt2, nb2, vals_s, head + 2)) return true;  // every bucket empty
         // 4. second-level accumulation over the affine buckets, reduction, recombination
         XYZZ<F> *Q0 = accumulate_chunks<F>(c, p2, Baff);
         std::vector<XYZZ<F>> W2;
         reduce_windows<F>(c, p2, Q0, W2);
-        for (unsigned w = 0; w < nwin; w++) {
-            XYZZ<F> t = W2[2 * w + 1];
-            for (unsigned i = 0; i < c2; i++) t = xyzz_dbl(t);
-            W[w] = xyzz_add(W2[2 * w], t);
-        }
+        for (unsigned w = 0; w < nwin; w++) W[w] = host::xyzz_add(W2[2 * w], host::xyzz_dbl_n(W2[2 * w + 1], c2));
         return true;
     }
 }
@@ -1124,20 +1357,33 @@ void msm_accumulate_impl(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, XYZZ
             p2.coff = iota;
             p2.cnt = live;
             reduce_windows<F>(c, p2, Bm, W);
+        } else if (pl.nwin <= 2 && bitsum_enabled()) {
+            reduce_bitsum<F>(c, pl, P0, W);
         } else {
             reduce_windows<F>(c, pl, P0, W);
         }
+    } else if (pl.nwin <= 2 && bitsum_enabled()) {
+        reduce_bitsum<F>(c, pl, P0, W);
     } else {
         if (!g2_second_level<F>(c, pl, P0, W)) reduce_windows<F>(c, pl, P0, W);
     }
-    const unsigned nwin = pl.nwin, cb = pl.cb;
-    XYZZ<F> acc = W[nwin - 1];
-    for (int w = (int)nwin - 2; w >= 0; w--) {
-        for (unsigned i = 0; i < cb; i++) acc = xyzz_dbl(acc);
-        acc = xyzz_add(acc, W[w]);
-    }
-    *result = acc;
+    *result = host::combine_windows(W, pl.cb);  // Horner over the windows in the host field (hostfield.h)
     c.timer.resolve();
+}
+
+// MSM over a window table (WinTable, ctx.h): points [lo, lo + n) of the table's base set
+template <class F>
+void msm_run_wt(Ctx &c, const WinTable &wt, uint64_t lo, const fr_t *scalars, const uint32_t *idx, uint64_t n,
+                XYZZ<F> *result) {
+    if (lo + n > wt.stride) throw std::invalid_argument("msm: range past the end of the window table");
+    ScopedTimer whole(c, sizeof(F) == sizeof(fq_t) ? &c.stats.msm_g1 : &c.stats.msm_g2, n);
+    MsmPlan pl;
+    (sizeof(F) == sizeof(fq_t) ? c.stats.wt_msms : c.stats.wt_msms_g2) += 1;
+    if (!msm_prepare_wt_impl(c, scalars, idx, n, wt.c, wt.nwin, wt.stride, pl)) {
+        *result = XYZZ<F>::inf();
+        return;
+    }
+    msm_accumulate_impl<F>(c, pl, reinterpret_cast<const Affine<F> *>(wt.p) + lo, result);
 }
 
 template <class F>

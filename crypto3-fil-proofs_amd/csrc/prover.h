@@ -42,6 +42,28 @@ struct Srs {
     g1_affine_t *h_perm = nullptr, *l = nullptr, *a = nullptr, *b_g1 = nullptr;
     // 2^128 multiples of h_perm, l and a: the split-mode MSM tables (msm_g1 bases_hi), built at load
     g1_affine_t *h_hi = nullptr, *l_hi = nullptr, *a_hi = nullptr;
+    // fixed-base window tables (WinTable, ctx.h) of h_perm, l, a, b_g1 (G1) and b_g2 (G2) for small keys (domain
+    // <= 2^21 by default), built at load when they fit: wt[q][w * n_q + i] = 2^(wt_c w) P_i
+    void *wt[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    unsigned wt_c = 0;
+    uint64_t wt_points(int q) const {
+        const uint64_t n[5] = {n_h, n_l, n_a, n_b, n_b};
+        return q >= 0 && q < 5 ? n[q] : 0;
+    }
+    uint64_t wt_bytes(int q) const {
+        if (q < 0 || q > 4 || !wt[q]) return 0;
+        return wt_points(q) * ((256 + wt_c - 1) / wt_c) * (q == 4 ? sizeof(g2_affine_t) : sizeof(g1_affine_t));
+    }
+    WinTable wt_of(int q) const {
+        WinTable t;
+        if (q < 0 || q > 4 || !wt[q]) return t;
+        t.p = wt[q];
+        t.stride = wt_points(q);
+        t.c = wt_c;
+        t.nwin = (256 + wt_c - 1) / wt_c;
+        return t;
+    }
+    bool has_tables() const { return h_hi || l_hi || a_hi || wt[0] || wt[1] || wt[2] || wt[3] || wt[4]; }
     g2_affine_t *b_g2 = nullptr;
     g1_affine_t alpha_g1, beta_g1, delta_g1;
     g2_affine_t beta_g2, gamma_g2, delta_g2;

@@ -24,6 +24,7 @@
 #include <unordered_map>
 
 #include "prover.h"
+#include "hostfield.h"
 #include <future>
 
 namespace mi {
@@ -302,11 +303,13 @@ __global__ void __launch_bounds__(256) k_batch_affine(const XYZZ<F> *__restrict_
 }
 
 // 2^128 * P, XYZZ (128 doublings); batch-normalised by k_batch_affine
-__global__ void __launch_bounds__(256) k_shift128(const g1_affine_t *__restrict__ in, uint64_t n, g1_xyzz_t *__restrict__ out) {
+template <class F>
+__global__ void __launch_bounds__(256) k_shift(const Affine<F> *__restrict__ in, uint64_t n, unsigned bits,
+                                               XYZZ<F> *__restrict__ out) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    g1_xyzz_t p = xyzz_from_affine(in[i]);
-    for (int k = 0; k < 128; k++) p = xyzz_dbl_inl(p);
+    XYZZ<F> p = xyzz_from_affine(in[i]);
+    for (unsigned k = 0; k < bits; k++) p = xyzz_dbl_inl(p);
     out[i] = p;
 }
 
@@ -366,7 +369,7 @@ T *dalloc(uint64_t count) {
 
 template <class F>
 Affine<F> host_mul_affine(const Affine<F> &p, const fr_t &k_raw) {
-    return xyzz_to_affine(xyzz_mul(xyzz_from_affine(p), k_raw.v, 8));
+    return host::xyzz_to_affine(host::xyzz_mul(xyzz_from_affine(p), k_raw.v, 8));
 }
 
 }  // namespace
@@ -488,7 +491,7 @@ Srs::~Srs() {
                 break;
             }
     }
-    void *ps[] = {h_perm, l, a, b_g1, b_g2, at, bt, ct, h_hi, l_hi, a_hi};
+    void *ps[] = {h_perm, l, a, b_g1, b_g2, at, bt, ct, h_hi, l_hi, a_hi, wt[0], wt[1], wt[2], wt[3], wt[4]};
     for (void *p : ps)
         if (p) hipFree(p);
 }
@@ -914,24 +917,89 @@ static void fixed_base_affine(Ctx &c, const Affine<F> *table, const fr_t *k_dev,
     }
 }
 
-void g1_shift128(Ctx &c, const g1_affine_t *in, uint64_t n, g1_affine_t *out) {
+// out[i] = 2^bits in[i] (affine), queued on c's stream
+template <class F>
+static void shift_async(Ctx &c, const Affine<F> *in, uint64_t n, unsigned bits, Affine<F> *out) {
     const uint64_t chunk = 1ull << 24;
-    g1_xyzz_t *tmp = c.scratch[10].as<g1_xyzz_t>(n < chunk ? (n ? n : 1) : chunk);
-    fq_t *pre = c.scratch[11].as<fq_t>(n < chunk ? (n ? n : 1) : chunk);
+    XYZZ<F> *tmp = c.scratch[10].as<XYZZ<F>>(n < chunk ? (n ? n : 1) : chunk);
+    F *pre = c.scratch[11].as<F>(n < chunk ? (n ? n : 1) : chunk);
     for (uint64_t o = 0; o < n; o += chunk) {
         uint64_t m = n - o < chunk ? n - o : chunk;
-        k_shift128<<<grid1(m), 256, 0, c.stream>>>(in + o, m, tmp);
+        k_shift<F><<<grid1(m), 256, 0, c.stream>>>(in + o, m, bits, tmp);
         constexpr int K = 32;
-        k_batch_affine<fq_t, K><<<grid1((m + K - 1) / K), 256, 0, c.stream>>>(tmp, m, pre, out + o);
+        k_batch_affine<F, K><<<grid1((m + K - 1) / K), 256, 0, c.stream>>>(tmp, m, pre, out + o);
         MI_HIP(hipGetLastError());
     }
+}
+
+void g1_shift128(Ctx &c, const g1_affine_t *in, uint64_t n, g1_affine_t *out) {
+    shift_async<fq_t>(c, in, n, 128, out);
     MI_HIP(hipStreamSynchronize(c.stream));
 }
 
+template <class F>
+static void window_table(Ctx &c, const Affine<F> *bases, uint64_t n, unsigned wbits, Affine<F> *dst) {
+    const unsigned nwin = (256 + wbits - 1) / wbits;
+    if (n) MI_HIP(hipMemcpyAsync(dst, bases, n * sizeof(Affine<F>), hipMemcpyDeviceToDevice, c.stream));
+    for (unsigned w = 1; w < nwin; w++)
+        shift_async<F>(c, dst + (uint64_t)(w - 1) * n, n, wbits, dst + (uint64_t)w * n);
+    MI_HIP(hipStreamSynchronize(c.stream));
+}
+void g1_window_table(Ctx &c, const g1_affine_t *bases, uint64_t n, unsigned wbits, g1_affine_t *dst) {
+    window_table<fq_t>(c, bases, n, wbits, dst);
+}
+void g2_window_table(Ctx &c, const g2_affine_t *bases, uint64_t n, unsigned wbits, g2_affine_t *dst) {
+    window_table<fq2_t>(c, bases, n, wbits, dst);
+}
+
 namespace {
+// Fixed-base window tables (WinTable) of the four G1 queries of a small key: domain <= 2^MI_MSM_WT_MAX_LOG (default
+// 2^21; 0 turns them off), and only while they leave a proof its working set (the split tables' admission rule).
+// A key's MSMs then run over one bucket set per query (msm_run_wt).  Read at each build (tests compare both).
+void build_window_tables(Ctx &c, Srs &S) {
+    const char *e = getenv("MI_MSM_WT_MAX_LOG");
+    const unsigned max_log = e ? (unsigned)atoi(e) : 21u;
+    if (max_log == 0 || S.log_d > max_log || S.has_tables()) return;
+    const void *src[5] = {S.h_perm, S.l, S.a, S.b_g1, S.b_g2};
+    uint64_t big = 0;
+    for (int q = 0; q < 5; q++) big = S.wt_points(q) > big ? S.wt_points(q) : big;
+    const unsigned wc = msm_wt_window_bits(big);
+    const unsigned nwin = (256 + wc - 1) / wc;
+    uint64_t need = 0;
+    for (int q = 0; q < 5; q++)
+        need += src[q] ? S.wt_points(q) * nwin * (q == 4 ? sizeof(g2_affine_t) : sizeof(g1_affine_t)) : 0;
+    size_t free_b = 0, total_b = 0;
+    MI_HIP(hipMemGetInfo(&free_b, &total_b));
+    // a proof's scratch: the witness and QAP vectors, and per lane (four on small proofs) a plan of nwin entries per
+    // point (keys / values sorted and unsorted, sort space: ~32 B an entry)
+    const uint64_t work = 32 * (S.n_l + 3 * S.d) + 4ull * 32 * nwin * big;
+    if (need + work + (8ull << 30) > free_b) return;
+    S.wt_c = wc;
+    try {
+        for (int q = 0; q < 5; q++) {
+            const uint64_t n = S.wt_points(q);
+            if (!src[q] || !n) continue;
+            if (q == 4) {
+                g2_affine_t *t = dalloc<g2_affine_t>(n * nwin);
+                S.wt[q] = t;
+                g2_window_table(c, S.b_g2, n, wc, t);
+            } else {
+                g1_affine_t *t = dalloc<g1_affine_t>(n * nwin);
+                S.wt[q] = t;
+                g1_window_table(c, (const g1_affine_t *)src[q], n, wc, t);
+            }
+        }
+    } catch (const hip_error &e) {
+        if (e.code != hipErrorOutOfMemory) throw;
+        (void)hipStreamSynchronize(c.stream);
+        (void)hipGetLastError();
+        srs_drop_split_tables(S);
+    }
+}
+
 // split-mode tables of the three G1 queries whose MSMs run alone (B_G1 shares B_G2's plan, which has
 // no table on the G2 side, so b_g1 gets none)
-void build_hi_tables(Ctx &c, Srs &S) {
+void build_split_tables(Ctx &c, Srs &S) {
     if (msm_glv_mode() == 1) return;  // GLV split mode needs no table (glv.h)
     struct Q {
         const g1_affine_t *src;
@@ -968,6 +1036,12 @@ void build_hi_tables(Ctx &c, Srs &S) {
         (void)hipGetLastError();
         srs_drop_split_tables(S);
     }
+}
+
+// every MSM table of a key: the window tables of a small key, else the split tables
+void build_hi_tables(Ctx &c, Srs &S) {
+    build_window_tables(c, S);
+    if (!S.has_tables()) build_split_tables(c, S);
 }
 }  // namespace
 
@@ -1270,6 +1344,11 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
         if (b1_lane > 2) b1_lane = 2;  // every value names a lane that computes B_G1
         auto run_b = [&](Ctx &x) {
             const uint64_t lo = rg.lo[3], cnt = rg.cnt[3];
+            const WinTable wt2 = srs.wt_of(4);
+            if (b1_lane != 0 && wt2.p) {  // B_G1 runs on another lane: B_G2 over its window table
+                msm_g2(x, srs.b_g2 + lo, z_dev, circ.idx_b + lo, cnt, &B2, &wt2, lo);
+                return;
+            }
             MsmPlan pb;
             msm_prepare(x, z_dev, circ.idx_b + lo, cnt, pb);
             if (b1_lane == 0) msm_g1_planned(x, pb, srs.b_g1 + lo, &B1);
@@ -1277,17 +1356,20 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
         };
         auto run_b1 = [&](Ctx &x) {
             const uint64_t lo = rg.lo[3], cnt = rg.cnt[3];
-            msm_g1(x, srs.b_g1 + lo, z_dev, circ.idx_b + lo, cnt, &B1, nullptr, srs.in_subgroup);
+            const WinTable wt = srs.wt_of(3);
+            msm_g1(x, srs.b_g1 + lo, z_dev, circ.idx_b + lo, cnt, &B1, nullptr, srs.in_subgroup, &wt, lo);
         };
         auto run_l = [&](Ctx &x) {
             const uint64_t l_lo = rg.lo[1], l_cnt = rg.cnt[1];
+            const WinTable wt = srs.wt_of(1);
             msm_g1(x, srs.l + l_lo, z_dev + circ.n_in + l_lo, nullptr, l_cnt, &Lq, srs.l_hi ? srs.l_hi + l_lo : nullptr,
-                   srs.in_subgroup);
+                   srs.in_subgroup, &wt, l_lo);
         };
         auto run_a = [&](Ctx &x) {
             const uint64_t a_lo = rg.lo[2], a_cnt = rg.cnt[2];
+            const WinTable wt = srs.wt_of(2);
             msm_g1(x, srs.a + a_lo, z_dev, circ.idx_a + a_lo, a_cnt, &As, srs.a_hi ? srs.a_hi + a_lo : nullptr,
-                   srs.in_subgroup);
+                   srs.in_subgroup, &wt, a_lo);
         };
         // aux-lane order: B before L (same-box A/B at 2^26: -2 ms per proof; MI_AUX_ORDER=l_first
         // restores L first)
@@ -1327,9 +1409,10 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
             if (inject_oom) (void)c.scratch[19].get(1ull << 50);  // a real failed growth (1 PiB), as a scratch
                                                                     // buffer's hipMalloc fails when HBM is short
             const uint64_t h_lo = rg.lo[0], h_cnt = rg.cnt[0];
+            const WinTable wt_h = srs.wt_of(0);
             if (need_h)
                 msm_g1(c, srs.h_perm + h_lo, a + h_lo, nullptr, h_cnt, &H, srs.h_hi ? srs.h_hi + h_lo : nullptr,
-                       srs.in_subgroup);
+                       srs.in_subgroup, &wt_h, h_lo);
             else
                 H = g1_xyzz_t::inf();
             if (!wide) run_a(c);
@@ -1378,6 +1461,12 @@ uint64_t srs_drop_split_tables(Srs &S) {
             *t.p = nullptr;
             freed += t.n * sizeof(g1_affine_t);
         }
+    for (int q = 0; q < 5; q++)
+        if (S.wt[q]) {
+            freed += S.wt_bytes(q);
+            (void)hipFree(S.wt[q]);
+            S.wt[q] = nullptr;
+        }
     return freed;
 }
 
@@ -1392,7 +1481,7 @@ uint64_t release_device_tables(int device, const Srs *first) {
         else if (k->device == device) order.push_back(k);
     uint64_t freed = 0;
     for (Srs *k : order) {
-        if (!k->h_hi && !k->l_hi && !k->a_hi && !k->at) continue;
+        if (!k->has_tables() && !k->at) continue;
         std::unique_lock<std::shared_mutex> ex(k->use_mu, std::try_to_lock);
         if (!ex.owns_lock()) continue;
         const uint64_t t = srs_drop_split_tables(*k);
@@ -1428,7 +1517,7 @@ uint64_t release_prover_scratch(Ctx &c, const void *keep) {
         }
     };
     rel(c, 21);
-    for (Ctx *x = c.aux; x; x = x->aux) rel(*x, 24);
+    for (Ctx *x = c.aux; x; x = x->aux) rel(*x, 26);
     return freed;
 }
 }  // namespace
@@ -1437,7 +1526,7 @@ uint64_t release_prover_scratch(Ctx &c, const void *keep) {
 // (build_hi_tables: only while they leave a proof its working set).  Returns the bytes of tables rebuilt.
 uint64_t srs_readmit(Ctx &c, Srs &S) {
     std::unique_lock<std::shared_mutex> ex(S.use_mu);  // no proof or MSM over the key while its tables change
-    if (!S.tables_dropped || S.h_hi || S.l_hi || S.a_hi) return 0;
+    if (!S.tables_dropped || S.has_tables()) return 0;
     release_prover_scratch(c, nullptr);  // this context's idle arenas would count against the admission
     build_hi_tables(c, S);
     MI_HIP(hipStreamSynchronize(c.stream));
@@ -1445,6 +1534,7 @@ uint64_t srs_readmit(Ctx &c, Srs &S) {
     if (S.h_hi) got += S.n_h * sizeof(g1_affine_t);
     if (S.l_hi) got += S.n_l * sizeof(g1_affine_t);
     if (S.a_hi) got += S.n_a * sizeof(g1_affine_t);
+    for (int q = 0; q < 5; q++) got += S.wt_bytes(q);
     if (got) S.tables_dropped = 0;
     return got;
 }
@@ -1514,26 +1604,26 @@ AssemblyKey assembly_key(const Srs &srs) {
 BlindTerms groth16_blind_terms(const AssemblyKey &k, const fr_t &r, const fr_t &s) {
     const fr_t rs = from_mont(to_mont(r) * to_mont(s));
     BlindTerms t;
-    t.A0 = xyzz_add_affine(xyzz_mul(xyzz_from_affine(k.delta_g1), r.v, 8), k.alpha_g1);
-    t.B0 = xyzz_add_affine(xyzz_mul(xyzz_from_affine(k.delta_g2), s.v, 8), k.beta_g2);
-    g1_xyzz_t C = xyzz_mul(xyzz_from_affine(k.delta_g1), rs.v, 8);
-    C = xyzz_add(C, xyzz_mul(xyzz_from_affine(k.alpha_g1), s.v, 8));
-    t.C0 = xyzz_add(C, xyzz_mul(xyzz_from_affine(k.beta_g1), r.v, 8));
+    t.A0 = host::xyzz_add_affine(host::xyzz_mul(xyzz_from_affine(k.delta_g1), r.v, 8), k.alpha_g1);
+    t.B0 = host::xyzz_add_affine(host::xyzz_mul(xyzz_from_affine(k.delta_g2), s.v, 8), k.beta_g2);
+    g1_xyzz_t C = host::xyzz_mul(xyzz_from_affine(k.delta_g1), rs.v, 8);
+    C = host::xyzz_add(C, host::xyzz_mul(xyzz_from_affine(k.alpha_g1), s.v, 8));
+    t.C0 = host::xyzz_add(C, host::xyzz_mul(xyzz_from_affine(k.beta_g1), r.v, 8));
     return t;
 }
 
 ProofPoints groth16_finish(const BlindTerms &t, const ProofSums &m, const fr_t &r, const fr_t &s) {
     // the two multiplications by MSM sums run side by side (one on a helper thread)
-    auto sA = std::async(std::launch::async, [&] { return xyzz_mul(m.A, s.v, 8); });
-    const g1_xyzz_t rB1 = xyzz_mul(m.B1, r.v, 8);
-    g1_xyzz_t C = xyzz_add(t.C0, sA.get());
-    C = xyzz_add(C, rB1);
-    C = xyzz_add(C, m.H);
-    C = xyzz_add(C, m.L);
+    auto sA = std::async(std::launch::async, [&] { return host::xyzz_mul(m.A, s.v, 8); });
+    const g1_xyzz_t rB1 = host::xyzz_mul(m.B1, r.v, 8);
+    g1_xyzz_t C = host::xyzz_add(t.C0, sA.get());
+    C = host::xyzz_add(C, rB1);
+    C = host::xyzz_add(C, m.H);
+    C = host::xyzz_add(C, m.L);
     ProofPoints out;
-    out.A = xyzz_to_affine(xyzz_add(m.A, t.A0));
-    out.B = xyzz_to_affine(xyzz_add(m.B2, t.B0));
-    out.C = xyzz_to_affine(C);
+    out.A = host::xyzz_to_affine(host::xyzz_add(m.A, t.A0));
+    out.B = host::xyzz_to_affine(host::xyzz_add(m.B2, t.B0));
+    out.C = host::xyzz_to_affine(C);
     return out;
 }
 
@@ -1552,11 +1642,11 @@ ProofPoints groth16_prove(Ctx &c, const Srs &srs, const Circuit &circ, const fr_
 }
 
 void sums_encode(const ProofSums &m, uint8_t out[576]) {
-    g1_encode(xyzz_to_affine(m.H), out);
-    g1_encode(xyzz_to_affine(m.L), out + 96);
-    g1_encode(xyzz_to_affine(m.A), out + 192);
-    g1_encode(xyzz_to_affine(m.B1), out + 288);
-    g2_encode(xyzz_to_affine(m.B2), out + 384);
+    g1_encode(host::xyzz_to_affine(m.H), out);
+    g1_encode(host::xyzz_to_affine(m.L), out + 96);
+    g1_encode(host::xyzz_to_affine(m.A), out + 192);
+    g1_encode(host::xyzz_to_affine(m.B1), out + 288);
+    g2_encode(host::xyzz_to_affine(m.B2), out + 384);
 }
 
 Ctx &ctx_aux(Ctx &c) {

@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "prover.h"
+#include "hostfield.h"
 
 namespace mi {
 
@@ -358,7 +359,7 @@ bool in_subgroup(const Affine<F> &a) {  // r * a == O
     const Big &r = consts().r;
     uint32_t w[8] = {0};
     for (size_t i = 0; i < r.size() && i < 8; i++) w[i] = r[i];
-    return xyzz_mul(xyzz_from_affine(a), w, 8).is_inf();
+    return host::xyzz_mul(xyzz_from_affine(a), w, 8).is_inf();
 }
 
 bool fq_sqrt(const fq_t &a, fq_t &out) {
@@ -483,7 +484,7 @@ g1_xyzz_t input_acc(const DecodedVk &V, const uint8_t *inputs) {
     for (size_t i = 1; i < V.ic.size(); i++) {
         fr_t x = fr_from_le(inputs + 32 * (i - 1));
         if (geq_raw(x, fr_t::modulus_raw())) throw std::invalid_argument("public input is not canonical (>= r)");
-        acc = xyzz_add(acc, xyzz_mul(xyzz_from_affine(V.ic[i]), x.v, 8));
+        acc = host::xyzz_add(acc, host::xyzz_mul(xyzz_from_affine(V.ic[i]), x.v, 8));
     }
     return acc;
 }
@@ -506,7 +507,7 @@ bool groth16_verify(const uint8_t *vk, const uint8_t *ic, uint64_t n_ic, const u
     if (n_ic == 0) throw std::invalid_argument("verifying key has no IC points");
     DecodedVk V = decode_vk(vk, ic, n_ic);
     DecodedProof pr = decode_proof(proof);
-    g1_affine_t acc = xyzz_to_affine(input_acc(V, inputs));
+    g1_affine_t acc = host::xyzz_to_affine(input_acc(V, inputs));
     std::vector<g1_affine_t> P = {pr.A, affine_neg(acc), affine_neg(pr.C), affine_neg(V.alpha)};
     std::vector<g2_affine_t> Q = {pr.B, V.gamma2, V.delta2, V.beta2};
     return fq12_is_one(final_exponentiation_verify(multi_miller_loop(P, Q)));
@@ -525,11 +526,11 @@ ProofPoints groth16_assemble_shares(const uint8_t *vk, const uint8_t *shares, ui
             g1_affine_t p;
             if (!g1_decode_host(sh + 96 * j, p) || !g1_on_curve_host(p))
                 throw std::domain_error("proof share: invalid G1 point");
-            *g1[j] = xyzz_add_affine(*g1[j], p);
+            *g1[j] = host::xyzz_add_affine(*g1[j], p);
         }
         g2_affine_t q;
         if (!g2_decode_host(sh + 384, q) || !g2_on_curve_host(q)) throw std::domain_error("proof share: invalid G2 point");
-        m.B2 = xyzz_add_affine(m.B2, q);
+        m.B2 = host::xyzz_add_affine(m.B2, q);
     }
     return groth16_assemble(AssemblyKey{V.alpha, V.beta1, V.delta1, V.beta2, V.delta2}, m, r, s);
 }
@@ -599,18 +600,18 @@ bool groth16_verify_batch(const uint8_t *vk, const uint8_t *ic, uint64_t n_ic, u
         memcpy(rho.v, weights.data() + 16 * i, 16);
         rho.v[0] |= 1;  // non-zero
         rsum = rsum + to_mont(rho);
-        P.push_back(xyzz_to_affine(xyzz_mul(xyzz_from_affine(pr.A), rho.v, 4)));
+        P.push_back(host::xyzz_to_affine(host::xyzz_mul(xyzz_from_affine(pr.A), rho.v, 4)));
         Q.push_back(pr.B);
         g1_xyzz_t acc = input_acc(V, inputs + 32 * (n_ic - 1) * i);
-        sacc = xyzz_add(sacc, xyzz_mul(acc, rho.v, 4));
-        sc = xyzz_add(sc, xyzz_mul(xyzz_from_affine(pr.C), rho.v, 4));
+        sacc = host::xyzz_add(sacc, host::xyzz_mul(acc, rho.v, 4));
+        sc = host::xyzz_add(sc, host::xyzz_mul(xyzz_from_affine(pr.C), rho.v, 4));
     }
     fr_t rs = from_mont(rsum);
-    P.push_back(affine_neg(xyzz_to_affine(sacc)));
+    P.push_back(affine_neg(host::xyzz_to_affine(sacc)));
     Q.push_back(V.gamma2);
-    P.push_back(affine_neg(xyzz_to_affine(sc)));
+    P.push_back(affine_neg(host::xyzz_to_affine(sc)));
     Q.push_back(V.delta2);
-    P.push_back(affine_neg(xyzz_to_affine(xyzz_mul(xyzz_from_affine(V.alpha), rs.v, 8))));
+    P.push_back(affine_neg(host::xyzz_to_affine(host::xyzz_mul(xyzz_from_affine(V.alpha), rs.v, 8))));
     Q.push_back(V.beta2);
     return fq12_is_one(final_exponentiation_verify(multi_miller_loop(P, Q)));
 }

@@ -37,6 +37,7 @@ EXPORTS = [
     "mi_srs_stream_begin", "mi_srs_stream_part", "mi_srs_stream_end", "mi_srs_stream_abort", "mi_srs_export_query_dev",
     "mi_stacked_build", "mi_post_build", "mi_stacked_info", "mi_stacked_r1cs", "mi_stacked_load", "mi_stacked_public_inputs", "mi_stacked_witness_dev",
     "mi_stacked_witness", "mi_stacked_free", "mi_circuit_check_dev",
+    "mi_points_precompute", "mi_points_table_info", "mi_ctx_get_table_msms", "mi_srs_window_tables",
 ]
 
 _lib = None
@@ -138,6 +139,10 @@ def lib():
         "mi_groth16_prove_batch_random": ([vp, vp, vp, u64, vp, c_int, vp], c_int),
         "mi_points_check_subgroup": ([vp, vp], c_int),
         "mi_points_info": ([vp, vp], c_int),
+        "mi_points_precompute": ([vp, vp, ctypes.c_uint, ctypes.c_uint64], c_int),
+        "mi_points_table_info": ([vp, vp], c_int),
+        "mi_ctx_get_table_msms": ([vp, vp], c_int),
+        "mi_srs_window_tables": ([vp, vp], c_int),
         "mi_groth16_prove": ([vp, vp, vp, u8p, u8p, u8p, c_int, vp, vp], c_int),
         "mi_groth16_prove_dev": ([vp, vp, vp, vp, u8p, u8p, c_int, vp, vp], c_int),
         "mi_groth16_prove_batch": ([vp, vp, vp, u64, vp, u8p, c_int, vp], c_int),

@@ -101,6 +101,13 @@ class Context:
         check(lib().mi_ctx_get_fallbacks(self.h, w))
         return {"oom_retries": int(w[0]), "freed_bytes": int(w[1])}
 
+    def table_msms(self, g2: bool = False) -> int:
+        """G1 (G2 with g2) MSMs that ran over a fixed-base window table since the last reset_stats
+        (mi_ctx_get_table_msms)"""
+        w = (ctypes.c_uint64 * 2)()
+        check(lib().mi_ctx_get_table_msms(self.h, w))
+        return int(w[1] if g2 else w[0])
+
     def inject_oom(self, count: int):
         """TEST ONLY (mi_ctx_inject_oom): the first attempt of each of the next ``count`` proofs fails with a real
         out-of-memory error after the NTT chain (-1: every proof, 0: off)"""
@@ -157,6 +164,17 @@ class Points:
         out = (ctypes.c_uint64 * 3)()
         check(lib().mi_points_info(self.h, out))
         return {"count": out[0], "split_table": bool(out[1]), "subgroup": bool(out[2])}
+
+    def precompute(self, window_bits: int = 0, n_points: int = None):
+        """Fixed-base window table of the first n_points bases (mi_points_precompute): later G1 MSMs over at most
+        n_points scalars run every window into one bucket set.  window_bits 0 = the library's choice."""
+        check(lib().mi_points_precompute(self.ctx.h, self.h, int(window_bits), int(self.n if n_points is None else n_points)))
+
+    def table_info(self):
+        """{"window_bits", "windows", "points"} of the window table (zeros without one)"""
+        out = (ctypes.c_uint64 * 3)()
+        check(lib().mi_points_table_info(self.h, out))
+        return {"window_bits": int(out[0]), "windows": int(out[1]), "points": int(out[2])}
 
     def msm_dev(self, scalars_ptr: int, n: int) -> bytes:
         out = ctypes.create_string_buffer(192 if self.g2 else 96)
@@ -336,6 +354,12 @@ class ProvingKey:
         out = (ctypes.c_uint64 * 3)()
         check(lib().mi_srs_table_state(self.h, out))
         return {"split_tables": bool(out[0]), "dropped": int(out[1]), "subgroup": bool(out[2])}
+
+    def window_tables(self):
+        """{"window_bits", "windows", "queries"}: the fixed-base window tables of a small key (mi_srs_window_tables)"""
+        out = (ctypes.c_uint64 * 3)()
+        check(lib().mi_srs_window_tables(self.h, out))
+        return {"window_bits": int(out[0]), "windows": int(out[1]), "queries": int(out[2])}
 
     def readmit(self) -> int:
         """rebuilds split tables an out-of-memory release took, once they fit again (mi_srs_readmit); returns the

@@ -170,6 +170,10 @@ int mi_srs_msm_info(const mi_srs *srs, uint64_t out[2]);
  * (e.g. after another key was freed); *rebuilt_bytes (may be NULL) = table bytes rebuilt, 0 when nothing was
  * released or there is still no room.  Waits for proofs running on the key. */
 int mi_srs_table_state(const mi_srs *srs, uint64_t out[3]);
+/* fixed-base window tables of a small key's G1 queries (built at load / generation when the domain is <= 2^21 and
+ * they fit; mi_points_precompute explains them): out[0] window bits, out[1] windows, out[2] queries with a table
+ * (0..5: h, l, a, b_g1, b_g2).  Out-of-memory releases take them like the split tables, and mi_srs_readmit rebuilds them. */
+int mi_srs_window_tables(const mi_srs *srs, uint64_t out[3]);
 int mi_srs_readmit(mi_ctx *ctx, mi_srs *srs, uint64_t *rebuilt_bytes);
 void mi_srs_free(mi_srs *srs);
 
@@ -319,6 +323,16 @@ int mi_points_check_subgroup(mi_ctx *ctx, mi_points *p);
 /* out: count, has a 2^128 split table, subgroup-known */
 int mi_points_info(const mi_points *p, uint64_t out[3]);
 uint64_t mi_points_count(const mi_points *p);
+/* Fixed-base window table of the first n_points G1 or G2 bases: T[w n + i] = 2^(c w) P_i, w < ceil(256 / c)
+ * (window_bits = c, 0 = the library's choice for n_points).  Later mi_msm_g1_dev / _g2_dev calls over <= n_points
+ * scalars run every window's digits into one set of 2^(c - 1) buckets (fewer reductions, no window combination,
+ * same result).  Costs ceil(256 / c) x the bases' memory; replaces a previous table.  A proving key's small
+ * queries carry tables of their own (built at key load, domain <= 2^21); a table built on a key query's point set
+ * (mi_points_from_srs) belongs to that point set and takes precedence for its MSMs.  No reference counterpart: the
+ * reference's multiexp (bellman / crypto3 algebra, [NOT IN TREE]) re-reads the same SRS bases on every proof. */
+int mi_points_precompute(mi_ctx *ctx, mi_points *p, unsigned window_bits, uint64_t n_points);
+/* out: window bits, windows, table points (all 0 without a table) */
+int mi_points_table_info(const mi_points *p, uint64_t out[3]);
 int mi_msm_g1_dev(mi_ctx *ctx, const mi_points *bases, const void *scalars_dev, uint64_t n, uint8_t out96[96]);
 int mi_msm_g2_dev(mi_ctx *ctx, const mi_points *bases, const void *scalars_dev, uint64_t n, uint8_t out192[192]);
 int mi_ntt_fr_dev(mi_ctx *ctx, void *data_dev, unsigned log_n, int inverse, int coset);
@@ -422,6 +436,9 @@ int mi_ctx_get_work(mi_ctx *ctx, uint64_t out[2]);
  * Replaces failing outright when several keys share one GPU, as GROTH_PARAM_MEMORY_CACHE keeps them
  * (libs/filecoin/include/nil/filecoin/proofs/caches.hpp:48-116). */
 int mi_ctx_get_fallbacks(mi_ctx *ctx, uint64_t out[2]);
+/* G1 (out[0]) and G2 (out[1]) MSMs run over a window table (mi_points_precompute, a small key's tables) since the
+ * last reset */
+int mi_ctx_get_table_msms(mi_ctx *ctx, uint64_t out[2]);
 /* TEST ONLY: the first attempt of each of the next `count` proofs on this context fails with a real out-of-memory
  * error after its NTT chain (count < 0: every proof until reset to 0), so the release-and-retry path runs at any
  * size.  Production code never calls it; nothing in the prove path reads the environment for it. */

@@ -119,6 +119,7 @@ def test_groth16_split_msm_vs_oracle(ctx, oracle, monkeypatch, split):
     split through the GLV endomorphism (no tables built at key generation)."""
     monkeypatch.setenv("MI_MSM_SPLIT", "2" if split == "glv" else split)
     monkeypatch.setenv("MI_MSM_GLV", "1" if split == "glv" else "0")
+    monkeypatch.setenv("MI_MSM_WT_MAX_LOG", "0")  # this key's MSMs on the split / plain paths, not window tables
     n_in, n_aux, rws, z = circuits.random_circuit(35, 5000, n_in=6, n_free=32)
     oc, gc = _load(ctx, oracle, n_in, n_aux, rws, z)
     tox = circuits.toxic(35)
@@ -139,6 +140,7 @@ def test_prove_out_of_memory_degrades_to_glv(ctx, oracle, monkeypatch):
     and the context counts the retry.  Every prove entry (host / device witness, batch, share) recovers alike.
     mi_srs_readmit then rebuilds the tables (the release is not one-way) and the proof is unchanged."""
     monkeypatch.setenv("MI_MSM_SPLIT", "2")  # split mode at this size, so the tables are in use
+    monkeypatch.setenv("MI_MSM_WT_MAX_LOG", "0")  # split tables, not window tables
     n_in, n_aux, rws, z = circuits.random_circuit(36, 5000, n_in=6, n_free=32)
     oc, gc = _load(ctx, oracle, n_in, n_aux, rws, z)
     tox = circuits.toxic(36)
@@ -172,6 +174,41 @@ def test_prove_out_of_memory_degrades_to_glv(ctx, oracle, monkeypatch):
     assert pk.table_state() == {"split_tables": True, "dropped": 0, "subgroup": True}
     assert pk.readmit() == 0  # nothing to rebuild
     assert fg.prove(ctx, pk, gc, zb, 11, 21) == want[1] and ctx.fallbacks()["oom_retries"] == 0
+
+
+def test_prove_window_tables(ctx, oracle, monkeypatch):
+    """A small key builds fixed-base window tables for h, l, a, b_g1 and b_g2 at generation (domain <= 2^21): its
+    proofs run those five MSMs over one bucket set each and equal the oracle's, as do latency-mode shares (table slices at
+    an offset); MI_MSM_WT=0 (the plain path) gives the same bytes.  An out-of-memory retry releases the tables like
+    the split tables, and mi_srs_readmit rebuilds them."""
+    monkeypatch.delenv("MI_MSM_WT_MAX_LOG", raising=False)
+    monkeypatch.delenv("MI_MSM_WT", raising=False)
+    n_in, n_aux, rws, z = circuits.random_circuit(37, 6000, n_in=5, n_free=40)
+    oc, gc = _load(ctx, oracle, n_in, n_aux, rws, z)
+    tox = circuits.toxic(37)
+    pk = fg.generate_random_parameters(ctx, gc, tox)
+    wt = pk.window_tables()
+    assert wt["queries"] == 5 and wt["windows"] == -(-256 // wt["window_bits"]), wt
+    op = oracle.OracleParams(oc, tox)
+    zb = circuits.z_bytes(z)
+    want = [op.prove(zb, 30 + k, 40 + k)[0] for k in range(2)]
+    ctx.reset_stats()
+    assert fg.prove(ctx, pk, gc, zb, 30, 40) == want[0]
+    assert ctx.table_msms() == 4 and ctx.table_msms(g2=True) == 1
+    vk, _ = pk.verifying_key()
+    assert fg.assemble(vk, [fg.prove_share(ctx, pk, gc, zb, k, 3) for k in range(3)], 31, 41) == want[1]
+    monkeypatch.setenv("MI_MSM_WT", "0")
+    ctx.reset_stats()
+    assert fg.prove(ctx, pk, gc, zb, 31, 41) == want[1] and ctx.table_msms() == 0 and ctx.table_msms(g2=True) == 0
+    monkeypatch.delenv("MI_MSM_WT")
+    ctx.inject_oom(1)
+    assert fg.prove(ctx, pk, gc, zb, 30, 40) == want[0]
+    assert ctx.fallbacks()["oom_retries"] == 1
+    assert pk.window_tables()["queries"] == 0 and pk.table_state()["dropped"] == 1
+    assert pk.readmit() > 0
+    assert pk.window_tables() == wt
+    ctx.reset_stats()
+    assert fg.prove(ctx, pk, gc, zb, 31, 41) == want[1] and ctx.table_msms() == 4
 
 
 def test_prove_batch_and_priority(ctx, oracle):

@@ -222,6 +222,7 @@ def test_msm_split_tables_vs_oracle(ctx, oracle, monkeypatch, split):
 
     monkeypatch.setenv("MI_MSM_SPLIT", "2" if split == "glv" else split)
     monkeypatch.setenv("MI_MSM_GLV", "1" if split == "glv" else "0")
+    monkeypatch.setenv("MI_MSM_WT_MAX_LOG", "0")  # split / plain paths, not the key's window tables
     n_in, n_aux, rws, z = circuits.random_circuit(91, 3000, n_in=6, n_free=32)
     gc = fg.Circuit(ctx, len(rws), n_in, n_aux, circuits.to_csr(rws))
     pk = fg.generate_random_parameters(ctx, gc, circuits.toxic())
@@ -235,10 +236,11 @@ def test_msm_split_tables_vs_oracle(ctx, oracle, monkeypatch, split):
             torch.cuda.synchronize()
 
 
-def test_msm_split_default_2_17(ctx, oracle):
+def test_msm_split_default_2_17(ctx, oracle, monkeypatch):
     """Default selection (split from 2^16 points on) on the l query of a 2^17-row synthetic circuit."""
     import torch
 
+    monkeypatch.setenv("MI_MSM_WT_MAX_LOG", "0")  # the split path, not the key's window tables
     from fil_groth16 import synth
 
     sc = synth.SynthCircuit(log_rows=17, n_in=4, seed=3)
@@ -342,3 +344,97 @@ def test_msm_glv_auto_uploaded_bases(ctx, oracle, monkeypatch):
     assert ctx.msm_g1(bases, sb) == want
     monkeypatch.setenv("MI_MSM_GLV", "0")
     assert ctx.msm_g1(bases, sb) == want
+
+
+# ---- fixed-base window tables (mi_points_precompute; small keys build them at load) ----
+
+@pytest.mark.parametrize("n,c", [(1, 8), (3, 13), (1000, 8), (1000, 16), (20000, 13), (20000, 20)])
+def test_msm_window_table_vs_oracle(ctx, oracle, n, c):
+    """Every window's digits in one bucket set over T[w n + i] = 2^(c w) P_i: the same sum as the oracle's MSM, for
+    uniform, zero, one, r - 1 and half-width scalars; prefixes of the table (MSMs over fewer points than it holds)
+    too.  c = 8 and 20 bracket the window sizes (32 / 13 windows, 128 / 2^19 buckets)."""
+    import torch
+
+    bases = _bases_g1(oracle, n, 5000 + n)
+    pts = fg.Points(ctx, bases)
+    pts.precompute(c)
+    assert pts.table_info() == {"window_bits": c, "windows": -(-256 // c), "points": n}
+    ctx.reset_stats()
+    for seed in (1, 2):
+        sb = _split_scalars(n, 10 * n + seed)
+        sd = torch.from_numpy(np.frombuffer(sb, dtype=np.uint8).copy()).cuda()
+        assert pts.msm_dev(sd.data_ptr(), n) == oracle.msm_g1(bases, sb), (n, c, seed)
+        m = max(1, n // 3)
+        assert pts.msm_dev(sd.data_ptr(), m) == oracle.msm_g1(bases[:96 * m], sb[:32 * m]), (n, c, seed, m)
+    assert ctx.table_msms() == 4
+
+
+@pytest.mark.parametrize("bitsum", ["1", "0"])
+def test_msm_window_table_linearity_2_20(ctx, oracle, monkeypatch, bitsum):
+    """BASELINE config-2 size over a window table at the library's window choice and at c = 20 (2^19 buckets in
+    one window): MSM(k_i G, s_i) == (sum s_i k_i) G.  bitsum "0" reduces the one window with the running-sum
+    kernels instead of the bit-row sums (MI_MSM_BITSUM)."""
+    import torch
+
+    monkeypatch.setenv("MI_MSM_BITSUM", bitsum)
+    n = 1 << 20
+    rng = np.random.default_rng(420)
+    kw = rng.integers(0, 2**64, size=(n, 4), dtype=np.uint64)
+    kw[:, 3] &= np.uint64(0x3FFFFFFFFFFFFFFF)
+    kb = kw.tobytes()
+    pts = fg.Points(ctx, oracle.g1_fixed_base(kb))
+    sb = rand_fr_bytes(n, 421)
+    s = np.frombuffer(sb, dtype=np.uint64).reshape(n, 4)
+    acc = 0
+    for i in range(0, n, 4096):
+        kk = [int(a) | int(b) << 64 | int(c) << 128 | int(d) << 192 for a, b, c, d in kw[i:i + 4096]]
+        ss = [int(a) | int(b) << 64 | int(c) << 128 | int(d) << 192 for a, b, c, d in s[i:i + 4096]]
+        acc = (acc + sum(x * y for x, y in zip(kk, ss))) % R
+    want = oracle.g1_mul(oracle.g1_generator(), acc)
+    sd = torch.from_numpy(np.frombuffer(sb, dtype=np.uint8).copy()).cuda()
+    for c in (0, 20):
+        pts.precompute(c)
+        assert pts.msm_dev(sd.data_ptr(), n) == want, (c, pts.table_info())
+
+
+def test_msm_window_table_boolean_heavy(ctx, oracle):
+    """Boolean-heavy scalars over a table: every window-0 digit 1 lands in one bucket (a deep chunk tree),
+    the other windows' digits are zero."""
+    import torch
+
+    n = 1 << 16
+    bases = _bases_g1(oracle, n, 6001)
+    rng = random.Random(6002)
+    sc = [1 if rng.random() < 0.7 else (0 if rng.random() < 0.5 else rng.randrange(R)) for _ in range(n)]
+    sb = b"".join(v.to_bytes(32, "little") for v in sc)
+    pts = fg.Points(ctx, bases)
+    pts.precompute(16)
+    sd = torch.from_numpy(np.frombuffer(sb, dtype=np.uint8).copy()).cuda()
+    assert pts.msm_dev(sd.data_ptr(), n) == oracle.msm_g1(bases, sb)
+
+
+@pytest.mark.parametrize("n,c", [(1, 8), (700, 13), (5000, 16)])
+def test_msm_g2_window_table_vs_oracle(ctx, oracle, n, c):
+    """G2 bases over a window table (lane-pair accumulation and bit-row reduction) against the oracle."""
+    import torch
+
+    bases = _bases_g2(oracle, n, 7000 + n)
+    pts = fg.Points(ctx, bases, g2=True)
+    pts.precompute(c)
+    assert pts.table_info() == {"window_bits": c, "windows": -(-256 // c), "points": n}
+    ctx.reset_stats()
+    sb = _split_scalars(n, 7100 + n)
+    sd = torch.from_numpy(np.frombuffer(sb, dtype=np.uint8).copy()).cuda()
+    assert pts.msm_dev(sd.data_ptr(), n) == oracle.msm_g2(bases, sb), (n, c)
+    assert ctx.table_msms(g2=True) == 1 and ctx.table_msms() == 0
+
+
+def test_precompute_argument_rules(ctx, oracle):
+    bases = _bases_g1(oracle, 16, 6003)
+    pts = fg.Points(ctx, bases)
+    for bad in ((7, 16), (23, 16), (16, 0), (16, 17)):
+        with pytest.raises(fg.FilGpuError):
+            pts.precompute(*bad)
+    assert pts.table_info() == {"window_bits": 0, "windows": 0, "points": 0}
+    pts.precompute(16, 8)
+    assert pts.table_info()["points"] == 8

@@ -38,9 +38,15 @@ def key17(ctx):
     test_gpu_groth16.py::test_groth16_golden_generated_srs), its l and b_g2 queries as wire bytes."""
     from fil_groth16 import synth
 
+    import os
+
     sc = synth.SynthCircuit(log_rows=17, n_in=4, seed=11)
     gc = sc.load(ctx)
-    pk = fg.generate_random_parameters(ctx, gc, circuits.toxic())
+    os.environ["MI_MSM_WT_MAX_LOG"] = "0"  # production-window paths: split tables, no window tables
+    try:
+        pk = fg.generate_random_parameters(ctx, gc, circuits.toxic())
+    finally:
+        del os.environ["MI_MSM_WT_MAX_LOG"]
     return {"pk": pk, "gc": gc, "l": pk.query(1), "b_g2": pk.query(4)}
 
 
@@ -81,6 +87,7 @@ def test_msm_g2_production_windows(ctx, oracle, key17, monkeypatch, c, level2):
 def test_groth16_production_window_vs_oracle(ctx, oracle, monkeypatch, split):
     """A full prove with every MSM at c = 22 (the 2^26 window), plain and split."""
     monkeypatch.setenv("MI_MSM_C", "22")
+    monkeypatch.setenv("MI_MSM_WT_MAX_LOG", "0")
     monkeypatch.setenv("MI_MSM_SPLIT", split)
     n_in, n_aux, rws, z = circuits.random_circuit(36, 5000, n_in=6, n_free=32)
     mats = circuits.to_csr(rws)

@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--log-rows", type=int, default=26)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--query", type=int, default=0, help="0 h, 1 l, 2 a, 3 b_g1, 4 b_g2")
+    ap.add_argument("--table", type=int, default=-1, help="window-table bits (0 = library choice; -1 none)")
+    ap.add_argument("--n", type=int, default=0, help="points (default: the whole query)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -32,7 +34,12 @@ def main():
     circ = sc.load(ctx)
     pk = fg.generate_random_parameters(ctx, circ, splitmix_frs(TOXIC_SEED, 5))
     pts = pk.points(a.query)
-    n = pts.n
+    n = a.n or pts.n
+    if a.table >= 0:
+        t = time.perf_counter()
+        pts.precompute(a.table, n)
+        ctx.synchronize()
+        print(f"table {pts.table_info()} built in {1e3 * (time.perf_counter() - t):.1f} ms", flush=True)
     rng = np.random.default_rng(7)
     sw = rng.integers(0, 2**64, size=(n, 4), dtype=np.uint64)
     sw[:, 3] &= np.uint64(0x3FFFFFFFFFFFFFFF)
@@ -48,7 +55,7 @@ def main():
     st = ctx.stats()
     grp = "g2" if a.query == 4 else "g1"
     per = {k: round(st[k]["ms"] / a.reps, 2) for k in ("sort", "accum_" + grp, "msm_" + grp)}
-    print(f"{grp.upper()} MSM query={a.query} n={n}: {dt:.1f} ms wall ({n / dt / 1e3:.1f} Mpts/s); per MSM {per}", flush=True)
+    print(f"{grp.upper()} MSM query={a.query} table={pts.table_info()['window_bits']} n={n}: {dt:.1f} ms wall ({n / dt / 1e3:.1f} Mpts/s); per MSM {per}", flush=True)
 
 
 if __name__ == "__main__":
