@@ -305,7 +305,8 @@ struct MsmPlan {
                    *chunk_bucket = nullptr, *order = nullptr;
     // buckets with more than one level-0 chunk (mlist[0, m)) and the first in-place tree level over them (per-bucket
     // partial counts qcnt / offsets qoff, l1_total partials), counted before the plan's one readback
-    uint32_t m = 0, l1_total = 0;
+    uint32_t m = 0, l1_total = 0, L1 = 16;
+    uint32_t level_total[16] = {};  // partials of tree level l (msm_impl.h TREE_MAXL)
     uint32_t *mlist = nullptr, *qcnt = nullptr, *qoff = nullptr;
 };
 // false when every scalar is zero (the MSM is the identity).  split: plan the 2n half-scalar points of

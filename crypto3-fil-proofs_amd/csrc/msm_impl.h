@@ -50,7 +50,8 @@ namespace {
 #define MI_WAVES_RED MI_WAVES2  // the reduction kernels keep the two-wave cap (see g2pair.h LaneRed)
 
 constexpr uint32_t L0_DEFAULT = 64;  // sorted entries per chunk at level 0 (mixed adds); MI_MSM_L0 overrides
-constexpr uint32_t L1 = 16;  // chunk partials summed per thread per tree level (full adds)
+constexpr uint32_t L1_DEFAULT = 16;  // chunk partials summed per thread per tree level (full adds); MI_MSM_L1 overrides
+constexpr unsigned TREE_MAXL = 16;   // chunk-tree levels counted with the plan (L1 >= 4: up to 4^16 chunks a bucket)
 
 MI_HD uint32_t word_of(const fr_t &s, unsigned k) {
     uint32_t r = 0;
@@ -457,7 +458,7 @@ __global__ void k_flag_multi(const uint32_t *__restrict__ ccnt, uint32_t nb, uin
 }
 
 __global__ void k_tree_count(const uint32_t *__restrict__ mlist, const uint32_t *__restrict__ ccnt, uint32_t m,
-                             uint32_t stride, uint32_t *__restrict__ qcnt) {
+                             uint32_t stride, uint32_t L1, uint32_t *__restrict__ qcnt) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
     uint32_t n = ccnt[mlist[i]];
@@ -465,12 +466,23 @@ __global__ void k_tree_count(const uint32_t *__restrict__ mlist, const uint32_t 
     qcnt[i] = (parts + L1 - 1) / L1;
 }
 
-// the first tree level's quotas before m is known on the host: over all nb slots, zero from *m_dev on
-__global__ void k_tree_count_l1(const uint32_t *__restrict__ mlist, const uint32_t *__restrict__ ccnt,
-                                const uint32_t *__restrict__ m_dev, uint32_t nb, uint32_t *__restrict__ qcnt) {
+// the first tree level's quotas before m is known on the host: over all nb slots, zero from *m_dev on; and every
+// level's partial count, totals[l] = sum_i ceil(ceil(n_i / L1^l) / L1) (wave sums, one atomic per wave and level),
+// so the tree runs without a host round trip per level
+__global__ void __launch_bounds__(256) k_tree_count_l1(const uint32_t *__restrict__ mlist,
+                                                       const uint32_t *__restrict__ ccnt,
+                                                       const uint32_t *__restrict__ m_dev, uint32_t nb, uint32_t L1,
+                                                       uint32_t *__restrict__ qcnt, uint32_t *__restrict__ totals) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nb) return;
-    qcnt[i] = i < *m_dev ? (ccnt[mlist[i]] + L1 - 1) / L1 : 0u;
+    const uint32_t n = i < nb && i < *m_dev ? ccnt[mlist[i]] : 0u;
+    if (i < nb) qcnt[i] = (n + L1 - 1) / L1;
+    uint64_t stride = 1;
+    for (unsigned l = 0; l < TREE_MAXL; l++) {
+        uint32_t q = n ? (uint32_t)(((n + stride - 1) / stride + L1 - 1) / L1) : 0u;
+        for (int o = 32; o; o >>= 1) q += __shfl_xor(q, o);
+        if ((threadIdx.x & 63) == 0 && q) atomicAdd(&totals[l], q);
+        stride *= L1;
+    }
 }
 
 __global__ void k_tree_heads(const uint32_t *__restrict__ qcnt, const uint32_t *__restrict__ qoff, uint32_t m,
@@ -486,7 +498,7 @@ __global__ void __launch_bounds__(256) MI_WAVES_RED k_tree_level(const uint32_t 
                                                     const uint32_t *__restrict__ mlist,
                                                     const uint32_t *__restrict__ coff,
                                                     const uint32_t *__restrict__ ccnt, uint32_t total,
-                                                    uint32_t stride, XYZZ<F> *__restrict__ P) {
+                                                    uint32_t stride, uint32_t L1, XYZZ<F> *__restrict__ P) {
     using LP = LaneRed<F>;
     using R = typename LP::R;
     uint32_t u = (blockIdx.x * blockDim.x + threadIdx.x) / LP::K;
@@ -769,16 +781,17 @@ inline void sort_pairs_u32(void *tmp, size_t &bytes, const uint32_t *k_in, uint3
 // list and the first chunk-tree level's quotas -- and the readback of those counts into pin[0, PLAN_PIN); the
 // caller reads them after ITS one synchronisation (with its own bucket maxima) and plan_finish completes the plan:
 // chunk -> bucket map, length-sorted chunk order.  false when there is no entry at all.
-constexpr unsigned PLAN_PIN = 5;
+constexpr unsigned PLAN_PIN = 5 + TREE_MAXL;
 inline void plan_counts(Ctx &c, MsmPlan &pl, const uint32_t *cntA, uint32_t *offB, uint32_t *cntB, uint32_t nb,
                         uint32_t *pin) {
     hipStream_t st = c.stream;
-    static const uint32_t L0 = [] {
-        const char *e = getenv("MI_MSM_L0");
-        uint32_t v = e ? (uint32_t)atoi(e) : L0_DEFAULT;
-        return v >= 2 && v <= 1024 ? v : L0_DEFAULT;
-    }();
+    // MI_MSM_L0 / MI_MSM_L1 (read per plan; tuning): entries per level-0 chunk, partials per tree-level thread
+    const char *e0 = getenv("MI_MSM_L0"), *e1 = getenv("MI_MSM_L1");
+    uint32_t L0 = e0 ? (uint32_t)atoi(e0) : L0_DEFAULT, L1 = e1 ? (uint32_t)atoi(e1) : L1_DEFAULT;
+    if (L0 < 2 || L0 > 1024) L0 = L0_DEFAULT;
+    if (L1 < 4 || L1 > 64) L1 = L1_DEFAULT;
     pl.L0 = L0;
+    pl.L1 = L1;
     uint32_t *coff = offB, *ccnt = cntB;
     // level 0: buckets cut into chunks of <= L0 sorted entries; one mixed-add chain per chunk
     k_chunk_count<<<grid_for(nb, 256), 256, 0, st>>>(cntA, nb, L0, ccnt);
@@ -790,8 +803,9 @@ inline void plan_counts(Ctx &c, MsmPlan &pl, const uint32_t *cntA, uint32_t *off
     MI_HIP(hipMemcpyAsync(&pin[0], coff + nb - 1, 4, hipMemcpyDeviceToHost, st));
     MI_HIP(hipMemcpyAsync(&pin[1], ccnt + nb - 1, 4, hipMemcpyDeviceToHost, st));
     // buckets of several chunks, and the first in-place tree level over their partials
-    uint32_t *mlist = c.scratch[24].as<uint32_t>(3 * (uint64_t)nb + 1), *m_dev = mlist + nb;
-    uint32_t *qcnt = m_dev + 1, *qoff = qcnt + nb;
+    uint32_t *mlist = c.scratch[24].as<uint32_t>(3 * (uint64_t)nb + 1 + TREE_MAXL), *m_dev = mlist + nb;
+    uint32_t *qcnt = m_dev + 1, *qoff = qcnt + nb, *totals = qoff + nb;
+    MI_HIP(hipMemsetAsync(totals, 0, sizeof(uint32_t) * TREE_MAXL, st));
     uint8_t *flag = c.scratch[25].as<uint8_t>(nb);
     k_flag_multi<<<grid_for(nb, 256), 256, 0, st>>>(ccnt, nb, flag);
     MI_LAUNCHED(c, "k_flag_multi");
@@ -800,7 +814,7 @@ inline void plan_counts(Ctx &c, MsmPlan &pl, const uint32_t *cntA, uint32_t *off
     MI_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, ids, flag, mlist, m_dev, nb, st));
     tmp = c.scratch[4].get(tb);
     MI_HIP(hipcub::DeviceSelect::Flagged(tmp, tb, ids, flag, mlist, m_dev, nb, st));
-    k_tree_count_l1<<<grid_for(nb, 256), 256, 0, st>>>(mlist, ccnt, m_dev, nb, qcnt);
+    k_tree_count_l1<<<grid_for(nb, 256), 256, 0, st>>>(mlist, ccnt, m_dev, nb, L1, qcnt, totals);
     MI_LAUNCHED(c, "k_tree_count_l1");
     tb = 0;
     MI_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, qcnt, qoff, nb, st));
@@ -809,6 +823,7 @@ inline void plan_counts(Ctx &c, MsmPlan &pl, const uint32_t *cntA, uint32_t *off
     MI_HIP(hipMemcpyAsync(&pin[2], m_dev, 4, hipMemcpyDeviceToHost, st));
     MI_HIP(hipMemcpyAsync(&pin[3], qoff + nb - 1, 4, hipMemcpyDeviceToHost, st));
     MI_HIP(hipMemcpyAsync(&pin[4], qcnt + nb - 1, 4, hipMemcpyDeviceToHost, st));
+    MI_HIP(hipMemcpyAsync(&pin[5], totals, 4 * TREE_MAXL, hipMemcpyDeviceToHost, st));
     pl.coff = coff;
     pl.ccnt = ccnt;
     pl.mlist = mlist;
@@ -826,6 +841,7 @@ inline bool plan_finish(Ctx &c, MsmPlan &pl, const uint32_t *offA, const uint32_
     pl.total = total;
     pl.m = pin[2];
     pl.l1_total = pin[3] + pin[4];
+    for (unsigned l = 0; l < TREE_MAXL; l++) pl.level_total[l] = pin[5 + l];
     if (total == 0) return false;  // every scalar is zero
     const uint32_t *coff = pl.coff, *ccnt = pl.ccnt;
     uint32_t *heads = c.scratch[15].as<uint32_t>(total + 1);
@@ -1074,26 +1090,31 @@ XYZZ<F> *accumulate_chunks(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, co
 
     const uint32_t maxchunks = (pl.maxcnt + L0 - 1) / L0;
     if (maxchunks > 1) {  // in-place strided tree over the chunk partials of multi-chunk buckets only
-        const uint32_t m = pl.m, *mlist = pl.mlist;
-        for (uint64_t stride = 1; stride < maxchunks; stride *= L1) {
+        const uint32_t m = pl.m, *mlist = pl.mlist, L1 = pl.L1;
+        unsigned level = 0;
+        for (uint64_t stride = 1; stride < maxchunks; stride *= L1, level++) {
             // the first level's quotas were counted with the plan; deeper levels (buckets of more than L0 L1
-            // entries) are counted here, into this accumulation's own scratch: a plan serves B_G1 and B_G2 alike,
-            // so its arrays stay as they are
+            // entries) are counted here, into this accumulation's own scratch (a plan serves B_G1 and B_G2 alike,
+            // so its arrays stay as they are); every level's partial count came with the plan's readback
             uint32_t total = pl.l1_total, *qcnt = pl.qcnt, *qoff = pl.qoff;
             if (stride > 1) {
                 qcnt = c.scratch[2].as<uint32_t>(m);
                 qoff = c.scratch[11].as<uint32_t>(m);
-                k_tree_count<<<grid_for(m, 256), 256, 0, st>>>(mlist, ccnt, m, (uint32_t)stride, qcnt);
+                k_tree_count<<<grid_for(m, 256), 256, 0, st>>>(mlist, ccnt, m, (uint32_t)stride, L1, qcnt);
                 MI_LAUNCHED(c, "k_tree_count");
                 size_t tb = 0;
                 MI_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, qcnt, qoff, m, st));
                 void *tmp = c.scratch[4].get(tb);
                 MI_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, qcnt, qoff, m, st));
-                uint32_t *tail = c.pin.as<uint32_t>(2);
-                MI_HIP(hipMemcpyAsync(&tail[0], qoff + m - 1, 4, hipMemcpyDeviceToHost, st));
-                MI_HIP(hipMemcpyAsync(&tail[1], qcnt + m - 1, 4, hipMemcpyDeviceToHost, st));
-                MI_HIP(hipStreamSynchronize(st));
-                total = tail[0] + tail[1];
+                if (level < TREE_MAXL) {
+                    total = pl.level_total[level];
+                } else {  // beyond the counted levels (L1 = 4 and > 4^16 chunks in one bucket): read it back
+                    uint32_t *tail = c.pin.as<uint32_t>(2);
+                    MI_HIP(hipMemcpyAsync(&tail[0], qoff + m - 1, 4, hipMemcpyDeviceToHost, st));
+                    MI_HIP(hipMemcpyAsync(&tail[1], qcnt + m - 1, 4, hipMemcpyDeviceToHost, st));
+                    MI_HIP(hipStreamSynchronize(st));
+                    total = tail[0] + tail[1];
+                }
             }
             uint32_t *heads = c.scratch[15].as<uint32_t>(total + 1), *map = c.scratch[13].as<uint32_t>(total + 1);
             MI_HIP(hipMemsetAsync(heads, 0, sizeof(uint32_t) * (total + 1), st));
@@ -1104,7 +1125,7 @@ XYZZ<F> *accumulate_chunks(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, co
             void *tmp = c.scratch[4].get(tb);
             MI_HIP(hipcub::DeviceScan::InclusiveScan(tmp, tb, heads, map, MaxOp(), total, st));
             k_tree_level<F><<<grid_for((uint64_t)total * KR, 256), 256, 0, st>>>(map, qoff, mlist, coff, ccnt, total,
-                                                                   (uint32_t)stride, P0);
+                                                                   (uint32_t)stride, L1, P0);
             MI_LAUNCHED(c, "k_tree_level");
         }
     }

@@ -9,8 +9,9 @@ reference's partition size.
   GPU, challenges by generate_leaf_challenge) yields witnesses the device check accepts, equal to the
   oracle's synthesis over the same openings.
 * One 32 GiB Window PoSt partition (2349 sectors x 10 challenges over 2^30-node 8-8-0 trees: 125,279,217
-  constraints, constants.hpp:85-89; BASELINE config 5's partition): the witness satisfies every row on the
-  device; the partition proves and pairing-verifies.
+  constraints, constants.hpp:85-89; BASELINE config 5's partition) and one 64 GiB partition (2300 x 10 over
+  2^31-node 8-8-2 trees: 129,887,900 constraints): the witness satisfies every row on the device; the partition
+  proves and pairing-verifies.
 Variable order beyond the reference's counts is parity-unpinned (oracle header).
 """
 import numpy as np
@@ -117,6 +118,59 @@ def test_post_32gib_window_partition_prove_verify(ctx):
     proof = fg.prove(ctx, pk, gc, z.data_ptr())
     note("proof")
     assert fg.verify(vk, ic, pub, proof)
+    del pk, gc, z
+    torch.cuda.synchronize()
+
+
+def test_post_64gib_window_partition_prove_verify(ctx):
+    """The 64 GiB Window-PoSt partition (constants.hpp:85-89: 2300 sectors x 10 challenges over 2^31-node 8-8-2
+    trees R-last, 129,887,900 constraints, domain 2^27): synthetic partition, witness satisfied on the device, key
+    generated, proof pairing-verified.  The memory fallbacks of keygen and prove (out-of-memory releases and
+    retries, mi_ctx_get_fallbacks) and the key's table state are printed for the record."""
+    import json
+    import time
+
+    import circuits
+
+    t0 = time.perf_counter()
+
+    def note(what):
+        print(f"[window-post-64] {what}: {time.perf_counter() - t0:.1f} s", flush=True)
+
+    c = stacked.FallbackPoStCircuit(2300, 10, 1 << 31, 8, 8, 2)
+    assert c.num_constraints == 129_887_900
+    note(f"R1CS built ({c.info['r1cs_entries']} entries, {c.num_inputs} inputs)")
+    _, sectors = stacked.synthetic_post_instance(ctx, c, seed=64)
+    slots = stacked.post_slots(c, sectors)
+    note("synthetic partition")
+    gc = c.load(ctx)
+    assert gc.d == 1 << 27
+    sd = torch.from_numpy(np.frombuffer(slots, dtype=np.uint8).copy()).cuda()
+    z = torch.empty(32 * c.num_vars, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    c.witness_dev(ctx, sd.data_ptr(), z.data_ptr())
+    note("witness")
+    assert stacked.circuit_check_dev(ctx, gc, z.data_ptr()) == (0, None)
+    note("R1CS check")
+    pub = c.public_inputs(slots)
+    assert z[32:32 * c.num_inputs].cpu().numpy().tobytes() == pub
+    ctx.reset_stats()
+    pk = fg.generate_random_parameters(ctx, gc, circuits.toxic())
+    keygen_fb = ctx.fallbacks()
+    note(f"keygen (fallbacks {keygen_fb}, tables {pk.table_state()})")
+    vk, ic = pk.verifying_key()
+    ctx.reset_stats()
+    t1 = time.perf_counter()
+    proof = fg.prove(ctx, pk, gc, z.data_ptr())
+    dt = time.perf_counter() - t1
+    prove_fb = ctx.fallbacks()
+    note(f"proof {1e3 * dt:.0f} ms (fallbacks {prove_fb})")
+    assert fg.verify(vk, ic, pub, proof)
+    free_b, total_b = torch.cuda.mem_get_info()
+    print("[window-post-64] record " + json.dumps({
+        "constraints": c.num_constraints, "inputs": c.num_inputs, "domain": gc.d, "prove_ms": 1e3 * dt,
+        "keygen_fallbacks": keygen_fb, "prove_fallbacks": prove_fb, "table_state": pk.table_state(),
+        "device_free_gb": free_b / 1e9, "device_total_gb": total_b / 1e9, "verified": True}), flush=True)
     del pk, gc, z
     torch.cuda.synchronize()
 
