@@ -241,6 +241,11 @@ struct CtxLock {
     std::lock_guard<std::recursive_mutex> lk;
     DeviceScope dev;
     CtxLock(mi_ctx *c, int priority = 0, int fence = NO_FENCE) : ctx(c), lk(c->c.mu), dev(c->c.device) {
+        if (priority && !c->high) {  // created at first use: every stream a process creates takes a hardware queue
+            int lo = 0, hi = 0;     // (GPU_MAX_HW_QUEUES, 4 by default) or shares one with another stream
+            MI_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            MI_HIP(hipStreamCreateWithPriority(&c->high, hipStreamNonBlocking, hi));
+        }
         c->c.stream = priority ? c->high : c->normal;
         if (fence == FENCE) caller_fence(c);
     }
@@ -417,11 +422,8 @@ int mi_ctx_create(int device, mi_ctx **out) {
         mi_ctx *c = new mi_ctx();
         try {
             c->c.device = device;
-            int lo = 0, hi = 0;
-            MI_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
             MI_HIP(hipStreamCreateWithFlags(&c->normal, hipStreamNonBlocking));
-            MI_HIP(hipStreamCreateWithPriority(&c->high, hipStreamNonBlocking, hi));
-            c->c.stream = c->normal;
+            c->c.stream = c->normal;  // the high-priority stream is created at its first use (CtxLock)
             mi::ntt_init_tables(c->c);
         } catch (...) {
             if (c->normal) hipStreamDestroy(c->normal);
@@ -471,7 +473,7 @@ int mi_ctx_synchronize(mi_ctx *ctx) {
         need(ctx != nullptr, "null ctx");
         CtxLock l(ctx);
         MI_HIP(hipStreamSynchronize(ctx->normal));
-        MI_HIP(hipStreamSynchronize(ctx->high));
+        if (ctx->high) MI_HIP(hipStreamSynchronize(ctx->high));
         ctx->c.timer.resolve();
     });
 }
@@ -1411,7 +1413,7 @@ int mi_ctx_get_stats(mi_ctx *ctx, double out[39]) {
         need(ctx && out, "null argument");
         CtxLock l(ctx);
         MI_HIP(hipStreamSynchronize(ctx->normal));
-        MI_HIP(hipStreamSynchronize(ctx->high));
+        if (ctx->high) MI_HIP(hipStreamSynchronize(ctx->high));
         ctx->c.timer.resolve();
         const mi::Stats &s = ctx->c.stats;
         const mi::KStat *ks[mi::Stats::NK] = {&s.accum_g1, &s.accum_g2, &s.msm_g1, &s.msm_g2, &s.sort,
@@ -1429,7 +1431,7 @@ int mi_ctx_reset_stats(mi_ctx *ctx) {
         need(ctx != nullptr, "null ctx");
         CtxLock l(ctx);
         MI_HIP(hipStreamSynchronize(ctx->normal));
-        MI_HIP(hipStreamSynchronize(ctx->high));
+        if (ctx->high) MI_HIP(hipStreamSynchronize(ctx->high));
         if (ctx->up.copy) MI_HIP(hipStreamSynchronize(ctx->up.copy));
         ctx->c.timer.resolve();
         ctx->c.stats = mi::Stats();

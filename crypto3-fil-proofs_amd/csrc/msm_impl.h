@@ -346,6 +346,25 @@ __global__ void k_bounds4(const uint32_t *__restrict__ keys, uint32_t np, uint32
     }
 }
 
+// last index i < n with a[i] <= x (a non-decreasing, a[0] <= x): the owner of slot x of an exclusive scan
+MI_HD uint32_t owner_of(const uint32_t *__restrict__ a, uint32_t n, uint32_t x) {
+    uint32_t lo = 0, hi = n;  // a[lo] <= x < a[hi] (a[n] = infinity)
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a[mid] <= x) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// one launch for a plan's bucket arrays: start = cnt = 0 over nb buckets, zstart = ~0 over nz windows
+__global__ void k_plan_init(uint32_t *__restrict__ start, uint32_t *__restrict__ cnt, uint32_t nb,
+                            uint32_t *__restrict__ zstart, uint32_t nz) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < nb) start[b] = cnt[b] = 0;
+    if (b < nz) zstart[b] = 0xffffffffu;
+}
+
 __global__ void k_end_to_cnt(const uint32_t *__restrict__ start, uint32_t *__restrict__ cnt, uint32_t nb) {
     uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nb) return;
@@ -353,18 +372,15 @@ __global__ void k_end_to_cnt(const uint32_t *__restrict__ start, uint32_t *__res
     cnt[b] = e ? e - start[b] : 0;
 }
 
-__global__ void k_chunk_count(const uint32_t *__restrict__ cnt, uint32_t nb, uint32_t L, uint32_t *__restrict__ ccnt) {
+// chunk counts; also zeroes the plan's per-level tree totals (k_tree_count_l1 adds into them later)
+__global__ void k_chunk_count(const uint32_t *__restrict__ cnt, uint32_t nb, uint32_t L, uint32_t *__restrict__ ccnt,
+                              uint32_t *__restrict__ totals, uint32_t ntot) {
     uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < ntot) totals[b] = 0;
     if (b >= nb) return;
     ccnt[b] = (cnt[b] + L - 1) / L;
 }
 
-__global__ void k_chunk_heads(const uint32_t *__restrict__ ccnt, const uint32_t *__restrict__ coff, uint32_t nb,
-                              uint32_t *__restrict__ chunk_bucket) {
-    uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= nb) return;
-    if (ccnt[b]) chunk_bucket[coff[b]] = b;
-}
 
 struct MaxOp {
     __device__ __host__ uint32_t operator()(uint32_t a, uint32_t b) const { return a > b ? a : b; }
@@ -373,12 +389,13 @@ struct MaxOp {
 // Level-0 chunk lengths, keyed so a radix sort puts equal lengths next to each other: a wave then
 // runs chunks of (nearly) one length instead of "full chunks + remainders" (~69% lane use for
 // Poisson(32) buckets).  key = L0 - len (full chunks first).
-__global__ void k_chunk_len_keys(const uint32_t *__restrict__ chunk_bucket, const uint32_t *__restrict__ coff,
-                                 const uint32_t *__restrict__ cnt, uint32_t total, uint32_t L0,
+__global__ void k_chunk_len_keys(const uint32_t *__restrict__ coff, const uint32_t *__restrict__ cnt, uint32_t nb,
+                                 uint32_t total, uint32_t L0, uint32_t *__restrict__ chunk_bucket,
                                  uint32_t *__restrict__ keys, uint32_t *__restrict__ ids) {
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= total) return;
-    uint32_t b = chunk_bucket[t];
+    const uint32_t b = owner_of(coff, nb, t);  // the bucket whose chunks start at or before t
+    chunk_bucket[t] = b;
     uint32_t local = t - coff[b];
     uint32_t rest = cnt[b] - local * L0;
     keys[t] = L0 - (rest < L0 ? rest : L0);
@@ -467,34 +484,47 @@ __global__ void k_tree_count(const uint32_t *__restrict__ mlist, const uint32_t 
 }
 
 // the first tree level's quotas before m is known on the host: over all nb slots, zero from *m_dev on; and every
-// level's partial count, totals[l] = sum_i ceil(ceil(n_i / L1^l) / L1) (wave sums, one atomic per wave and level),
-// so the tree runs without a host round trip per level
+// level's partial count, totals[l] = sum_i ceil(ceil(n_i / L1^l) / L1) for the levels the largest bucket needs
+// (stride L1^l below ceil(*maxcnt / L0); wave sums, one atomic per wave and level), so the tree runs without a host
+// round trip per level.  L1 is a power of two (shifts, no division).
 __global__ void __launch_bounds__(256) k_tree_count_l1(const uint32_t *__restrict__ mlist,
                                                        const uint32_t *__restrict__ ccnt,
-                                                       const uint32_t *__restrict__ m_dev, uint32_t nb, uint32_t L1,
-                                                       uint32_t *__restrict__ qcnt, uint32_t *__restrict__ totals) {
+                                                       const uint32_t *__restrict__ m_dev,
+                                                       const uint32_t *__restrict__ maxcnt, uint32_t L0, uint32_t nb,
+                                                       unsigned lg1, uint32_t *__restrict__ qcnt,
+                                                       uint32_t *__restrict__ totals) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n = i < nb && i < *m_dev ? ccnt[mlist[i]] : 0u;
-    if (i < nb) qcnt[i] = (n + L1 - 1) / L1;
-    uint64_t stride = 1;
-    for (unsigned l = 0; l < TREE_MAXL; l++) {
-        uint32_t q = n ? (uint32_t)(((n + stride - 1) / stride + L1 - 1) / L1) : 0u;
+    const uint32_t mask1 = (1u << lg1) - 1;
+    if (i < nb) qcnt[i] = (n + mask1) >> lg1;
+    const uint32_t maxchunks = (*maxcnt + L0 - 1) / L0;
+    unsigned s = 0;  // stride = 2^s
+    for (unsigned l = 0; l < TREE_MAXL && s < 32 && (1u << s) < maxchunks; l++, s += lg1) {
+        const uint32_t parts = n ? ((n - 1) >> s) + 1 : 0u;
+        uint32_t q = (parts + mask1) >> lg1;
         for (int o = 32; o; o >>= 1) q += __shfl_xor(q, o);
         if ((threadIdx.x & 63) == 0 && q) atomicAdd(&totals[l], q);
-        stride *= L1;
     }
 }
 
-__global__ void k_tree_heads(const uint32_t *__restrict__ qcnt, const uint32_t *__restrict__ qoff, uint32_t m,
-                             uint32_t *__restrict__ heads) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
-    if (qcnt[i]) heads[qoff[i]] = i;
+
+// the plan's counts into one staging block (one readback): chunk total (coff / ccnt tails), m, the first tree level's
+// total (qoff / qcnt tails), every level's total
+__global__ void k_plan_gather(const uint32_t *__restrict__ coff, const uint32_t *__restrict__ ccnt, uint32_t nb,
+                              const uint32_t *__restrict__ m_dev, const uint32_t *__restrict__ qoff,
+                              const uint32_t *__restrict__ qcnt, const uint32_t *__restrict__ totals,
+                              uint32_t *__restrict__ stage) {
+    const uint32_t t = threadIdx.x;
+    if (t == 0) stage[0] = coff[nb - 1];
+    if (t == 1) stage[1] = ccnt[nb - 1];
+    if (t == 2) stage[2] = *m_dev;
+    if (t == 3) stage[3] = qoff[nb - 1];
+    if (t == 4) stage[4] = qcnt[nb - 1];
+    if (t >= 5 && t < 5 + TREE_MAXL) stage[t] = totals[t - 5];
 }
 
 template <class F>
-__global__ void __launch_bounds__(256) MI_WAVES_RED k_tree_level(const uint32_t *__restrict__ map,
-                                                    const uint32_t *__restrict__ qoff,
+__global__ void __launch_bounds__(256) MI_WAVES_RED k_tree_level(const uint32_t *__restrict__ qoff, uint32_t m,
                                                     const uint32_t *__restrict__ mlist,
                                                     const uint32_t *__restrict__ coff,
                                                     const uint32_t *__restrict__ ccnt, uint32_t total,
@@ -503,7 +533,7 @@ __global__ void __launch_bounds__(256) MI_WAVES_RED k_tree_level(const uint32_t 
     using R = typename LP::R;
     uint32_t u = (blockIdx.x * blockDim.x + threadIdx.x) / LP::K;
     if (u >= total) return;
-    uint32_t i = map[u];
+    uint32_t i = owner_of(qoff, m, u);  // the multi-chunk bucket this partial belongs to
     uint32_t b = mlist[i];
     uint32_t q = u - qoff[i];
     uint32_t n = ccnt[b];
@@ -783,29 +813,29 @@ inline void sort_pairs_u32(void *tmp, size_t &bytes, const uint32_t *k_in, uint3
 // chunk -> bucket map, length-sorted chunk order.  false when there is no entry at all.
 constexpr unsigned PLAN_PIN = 5 + TREE_MAXL;
 inline void plan_counts(Ctx &c, MsmPlan &pl, const uint32_t *cntA, uint32_t *offB, uint32_t *cntB, uint32_t nb,
-                        uint32_t *pin) {
+                        const uint32_t *maxcnt_dev, uint32_t *stage) {
     hipStream_t st = c.stream;
-    // MI_MSM_L0 / MI_MSM_L1 (read per plan; tuning): entries per level-0 chunk, partials per tree-level thread
+    // MI_MSM_L0 / MI_MSM_L1 (read per plan; tuning): entries per level-0 chunk, partials per tree-level thread (a
+    // power of two)
     const char *e0 = getenv("MI_MSM_L0"), *e1 = getenv("MI_MSM_L1");
     uint32_t L0 = e0 ? (uint32_t)atoi(e0) : L0_DEFAULT, L1 = e1 ? (uint32_t)atoi(e1) : L1_DEFAULT;
     if (L0 < 2 || L0 > 1024) L0 = L0_DEFAULT;
-    if (L1 < 4 || L1 > 64) L1 = L1_DEFAULT;
+    if (L1 < 4 || L1 > 64 || (L1 & (L1 - 1))) L1 = L1_DEFAULT;
+    unsigned lg1 = 0;
+    while ((1u << lg1) < L1) lg1++;
     pl.L0 = L0;
     pl.L1 = L1;
     uint32_t *coff = offB, *ccnt = cntB;
+    uint32_t *mlist = c.scratch[24].as<uint32_t>(3 * (uint64_t)nb + 1 + TREE_MAXL), *m_dev = mlist + nb;
+    uint32_t *qcnt = m_dev + 1, *qoff = qcnt + nb, *totals = qoff + nb;
     // level 0: buckets cut into chunks of <= L0 sorted entries; one mixed-add chain per chunk
-    k_chunk_count<<<grid_for(nb, 256), 256, 0, st>>>(cntA, nb, L0, ccnt);
+    k_chunk_count<<<grid_for(nb > TREE_MAXL ? nb : TREE_MAXL, 256), 256, 0, st>>>(cntA, nb, L0, ccnt, totals, TREE_MAXL);
     MI_LAUNCHED(c, "k_chunk_count");
     size_t tmp_bytes = 0;
     MI_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, ccnt, coff, nb, st));
     void *tmp = c.scratch[4].get(tmp_bytes);
     MI_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, ccnt, coff, nb, st));
-    MI_HIP(hipMemcpyAsync(&pin[0], coff + nb - 1, 4, hipMemcpyDeviceToHost, st));
-    MI_HIP(hipMemcpyAsync(&pin[1], ccnt + nb - 1, 4, hipMemcpyDeviceToHost, st));
     // buckets of several chunks, and the first in-place tree level over their partials
-    uint32_t *mlist = c.scratch[24].as<uint32_t>(3 * (uint64_t)nb + 1 + TREE_MAXL), *m_dev = mlist + nb;
-    uint32_t *qcnt = m_dev + 1, *qoff = qcnt + nb, *totals = qoff + nb;
-    MI_HIP(hipMemsetAsync(totals, 0, sizeof(uint32_t) * TREE_MAXL, st));
     uint8_t *flag = c.scratch[25].as<uint8_t>(nb);
     k_flag_multi<<<grid_for(nb, 256), 256, 0, st>>>(ccnt, nb, flag);
     MI_LAUNCHED(c, "k_flag_multi");
@@ -814,16 +844,14 @@ inline void plan_counts(Ctx &c, MsmPlan &pl, const uint32_t *cntA, uint32_t *off
     MI_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, ids, flag, mlist, m_dev, nb, st));
     tmp = c.scratch[4].get(tb);
     MI_HIP(hipcub::DeviceSelect::Flagged(tmp, tb, ids, flag, mlist, m_dev, nb, st));
-    k_tree_count_l1<<<grid_for(nb, 256), 256, 0, st>>>(mlist, ccnt, m_dev, nb, L1, qcnt, totals);
+    k_tree_count_l1<<<grid_for(nb, 256), 256, 0, st>>>(mlist, ccnt, m_dev, maxcnt_dev, L0, nb, lg1, qcnt, totals);
     MI_LAUNCHED(c, "k_tree_count_l1");
     tb = 0;
     MI_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, qcnt, qoff, nb, st));
     tmp = c.scratch[4].get(tb);
     MI_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, qcnt, qoff, nb, st));
-    MI_HIP(hipMemcpyAsync(&pin[2], m_dev, 4, hipMemcpyDeviceToHost, st));
-    MI_HIP(hipMemcpyAsync(&pin[3], qoff + nb - 1, 4, hipMemcpyDeviceToHost, st));
-    MI_HIP(hipMemcpyAsync(&pin[4], qcnt + nb - 1, 4, hipMemcpyDeviceToHost, st));
-    MI_HIP(hipMemcpyAsync(&pin[5], totals, 4 * TREE_MAXL, hipMemcpyDeviceToHost, st));
+    k_plan_gather<<<1, 64, 0, st>>>(coff, ccnt, nb, m_dev, qoff, qcnt, totals, stage);
+    MI_LAUNCHED(c, "k_plan_gather");
     pl.coff = coff;
     pl.ccnt = ccnt;
     pl.mlist = mlist;
@@ -843,20 +871,13 @@ inline bool plan_finish(Ctx &c, MsmPlan &pl, const uint32_t *offA, const uint32_
     pl.l1_total = pin[3] + pin[4];
     for (unsigned l = 0; l < TREE_MAXL; l++) pl.level_total[l] = pin[5 + l];
     if (total == 0) return false;  // every scalar is zero
-    const uint32_t *coff = pl.coff, *ccnt = pl.ccnt;
-    uint32_t *heads = c.scratch[15].as<uint32_t>(total + 1);
+    const uint32_t *coff = pl.coff;
     uint32_t *chunk_bucket = c.scratch[17].as<uint32_t>(total + 1);
-    MI_HIP(hipMemsetAsync(heads, 0, sizeof(uint32_t) * (total + 1), st));
-    k_chunk_heads<<<grid_for(nb, 256), 256, 0, st>>>(ccnt, coff, nb, heads);
-    MI_LAUNCHED(c, "k_chunk_heads");
-    size_t tmp_bytes = 0;
-    MI_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tmp_bytes, heads, chunk_bucket, MaxOp(), total, st));
-    void *tmp = c.scratch[4].get(tmp_bytes);
-    MI_HIP(hipcub::DeviceScan::InclusiveScan(tmp, tmp_bytes, heads, chunk_bucket, MaxOp(), total, st));
-    // length-sorted chunk order (keys/vals scratch of the main sort are free by now)
+    // chunk -> bucket (binary search over the chunk offsets) and the length-sorted chunk order (keys/vals scratch of
+    // the main sort are free by now)
     uint32_t *lkeys = c.scratch[0].as<uint32_t>(total), *lids = c.scratch[1].as<uint32_t>(total);
     uint32_t *lkeys_s = c.scratch[2].as<uint32_t>(total), *order = c.scratch[16].as<uint32_t>(total);
-    k_chunk_len_keys<<<grid_for(total, 256), 256, 0, st>>>(chunk_bucket, coff, cntA, total, L0, lkeys, lids);
+    k_chunk_len_keys<<<grid_for(total, 256), 256, 0, st>>>(coff, cntA, nb, total, L0, chunk_bucket, lkeys, lids);
     MI_LAUNCHED(c, "k_chunk_len_keys");
     size_t tb = 0;
     sort_pairs_u32(nullptr, tb, lkeys, lkeys_s, lids, order, total, len_bits, st);
@@ -922,7 +943,8 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
     uint32_t *cntA = c.scratch[6].as<uint32_t>(nb);
     uint32_t *offB = c.scratch[7].as<uint32_t>(nb);
     uint32_t *cntB = c.scratch[8].as<uint32_t>(nb);
-    uint32_t *dmax = c.scratch[9].as<uint32_t>(4 + 2 * nwin);  // [max bucket size, pad, zstart[nwin], wcount[nwin]]
+    // [max bucket size, pad x 3, zstart[nwin], wcount[nwin], the plan's counts (PLAN_PIN)]: one readback
+    uint32_t *dmax = c.scratch[9].as<uint32_t>(4 + 2 * nwin + PLAN_PIN);
     uint32_t *zstart = dmax + 4, *wcount = zstart + nwin;
     const bool compact = !one_sort && nwin <= MAXW_C;  // large MSMs: only non-zero digits are sorted
     if (split && !compact) throw std::logic_error("msm: split mode needs the compacted digit path");
@@ -975,9 +997,8 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
                 }
             }
         }
-        MI_HIP(hipMemsetAsync(offA, 0, sizeof(uint32_t) * nb, st));
-        MI_HIP(hipMemsetAsync(cntA, 0, sizeof(uint32_t) * nb, st));
-        MI_HIP(hipMemsetAsync(zstart, 0xff, sizeof(uint32_t) * nwin, st));
+        k_plan_init<<<grid_for(nb > nwin ? nb : nwin, 256), 256, 0, st>>>(offA, cntA, nb, zstart, nwin);
+        MI_LAUNCHED(c, "k_plan_init");
         const uint32_t nq = (np + 3) / 4;
         k_bounds4<<<grid_for(nq, 256), 256, 0, st>>>(keys_s, np, (uint32_t)n, nbk, wk, compact ? wcount : nullptr,
                                                       offA, cntA, zstart);
@@ -988,14 +1009,15 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
 
     // largest bucket (the number of chunk-tree levels), each window's zero-digit start and the plan's counts: one
     // readback
-    uint32_t *pin = c.pin.as<uint32_t>(4 + nwin + PLAN_PIN);
+    const unsigned H = 4 + 2 * nwin;
+    uint32_t *pin = c.pin.as<uint32_t>(H + PLAN_PIN);
     {
         size_t tmp_bytes = 0;
         MI_HIP(hipcub::DeviceReduce::Max(nullptr, tmp_bytes, cntA, dmax, nb, st));
         void *tmp = c.scratch[4].get(tmp_bytes);
         MI_HIP(hipcub::DeviceReduce::Max(tmp, tmp_bytes, cntA, dmax, nb, st));
-        MI_HIP(hipMemcpyAsync(pin, dmax, sizeof(uint32_t) * (4 + nwin), hipMemcpyDeviceToHost, st));
-        plan_counts(c, pl, cntA, offB, cntB, nb, pin + 4 + nwin);
+        plan_counts(c, pl, cntA, offB, cntB, nb, dmax, dmax + H);
+        MI_HIP(hipMemcpyAsync(pin, dmax, sizeof(uint32_t) * (H + PLAN_PIN), hipMemcpyDeviceToHost, st));
         MI_HIP(hipStreamSynchronize(st));
     }
     pl.maxcnt = pin[0];
@@ -1003,7 +1025,7 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
     for (unsigned w = 0; w < nwin; w++)
         pl.entries += compact ? wn[w] : pin[4 + w] == 0xffffffffu ? n : pin[4 + w] - (uint64_t)w * n;
 
-    return plan_finish(c, pl, offA, cntA, nb, vals_s, pin + 4 + nwin);
+    return plan_finish(c, pl, offA, cntA, nb, vals_s, pin + H);
 }
 
 // MI_MSM_BITSUM=0 sends one-window plans through reduce_windows (A/B); read per call
@@ -1033,7 +1055,7 @@ inline bool msm_prepare_wt_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx
     uint32_t *keys_s = c.scratch[2].as<uint32_t>(np), *vals_s = c.scratch[3].as<uint32_t>(np);
     uint32_t *offA = c.scratch[5].as<uint32_t>(nbk), *cntA = c.scratch[6].as<uint32_t>(nbk);
     uint32_t *offB = c.scratch[7].as<uint32_t>(nbk), *cntB = c.scratch[8].as<uint32_t>(nbk);
-    uint32_t *dmax = c.scratch[9].as<uint32_t>(8), *zstart = dmax + 4;
+    uint32_t *dmax = c.scratch[9].as<uint32_t>(8 + PLAN_PIN), *zstart = dmax + 4;  // [max, pad x 3, zstart, pad x 3, counts]
     {
         ScopedTimer tsort(c, &c.stats.sort, nscal);
         k_digits_wt<<<grid_for(nscal, 256), 256, 0, st>>>(scalars, idx, (uint32_t)nscal, cb, nwin, (uint32_t)stride,
@@ -1043,9 +1065,8 @@ inline bool msm_prepare_wt_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx
         sort_pairs_u32(nullptr, tmp_bytes, keys, keys_s, vals, vals_s, np, cb, st);
         void *tmp = c.scratch[4].get(tmp_bytes);
         sort_pairs_u32(tmp, tmp_bytes, keys, keys_s, vals, vals_s, np, cb, st);
-        MI_HIP(hipMemsetAsync(offA, 0, sizeof(uint32_t) * nbk, st));
-        MI_HIP(hipMemsetAsync(cntA, 0, sizeof(uint32_t) * nbk, st));
-        MI_HIP(hipMemsetAsync(zstart, 0xff, sizeof(uint32_t), st));
+        k_plan_init<<<grid_for(nbk, 256), 256, 0, st>>>(offA, cntA, nbk, zstart, 1);
+        MI_LAUNCHED(c, "k_plan_init");
         k_bounds4<<<grid_for((np + 3) / 4, 256), 256, 0, st>>>(keys_s, np, np, nbk, 0, nullptr, offA, cntA, zstart);
         MI_LAUNCHED(c, "k_bounds4");
         k_end_to_cnt<<<grid_for(nbk, 256), 256, 0, st>>>(offA, cntA, nbk);
@@ -1055,13 +1076,13 @@ inline bool msm_prepare_wt_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx
         tmp = c.scratch[4].get(tb);
         MI_HIP(hipcub::DeviceReduce::Max(tmp, tb, cntA, dmax, nbk, st));
     }
-    uint32_t *pin = c.pin.as<uint32_t>(5 + PLAN_PIN);  // one readback: bucket maximum, zero-digit start, plan counts
-    MI_HIP(hipMemcpyAsync(pin, dmax, sizeof(uint32_t) * 5, hipMemcpyDeviceToHost, st));
-    plan_counts(c, pl, cntA, offB, cntB, nbk, pin + 5);
+    uint32_t *pin = c.pin.as<uint32_t>(8 + PLAN_PIN);  // one readback: bucket maximum, zero-digit start, plan counts
+    plan_counts(c, pl, cntA, offB, cntB, nbk, dmax, dmax + 8);
+    MI_HIP(hipMemcpyAsync(pin, dmax, sizeof(uint32_t) * (8 + PLAN_PIN), hipMemcpyDeviceToHost, st));
     MI_HIP(hipStreamSynchronize(st));
     pl.maxcnt = pin[0];
     pl.entries = pin[4] == 0xffffffffu ? np : pin[4];
-    return plan_finish(c, pl, offA, cntA, nbk, vals_s, pin + 5);
+    return plan_finish(c, pl, offA, cntA, nbk, vals_s, pin + 8);
 }
 
 // ---- phase 2 (per base set): accumulation, chunk tree, bucket reduction, window combination ----
@@ -1116,15 +1137,7 @@ XYZZ<F> *accumulate_chunks(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, co
                     total = tail[0] + tail[1];
                 }
             }
-            uint32_t *heads = c.scratch[15].as<uint32_t>(total + 1), *map = c.scratch[13].as<uint32_t>(total + 1);
-            MI_HIP(hipMemsetAsync(heads, 0, sizeof(uint32_t) * (total + 1), st));
-            k_tree_heads<<<grid_for(m, 256), 256, 0, st>>>(qcnt, qoff, m, heads);
-            MI_LAUNCHED(c, "k_tree_heads");
-            size_t tb = 0;
-            MI_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, heads, map, MaxOp(), total, st));
-            void *tmp = c.scratch[4].get(tb);
-            MI_HIP(hipcub::DeviceScan::InclusiveScan(tmp, tb, heads, map, MaxOp(), total, st));
-            k_tree_level<F><<<grid_for((uint64_t)total * KR, 256), 256, 0, st>>>(map, qoff, mlist, coff, ccnt, total,
+            k_tree_level<F><<<grid_for((uint64_t)total * KR, 256), 256, 0, st>>>(qoff, m, mlist, coff, ccnt, total,
                                                                    (uint32_t)stride, L1, P0);
             MI_LAUNCHED(c, "k_tree_level");
         }
@@ -1321,14 +1334,14 @@ bool g2_second_level(Ctx &c, const MsmPlan &pl, XYZZ<F> *P0, std::vector<XYZZ<F>
         sort_pairs_u32(tmp, tmp_bytes, keys, keys_s, vals, vals_s, np2, bits, st);
         // 3. buckets of the second level
         uint32_t *off2 = c.scratch[5].as<uint32_t>(nb2), *cnt2 = c.scratch[6].as<uint32_t>(nb2);
-        MI_HIP(hipMemsetAsync(off2, 0, sizeof(uint32_t) * nb2, st));
-        MI_HIP(hipMemsetAsync(cnt2, 0, sizeof(uint32_t) * nb2, st));
+        k_plan_init<<<grid_for(nb2, 256), 256, 0, st>>>(off2, cnt2, nb2, nullptr, 0);
+        MI_LAUNCHED(c, "k_plan_init");
         k_bounds_flat<<<grid_for(np2, 256), 256, 0, st>>>(keys_s, np2, invalid2, off2, cnt2);
         MI_LAUNCHED(c, "k_bounds_flat");
         k_end_to_cnt<<<grid_for(nb2, 256), 256, 0, st>>>(off2, cnt2, nb2);
         MI_LAUNCHED(c, "k_end_to_cnt");
-        uint32_t *dm = c.scratch[9].as<uint32_t>(4);
-        uint32_t *head = c.pin.as<uint32_t>(2 + PLAN_PIN);
+        uint32_t *dm = c.scratch[9].as<uint32_t>(4 + PLAN_PIN);  // [max, sum, pad x 2, the plan's counts]
+        uint32_t *head = c.pin.as<uint32_t>(4 + PLAN_PIN);
         tmp_bytes = 0;
         MI_HIP(hipcub::DeviceReduce::Max(nullptr, tmp_bytes, cnt2, dm, nb2, st));
         size_t tb2 = 0;
@@ -1336,9 +1349,9 @@ bool g2_second_level(Ctx &c, const MsmPlan &pl, XYZZ<F> *P0, std::vector<XYZZ<F>
         tmp = c.scratch[4].get(tmp_bytes > tb2 ? tmp_bytes : tb2);
         MI_HIP(hipcub::DeviceReduce::Max(tmp, tmp_bytes, cnt2, dm, nb2, st));
         MI_HIP(hipcub::DeviceReduce::Sum(tmp, tb2, cnt2, dm + 1, nb2, st));
-        MI_HIP(hipMemcpyAsync(head, dm, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         MsmPlan p2;
-        plan_counts(c, p2, cnt2, c.scratch[7].as<uint32_t>(nb2), c.scratch[8].as<uint32_t>(nb2), nb2, head + 2);
+        plan_counts(c, p2, cnt2, c.scratch[7].as<uint32_t>(nb2), c.scratch[8].as<uint32_t>(nb2), nb2, dm, dm + 4);
+        MI_HIP(hipMemcpyAsync(head, dm, sizeof(uint32_t) * (4 + PLAN_PIN), hipMemcpyDeviceToHost, st));
         MI_HIP(hipStreamSynchronize(st));
         p2.n = head[1];
         p2.cb = c2;
@@ -1348,7 +1361,7 @@ bool g2_second_level(Ctx &c, const MsmPlan &pl, XYZZ<F> *P0, std::vector<XYZZ<F>
         p2.maxcnt = head[0];
         p2.entries = head[1];
         W.assign(nwin, XYZZ<F>::inf());
-        if (!plan_finish(c, p2, off2, cnt2, nb2, vals_s, head + 2)) return true;  // every bucket empty
+        if (!plan_finish(c, p2, off2, cnt2, nb2, vals_s, head + 4)) return true;  // every bucket empty
         // 4. second-level accumulation over the affine buckets, reduction, recombination
         XYZZ<F> *Q0 = accumulate_chunks<F>(c, p2, Baff);
         std::vector<XYZZ<F>> W2;

@@ -1653,16 +1653,6 @@ Ctx &ctx_aux(Ctx &c) {
     if (!c.aux) {
         Ctx *x = new Ctx();
         x->device = c.device;
-        try {
-            int lo = 0, hi = 0;
-            MI_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-            MI_HIP(hipStreamCreateWithFlags(&x->aux_streams[0], hipStreamNonBlocking));
-            MI_HIP(hipStreamCreateWithPriority(&x->aux_streams[1], hipStreamNonBlocking, hi));
-        } catch (...) {
-            if (x->aux_streams[0]) hipStreamDestroy(x->aux_streams[0]);
-            delete x;
-            throw;
-        }
         c.aux = x;
     }
     int prio = 0, lo = 0, hi = 0;
@@ -1675,7 +1665,17 @@ Ctx &ctx_aux(Ctx &c) {
         return !e ? 0 : strcmp(e, "aux") == 0 ? 1 : strcmp(e, "main") == 0 ? 2 : 0;
     }();
     const bool aux_hi = lane_prio == 1 ? true : lane_prio == 2 ? false : (prio == hi && hi != lo);
-    c.aux->stream = aux_hi ? c.aux->aux_streams[1] : c.aux->aux_streams[0];
+    // each lane's stream of the needed priority is created at its first use: every stream takes a hardware queue
+    // (GPU_MAX_HW_QUEUES) or shares one, and two streams on one queue run in order (a lane behind another's
+    // accumulation)
+    hipStream_t &s = c.aux->aux_streams[aux_hi ? 1 : 0];
+    if (!s) {
+        if (aux_hi)
+            MI_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, hi));
+        else
+            MI_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    }
+    c.aux->stream = s;
     return *c.aux;
 }
 

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("db")
     ap.add_argument("--call", type=int, default=-2)
     ap.add_argument("--min-ms", type=float, default=0.3)
+    ap.add_argument("--kernels", action="store_true", help="each stream's kernels (start, duration) in call order")
     a = ap.parse_args()
     db = sqlite3.connect(a.db)
     k = [(short(n), s, e, st) for n, s, e, st in db.execute("select name, start, end, stream_id from kernels order by start")]
@@ -34,6 +35,17 @@ def main():
         per[st].append((n, (s - t0) / 1e6, (e - t0) / 1e6))
     for st, v in per.items():
         print(f"stream {st}: {len(v)} kernels, {v[0][1]:.2f} .. {max(e for _, _, e in v):.2f} ms, busy {sum(e - s for _, s, e in v):.2f}")
+        if a.kernels:  # runs of one kernel name merged
+            run = None
+            for n, s, e in v:
+                if run and run[0] == n and s - run[2] < 0.05:
+                    run = (n, run[1], e, run[3] + 1, run[4] + e - s)
+                else:
+                    if run:
+                        print(f"    {run[1]:7.3f} +{run[2] - run[1]:6.3f} ms  x{run[3]:<3d} busy {run[4]:.3f}  {run[0]}")
+                    run = (n, s, e, 1, e - s)
+            if run:
+                print(f"    {run[1]:7.3f} +{run[2] - run[1]:6.3f} ms  x{run[3]:<3d} busy {run[4]:.3f}  {run[0]}")
     iv = sorted((s, e) for _, s, e in sum(per.values(), []))
     gaps, cur = [], iv[0][1]
     for s, e in iv[1:]:
