@@ -323,6 +323,8 @@ struct WinTable {
     const void *p = nullptr;  // g1_affine_t or g2_affine_t
     uint64_t stride = 0;
     unsigned c = 0, nwin = 0;
+    // the MSM's scalars are mostly zero digits (a witness vector): compact the entries before the sort
+    bool sparse = false;
 };
 // window bits of the tables built for n-point base sets (MI_MSM_WT_C overrides; read per call)
 unsigned msm_wt_window_bits(uint64_t n);

@@ -61,7 +61,7 @@ void msm_g1(Ctx &c, const g1_affine_t *bases, const fr_t *scalars, const uint32_
     // MI_MSM_WT=0 ignores the window tables (A/B; read per call)
     const char *e = getenv("MI_MSM_WT");
     if (wt && wt->p && n && !(e && atoi(e) == 0)) {
-        msm_run_wt<fq_t>(c, *wt, wt_lo, scalars, idx, n, result_host);
+        msm_run_wt<fq_t>(c, *wt, wt_lo, scalars, idx, n, result_host, wt->sparse);
         return;
     }
     msm_run<fq_t>(c, bases, scalars, idx, n, result_host, bases_hi, subgroup);

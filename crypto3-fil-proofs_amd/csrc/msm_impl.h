@@ -125,6 +125,64 @@ __global__ void k_digits_wt(const fr_t *__restrict__ scalars, const uint32_t *__
     }
 }
 
+// The same for sparse scalars (witness vectors: mostly 0 / 1, so most window digits are zero): only the non-zero
+// digits are written, compacted at [0, *count) in arbitrary order (per-thread counts, a wave prefix sum and one
+// atomic per wave).  The sort then runs over the entries alone.
+__global__ void __launch_bounds__(256) k_digits_wt_c(const fr_t *__restrict__ scalars, const uint32_t *__restrict__ idx,
+                                                     uint32_t n, unsigned c, unsigned nwin, uint32_t stride,
+                                                     uint32_t *__restrict__ count, uint32_t *__restrict__ keys,
+                                                     uint32_t *__restrict__ vals) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned lane = threadIdx.x & 63;
+    fr_t s = fr_t::zero();
+    if (i < n) s = scalars[idx ? idx[i] : i];
+    const uint32_t nbk = 1u << (c - 1), mask = (1u << c) - 1;
+    // pass 1: this thread's non-zero digits
+    uint32_t mine = 0, carry = 0;
+    for (unsigned w = 0; w < nwin; w++) {
+        const unsigned bit = w * c, word = bit >> 5, sh = bit & 31;
+        uint32_t d = 0;
+        if (word < 8) {
+            d = word_of(s, word) >> sh;
+            if (sh + c > 32 && word + 1 < 8) d |= word_of(s, word + 1) << (32 - sh);
+        }
+        d = (d & mask) + carry;
+        if (d > nbk) d = (1u << c) - d, carry = 1;
+        else carry = 0;
+        mine += d != 0;
+    }
+    // exclusive prefix over the wave, one atomic for the wave's total
+    uint32_t incl = mine;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= (unsigned)o) incl += y;
+    }
+    const uint32_t total = __shfl(incl, 63);
+    uint32_t base = 0;
+    if (lane == 63 && total) base = atomicAdd(count, total);
+    base = __shfl(base, 63) + incl - mine;
+    if (!mine) return;
+    // pass 2: write them
+    carry = 0;
+    for (unsigned w = 0; w < nwin; w++) {
+        const unsigned bit = w * c, word = bit >> 5, sh = bit & 31;
+        uint32_t d = 0;
+        if (word < 8) {
+            d = word_of(s, word) >> sh;
+            if (sh + c > 32 && word + 1 < 8) d |= word_of(s, word + 1) << (32 - sh);
+        }
+        d = (d & mask) + carry;
+        uint32_t neg = 0;
+        if (d > nbk) d = (1u << c) - d, neg = 1, carry = 1;
+        else carry = 0;
+        if (d) {
+            keys[base] = d - 1;
+            vals[base] = (w * stride + i) | (neg << 31);
+            base++;
+        }
+    }
+}
+
 // Large MSMs: the same digits, but only the NON-ZERO ones are written, compacted per window at
 // [w * n, w * n + wcount[w]) (wave ballots, one atomic per window per workgroup).  Witness scalars are
 // boolean-heavy (0/1 and small values): 43 % of the L/A/B digit slots of the synthetic 2^26 circuit
@@ -667,8 +725,10 @@ __global__ void __launch_bounds__(256) MI_WAVES_RED k_sum_groups(const XYZZ<F> *
 // so the device part is a tree of depth ~log2(nseg) instead of running sums over the segments (depth ~2 nseg /
 // parallelism) -- the reduction of a one-window plan is latency-bound, not work-bound.  Thread (row, g) sums G
 // items of its row; bit rows hold nseg / 2 items, so their upper half of partials is the identity.
+// The bit-row kernels run a few waves per SIMD at most (latency-bound trees), so they carry no two-wave register cap:
+// the G2 lane-pair full addition then keeps its values in registers instead of ~260 spilled dwords
 template <class F>
-__global__ void __launch_bounds__(256) MI_WAVES_RED k_bitsum_first(const XYZZ<F> *__restrict__ acc,
+__global__ void __launch_bounds__(256) k_bitsum_first(const XYZZ<F> *__restrict__ acc,
                                                       const XYZZ<F> *__restrict__ run, uint32_t nwin, uint32_t nseg,
                                                       unsigned lseg, unsigned G, XYZZ<F> *__restrict__ out) {
     using LP = LaneRed<F>;  // a lane pair per element for G2 (g2pair.h)
@@ -695,7 +755,7 @@ __global__ void __launch_bounds__(256) MI_WAVES_RED k_bitsum_first(const XYZZ<F>
 
 // out[b] = sum of in[b m, b m + m) (m <= 256 / K, a power of two): one block per output, pairwise tree in LDS
 template <class F>
-__global__ void __launch_bounds__(256) MI_WAVES_RED k_sum_lds(const XYZZ<F> *__restrict__ in, uint32_t m,
+__global__ void __launch_bounds__(256) k_sum_lds(const XYZZ<F> *__restrict__ in, uint32_t m,
                                                  XYZZ<F> *__restrict__ out) {
     using LP = LaneRed<F>;
     __shared__ __align__(16) unsigned char raw[256 / LP::K * sizeof(XYZZ<F>)];
@@ -1037,16 +1097,18 @@ inline bool bitsum_enabled() {
 // Window-table plan (msm_run_wt): nscal scalars, nwin windows of cb bits, over the table whose window w starts at
 // point w * stride (relative to the bases pointer the accumulation gets).  Every window's digits share one set of
 // 2^(cb - 1) buckets, so the plan has ONE window (pl.nwin = 1) of nwin * nscal entries.
+// sparse: the scalars are mostly zero digits (a witness): compact the non-zero ones first (one more readback, the
+// entry count), so the sort runs over the entries only
 inline bool msm_prepare_wt_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, uint64_t nscal, unsigned cb,
-                                unsigned nwin, uint64_t stride, MsmPlan &pl) {
+                                unsigned nwin, uint64_t stride, MsmPlan &pl, bool sparse = false) {
     pl = MsmPlan();
     if (nscal == 0) return false;
     const uint64_t np64 = (uint64_t)nwin * nscal;
     if (np64 >= 0xffffffffull || (uint64_t)nwin * stride >= 0x80000000ull || cb < 2 || cb > 24)
         throw std::runtime_error("msm: window-table instance too large for 32-bit sort indices");
     hipStream_t st = c.stream;
-    const uint32_t nbk = 1u << (cb - 1), np = (uint32_t)np64, invalid = nbk;
-    pl.n = np;
+    const uint32_t nbk = 1u << (cb - 1), invalid = nbk;
+    uint32_t np = (uint32_t)np64;
     pl.cb = cb;
     pl.nwin = 1;
     pl.nbk = nbk;
@@ -1058,9 +1120,23 @@ inline bool msm_prepare_wt_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx
     uint32_t *dmax = c.scratch[9].as<uint32_t>(8 + PLAN_PIN), *zstart = dmax + 4;  // [max, pad x 3, zstart, pad x 3, counts]
     {
         ScopedTimer tsort(c, &c.stats.sort, nscal);
-        k_digits_wt<<<grid_for(nscal, 256), 256, 0, st>>>(scalars, idx, (uint32_t)nscal, cb, nwin, (uint32_t)stride,
-                                                          invalid, keys, vals);
-        MI_LAUNCHED(c, "k_digits_wt");
+        if (sparse) {
+            uint32_t *cnt_dev = dmax + 7;
+            MI_HIP(hipMemsetAsync(cnt_dev, 0, 4, st));
+            k_digits_wt_c<<<grid_for(nscal, 256), 256, 0, st>>>(scalars, idx, (uint32_t)nscal, cb, nwin,
+                                                                (uint32_t)stride, cnt_dev, keys, vals);
+            MI_LAUNCHED(c, "k_digits_wt_c");
+            uint32_t *pc = c.pin.as<uint32_t>(1);
+            MI_HIP(hipMemcpyAsync(pc, cnt_dev, 4, hipMemcpyDeviceToHost, st));
+            MI_HIP(hipStreamSynchronize(st));
+            np = *pc;
+            if (np == 0) return false;  // every scalar is zero
+        } else {
+            k_digits_wt<<<grid_for(nscal, 256), 256, 0, st>>>(scalars, idx, (uint32_t)nscal, cb, nwin, (uint32_t)stride,
+                                                              invalid, keys, vals);
+            MI_LAUNCHED(c, "k_digits_wt");
+        }
+        pl.n = np;
         size_t tmp_bytes = 0;
         sort_pairs_u32(nullptr, tmp_bytes, keys, keys_s, vals, vals_s, np, cb, st);
         void *tmp = c.scratch[4].get(tmp_bytes);
@@ -1408,12 +1484,12 @@ void msm_accumulate_impl(Ctx &c, const MsmPlan &pl, const Affine<F> *bases, XYZZ
 // MSM over a window table (WinTable, ctx.h): points [lo, lo + n) of the table's base set
 template <class F>
 void msm_run_wt(Ctx &c, const WinTable &wt, uint64_t lo, const fr_t *scalars, const uint32_t *idx, uint64_t n,
-                XYZZ<F> *result) {
+                XYZZ<F> *result, bool sparse = false) {
     if (lo + n > wt.stride) throw std::invalid_argument("msm: range past the end of the window table");
     ScopedTimer whole(c, sizeof(F) == sizeof(fq_t) ? &c.stats.msm_g1 : &c.stats.msm_g2, n);
     MsmPlan pl;
     (sizeof(F) == sizeof(fq_t) ? c.stats.wt_msms : c.stats.wt_msms_g2) += 1;
-    if (!msm_prepare_wt_impl(c, scalars, idx, n, wt.c, wt.nwin, wt.stride, pl)) {
+    if (!msm_prepare_wt_impl(c, scalars, idx, n, wt.c, wt.nwin, wt.stride, pl, sparse)) {
         *result = XYZZ<F>::inf();
         return;
     }

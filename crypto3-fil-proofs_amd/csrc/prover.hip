@@ -1344,7 +1344,8 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
         if (b1_lane > 2) b1_lane = 2;  // every value names a lane that computes B_G1
         auto run_b = [&](Ctx &x) {
             const uint64_t lo = rg.lo[3], cnt = rg.cnt[3];
-            const WinTable wt2 = srs.wt_of(4);
+            WinTable wt2 = srs.wt_of(4);
+            wt2.sparse = true;  // witness scalars
             if (b1_lane != 0 && wt2.p) {  // B_G1 runs on another lane: B_G2 over its window table
                 msm_g2(x, srs.b_g2 + lo, z_dev, circ.idx_b + lo, cnt, &B2, &wt2, lo);
                 return;
@@ -1356,18 +1357,21 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
         };
         auto run_b1 = [&](Ctx &x) {
             const uint64_t lo = rg.lo[3], cnt = rg.cnt[3];
-            const WinTable wt = srs.wt_of(3);
+            WinTable wt = srs.wt_of(3);
+            wt.sparse = true;  // witness scalars
             msm_g1(x, srs.b_g1 + lo, z_dev, circ.idx_b + lo, cnt, &B1, nullptr, srs.in_subgroup, &wt, lo);
         };
         auto run_l = [&](Ctx &x) {
             const uint64_t l_lo = rg.lo[1], l_cnt = rg.cnt[1];
-            const WinTable wt = srs.wt_of(1);
+            WinTable wt = srs.wt_of(1);
+            wt.sparse = true;  // witness scalars
             msm_g1(x, srs.l + l_lo, z_dev + circ.n_in + l_lo, nullptr, l_cnt, &Lq, srs.l_hi ? srs.l_hi + l_lo : nullptr,
                    srs.in_subgroup, &wt, l_lo);
         };
         auto run_a = [&](Ctx &x) {
             const uint64_t a_lo = rg.lo[2], a_cnt = rg.cnt[2];
-            const WinTable wt = srs.wt_of(2);
+            WinTable wt = srs.wt_of(2);
+            wt.sparse = true;  // witness scalars
             msm_g1(x, srs.a + a_lo, z_dev, circ.idx_a + a_lo, a_cnt, &As, srs.a_hi ? srs.a_hi + a_lo : nullptr,
                    srs.in_subgroup, &wt, a_lo);
         };
