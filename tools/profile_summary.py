@@ -61,10 +61,12 @@ def step_launch_avg_ms(trace_dir, kernel_substr, bench):
 
 def g1_launch_points(bench):
     """points processed by each k_accum_level0<G1> launch of `bench.py --warmup W --steps K` in submission
-    (dispatch-id) order: per prove H, L, A, B_G1; then the standalone MSM (1 warm + msm_reps)."""
+    (dispatch-id) order: per prove H, L, A, B_G1 (the warm-up and timed proves, then the one-lane proof of
+    valu_roofline.one_lane when the line has it); then the standalone MSM (1 warm + msm_reps)."""
     cfg = bench["config"]
     per_prove = [cfg["domain"] - 1, cfg["num_aux"], cfg["a_query"], cfg["b_query"]]
-    proves = bench["warmup"] + bench["steps"]
+    one_lane = (bench.get("valu_roofline") or {}).get("one_lane") or {}
+    proves = bench["warmup"] + bench["steps"] + (1 if "avg_launch_ms" in one_lane else 0)
     msm = [bench["msm_g1_points"]] * (1 + bench.get("msm_reps", 1))
     return per_prove * proves + msm
 
