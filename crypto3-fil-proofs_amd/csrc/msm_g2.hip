@@ -1,4 +1,7 @@
 // msm_g2.hip -- G2 (Fq2) instantiation of the Pippenger MSM (msm_impl.h).
+#ifdef MI_G2_RED_UNCAPPED
+#define MI_WAVES_RED  // A/B: the G2 reduction kernels without the two-wave register cap
+#endif
 #include "msm_impl.h"
 
 namespace mi {

@@ -47,7 +47,9 @@ namespace {
 #ifndef MI_WAVES_ACC
 #define MI_WAVES_ACC MI_WAVES2
 #endif
+#ifndef MI_WAVES_RED
 #define MI_WAVES_RED MI_WAVES2  // the reduction kernels keep the two-wave cap (see g2pair.h LaneRed)
+#endif
 
 constexpr uint32_t L0_DEFAULT = 64;  // sorted entries per chunk at level 0 (mixed adds); MI_MSM_L0 overrides
 constexpr uint32_t L1_DEFAULT = 16;  // chunk partials summed per thread per tree level (full adds); MI_MSM_L1 overrides
