@@ -1243,7 +1243,7 @@ void reduce_windows(Ctx &c, const MsmPlan &pl, XYZZ<F> *P0, std::vector<XYZZ<F>>
     }();
     // small MSMs (<= 2^20 buckets in all) aim at 2^17 first-level segments: 4 buckets per running sum instead of 1
     // leaves the second level a quarter of the segments (Winning PoSt: 20.8-21.8 -> 20.1-20.2 ms, same box,
-    // tools/gpu_round4_r.sh)
+    // tools/gpu_round4_r.sh at 78a06f8)
     const uint64_t segA_target = sega_env > 0 ? (1ull << sega_env)
                                  : nb <= (1u << 20)           ? (1u << 17)
                                  : sizeof(F) == sizeof(fq_t)  ? (1u << 20)
