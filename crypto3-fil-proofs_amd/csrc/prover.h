@@ -148,6 +148,10 @@ struct ProofPoints {
 struct ProofSums {  // every sum starts as the identity: a lane that never runs leaves a valid (if wrong) point
     g1_xyzz_t H = g1_xyzz_t::inf(), L = g1_xyzz_t::inf(), A = g1_xyzz_t::inf(), B1 = g1_xyzz_t::inf();
     g2_xyzz_t B2 = g2_xyzz_t::inf();
+    // s A and r B1, computed by the lane that produced A / B1 as soon as it has (SumRanges::premul_*), so the
+    // assembly after the last lane only adds
+    g1_xyzz_t sA = g1_xyzz_t::inf(), rB1 = g1_xyzz_t::inf();
+    bool premul = false;
 };
 // The verifying-key points the assembly adds (scheme_params vk: alpha_g1, beta_g1, beta_g2, delta_g1, delta_g2).
 struct AssemblyKey {
@@ -168,6 +172,8 @@ ProofSums groth16_sums(Ctx &c, const Srs &srs, const Circuit &circ, const fr_t *
 // spread L, A and B over the others (fil_groth16.distributed.latency_ranges).
 struct SumRanges {
     uint64_t lo[4] = {0, 0, 0, 0}, cnt[4] = {0, 0, 0, 0};
+    // whole proofs only: the blinding scalars, so the lanes also return s A and r B1 (ProofSums::premul)
+    const fr_t *premul_r = nullptr, *premul_s = nullptr;
 };
 // h_in (optional): the d H coefficients of mi_groth16_h_coeffs_dev (canonical, bit-reversed); the share then skips
 // the witness map and the NTT chain

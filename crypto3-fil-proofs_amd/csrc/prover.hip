@@ -1308,6 +1308,10 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
     ProofSums out;
     g1_xyzz_t &H = out.H, &Lq = out.L, &As = out.A, &B1 = out.B1;
     g2_xyzz_t &B2 = out.B2;
+    out.premul = rg.premul_r && rg.premul_s;
+    auto premul_b1 = [&] {
+        if (out.premul) out.rB1 = host::xyzz_mul(B1, rg.premul_r->v, 8);
+    };
     {
     ScopedTimer whole(c, &c.stats.prove, circ.n);
     {
@@ -1352,7 +1356,10 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
             }
             MsmPlan pb;
             msm_prepare(x, z_dev, circ.idx_b + lo, cnt, pb);
-            if (b1_lane == 0) msm_g1_planned(x, pb, srs.b_g1 + lo, &B1);
+            if (b1_lane == 0) {
+                msm_g1_planned(x, pb, srs.b_g1 + lo, &B1);
+                premul_b1();
+            }
             msm_g2_planned(x, pb, srs.b_g2 + lo, &B2);
         };
         auto run_b1 = [&](Ctx &x) {
@@ -1360,6 +1367,7 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
             WinTable wt = srs.wt_of(3);
             wt.sparse = true;  // witness scalars
             msm_g1(x, srs.b_g1 + lo, z_dev, circ.idx_b + lo, cnt, &B1, nullptr, srs.in_subgroup, &wt, lo);
+            premul_b1();
         };
         auto run_l = [&](Ctx &x) {
             const uint64_t l_lo = rg.lo[1], l_cnt = rg.cnt[1];
@@ -1374,6 +1382,7 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
             wt.sparse = true;  // witness scalars
             msm_g1(x, srs.a + a_lo, z_dev, circ.idx_a + a_lo, a_cnt, &As, srs.a_hi ? srs.a_hi + a_lo : nullptr,
                    srs.in_subgroup, &wt, a_lo);
+            if (out.premul) out.sA = host::xyzz_mul(As, rg.premul_s->v, 8);
         };
         // aux-lane order: B before L (same-box A/B at 2^26: -2 ms per proof; MI_AUX_ORDER=l_first
         // restores L first)
@@ -1617,10 +1626,14 @@ BlindTerms groth16_blind_terms(const AssemblyKey &k, const fr_t &r, const fr_t &
 }
 
 ProofPoints groth16_finish(const BlindTerms &t, const ProofSums &m, const fr_t &r, const fr_t &s) {
-    // the two multiplications by MSM sums run side by side (one on a helper thread)
-    auto sA = std::async(std::launch::async, [&] { return host::xyzz_mul(m.A, s.v, 8); });
-    const g1_xyzz_t rB1 = host::xyzz_mul(m.B1, r.v, 8);
-    g1_xyzz_t C = host::xyzz_add(t.C0, sA.get());
+    // s A and r B1: from the lanes (premul), else side by side here (one on a helper thread)
+    g1_xyzz_t sAv = m.sA, rB1 = m.rB1;
+    if (!m.premul) {
+        auto sA = std::async(std::launch::async, [&] { return host::xyzz_mul(m.A, s.v, 8); });
+        rB1 = host::xyzz_mul(m.B1, r.v, 8);
+        sAv = sA.get();
+    }
+    g1_xyzz_t C = host::xyzz_add(t.C0, sAv);
     C = host::xyzz_add(C, rB1);
     C = host::xyzz_add(C, m.H);
     C = host::xyzz_add(C, m.L);
@@ -1641,7 +1654,10 @@ ProofPoints groth16_prove(Ctx &c, const Srs &srs, const Circuit &circ, const fr_
     // multiplications off a ~25 ms proof)
     const AssemblyKey key = assembly_key(srs);
     auto terms = std::async(std::launch::async, [&] { return groth16_blind_terms(key, r, s); });
-    const ProofSums m = groth16_sums(c, srs, circ, z_dev);
+    SumRanges rg = share_ranges(circ, 0, 1);
+    rg.premul_r = &r;
+    rg.premul_s = &s;
+    const ProofSums m = groth16_sums_ranges(c, srs, circ, z_dev, rg);
     return groth16_finish(terms.get(), m, r, s);
 }
 
