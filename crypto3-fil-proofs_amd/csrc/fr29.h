@@ -72,49 +72,6 @@ MI_HD fr29_t fr29_dot(const fr29_t *a, const fr29_t *b) {
 }
 MI_HD fr29_t fr29_mul(const fr29_t &a, const fr29_t &b) { return fr29_dot<1>(&a, &b); }
 
-// The same sum with a short dependency chain, for latency-bound code (a lone wave per SIMD: the witness's Poseidon
-// chains).  fr29_dot's single accumulator makes every MAD wait for the previous one (9 (K + 1) 9 dependent MADs);
-// here the product's 17 columns are summed independently, each column as K chains of at most 9 MADs, and the
-// reduction then runs word by word (m_i from the carried low word, m_i p added to nine different columns), about
-// 50 dependent instructions per product.  The m_i are the same as fr29_dot's, so the result is the same integer.
-// Column bound: 9 K + 9 products < 2^58 and the carries stay below 2^63 for K <= 6.
-template <int K>
-MI_HD fr29_t fr29_dot_lat(const fr29_t *a, const fr29_t *b) {
-    static_assert(K >= 1 && K <= 6, "fr29_dot_lat: at most 6 products per reduction");
-    constexpr int L = 9;
-    uint64_t t[2 * L];
-    MI_UNROLL for (int k = 0; k < 2 * L - 1; k++) {
-        uint64_t part[K];
-        MI_UNROLL for (int q = 0; q < K; q++) {
-            part[q] = 0;
-            MI_UNROLL for (int i = (k < L ? 0 : k - L + 1); i <= (k < L ? k : L - 1); i++)
-                part[q] += (uint64_t)a[q].v[i] * b[q].v[k - i];
-        }
-        uint64_t col = part[0];
-        MI_UNROLL for (int q = 1; q < K; q++) col += part[q];
-        t[k] = col;
-    }
-    t[2 * L - 1] = 0;
-    MI_UNROLL for (int i = 0; i < L; i++) {
-        const uint32_t m = ((uint32_t)t[i] * FrDesc::INV29) & M29;
-        MI_UNROLL for (int j = 0; j < L; j++) t[i + j] += (uint64_t)m * FrDesc::MOD29[j];
-        t[i + 1] += t[i] >> 29;  // t[i] is now 0 mod 2^29
-    }
-    fr29_t r;
-    MI_UNROLL for (int k = 0; k < L - 1; k++) {
-        r.v[k] = (uint32_t)t[L + k] & M29;
-        t[L + k + 1] += t[L + k] >> 29;
-    }
-    r.v[L - 1] = (uint32_t)t[2 * L - 1];
-    return r;
-}
-MI_HD fr29_t fr29_mul_lat(const fr29_t &a, const fr29_t &b) { return fr29_dot_lat<1>(&a, &b); }
-MI_HD fr29_t fr29_sbox_lat(const fr29_t &x) {  // x^5
-    const fr29_t x2 = fr29_mul_lat(x, x);
-    const fr29_t x4 = fr29_mul_lat(x2, x2);
-    return fr29_mul_lat(x4, x);
-}
-
 // a + b, carry-normalised, not reduced
 MI_HD fr29_t fr29_add(const fr29_t &a, const fr29_t &b) {
     fr29_t r;

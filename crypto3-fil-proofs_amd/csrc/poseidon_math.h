@@ -29,17 +29,6 @@ MI_HD fr29_t fr29_row(const fr29_t *row, const fr29_t *s) {
     }
 }
 
-// the same row product with fr29_dot_lat (latency-bound callers: k_wit_poseidon_lanes)
-template <int T>
-MI_HD fr29_t fr29_row_lat(const fr29_t *row, const fr29_t *s) {
-    if constexpr (T <= 6) {
-        return fr29_dot_lat<T>(row, s);
-    } else {
-        constexpr int A = (T + 1) / 2;
-        return fr29_add(fr29_row_lat<A>(row, s), fr29_row_lat<T - A>(row + A, s + A));
-    }
-}
-
 // ---------------------------------------------------------------------------------------------
 // constants (host derivation) and their device image
 // ---------------------------------------------------------------------------------------------

@@ -381,7 +381,7 @@ k_wit_poseidon(const WOp *__restrict__ ops, const uint64_t *__restrict__ idx, ui
 //   partial      lane 0 its S-box, s0 broadcast; lane j >= 1 updates s_j += w_j s0 while every lane forms its
 //                term row_j s_j of the new s0, summed by a 4-level butterfly (each level reduced below 2r).
 // The same field values as pos_run (exact arithmetic, lazy representatives < 4r, canonical digest), ~5x
-// shorter per hash; its products use fr29_dot_lat (short dependency chains: a level holds one wave per SIMD).  Phase B (EXPAND) uses the same kernel and writes each S-box's variables from its lane.
+// shorter per hash.  Phase B (EXPAND) uses the same kernel and writes each S-box's variables from its lane.
 __device__ __forceinline__ fr29_t shfl29(const fr29_t &x, int src) {
     fr29_t r;
     MI_UNROLL for (int l = 0; l < 9; l++) r.v[l] = (uint32_t)__shfl((int)x.v[l], src, 16);
@@ -402,7 +402,7 @@ template <int T>
 __device__ __forceinline__ fr29_t group_row(const fr29_t &x, const fr29_t *__restrict__ m, int j) {
     fr29_t all[T];
     sfor<T>([&](auto i) { all[i] = shfl29(x, i); });
-    return j < T ? fr29_row_lat<T>(m + j * T, all) : zero29();
+    return j < T ? fr29_row<T>(m + j * T, all) : zero29();
 }
 
 // EXPAND (phase B): every lane also writes its own S-box variables at their fixed offsets in the gadget's
@@ -426,13 +426,13 @@ __global__ void __launch_bounds__(64) k_wit_poseidon_lanes(const WOp *__restrict
     if (j == 0) {
         MI_UNROLL for (int l = 0; l < 9; l++) x.v[l] = img[k.off_tag].v[l];
     } else if (j < T) {
-        x = fr29_mul_lat(fr29_from_fr(zget(z, pin[op.a + j - 1])), img[k.off_tag + 1]);
+        x = fr29_mul(fr29_from_fr(zget(z, pin[op.a + j - 1])), img[k.off_tag + 1]);
     }
     const fr29_t *mds = img + k.off_mds;
     const int half = k.rf / 2;
     // S-box with the gadget's variables written at z[at ..]: (v,) v^2, v^4, v^5
     auto sbox_emit = [&](const fr29_t &v, uint64_t at, bool with_v) -> fr29_t {
-        const fr29_t v2 = fr29_mul_lat(v, v), v4 = fr29_mul_lat(v2, v2), v5 = fr29_mul_lat(v4, v);
+        const fr29_t v2 = fr29_sqr(v), v4 = fr29_sqr(v2), v5 = fr29_mul(v4, v);
         if (EXPAND) {
             if (with_v) zput29(z, at++, v);
             zput29(z, at++, v2);
@@ -449,7 +449,7 @@ __global__ void __launch_bounds__(64) k_wit_poseidon_lanes(const WOp *__restrict
     for (int r = 0; r < half; r++) {
         if (j < T) {
             const fr29_t v = fr29_add(x, img[k.off_rc_first + r * T + j]);
-            if (r == 0 && j == 0) x = fr29_sbox_lat(v);  // the domain tag's first S-box: a constant, no variables
+            if (r == 0 && j == 0) x = fr29_sbox(v);  // the domain tag's first S-box: a constant, no variables
             else if (r == 0) x = sbox_emit(v, base + 3 * (uint64_t)(j - 1), false);
             else x = sbox_emit(v, base + o_full + 4 * (uint64_t)T * (r - 1) + 4 * (uint64_t)j, true);
         }
@@ -460,11 +460,11 @@ __global__ void __launch_bounds__(64) k_wit_poseidon_lanes(const WOp *__restrict
     for (int q = 0; q < k.rp - 1; q++, sp += 2 * T - 1) {
         if (j == 0) x = sbox_emit(fr29_add(x, img[k.off_rc_part + q]), base + o_part + 4 * (uint64_t)q, true);
         const fr29_t s0 = shfl29(x, 0);
-        fr29_t term = j < T ? fr29_mul_lat(sp[j], x) : zero29();  // row_j s_j (s_0 after its S-box)
+        fr29_t term = j < T ? fr29_mul(sp[j], x) : zero29();  // row_j s_j (s_0 after its S-box)
         MI_UNROLL for (int m = 1; m < 16; m <<= 1)
             term = fr29_sub_if_ge(fr29_add(term, shfl_xor29(term, m)), R2X29);
         if (j == 0) x = term;
-        else if (j < T) x = fr29_sub_if_ge(fr29_add(x, fr29_mul_lat(sp[T + j - 1], s0)), R2X29);
+        else if (j < T) x = fr29_sub_if_ge(fr29_add(x, fr29_mul(sp[T + j - 1], s0)), R2X29);
     }
     if (j == 0)
         x = sbox_emit(fr29_add(x, img[k.off_rc_part + k.rp - 1]), base + o_part + 4 * (uint64_t)(k.rp - 1), true);

@@ -25,42 +25,7 @@ static fr_t fr_from_hex(const std::string &h) {
     return r;
 }
 
-// fr29_dot_lat (the latency-bound witness kernels' product) against fr29_dot: the same integer for K = 1 .. 6 terms
-// over random carry-normalised operands below 8r, and the edge operands 0, 1, r - 1, 8r - 1
-template <int K>
-static bool check_dot_lat(uint64_t &seed) {
-    auto rnd = [&] {
-        seed ^= seed << 13, seed ^= seed >> 7, seed ^= seed << 17;
-        return seed;
-    };
-    for (int it = 0; it < 20000; it++) {
-        fr29_t a[K], b[K];
-        for (int q = 0; q < K; q++) {
-            for (int l = 0; l < 9; l++) a[q].v[l] = (uint32_t)rnd() & M29, b[q].v[l] = (uint32_t)rnd() & M29;
-            a[q].v[8] &= (1u << 26) - 1, b[q].v[8] &= (1u << 26) - 1;  // < 2^258 (~8r)
-            const int kind = (int)(rnd() % 8);
-            if (kind == 0) std::memset(&a[q], 0, sizeof a[q]);
-            if (kind == 1) for (int l = 0; l < 9; l++) a[q].v[l] = l == 0;
-            if (kind == 2) for (int l = 0; l < 9; l++) a[q].v[l] = FrDesc::MOD29[l] - (l == 0);
-            if (kind == 3) for (int l = 0; l < 9; l++) b[q].v[l] = l < 8 ? M29 : (1u << 26) - 1;
-        }
-        const fr29_t x = fr29_dot<K>(a, b), y = fr29_dot_lat<K>(a, b);
-        if (std::memcmp(&x, &y, sizeof x) != 0) {
-            std::printf("fr29_dot_lat<%d> differs at iteration %d\n", K, it);
-            return false;
-        }
-    }
-    return true;
-}
-
-int main(int argc, char **argv) {
-    if (argc > 1 && std::strcmp(argv[1], "lat") == 0) {
-        uint64_t seed = 0x9E3779B97F4A7C15ull;
-        const bool ok = check_dot_lat<1>(seed) && check_dot_lat<2>(seed) && check_dot_lat<3>(seed) &&
-                        check_dot_lat<4>(seed) && check_dot_lat<5>(seed) && check_dot_lat<6>(seed);
-        std::printf(ok ? "dot_lat OK\n" : "dot_lat FAILED\n");
-        return ok ? 0 : 1;
-    }
+int main() {
     std::map<unsigned, PoseidonHost> tabs;
     std::string line;
     while (std::getline(std::cin, line)) {

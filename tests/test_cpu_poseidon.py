@@ -71,13 +71,6 @@ def test_device_arithmetic_on_host_equals_oracle(host_poseidon):
     assert r.stdout.split() == want
 
 
-def test_latency_form_of_the_fr_product_equals_the_chain_form(host_poseidon):
-    """fr29_dot_lat (k_wit_poseidon_lanes: independent column sums, word-by-word reduction) returns the same integer
-    as fr29_dot (one accumulator, product scanning) for 1..6 products over lazy operands below 8r."""
-    r = subprocess.run([host_poseidon, "lat"], capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0 and "dot_lat OK" in r.stdout, r.stdout + r.stderr
-
-
 def test_tree_cache_size_semantics():
     # base row excluded, then the rows_to_discard lowest rows (merkletree get_merkle_tree_cache_size)
     assert fg.tree.get_merkle_tree_cache_size(8 ** 4, 8, 0) == 512 + 64 + 8 + 1
