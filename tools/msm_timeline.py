@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Per-call timeline of standalone MSMs from a rocprofv3 --kernel-trace SQLite output (tools/msm_bench.py under
-a rocprofv3 --kernel-trace run of msm_bench.py).  A call starts at each digit kernel (k_digits*); the last `--reps` calls are summarised:
+"""Per-call timeline of standalone MSMs from a rocprofv3 --kernel-trace SQLite output (tools/msm_bench.py run
+under the profiler).  A call starts at each digit kernel (k_digits*); the last `--reps` calls are summarised:
 span (first kernel start to last kernel end), device-busy time, the kernel-free gaps (host round trips and launch
 latency) and device time per kernel.
 
