@@ -6,6 +6,7 @@
 #   trace     Winning-PoSt breakdown: rocprofv3 kernel + HIP runtime traces (databases in /tmp), timelines to $O
 #   suite     the whole GPU suite and smoke(), as the driver runs them
 #   post64    the 64 GiB Window-PoSt partition test with its record lines
+#   witness   the stacked / PoSt witness and Poseidon parity tests
 # usage: /usr/local/graft/bin/gpurun --timeout 1200 -- bash tools/gpu_checks.sh parity winning
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
@@ -37,6 +38,10 @@ for mode in "$@"; do
       tail -1 $O/gpu_tests.log
       timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
       tail -1 $O/smoke.log ;;
+    witness)
+      timeout -k 10 900 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_stacked.py \
+          tests/test_gpu_post.py tests/test_gpu_poseidon.py -k "not 64gib" > $O/witness.log 2>&1 || { tail -20 $O/witness.log; exit 1; }
+      tail -1 $O/witness.log ;;
     post64)
       timeout -k 10 900 python3 -u -m pytest -x -q -s --timeout 800 --timeout-method thread tests/test_gpu_post.py -k 64gib > $O/post64.log 2>&1 || exit 1
       grep "window-post-64\|passed" $O/post64.log ;;
