@@ -7,6 +7,7 @@
 #   suite     the whole GPU suite and smoke(), as the driver runs them
 #   post64    the 64 GiB Window-PoSt partition test with its record lines
 #   witness   the stacked / PoSt witness and Poseidon parity tests
+#   bench     the default bench line (python3 bench.py) into $O/bench.json
 # usage: /usr/local/graft/bin/gpurun --timeout 1200 -- bash tools/gpu_checks.sh parity winning
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
@@ -42,6 +43,9 @@ for mode in "$@"; do
       timeout -k 10 900 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_stacked.py \
           tests/test_gpu_post.py tests/test_gpu_poseidon.py -k "not 64gib" > $O/witness.log 2>&1 || { tail -20 $O/witness.log; exit 1; }
       tail -1 $O/witness.log ;;
+    bench)
+      timeout -k 10 900 python3 bench.py > $O/bench.json 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
+      tail -c 400 $O/bench.json ;;
     post64)
       timeout -k 10 900 python3 -u -m pytest -x -q -s --timeout 800 --timeout-method thread tests/test_gpu_post.py -k 64gib > $O/post64.log 2>&1 || exit 1
       grep "window-post-64\|passed" $O/post64.log ;;
