@@ -19,7 +19,13 @@
 //      then a second running-sum level over the segment sums (k_bucket_reduce_dense), whose <= 8192
 //      segments per window are offset by a short double-and-add (k_seg_fold).
 //   6. k_sum_groups : stacked per-window tree sums; host combines W = sum acc + S (V - R).
-//   7. host         : Horner over windows (c doublings each) on the CPU.
+//   7. host         : Horner over windows (c doublings each) on the CPU, in the 64-bit host field (hostfield.h).
+// A plan reads its counts back ONCE (plan_counts / plan_finish: chunk totals, the multi-chunk bucket list and every
+// chunk-tree level's size), then the result once.
+// Window-table plans (msm_run_wt; a small key's queries, mi_points_precompute): the table holds 2^(c w) P_i for
+// every window w, so k_digits_wt / k_digits_wt_c (witness scalars: non-zero digits compacted) put every window's
+// digits into ONE bucket set; the one window is reduced by bit rows (reduce_bitsum: k_bitsum_first, k_sum_lds)
+// and there is no window combination.
 #pragma once
 #include <hipcub/hipcub.hpp>
 #include <cstring>
@@ -442,9 +448,6 @@ __global__ void k_chunk_count(const uint32_t *__restrict__ cnt, uint32_t nb, uin
 }
 
 
-struct MaxOp {
-    __device__ __host__ uint32_t operator()(uint32_t a, uint32_t b) const { return a > b ? a : b; }
-};
 
 // Level-0 chunk lengths, keyed so a radix sort puts equal lengths next to each other: a wave then
 // runs chunks of (nearly) one length instead of "full chunks + remainders" (~69% lane use for
