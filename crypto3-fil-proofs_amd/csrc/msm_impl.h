@@ -159,16 +159,24 @@ __global__ void __launch_bounds__(256) k_digits_wt_c(const fr_t *__restrict__ sc
         else carry = 0;
         mine += d != 0;
     }
-    // exclusive prefix over the wave, one atomic for the wave's total
+    // exclusive prefix over the wave, then over the block's four waves: one atomic per block (the counter is shared
+    // by every block of the launch, so per-wave atomics queued behind each other)
+    __shared__ uint32_t wsum[4], bbase;
+    const unsigned wave = threadIdx.x >> 6;
     uint32_t incl = mine;
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t y = __shfl_up(incl, o);
         if (lane >= (unsigned)o) incl += y;
     }
-    const uint32_t total = __shfl(incl, 63);
-    uint32_t base = 0;
-    if (lane == 63 && total) base = atomicAdd(count, total);
-    base = __shfl(base, 63) + incl - mine;
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t t = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        bbase = t ? atomicAdd(count, t) : 0u;
+    }
+    __syncthreads();
+    uint32_t base = bbase + incl - mine;
+    for (unsigned w = 0; w < wave; w++) base += wsum[w];
     if (!mine) return;
     // pass 2: write them
     carry = 0;
