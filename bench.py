@@ -930,6 +930,8 @@ def main():
                     help="secondary: tree C over 2^N columns x 11 layers (N a multiple of 3; 0 skips)")
     ap.add_argument("--sdr-log-labels", type=int, default=24,
                     help="secondary: SDR labelling-proof labels of 2^N challenges (0 skips)")
+    ap.add_argument("--tune", action="append", default=[], metavar="NAME=VALUE",
+                    help="library A/B switch for the whole run (mi_tune_set, csrc/tune.h; tools' A/B runs only)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" in os.environ:
@@ -960,6 +962,10 @@ def main():
     device = torch.device("cuda", dev_index)
 
     import fil_groth16 as fg
+
+    for kv in args.tune:  # A/B runs of the tools: library switches, never set by the default bench line
+        k, _, v = kv.partition("=")
+        fg.tune_set(k, int(v))
     from fil_groth16 import synth as synth_mod
     from fil_groth16.compound import shard_partitions
     from fil_groth16.distributed import gather_multiproof, prove_partitions
@@ -977,7 +983,7 @@ def main():
     ctx.synchronize()
     t_srs = time.perf_counter() - t_setup - t_synth - t_load
     free_b, total_b = torch.cuda.mem_get_info(dev_index)
-    dev_used_gb = (total_b - free_b) / 1e9  # circuit + proving key (+ split tables unless MI_MSM_GLV=1)
+    dev_used_gb = (total_b - free_b) / 1e9  # circuit + proving key (+ split tables unless msm_glv=1)
     # the witness in page-locked host memory, where a synthesiser would write it (mi_host_alloc)
     zhost = fg.HostBuffer(32 * sc.num_vars)
     np.copyto(zhost.array, sc.z_array())
@@ -1063,21 +1069,19 @@ def main():
                     "note": "witness resident in HBM before the timer (no H2D): the round-1 definition"}
         del zdev
 
-    # the dominant kernel measured alone: one proof with MI_PROVE_LANES=1 (the auxiliary lane's MSMs run after the
+    # the dominant kernel measured alone: one proof with prove_lanes=1 (the auxiliary lane's MSMs run after the
     # main lane's, on the same stream), so k_accum_level0's launch times are the kernel's own and not stretched by
     # the other lane's sorts and NTTs (the timed proofs' two-lane figure is reported beside it)
     one_lane = None
     if rank == 0:
-        os.environ["MI_PROVE_LANES"] = "1"
         try:
-            ctx.reset_stats()
-            fg.prove_batch(ctx, pk, circ, [zhost], [blinding(0, 0)], priority=prio)
-            ctx.synchronize()
+            with fg.tuned(prove_lanes=1):
+                ctx.reset_stats()
+                fg.prove_batch(ctx, pk, circ, [zhost], [blinding(0, 0)], priority=prio)
+                ctx.synchronize()
             one_lane = ctx.stats()
         except Exception as e:  # reported, never fatal
             one_lane = {"error": str(e)}
-        finally:
-            del os.environ["MI_PROVE_LANES"]
 
     # secondary metric: standalone G1 MSM over the resident 2^log_rows - 1 h-query points
     msm_n = pk.n_h
@@ -1383,8 +1387,9 @@ def main():
         "timers_ms": {k: round(v["ms"], 3) for k, v in stats.items()},
         "setup_s": {"synth": t_synth, "circuit_load": t_load, "srs": t_srs},
         "device_gb_after_setup": round(dev_used_gb, 2),
-        "msm_split": {"1": "glv", "0": "2^128 tables"}.get(os.environ.get("MI_MSM_GLV", ""),
-                                                          "auto: 2^128 tables when they fit in HBM, else glv"),
+        "msm_split": {1: "glv", 0: "2^128 tables"}.get(fg.tune_get("msm_glv"),
+                                                      "auto: 2^128 tables when they fit in HBM, else glv"),
+        "tune": args.tune,
         "multiproof_bytes": 192 * len(proofs),
         "msm_reps": args.msm_reps,
     }

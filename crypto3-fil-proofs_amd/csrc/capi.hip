@@ -689,6 +689,37 @@ int mi_ctx_inject_oom(mi_ctx *ctx, int64_t count) {
     });
 }
 
+int mi_tune_set(const char *name, int64_t value) {
+    return guard([&] {
+        const int k = mi::tune::find(name);
+        need(k >= 0, std::string("unknown tuning switch: ") + (name ? name : "(null)"));
+        need(value != mi::tune::UNSET, "value reserved for 'unset'");
+        mi::tune::set((mi::tune::Knob)k, value);
+    });
+}
+
+int mi_tune_clear(const char *name) {
+    return guard([&] {
+        if (!name) {
+            mi::tune::reset();
+            return;
+        }
+        const int k = mi::tune::find(name);
+        need(k >= 0, std::string("unknown tuning switch: ") + name);
+        mi::tune::set((mi::tune::Knob)k, mi::tune::UNSET);
+    });
+}
+
+int mi_tune_get(const char *name, int64_t *value, int *is_set) {
+    return guard([&] {
+        const int k = mi::tune::find(name);
+        need(k >= 0 && value && is_set, "unknown tuning switch or null argument");
+        const int64_t v = mi::tune::get((mi::tune::Knob)k, mi::tune::UNSET);
+        *is_set = v != mi::tune::UNSET;
+        *value = *is_set ? v : 0;
+    });
+}
+
 int mi_srs_export_query_dev(mi_ctx *ctx, const mi_srs *srs, int which, uint64_t first, uint64_t n, void *dev_out) {
     return guard([&] {
         need(ctx && srs && (dev_out || !n), "null argument");
@@ -1659,10 +1690,9 @@ struct TreeUploads {
     }
 };
 
-uint64_t tree_batch() {  // columns / leaves per upload batch (MI_TREE_BATCH overrides, for tests)
-    const char *e = getenv("MI_TREE_BATCH");
-    const uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
-    return v ? v : (1ull << 21);
+uint64_t tree_batch() {  // columns / leaves per upload batch (tune::TREE_BATCH overrides, for tests)
+    const int64_t v = mi::tune::get(mi::tune::TREE_BATCH, 0);
+    return v > 0 ? (uint64_t)v : (1ull << 21);
 }
 
 void check_dev_canonical(mi::Ctx &c, const mi::fr_t *d, uint64_t n, const char *what) {

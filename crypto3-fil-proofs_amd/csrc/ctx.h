@@ -16,6 +16,7 @@
 #include "curve.h"
 #include "field.h"
 #include "fr29.h"
+#include "tune.h"
 
 namespace mi {
 

@@ -169,8 +169,7 @@ inline unsigned grid1(uint64_t n) { return (unsigned)((n + 255) / 256); }
 }  // namespace
 
 void debug_sync(Ctx &c, const char *what) {
-    static const bool on = getenv("MI_DEBUG_SYNC") && getenv("MI_DEBUG_SYNC")[0] == '1';
-    if (!on) return;
+    if (tune::get(tune::DEBUG_SYNC, 0) != 1) return;  // tune::DEBUG_SYNC (debugging only)
     hipError_t e = hipStreamSynchronize(c.stream);
     fprintf(stderr, "[mi] %s: %s\n", what, hipGetErrorString(e));
     if (e != hipSuccess) throw hip_error(e, std::string("kernel ") + what + " failed: " + hipGetErrorString(e));

@@ -11,12 +11,10 @@ unsigned msm_window_bits_for(uint64_t n, unsigned sbits, bool glv) {
     // minimise (mixed adds) + 1.4 x (bucket-reduction full adds) over c; split plans (129-bit scalars)
     // keep c >= 9 so their ceil(129 / c) windows fit the split digit kernel (MAXW_S = 16)
     const unsigned cmin = sbits < 256 ? 9 : 4;
-    // MI_MSM_C forces the window size of every MSM (read per call; clamped to [cmin, 22]) so the tests
+    // tune::MSM_C forces the window size of every MSM (test only; clamped to [cmin, 22]) so the tests
     // can run the production windows (c = 20..22 at 2^26 / 2^27) on instances the oracle checks quickly
-    if (const char *e = getenv("MI_MSM_C")) {
-        const int cf = atoi(e);
-        if (cf > 0) return (unsigned)(cf < (int)cmin ? (int)cmin : cf > 22 ? 22 : cf);
-    }
+    if (const int64_t cf = tune::get(tune::MSM_C, 0); cf > 0)
+        return (unsigned)(cf < (int64_t)cmin ? (int64_t)cmin : cf > 22 ? 22 : cf);
     unsigned best = cmin;
     double best_cost = 1e300;
     for (unsigned c = cmin; c <= 22; c++) {
@@ -33,34 +31,32 @@ unsigned msm_window_bits_for(uint64_t n, unsigned sbits, bool glv) {
 }
 
 bool msm_use_split(uint64_t n) {
-    // MI_MSM_SPLIT: 0 off, 1 (default) above 2^20 points, 2 always (tests); read per call.  Up to 2^20 points the
+    // tune::MSM_SPLIT: 0 off, 1 (default) above 2^20 points, 2 always (tests).  Up to 2^20 points the
     // plain plan sorts every window in one onesweep call while the split plan sorts window by window: same box,
     // the 2^20 G1 MSM 6.05 -> 5.39 ms unsplit, the Winning-PoSt proof (2^19-point MSMs) unchanged, the 2^21
     // proof 40.6 -> 41.4 ms if its 2^21 - 1-point H MSM went unsplit (tools/split_sweep.sh).
-    // MI_MSM_SPLIT_MIN = k splits from 2^k points instead.
-    const char *e = getenv("MI_MSM_SPLIT");
-    const int mode = e ? atoi(e) : 1;
+    // tune::MSM_SPLIT_MIN = k splits from 2^k points instead.
+    const int64_t mode = tune::get(tune::MSM_SPLIT, 1);
     if (mode == 2) return true;
     if (mode != 1) return false;
-    if (const char *m = getenv("MI_MSM_SPLIT_MIN")) {
-        const int lg = atoi(m);
+    if (tune::is_set(tune::MSM_SPLIT_MIN)) {
+        const int64_t lg = tune::get(tune::MSM_SPLIT_MIN, 0);
         return n >= (1ull << (lg < 0 ? 0 : lg > 40 ? 40 : lg));
     }
     return n > (1ull << 20);
 }
 
 int msm_glv_mode() {
-    // MI_MSM_GLV (read per call): unset = auto (the 2^128 table where the key has one, GLV otherwise),
+    // tune::MSM_GLV (test only): unset = auto (the 2^128 table where the key has one, GLV otherwise),
     // 0 = never GLV, 1 = always GLV (and key load builds no tables)
-    const char *e = getenv("MI_MSM_GLV");
-    return e && *e ? (atoi(e) != 0 ? 1 : 0) : 2;
+    const int64_t v = tune::get(tune::MSM_GLV, tune::UNSET);
+    return v == tune::UNSET ? 2 : v != 0 ? 1 : 0;
 }
 
 void msm_g1(Ctx &c, const g1_affine_t *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,
             g1_xyzz_t *result_host, const g1_affine_t *bases_hi, bool subgroup, const WinTable *wt, uint64_t wt_lo) {
-    // MI_MSM_WT=0 ignores the window tables (A/B; read per call)
-    const char *e = getenv("MI_MSM_WT");
-    if (wt && wt->p && n && !(e && atoi(e) == 0)) {
+    // tune::MSM_WT = 0 ignores the window tables (A/B, tests)
+    if (wt && wt->p && n && tune::get(tune::MSM_WT, 1) != 0) {
         msm_run_wt<fq_t>(c, *wt, wt_lo, scalars, idx, n, result_host, wt->sparse);
         return;
     }
@@ -68,10 +64,7 @@ void msm_g1(Ctx &c, const g1_affine_t *bases, const fr_t *scalars, const uint32_
 }
 
 unsigned msm_wt_window_bits(uint64_t n) {
-    if (const char *e = getenv("MI_MSM_WT_C")) {
-        const int cf = atoi(e);
-        if (cf > 0) return (unsigned)(cf < 8 ? 8 : cf > 22 ? 22 : cf);
-    }
+    if (const int64_t cf = tune::get(tune::MSM_WT_C, 0); cf > 0) return (unsigned)(cf < 8 ? 8 : cf > 22 ? 22 : cf);
     // One bucket set for every window.  Per entry (n ceil(256 / c) of them): a mixed add (1 / 6.6e9 s, measured at
     // 2^20) and its sort (~0.03 ns); per bucket: the first reduction level's two full adds (~3e9 / s); plus the
     // latency-bound bit-row tree (~0.4 ms).  The top window of a 255-bit scalar holds 255 - (nwin - 1) c bits: a c

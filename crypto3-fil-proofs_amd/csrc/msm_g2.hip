@@ -8,8 +8,7 @@ namespace mi {
 
 void msm_g2(Ctx &c, const g2_affine_t *bases, const fr_t *scalars, const uint32_t *idx, uint64_t n,
             g2_xyzz_t *result_host, const WinTable *wt, uint64_t wt_lo) {
-    const char *e = getenv("MI_MSM_WT");  // 0: ignore the window tables (A/B; read per call)
-    if (wt && wt->p && n && !(e && atoi(e) == 0)) {
+    if (wt && wt->p && n && tune::get(tune::MSM_WT, 1) != 0) {  // tune::MSM_WT = 0: ignore the window tables
         msm_run_wt<fq2_t>(c, *wt, wt_lo, scalars, idx, n, result_host, wt->sparse);
         return;
     }

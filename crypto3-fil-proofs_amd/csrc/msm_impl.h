@@ -57,8 +57,8 @@ namespace {
 #define MI_WAVES_RED MI_WAVES2  // the reduction kernels keep the two-wave cap (see g2pair.h LaneRed)
 #endif
 
-constexpr uint32_t L0_DEFAULT = 64;  // sorted entries per chunk at level 0 (mixed adds); MI_MSM_L0 overrides
-constexpr uint32_t L1_DEFAULT = 16;  // chunk partials summed per thread per tree level (full adds); MI_MSM_L1 overrides
+constexpr uint32_t L0_DEFAULT = 64;  // sorted entries per chunk at level 0 (mixed adds); tune::MSM_L0 overrides
+constexpr uint32_t L1_DEFAULT = 16;  // chunk partials summed per thread per tree level (full adds); tune::MSM_L1 overrides
 constexpr unsigned TREE_MAXL = 16;   // chunk-tree levels counted with the plan (L1 >= 4: up to 4^16 chunks a bucket)
 
 MI_HD uint32_t word_of(const fr_t &s, unsigned k) {
@@ -888,11 +888,9 @@ constexpr unsigned PLAN_PIN = 5 + TREE_MAXL;
 inline void plan_counts(Ctx &c, MsmPlan &pl, const uint32_t *cntA, uint32_t *offB, uint32_t *cntB, uint32_t nb,
                         const uint32_t *maxcnt_dev, uint32_t *stage) {
     hipStream_t st = c.stream;
-    // MI_MSM_L0 / MI_MSM_L1 (read per plan; tuning): entries per level-0 chunk, partials per tree-level thread (a
-    // power of two)
-    const char *e0 = getenv("MI_MSM_L0"), *e1 = getenv("MI_MSM_L1");
-    uint32_t L0 = e0 ? (uint32_t)atoi(e0) : L0_DEFAULT, L1 = e1 ? (uint32_t)atoi(e1) : L1_DEFAULT;
-    if (L0 < 2 || L0 > 1024) L0 = L0_DEFAULT;
+    // tune::MSM_L0 / MSM_L1 (tuning A/B): entries per level-0 chunk, partials per tree-level thread (a power of two)
+    const int64_t t0 = tune::get(tune::MSM_L0, L0_DEFAULT), t1 = tune::get(tune::MSM_L1, L1_DEFAULT);
+    uint32_t L0 = t0 >= 2 && t0 <= 1024 ? (uint32_t)t0 : L0_DEFAULT, L1 = t1 >= 4 && t1 <= 64 ? (uint32_t)t1 : L1_DEFAULT;
     if (L1 < 4 || L1 > 64 || (L1 & (L1 - 1))) L1 = L1_DEFAULT;
     unsigned lg1 = 0;
     while ((1u << lg1) < L1) lg1++;
@@ -997,10 +995,9 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
     // two 11-bit onesweep places (2^20: 2 launches instead of 32); large ones sort window by window.
     unsigned all_bits = 1;
     while ((1ull << all_bits) <= (uint64_t)nwin * (nbk + 1) - 1) all_bits++;
-    // MI_MSM_SORT=windowed forces the per-window path (and with it the zero-digit compaction when
+    // tune::MSM_SORT = 1 forces the per-window path (and with it the zero-digit compaction when
     // nwin <= MAXW_C) at any size: tests use it to cover the large-MSM path at 2^20
-    const char *sort_env = getenv("MI_MSM_SORT");
-    const bool force_windowed = sort_env && strcmp(sort_env, "windowed") == 0;
+    const bool force_windowed = tune::get(tune::MSM_SORT, 0) == 1;
     const bool one_sort = !force_windowed && !split && all_bits <= 22 && nwin > 1;
     const uint32_t wk = one_sort ? nbk + 1 : 0;
     pl.cb = cb;
@@ -1101,11 +1098,8 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
     return plan_finish(c, pl, offA, cntA, nb, vals_s, pin + H);
 }
 
-// MI_MSM_BITSUM=0 sends one-window plans through reduce_windows (A/B); read per call
-inline bool bitsum_enabled() {
-    const char *e = getenv("MI_MSM_BITSUM");
-    return !(e && atoi(e) == 0);
-}
+// tune::MSM_BITSUM = 0 sends one-window plans through reduce_windows (A/B, tests)
+inline bool bitsum_enabled() { return tune::get(tune::MSM_BITSUM, 1) != 0; }
 
 // Window-table plan (msm_run_wt): nscal scalars, nwin windows of cb bits, over the table whose window w starts at
 // point w * stride (relative to the bases pointer the accumulation gets).  Every window's digits share one set of
@@ -1247,15 +1241,12 @@ void reduce_windows(Ctx &c, const MsmPlan &pl, XYZZ<F> *P0, std::vector<XYZZ<F>>
     //   accA_s = sum_j (j+1) B_{sS+j},  runA_s = sum_j B_{sS+j},  R = sum_s runA_s,  V = sum_s (s+1) runA_s,
     // V by a second running-sum level over runA (segments of SB) whose few segment offsets are folded
     // by double-and-add (k_seg_fold).
-    // first-level segment count target (threads of k_bucket_reduce); MI_MSM_SEGA_LOG overrides (tuning)
-    static const int sega_env = [] {
-        const char *e = getenv("MI_MSM_SEGA_LOG");
-        return e ? atoi(e) : 0;
-    }();
+    // first-level segment count target (threads of k_bucket_reduce); tune::MSM_SEGA_LOG overrides (tuning)
+    const int64_t sega_env = tune::get(tune::MSM_SEGA_LOG, 0);
     // small MSMs (<= 2^20 buckets in all) aim at 2^17 first-level segments: 4 buckets per running sum instead of 1
     // leaves the second level a quarter of the segments (Winning PoSt: 20.8-21.8 -> 20.1-20.2 ms, same box,
     // tools/gpu_round4_r.sh at 78a06f8)
-    const uint64_t segA_target = sega_env > 0 ? (1ull << sega_env)
+    const uint64_t segA_target = sega_env > 0 && sega_env < 40 ? (1ull << sega_env)
                                  : nb <= (1u << 20)           ? (1u << 17)
                                  : sizeof(F) == sizeof(fq_t)  ? (1u << 20)
                                                               : (1u << 18);
@@ -1265,11 +1256,8 @@ void reduce_windows(Ctx &c, const MsmPlan &pl, XYZZ<F> *P0, std::vector<XYZZ<F>>
     // second-level segments per window: 8192 for large MSMs.  Small ones (<= 2^19 first-level segments in all,
     // Winning PoSt's 2^18-2^19-point MSMs) take 2048: k_seg_fold's double-and-add over ~14-bit offsets per
     // segment was the largest reduction kernel there (thousands of full additions per window for a weighted
-    // sum the running sums of k_bucket_reduce_dense do with 2 per segment).  MI_MSM_SEGB_LOG = k forces 2^k.
-    static const int segb_env = [] {
-        const char *e = getenv("MI_MSM_SEGB_LOG");
-        return e ? atoi(e) : 0;
-    }();
+    // sum the running sums of k_bucket_reduce_dense do with 2 per segment).  tune::MSM_SEGB_LOG = k forces 2^k.
+    const int64_t segb_env = tune::get(tune::MSM_SEGB_LOG, 0);
     const uint32_t segB_cap = segb_env > 0 ? (1u << (segb_env > 13 ? 13 : segb_env))
                                            : totA <= (1u << 19) ? 2048u : 8192u;
     const uint32_t nsegB = nsegA < segB_cap ? nsegA : segB_cap, SB = nsegA / nsegB, totB = nwin * nsegB;
@@ -1316,10 +1304,10 @@ void reduce_bitsum(Ctx &c, const MsmPlan &pl, XYZZ<F> *P0, std::vector<XYZZ<F>> 
     hipStream_t st = c.stream;
     const unsigned nwin = pl.nwin;
     const uint32_t nbk = pl.nbk;
-    // first-level segments in all (threads of k_bucket_reduce): >= 2^MI_MSM_BS_SEG_LOG (default 2^16) while a
-    // segment holds more than one bucket; read per call (tuning)
-    const char *e = getenv("MI_MSM_BS_SEG_LOG");
-    const unsigned seg_log = e && atoi(e) > 0 ? (unsigned)atoi(e) : 16u;
+    // first-level segments in all (threads of k_bucket_reduce): >= 2^tune::MSM_BS_SEG_LOG (default 2^16) while a
+    // segment holds more than one bucket
+    const int64_t bs_seg = tune::get(tune::MSM_BS_SEG_LOG, 16);
+    const unsigned seg_log = bs_seg > 0 && bs_seg < 32 ? (unsigned)bs_seg : 16u;
     unsigned SA = 1, log_sa = 0;
     while (SA < nbk && (uint64_t)nbk * nwin / (SA * 2) >= (1ull << seg_log)) SA *= 2, log_sa++;
     const uint32_t nseg = nbk / SA, totA = nwin * nseg;
@@ -1331,12 +1319,12 @@ void reduce_bitsum(Ctx &c, const MsmPlan &pl, XYZZ<F> *P0, std::vector<XYZZ<F>> 
     MI_LAUNCHED(c, "k_bucket_reduce");
     // rows per window: the two halves of sum acc, then T_k; nseg / 2 items each.  Items per thread of the first
     // level: enough that <= 2^15 threads run it (the LDS tree passes after it are latency-bound: fewer, shallower
-    // blocks; 2^20 over a c = 20 table, same box: 3.29 / 3.26 / 3.24 ms at 4 / 8 / 16 items), MI_MSM_BS_G0 overrides
+    // blocks; 2^20 over a c = 20 table, same box: 3.29 / 3.26 / 3.24 ms at 4 / 8 / 16 items), tune::MSM_BS_G0 overrides
     const uint32_t rows = nwin * (2 + lseg), half = nseg / 2 ? nseg / 2 : 1;
-    const char *ge = getenv("MI_MSM_BS_G0");
+    const int64_t g0 = tune::get(tune::MSM_BS_G0, 0);
     unsigned G = 1;
-    if (ge && atoi(ge) > 0) {
-        G = (unsigned)atoi(ge);
+    if (g0 > 0 && g0 <= 1024) {
+        G = (unsigned)g0;
     } else {
         while ((uint64_t)rows * half / (G * 2) >= (1u << 15) && G < 64) G *= 2;
     }
@@ -1378,15 +1366,14 @@ void reduce_bitsum(Ctx &c, const MsmPlan &pl, XYZZ<F> *P0, std::vector<XYZZ<F>> 
 // Pippenger over those affine points with the small scalars j + 1 split into two c2-bit digits
 // (windows 2w, 2w + 1; about 2 mixed additions per bucket, ~2^c2 second-level buckets per window),
 // and W_w = W'_{2w} + 2^c2 W'_{2w+1}.  Reuses the level-1 plan's scratch: the plan is consumed.
-// MI_G2_L2=0 turns it off (the plain reduction), MI_G2_L2=2 forces it at any size (tests).
+// tune::G2_L2 = 0 turns it off (the plain reduction), 2 forces it at any size (tests).
 template <class F>
 bool g2_second_level(Ctx &c, const MsmPlan &pl, XYZZ<F> *P0, std::vector<XYZZ<F>> &W) {
     if constexpr (sizeof(F) != sizeof(fq2_t)) {
         return false;
     } else {
-        // MI_G2_L2: 0 off, 1 (default) from 2^20 level-1 buckets on, 2 always (tests); read per call
-        const char *e = getenv("MI_G2_L2");
-        const int mode = e ? atoi(e) : 1;
+        // tune::G2_L2: 0 off, 1 (default) from 2^20 level-1 buckets on, 2 always (tests)
+        const int64_t mode = tune::get(tune::G2_L2, 1);
         if (mode == 0 || (mode == 1 && pl.nb < (1u << 20))) return false;
         hipStream_t st = c.stream;
         const unsigned nwin = pl.nwin, cb = pl.cb;
@@ -1396,9 +1383,8 @@ bool g2_second_level(Ctx &c, const MsmPlan &pl, XYZZ<F> *P0, std::vector<XYZZ<F>
         // 1. bucket sums -> affine
         Affine<F> *Baff = c.scratch[18].as<Affine<F>>(nb);
         F *pre = c.scratch[19].as<F>(nb);
-        // MI_G2_AFF_K buckets per inversion (Montgomery's trick; read per call for A/B)
-        const char *ek = getenv("MI_G2_AFF_K");
-        const int kaff = ek ? atoi(ek) : 64;  // same-box: 538.2 (32) vs 535.8 (64) vs 536.1 (128) ms per proof
+        // tune::G2_AFF_K buckets per inversion (Montgomery's trick; A/B)
+        const int64_t kaff = tune::get(tune::G2_AFF_K, 64);  // same-box: 538.2 (32) vs 535.8 (64) vs 536.1 (128) ms per proof
         if (kaff == 128)
             k_bucket_affine<F, 128><<<grid_for(((uint64_t)nb + 127) / 128, 256), 256, 0, st>>>(pl.coff, pl.cnt, P0, nb,
                                                                                              pre, Baff);
@@ -1514,7 +1500,7 @@ void msm_run(Ctx &c, const Affine<F> *bases, const fr_t *scalars, const uint32_t
              XYZZ<F> *result, const Affine<F> *bases_hi = nullptr, bool subgroup = false) {
     ScopedTimer whole(c, sizeof(F) == sizeof(fq_t) ? &c.stats.msm_g1 : &c.stats.msm_g2, n);
     MsmPlan pl;
-    // G1 split mode: the GLV endomorphism (no table) when MI_MSM_GLV selects it, else the 2^128 table.
+    // G1 split mode: the GLV endomorphism (no table) when tune::MSM_GLV selects it, else the 2^128 table.
     // phi(P) = lambda P holds only on the r-torsion, so auto mode takes GLV only for bases known to be in
     // the prime-order subgroup (generated / checked keys, mi_points_check_subgroup); other on-curve bases
     // run the plain path, which computes sum k_i P_i exactly like bellman's multiexp.

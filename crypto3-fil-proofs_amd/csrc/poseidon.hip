@@ -222,10 +222,10 @@ void poseidon_hash_dev(Ctx &c, unsigned arity, const fr_t *in, uint64_t n, uint6
     PosK k;
     poseidon_tables(c, arity, &k);
     ScopedTimer tm(c, &c.stats.poseidon, n);
-    // MI_POSEIDON_PAIR (read per call, for A/B): 1 wave-pair kernel, 0 one thread per hash; unset = the
-    // measured choice, pairs for the wide states (arity 8, 11) and one thread per hash for arity 2, 4
-    const char *pe = getenv("MI_POSEIDON_PAIR");
-    const bool pair = pe ? atoi(pe) != 0 : arity >= 8;
+    // tune::POSEIDON_PAIR (A/B): 1 wave-pair kernel, 0 one thread per hash; unset = the measured choice, pairs for
+    // the wide states (arity 8, 11) and one thread per hash for arity 2, 4
+    const int64_t pt = tune::get(tune::POSEIDON_PAIR, tune::UNSET);
+    const bool pair = pt != tune::UNSET ? pt != 0 : arity >= 8;
     const unsigned gp = (unsigned)((n + 63) / 64);
     switch (arity) {
         case 2:

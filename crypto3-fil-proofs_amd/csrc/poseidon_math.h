@@ -150,11 +150,10 @@ inline Mat mat_inv(Mat a) {  // Gauss-Jordan over Fr
 
 }  // namespace pos_detail
 
-// S-box field of the Grain LFSR seed (oracle/poseidon_ref.py SBOX_FIELD); env MI_POSEIDON_SBOX_FIELD overrides
-inline unsigned poseidon_sbox_field() {
-    const char *e = getenv("MI_POSEIDON_SBOX_FIELD");
-    return e ? (unsigned)atoi(e) & 15u : 1u;
-}
+// S-box field of the Grain LFSR seed: 1, the value Filecoin's Poseidon seeds it with (oracle/poseidon_ref.py
+// SBOX_FIELD).  A fixed constant: nothing at run time changes the round constants (and with them every tree root).
+constexpr unsigned kPoseidonSboxField = 1;
+inline constexpr unsigned poseidon_sbox_field() { return kPoseidonSboxField; }
 
 // Host-side derivation of the device constant image (layout in poseidon.h: PosK offsets).
 inline PoseidonHost poseidon_derive(unsigned arity, unsigned sbox_field) {

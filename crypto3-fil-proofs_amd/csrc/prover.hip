@@ -953,12 +953,12 @@ void g2_window_table(Ctx &c, const g2_affine_t *bases, uint64_t n, unsigned wbit
 }
 
 namespace {
-// Fixed-base window tables (WinTable) of the four G1 queries of a small key: domain <= 2^MI_MSM_WT_MAX_LOG (default
+// Fixed-base window tables (WinTable) of the four G1 queries of a small key: domain <= 2^tune::MSM_WT_MAX_LOG (default
 // 2^21; 0 turns them off), and only while they leave a proof its working set (the split tables' admission rule).
 // A key's MSMs then run over one bucket set per query (msm_run_wt).  Read at each build (tests compare both).
 void build_window_tables(Ctx &c, Srs &S) {
-    const char *e = getenv("MI_MSM_WT_MAX_LOG");
-    const unsigned max_log = e ? (unsigned)atoi(e) : 21u;
+    const int64_t wt_max = tune::get(tune::MSM_WT_MAX_LOG, 21);
+    const unsigned max_log = wt_max >= 0 && wt_max < 64 ? (unsigned)wt_max : 21u;
     if (max_log == 0 || S.log_d > max_log || S.has_tables()) return;
     const void *src[5] = {S.h_perm, S.l, S.a, S.b_g1, S.b_g2};
     uint64_t big = 0;
@@ -1273,12 +1273,9 @@ fr_t *compute_h(Ctx &c, const Circuit &circ, const fr_t *z_dev) {
     fr_t g = fr_small_mont(7);
     fr_t zinv = inverse(pow_u64(g, d) - fr_t::one());
     // ifft, * g^i / d, fft on the coset (natural order) for a and b; c's last pass also forms
-    // (a b - c) / Z and starts the inverse coset transform (ntt_coset_qap); MI_QAP_FUSED=0 runs
+    // (a b - c) / Z and starts the inverse coset transform (ntt_coset_qap); tune::QAP_FUSED = 0 runs
     // the separate division pass (A/B)
-    static const bool qap_fused = [] {
-        const char *e = getenv("MI_QAP_FUSED");
-        return !(e && atoi(e) == 0);
-    }();
+    const bool qap_fused = tune::get(tune::QAP_FUSED, 1) != 0;
     ntt_coset_roundtrip(c, a, L, dinv);
     ntt_coset_roundtrip(c, b, L, dinv);
     if (!qap_fused || !ntt_coset_qap(c, a, b, cc, L, dinv, zinv)) {
@@ -1317,17 +1314,16 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
     {
         // L, B_G1 and B_G2 do not depend on the QAP: they run on the auxiliary lane (second stream,
         // second host thread) while this stream runs the witness map, the NTT chain, H and A.
-        // MI_PROVE_LANES=1 runs the auxiliary work after the main lane on the same stream (measurement
-        // only: every phase's device time without the other lane's kernels beside it)
-        const char *ole = getenv("MI_PROVE_LANES");  // read per call: bench.py times a one-lane proof beside the default
-        const bool one_lane = ole && atoi(ole) == 1;
-        // Small proofs (domain <= 2^MI_PROVE_WIDE_LOG, default 2^21: Winning PoSt, 2^19) are latency-bound: their
+        // tune::PROVE_LANES = 1 runs the auxiliary work after the main lane on the same stream (measurement
+        // only: every phase's device time without the other lane's kernels beside it; bench.py's one-lane proof)
+        const bool one_lane = tune::get(tune::PROVE_LANES, 2) == 1;
+        // Small proofs (domain <= 2^tune::PROVE_WIDE_LOG, default 2^21: Winning PoSt, 2^19) are latency-bound: their
         // MSMs' bucket reductions, sorts and host round trips leave most CUs idle, so B_G2, L and A + B_G1 each get
         // a lane of their own (three auxiliary streams and host threads beside the main lane's witness map, NTT
         // chain and H).  Large proofs keep two lanes: their accumulation fills the chip and every lane holds a scratch
-        // arena sized to its MSMs.  Read per call (tests compare the two layouts).
-        const char *we = getenv("MI_PROVE_WIDE_LOG");
-        const unsigned wide_log = we ? (unsigned)atoi(we) : 21u;
+        // arena sized to its MSMs.  Tests compare the two layouts.
+        const int64_t wl = tune::get(tune::PROVE_WIDE_LOG, 21);
+        const unsigned wide_log = wl >= 0 && wl < 64 ? (unsigned)wl : 21u;
         const bool wide = !one_lane && L <= wide_log;
         const unsigned nlanes = wide ? 3 : 1;
         Ctx *lane_ctx[3] = {one_lane ? &c : &ctx_aux(c), nullptr, nullptr};
@@ -1340,12 +1336,11 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
         }
         std::exception_ptr err[3];
         // B_G1 and B_G2 share the scalars (z over the B-density): sort them once on large proofs.  Small proofs run
-        // B_G1 after A on A's lane (MI_PROVE_B1_LANE: 2 default, 1 after L, 0 with B_G2), which sorts the scalars
+        // B_G1 after A on A's lane (tune::PROVE_B1_LANE: 2 default, 1 after L, 0 with B_G2), which sorts the scalars
         // again for itself (no plan is shared between lanes: the G2 second level reuses its plan's scratch).
         // Same box, Winning PoSt: 23.1 ms with B_G1 beside B_G2, 20.5 ms after A.
-        const char *b1e = getenv("MI_PROVE_B1_LANE");
-        unsigned b1_lane = wide ? (b1e ? (unsigned)atoi(b1e) : 2u) : 0u;
-        if (b1_lane > 2) b1_lane = 2;  // every value names a lane that computes B_G1
+        const int64_t b1t = tune::get(tune::PROVE_B1_LANE, 2);
+        const unsigned b1_lane = wide ? (b1t < 0 || b1t > 2 ? 2u : (unsigned)b1t) : 0u;  // every value names a lane that computes B_G1
         auto run_b = [&](Ctx &x) {
             const uint64_t lo = rg.lo[3], cnt = rg.cnt[3];
             WinTable wt2 = srs.wt_of(4);
@@ -1384,12 +1379,9 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
                    srs.in_subgroup, &wt, a_lo);
             if (out.premul) out.sA = host::xyzz_mul(As, rg.premul_s->v, 8);
         };
-        // aux-lane order: B before L (same-box A/B at 2^26: -2 ms per proof; MI_AUX_ORDER=l_first
+        // aux-lane order: B before L (same-box A/B at 2^26: -2 ms per proof; tune::AUX_ORDER = 1
         // restores L first)
-        static const bool b_first = [] {
-            const char *e = getenv("MI_AUX_ORDER");
-            return !(e && strcmp(e, "l_first") == 0);
-        }();
+        const bool b_first = tune::get(tune::AUX_ORDER, 0) != 1;
         auto lane_work = [&](unsigned k) {
             try {
                 Ctx &x = *lane_ctx[k];
@@ -1678,12 +1670,9 @@ Ctx &ctx_aux(Ctx &c) {
     int prio = 0, lo = 0, hi = 0;
     MI_HIP(hipStreamGetPriority(c.stream, &prio));
     MI_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    // the auxiliary lane follows the caller's priority; MI_LANE_PRIO=aux puts it above a normal main lane,
-    // MI_LANE_PRIO=main keeps it normal under a high-priority main lane (lane-contention A/B)
-    static const int lane_prio = [] {
-        const char *e = getenv("MI_LANE_PRIO");
-        return !e ? 0 : strcmp(e, "aux") == 0 ? 1 : strcmp(e, "main") == 0 ? 2 : 0;
-    }();
+    // the auxiliary lane follows the caller's priority; tune::LANE_PRIO = 1 puts it above a normal main lane,
+    // 2 keeps it normal under a high-priority main lane (lane-contention A/B)
+    const int64_t lane_prio = tune::get(tune::LANE_PRIO, 0);
     const bool aux_hi = lane_prio == 1 ? true : lane_prio == 2 ? false : (prio == hi && hi != lo);
     // each lane's stream of the needed priority is created at its first use: every stream takes a hardware queue
     // (GPU_MAX_HW_QUEUES) or shares one, and two streams on one queue run in order (a lane behind another's

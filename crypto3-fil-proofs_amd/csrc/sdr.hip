@@ -332,9 +332,8 @@ void sdr_labels_gather_dev(Ctx &c, const SdrReplica &rid, const void *layer_labe
     if (!n) return;
     if (n_base + n_exp > kTotalParents || n_base == 0)
         throw std::invalid_argument("sdr: 1 <= n_base and n_base + n_exp <= 37");
-    // MI_SDR_PREFETCH (read per call, for A/B): 1 = software-pipelined parent gathers, 0 = load at use
-    const char *pe = getenv("MI_SDR_PREFETCH");
-    const bool pf = pe ? atoi(pe) != 0 : false;
+    // tune::SDR_PREFETCH (A/B, tests): 1 = software-pipelined parent gathers, 0 = load at use
+    const bool pf = tune::get(tune::SDR_PREFETCH, 0) != 0;
     if (pf)
         k_sdr_labels_gather<true><<<grid256(n), 256, 0, c.stream>>>(rid, (const uint4 *)layer_labels,
                                                                     nodes_per_layer, layers, challenges, parent_idx,

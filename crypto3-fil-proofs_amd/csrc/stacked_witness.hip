@@ -490,11 +490,9 @@ void launch_poseidon(int kind, hipStream_t st, const WOp *ops, const uint64_t *i
     // chip with one thread per hash (phase A levels -- 23 K hashes per level of the Window-PoSt partition are 367
     // waves for 1,024 SIMDs --, the stacked partition's 3,151 and the Winning-PoSt proof's 726 phase-B gadgets).
     // The Window-PoSt partition's 237 K phase-B gadgets (3.7 K waves) keep one thread per hash: on lanes they
-    // took 17.5 ms instead of 6.  MI_WIT_POS_LANES (read once): the largest launch on lanes, 0 = never.
-    static const uint64_t lanes_max = [] {
-        const char *e = getenv("MI_WIT_POS_LANES");
-        return e ? (uint64_t)atoll(e) : (uint64_t)65536;
-    }();
+    // took 17.5 ms instead of 6.  tune::WIT_POS_LANES (A/B): the largest launch on lanes, 0 = never.
+    const int64_t lm = tune::get(tune::WIT_POS_LANES, 65536);
+    const uint64_t lanes_max = lm < 0 ? 0 : (uint64_t)lm;
     if (n <= lanes_max) {
         const unsigned g4 = (unsigned)((n + 3) / 4);
         switch (kind) {

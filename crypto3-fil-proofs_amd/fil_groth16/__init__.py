@@ -15,3 +15,4 @@ from .compound import (MultiProof, partition_count, get_partitions_for_window_po
 from . import tree  # noqa: F401  (Poseidon + tree C / tree R-last builders)
 from . import stacked  # noqa: F401  (stacked-PoRep circuit: R1CS + GPU witness)
 from . import sdr  # noqa: F401  (SDR labelling witness: SHA-256 labels of challenged nodes)
+from .tuning import tune_clear, tune_get, tune_set, tuned  # noqa: F401  (test / A/B switches, csrc/tune.h)

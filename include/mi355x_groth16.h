@@ -443,6 +443,16 @@ int mi_ctx_get_table_msms(mi_ctx *ctx, uint64_t out[2]);
  * error after its NTT chain (count < 0: every proof until reset to 0), so the release-and-retry path runs at any
  * size.  Production code never calls it; nothing in the prove path reads the environment for it. */
 int mi_ctx_inject_oom(mi_ctx *ctx, int64_t count);
+/* TEST / BENCHMARK ONLY: process-wide A/B switches (csrc/tune.h lists them with their meaning: "msm_c", "msm_split",
+ * "msm_glv", "msm_wt", "msm_wt_max_log", "msm_sort", "g2_l2", "prove_lanes", "prove_b1_lane", "tree_batch",
+ * "sdr_prefetch", "msm_countsort", ...).  Every switch defaults to the measured production choice, and the library
+ * reads no environment variable for them: a production prove runs the same windows, lanes and kernels whatever its
+ * process environment holds.  mi_tune_set refuses an unknown name (MI_ERR_ARG); mi_tune_clear(name) restores one
+ * default, mi_tune_clear(NULL) all of them; mi_tune_get reports whether a switch is set and its value.  No reference
+ * counterpart (the reference has no GPU path to tune). */
+int mi_tune_set(const char *name, int64_t value);
+int mi_tune_clear(const char *name);
+int mi_tune_get(const char *name, int64_t *value, int *is_set);
 /* msm window size chosen for n points (exposed for tests / reports) */
 unsigned mi_msm_window_bits(uint64_t n);
 

@@ -37,3 +37,26 @@ def ctx():
     c = fil_groth16.Context(0)
     yield c
     c.close()
+
+
+class _Tune:
+    """Library A/B switches for one test (fil_groth16.tuning; csrc/tune.h): set(name, value) / clear(name)."""
+
+    def set(self, name, value):
+        import fil_groth16
+
+        fil_groth16.tune_set(name, value)
+
+    def clear(self, name):
+        import fil_groth16
+
+        fil_groth16.tune_clear(name)
+
+
+@pytest.fixture
+def tune():
+    """Switches set through this fixture are all cleared after the test (the library's defaults come back)."""
+    import fil_groth16
+
+    yield _Tune()
+    fil_groth16.tune_clear()

@@ -165,3 +165,28 @@ def test_post_partition_derivation():
     assert _post_partitions(10 * 2349 + 2348, 2349) == 10
     assert _post_partitions(2349, 2349) == 1
     assert _post_partitions(5, 2349) == 1
+
+
+def test_tuning_switches_are_explicit_not_environment():
+    """the library reads no environment variable that changes window sizes, lanes, kernels or hash
+    constants; the A/B switches are set through mi_tune_set (test only), and an unknown name is refused.  The only
+    getenv left in csrc/ is FIL_PROOFS_PARAMETER_CACHE (the reference's parameter-cache directory,
+    parameter_cache.hpp:52)."""
+    csrc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "crypto3-fil-proofs_amd", "csrc")
+    reads = []
+    for f in sorted(os.listdir(csrc)):
+        with open(os.path.join(csrc, f)) as fh:
+            reads += re.findall(r'getenv\("([A-Z0-9_]+)"\)', fh.read())
+    assert reads == ["FIL_PROOFS_PARAMETER_CACHE"], reads
+    assert fg.tune_get("msm_c") is None
+    with fg.tuned(msm_c=12, prove_lanes=1):
+        assert fg.tune_get("msm_c") == 12 and fg.tune_get("prove_lanes") == 1
+        assert fg.msm_window_bits(1 << 20) == 12  # the window heuristic follows the switch
+    assert fg.tune_get("msm_c") is None and fg.tune_get("prove_lanes") is None
+    with pytest.raises(fg.FilGpuError):
+        fg.tune_set("no_such_switch", 1)
+    os.environ["MI_MSM_C"] = "9"  # the old environment knob no longer changes anything
+    try:
+        assert fg.msm_window_bits(1 << 20) != 9
+    finally:
+        del os.environ["MI_MSM_C"]

@@ -94,12 +94,12 @@ def test_groth16_random_vs_oracle_and_pairing(ctx, oracle, rows, seed):
     assert fg.prove(ctx, pk, gc, zb, 0, 0) == op.prove(zb, 0, 0)[0]
 
 
-def test_groth16_windowed_sort_vs_oracle(ctx, oracle, monkeypatch):
+def test_groth16_windowed_sort_vs_oracle(ctx, oracle, tune):
     """The large-MSM paths of a prove (per-window sort of the compacted non-zero digits, the B_G1 / B_G2
     plan shared in that mode, G2 second-level bucket reduction), forced at a size the oracle proves in
     seconds."""
-    monkeypatch.setenv("MI_MSM_SORT", "windowed")
-    monkeypatch.setenv("MI_G2_L2", "2")  # and B_G2's bucket reduction as the second-level MSM
+    tune.set("msm_sort", 1 if "windowed" == "windowed" else 0)
+    tune.set("g2_l2", 2)  # and B_G2's bucket reduction as the second-level MSM
     n_in, n_aux, rws, z = circuits.random_circuit(34, 5000, n_in=6, n_free=32)
     oc, gc = _load(ctx, oracle, n_in, n_aux, rws, z)
     tox = circuits.toxic(34)
@@ -113,13 +113,13 @@ def test_groth16_windowed_sort_vs_oracle(ctx, oracle, monkeypatch):
 
 
 @pytest.mark.parametrize("split", ["0", "2", "glv"])
-def test_groth16_split_msm_vs_oracle(ctx, oracle, monkeypatch, split):
+def test_groth16_split_msm_vs_oracle(ctx, oracle, tune, split):
     """H, L and A through the split-mode MSM (2^128 base tables, two 128-bit half scalars per point)
     forced at a size the oracle proves in seconds; "0" is the plain path at the same size, "glv" the
     split through the GLV endomorphism (no tables built at key generation)."""
-    monkeypatch.setenv("MI_MSM_SPLIT", "2" if split == "glv" else split)
-    monkeypatch.setenv("MI_MSM_GLV", "1" if split == "glv" else "0")
-    monkeypatch.setenv("MI_MSM_WT_MAX_LOG", "0")  # this key's MSMs on the split / plain paths, not window tables
+    tune.set("msm_split", int("2" if split == "glv" else split))
+    tune.set("msm_glv", int("1" if split == "glv" else "0"))
+    tune.set("msm_wt_max_log", 0)  # this key's MSMs on the split / plain paths, not window tables
     n_in, n_aux, rws, z = circuits.random_circuit(35, 5000, n_in=6, n_free=32)
     oc, gc = _load(ctx, oracle, n_in, n_aux, rws, z)
     tox = circuits.toxic(35)
@@ -133,14 +133,14 @@ def test_groth16_split_msm_vs_oracle(ctx, oracle, monkeypatch, split):
     assert fg.assemble(vk, shares, r, s) == op.prove(zb, r, s)[0]
 
 
-def test_prove_out_of_memory_degrades_to_glv(ctx, oracle, monkeypatch):
+def test_prove_out_of_memory_degrades_to_glv(ctx, oracle, tune):
     """A proof whose scratch allocation fails (mi_ctx_inject_oom, a test-only entry: the main lane raises
     hipMalloc's out-of-memory error after the NTT chain while the auxiliary lane runs) is re-run in-process after
     the key's 2^128 split tables are released: the bytes equal the oracle's, the key reports no tables afterwards,
     and the context counts the retry.  Every prove entry (host / device witness, batch, share) recovers alike.
     mi_srs_readmit then rebuilds the tables (the release is not one-way) and the proof is unchanged."""
-    monkeypatch.setenv("MI_MSM_SPLIT", "2")  # split mode at this size, so the tables are in use
-    monkeypatch.setenv("MI_MSM_WT_MAX_LOG", "0")  # split tables, not window tables
+    tune.set("msm_split", 2)  # split mode at this size, so the tables are in use
+    tune.set("msm_wt_max_log", 0)  # split tables, not window tables
     n_in, n_aux, rws, z = circuits.random_circuit(36, 5000, n_in=6, n_free=32)
     oc, gc = _load(ctx, oracle, n_in, n_aux, rws, z)
     tox = circuits.toxic(36)
@@ -176,13 +176,13 @@ def test_prove_out_of_memory_degrades_to_glv(ctx, oracle, monkeypatch):
     assert fg.prove(ctx, pk, gc, zb, 11, 21) == want[1] and ctx.fallbacks()["oom_retries"] == 0
 
 
-def test_prove_window_tables(ctx, oracle, monkeypatch):
+def test_prove_window_tables(ctx, oracle, tune):
     """A small key builds fixed-base window tables for h, l, a, b_g1 and b_g2 at generation (domain <= 2^21): its
     proofs run those five MSMs over one bucket set each and equal the oracle's, as do latency-mode shares (table slices at
     an offset); MI_MSM_WT=0 (the plain path) gives the same bytes.  An out-of-memory retry releases the tables like
     the split tables, and mi_srs_readmit rebuilds them."""
-    monkeypatch.delenv("MI_MSM_WT_MAX_LOG", raising=False)
-    monkeypatch.delenv("MI_MSM_WT", raising=False)
+    tune.clear("msm_wt_max_log")
+    tune.clear("msm_wt")
     n_in, n_aux, rws, z = circuits.random_circuit(37, 6000, n_in=5, n_free=40)
     oc, gc = _load(ctx, oracle, n_in, n_aux, rws, z)
     tox = circuits.toxic(37)
@@ -197,10 +197,10 @@ def test_prove_window_tables(ctx, oracle, monkeypatch):
     assert ctx.table_msms() == 4 and ctx.table_msms(g2=True) == 1
     vk, _ = pk.verifying_key()
     assert fg.assemble(vk, [fg.prove_share(ctx, pk, gc, zb, k, 3) for k in range(3)], 31, 41) == want[1]
-    monkeypatch.setenv("MI_MSM_WT", "0")
+    tune.set("msm_wt", 0)
     ctx.reset_stats()
     assert fg.prove(ctx, pk, gc, zb, 31, 41) == want[1] and ctx.table_msms() == 0 and ctx.table_msms(g2=True) == 0
-    monkeypatch.delenv("MI_MSM_WT")
+    tune.clear("msm_wt")
     ctx.inject_oom(1)
     assert fg.prove(ctx, pk, gc, zb, 30, 40) == want[0]
     assert ctx.fallbacks()["oom_retries"] == 1
@@ -225,7 +225,7 @@ def test_prove_batch_and_priority(ctx, oracle):
     assert fg.MultiProof.from_bytes(mp.to_bytes()).circuit_proofs == proofs
 
 
-def test_prove_lane_layouts_identical(ctx, oracle, monkeypatch):
+def test_prove_lane_layouts_identical(ctx, oracle, tune):
     """Small proofs (domain <= 2^MI_PROVE_WIDE_LOG, default 2^21) run B, L and A on three auxiliary lanes of their
     own; large ones keep the two-lane layout (prover.hip groth16_sums_once).  Both layouts give the oracle's
     proof, for several witnesses in a row on the same context (the lanes' scratch arenas are reused)."""
@@ -236,8 +236,8 @@ def test_prove_lane_layouts_identical(ctx, oracle, monkeypatch):
     zb = circuits.z_bytes(z)
     want = [op.prove(zb, r, s)[0] for r, s in [(7, 8), (9, 10)]]
     for wide_log, b1_lane in (("0", "0"), ("21", "0"), ("21", "1"), ("21", "2")):
-        monkeypatch.setenv("MI_PROVE_WIDE_LOG", wide_log)
-        monkeypatch.setenv("MI_PROVE_B1_LANE", b1_lane)
+        tune.set("prove_wide_log", int(wide_log))
+        tune.set("prove_b1_lane", int(b1_lane))
         got = [fg.prove(ctx, pk, gc, zb, r, s) for r, s in [(7, 8), (9, 10)]]
         assert got == want, f"MI_PROVE_WIDE_LOG={wide_log} MI_PROVE_B1_LANE={b1_lane}"
 

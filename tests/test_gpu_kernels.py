@@ -81,10 +81,10 @@ def test_msm_g1_random(ctx, oracle, n):
 
 
 @pytest.fixture(params=["0", "2"])
-def g2_level2(request, monkeypatch):
+def g2_level2(request, tune):
     """G2 bucket reduction: "0" the running-sum kernels, "2" the second-level MSM over affine buckets
     (forced at every size; by default it takes over from 2^20 level-1 buckets, MI_G2_L2)."""
-    monkeypatch.setenv("MI_G2_L2", request.param)
+    tune.set("g2_l2", int(request.param))
     return request.param
 
 
@@ -136,10 +136,10 @@ def test_msm_rejects_bad_points(ctx, oracle):
 
 
 @pytest.fixture(params=["auto", "windowed"])
-def sort_mode(request, monkeypatch):
+def sort_mode(request, tune):
     """auto: 2^20 sorts every window in one call; windowed: the per-window sort with zero-digit
     compaction that MSMs of 2^22+ points take (MI_MSM_SORT, read at every MSM)."""
-    monkeypatch.setenv("MI_MSM_SORT", request.param)
+    tune.set("msm_sort", 1 if request.param == "windowed" else 0)
     return request.param
 
 
@@ -214,15 +214,15 @@ def _split_scalars(n, seed):
 
 
 @pytest.mark.parametrize("split", ["0", "2", "glv"])
-def test_msm_split_tables_vs_oracle(ctx, oracle, monkeypatch, split):
+def test_msm_split_tables_vs_oracle(ctx, oracle, tune, split):
     """Split mode (MI_MSM_SPLIT=2 forces it at any size): the l and a queries' MSMs over their 2^128
     tables, against the oracle's MSM over the same points; "glv": keys generated and MSMs run with
     MI_MSM_GLV=1 (no tables)."""
     import torch
 
-    monkeypatch.setenv("MI_MSM_SPLIT", "2" if split == "glv" else split)
-    monkeypatch.setenv("MI_MSM_GLV", "1" if split == "glv" else "0")
-    monkeypatch.setenv("MI_MSM_WT_MAX_LOG", "0")  # split / plain paths, not the key's window tables
+    tune.set("msm_split", int("2" if split == "glv" else split))
+    tune.set("msm_glv", int("1" if split == "glv" else "0"))
+    tune.set("msm_wt_max_log", 0)  # split / plain paths, not the key's window tables
     n_in, n_aux, rws, z = circuits.random_circuit(91, 3000, n_in=6, n_free=32)
     gc = fg.Circuit(ctx, len(rws), n_in, n_aux, circuits.to_csr(rws))
     pk = fg.generate_random_parameters(ctx, gc, circuits.toxic())
@@ -236,11 +236,11 @@ def test_msm_split_tables_vs_oracle(ctx, oracle, monkeypatch, split):
             torch.cuda.synchronize()
 
 
-def test_msm_split_default_2_17(ctx, oracle, monkeypatch):
+def test_msm_split_default_2_17(ctx, oracle, tune):
     """Default selection (split from 2^16 points on) on the l query of a 2^17-row synthetic circuit."""
     import torch
 
-    monkeypatch.setenv("MI_MSM_WT_MAX_LOG", "0")  # the split path, not the key's window tables
+    tune.set("msm_wt_max_log", 0)  # the split path, not the key's window tables
     from fil_groth16 import synth
 
     sc = synth.SynthCircuit(log_rows=17, n_in=4, seed=3)
@@ -269,25 +269,25 @@ def _glv_scalars(n, seed):
 
 
 @pytest.mark.parametrize("n,c", [(1, ""), (13, ""), (5000, ""), (5000, "12"), (5000, "22")])
-def test_msm_glv_vs_oracle(ctx, oracle, monkeypatch, n, c):
+def test_msm_glv_vs_oracle(ctx, oracle, tune, n, c):
     """G1 split mode through the GLV endomorphism (MI_MSM_GLV=1; MI_MSM_SPLIT=2 forces split at any size)
     over caller-uploaded bases, which have no 2^128 table: edge scalars of the k = k1 + lambda k2
     decomposition, at the default window, c = 12 and the production c = 22 (2^22 sub-buckets per window)."""
-    monkeypatch.setenv("MI_MSM_GLV", "1")
-    monkeypatch.setenv("MI_MSM_SPLIT", "2")
+    tune.set("msm_glv", 1)
+    tune.set("msm_split", 2)
     if c:
-        monkeypatch.setenv("MI_MSM_C", c)
+        tune.set("msm_c", int(c))
     bases = _bases_g1(oracle, n, 555 + n)
     sb = _glv_scalars(n, 7 + n)
     assert ctx.msm_g1(bases, sb) == oracle.msm_g1(bases, sb)
 
 
-def test_msm_glv_repeated_base_and_negation(ctx, oracle, monkeypatch):
+def test_msm_glv_repeated_base_and_negation(ctx, oracle, tune):
     """GLV sub-bucket merge branches: one base repeated (P and phi(P) sums in the same bucket), P with -P
     (a sub-bucket sum at infinity), and scalars lambda / 1 on the same base (phi(P) + ... hits the doubling
     of the merge when k2 = 1, k1 = 0 meets k1 = 1)."""
-    monkeypatch.setenv("MI_MSM_GLV", "1")
-    monkeypatch.setenv("MI_MSM_SPLIT", "2")
+    tune.set("msm_glv", 1)
+    tune.set("msm_split", 2)
     g = oracle.g1_generator()
     neg = oracle.g1_mul(g, R - 1)
     pts = (g + neg) * 20 + g * 24
@@ -301,10 +301,10 @@ def test_msm_glv_repeated_base_and_negation(ctx, oracle, monkeypatch):
     assert ctx.msm_g1(lam_pts, lam_sc) == oracle.msm_g1(lam_pts, lam_sc)
 
 
-def test_msm_glv_boolean_heavy_2_20(ctx, oracle, monkeypatch):
+def test_msm_glv_boolean_heavy_2_20(ctx, oracle, tune):
     """GLV at the 2^20 config-2 size with Filecoin-like boolean-heavy scalars, against the table-free
     plain path's result (the plain path is pinned against the oracle by the linearity tests)."""
-    monkeypatch.setenv("MI_MSM_SPLIT", "2")
+    tune.set("msm_split", 2)
     n = 1 << 20
     rng = np.random.default_rng(11)
     small = _bases_g1(oracle, 64, 91)
@@ -317,11 +317,11 @@ def test_msm_glv_boolean_heavy_2_20(ctx, oracle, monkeypatch):
     w[full] = rng.integers(0, 2**64, size=(int(full.sum()), 4), dtype=np.uint64)
     w[full, 3] &= np.uint64(0x3FFFFFFFFFFFFFFF)
     sb = w.tobytes()
-    monkeypatch.setenv("MI_MSM_GLV", "0")
-    monkeypatch.setenv("MI_MSM_SPLIT", "0")
+    tune.set("msm_glv", 0)
+    tune.set("msm_split", 0)
     plain = ctx.msm_g1(bases, sb)
-    monkeypatch.setenv("MI_MSM_GLV", "1")
-    monkeypatch.setenv("MI_MSM_SPLIT", "2")
+    tune.set("msm_glv", 1)
+    tune.set("msm_split", 2)
     assert ctx.msm_g1(bases, sb) == plain
     # and the oracle on the 64 distinct bases: sum over i of s_i P_(i mod 64) = sum_j (sum_{i = j mod 64} s_i) P_j
     agg = [0] * 64
@@ -332,17 +332,17 @@ def test_msm_glv_boolean_heavy_2_20(ctx, oracle, monkeypatch):
     assert plain == oracle.msm_g1(small, ab)
 
 
-def test_msm_glv_auto_uploaded_bases(ctx, oracle, monkeypatch):
+def test_msm_glv_auto_uploaded_bases(ctx, oracle, tune):
     """Default policy (MI_MSM_GLV unset): caller-uploaded bases have no 2^128 table, so a split-size G1 MSM
     takes the GLV split; the same MSM with MI_MSM_GLV=0 runs the plain 256-bit path."""
-    monkeypatch.delenv("MI_MSM_GLV", raising=False)
-    monkeypatch.setenv("MI_MSM_SPLIT", "2")
+    tune.clear("msm_glv")
+    tune.set("msm_split", 2)
     n = 3001
     bases = _bases_g1(oracle, n, 4242)
     sb = _glv_scalars(n, 99)
     want = oracle.msm_g1(bases, sb)
     assert ctx.msm_g1(bases, sb) == want
-    monkeypatch.setenv("MI_MSM_GLV", "0")
+    tune.set("msm_glv", 0)
     assert ctx.msm_g1(bases, sb) == want
 
 
@@ -370,13 +370,13 @@ def test_msm_window_table_vs_oracle(ctx, oracle, n, c):
 
 
 @pytest.mark.parametrize("bitsum", ["1", "0"])
-def test_msm_window_table_linearity_2_20(ctx, oracle, monkeypatch, bitsum):
+def test_msm_window_table_linearity_2_20(ctx, oracle, tune, bitsum):
     """BASELINE config-2 size over a window table at the library's window choice and at c = 20 (2^19 buckets in
     one window): MSM(k_i G, s_i) == (sum s_i k_i) G.  bitsum "0" reduces the one window with the running-sum
     kernels instead of the bit-row sums (MI_MSM_BITSUM)."""
     import torch
 
-    monkeypatch.setenv("MI_MSM_BITSUM", bitsum)
+    tune.set("msm_bitsum", int(bitsum))
     n = 1 << 20
     rng = np.random.default_rng(420)
     kw = rng.integers(0, 2**64, size=(n, 4), dtype=np.uint64)

@@ -25,7 +25,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_two_32gib_keys_in_one_context(monkeypatch):
+def test_two_32gib_keys_in_one_context(tune):
     import time
 
     import circuits

@@ -93,11 +93,11 @@ def test_tree_c_golden(ctx, layers):
     assert ints(tree) == P.tree_data(P.hash_columns(labs), 8, 0)
 
 
-def test_tree_c_batched_uploads(ctx, monkeypatch):
+def test_tree_c_batched_uploads(ctx, tune):
     # ragged upload batches (100 columns each over 512 nodes) must not change the result
     labs = [seeded(200 + l, 512) for l in range(11)]
     ref_base = P.hash_columns(labs)
-    monkeypatch.setenv("MI_TREE_BATCH", "100")
+    tune.set("tree_batch", 100)
     base, tree = fg.tree.ColumnTreeBuilder(ctx, 11, 8).add_final_columns(labs)
     assert ints(base) == ref_base
     assert ints(tree) == P.tree_data(ref_base, 8, 0)
@@ -120,11 +120,11 @@ def test_tree_c_device_equals_host(ctx):
 
 
 @pytest.mark.parametrize("discard", [0, 2])
-def test_tree_r_last(ctx, discard, monkeypatch):
+def test_tree_r_last(ctx, discard, tune):
     nodes = 512
     labels, data = seeded(11, nodes), seeded(12, nodes)
     data[0], labels[1] = P.R - 1, P.R - 1  # wrap-around in the encoding
-    monkeypatch.setenv("MI_TREE_BATCH", "96")
+    tune.set("tree_batch", 96)
     replica, tree = fg.tree.generate_tree_r_last(ctx, labels, data, 8, discard)
     ref_rep = [P.encode(k, d) for k, d in zip(labels, data)]
     assert ints(replica) == ref_rep

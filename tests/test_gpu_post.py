@@ -233,14 +233,8 @@ def test_winning_post_32gib_prove_verify(ctx, oracle):
     assert not fg.verify(vk, ic, pub[:-32] + bytes(32), proof)
     # every lane layout and MSM path gives the same bytes: B_G1 on its own lane (default) or sharing B_G2's plan
     # (boolean-heavy B scalars: chunk trees of several levels over one plan), one lane, no window tables
-    import os
-
     want = fg.prove(ctx, pk, gc, z.data_ptr(), 5, 6)
     assert fg.verify(vk, ic, pub, want)
-    for env in ({"MI_PROVE_B1_LANE": "0"}, {"MI_PROVE_B1_LANE": "1"}, {"MI_PROVE_LANES": "1"}, {"MI_MSM_WT": "0"}):
-        os.environ.update(env)
-        try:
-            assert fg.prove(ctx, pk, gc, z.data_ptr(), 5, 6) == want, env
-        finally:
-            for k in env:
-                del os.environ[k]
+    for knobs in ({"prove_b1_lane": 0}, {"prove_b1_lane": 1}, {"prove_lanes": 1}, {"msm_wt": 0}):
+        with fg.tuned(**knobs):
+            assert fg.prove(ctx, pk, gc, z.data_ptr(), 5, 6) == want, knobs

@@ -38,15 +38,10 @@ def key17(ctx):
     test_gpu_groth16.py::test_groth16_golden_generated_srs), its l and b_g2 queries as wire bytes."""
     from fil_groth16 import synth
 
-    import os
-
     sc = synth.SynthCircuit(log_rows=17, n_in=4, seed=11)
     gc = sc.load(ctx)
-    os.environ["MI_MSM_WT_MAX_LOG"] = "0"  # production-window paths: split tables, no window tables
-    try:
+    with fg.tuned(msm_wt_max_log=0):  # production-window paths: split tables, no window tables
         pk = fg.generate_random_parameters(ctx, gc, circuits.toxic())
-    finally:
-        del os.environ["MI_MSM_WT_MAX_LOG"]
     return {"pk": pk, "gc": gc, "l": pk.query(1), "b_g2": pk.query(4)}
 
 
@@ -58,9 +53,9 @@ def _dev(b):
 
 @pytest.mark.parametrize("c", [20, 21, 22])
 @pytest.mark.parametrize("split", ["0", "2"])
-def test_msm_g1_production_windows(ctx, oracle, key17, monkeypatch, c, split):
-    monkeypatch.setenv("MI_MSM_C", str(c))
-    monkeypatch.setenv("MI_MSM_SPLIT", split)
+def test_msm_g1_production_windows(ctx, oracle, key17, tune, c, split):
+    tune.set("msm_c", int(c))
+    tune.set("msm_split", int(split))
     q = key17["l"]
     n = len(q) // 96
     assert n >= 1 << 16
@@ -71,11 +66,11 @@ def test_msm_g1_production_windows(ctx, oracle, key17, monkeypatch, c, split):
 
 @pytest.mark.parametrize("c", [20, 22])
 @pytest.mark.parametrize("level2", ["0", "1"])
-def test_msm_g2_production_windows(ctx, oracle, key17, monkeypatch, c, level2):
+def test_msm_g2_production_windows(ctx, oracle, key17, tune, c, level2):
     """G2 at c = 20 / 22: with 2^19+ level-1 buckets per window the default reduction is the
     second-level MSM ("1"); "0" forces the running-sum kernels."""
-    monkeypatch.setenv("MI_MSM_C", str(c))
-    monkeypatch.setenv("MI_G2_L2", level2)
+    tune.set("msm_c", int(c))
+    tune.set("g2_l2", int(level2))
     q = key17["b_g2"]
     n = min(len(q) // 192, 1 << 15)
     sb = _scalars(n, 7 * c + int(level2))
@@ -84,11 +79,11 @@ def test_msm_g2_production_windows(ctx, oracle, key17, monkeypatch, c, level2):
 
 
 @pytest.mark.parametrize("split", ["0", "2"])
-def test_groth16_production_window_vs_oracle(ctx, oracle, monkeypatch, split):
+def test_groth16_production_window_vs_oracle(ctx, oracle, tune, split):
     """A full prove with every MSM at c = 22 (the 2^26 window), plain and split."""
-    monkeypatch.setenv("MI_MSM_C", "22")
-    monkeypatch.setenv("MI_MSM_WT_MAX_LOG", "0")
-    monkeypatch.setenv("MI_MSM_SPLIT", split)
+    tune.set("msm_c", 22)
+    tune.set("msm_wt_max_log", 0)
+    tune.set("msm_split", int(split))
     n_in, n_aux, rws, z = circuits.random_circuit(36, 5000, n_in=6, n_free=32)
     mats = circuits.to_csr(rws)
     gc = fg.Circuit(ctx, len(rws), n_in, n_aux, mats)
@@ -128,7 +123,7 @@ def test_groth16_2_26_default_settings_verified(ctx, oracle):
     torch.cuda.synchronize()
 
 
-def test_groth16_2_27_config4_default_settings_verified(ctx, oracle, monkeypatch):
+def test_groth16_2_27_config4_default_settings_verified(ctx, oracle, tune):
     """BASELINE config 4 shape (2^27 domain, ~1.3e8 constraints: the 32 GiB PoRep partition size) with
     default settings, as bench.py's config4 leg times it.  The trapdoor discrete logs and both pairing
     verifiers check the proof.  Then the G1 split mode the auto policy did NOT pick is forced on the same
@@ -138,7 +133,7 @@ def test_groth16_2_27_config4_default_settings_verified(ctx, oracle, monkeypatch
 
     from fil_groth16 import synth
 
-    monkeypatch.delenv("MI_MSM_GLV", raising=False)
+    tune.clear("msm_glv")
     sc = synth.SynthCircuit(log_rows=27, n_in=4, seed=3)
     gc = sc.load(ctx)
     assert gc.d == 1 << 27
@@ -159,20 +154,20 @@ def test_groth16_2_27_config4_default_settings_verified(ctx, oracle, monkeypatch
     vk, ic = pk.verifying_key()
     assert fg.verify(vk, ic, sc.z_array()[32:32 * sc.n_in].tobytes(), proof)
     assert oracle.groth16_verify(vk, ic, sc.z_array()[:32 * sc.n_in].tobytes(), raw)
-    monkeypatch.setenv("MI_MSM_GLV", "1" if mode["split_tables"] else "0")
+    tune.set("msm_glv", int("1" if mode["split_tables"] else "0"))
     assert fg.prove(ctx, pk, gc, z.data_ptr(), r, s) == proof
     del z, pk, gc
     torch.cuda.synchronize()
 
 
-def test_msm_g1_non_subgroup_base_stays_exact(ctx, oracle, key17, monkeypatch):
+def test_msm_g1_non_subgroup_base_stays_exact(ctx, oracle, key17, tune):
     """the GLV split assumes phi(P) = lambda P, true only on the r-torsion.  Caller bases are
     checked for the curve equation only, so a 2^16-point MSM (split size) over bases holding on-curve
     points outside the subgroup must still equal sum k_i P_i: auto mode takes the exact plain path for
     them, and mi_points_check_subgroup refuses them.  Clean bases that pass the check take GLV."""
     import badpoints
 
-    monkeypatch.delenv("MI_MSM_GLV", raising=False)
+    tune.clear("msm_glv")
     n = 1 << 16
     q = key17["l"][:96 * n]
     assert key17["pk"].msm_info()["subgroup"]

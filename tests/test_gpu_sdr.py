@@ -78,8 +78,8 @@ def _host_parents(labels, layer, pidx_row):
 
 @pytest.mark.parametrize("prefetch", ["0", "1"])
 @pytest.mark.parametrize("n_layers,nodes,count", [(2, 64, 50), (11, 4096, 3000)])
-def test_sdr_labeling_proofs_gather_vs_oracle(ctx, oracle, n_layers, nodes, count, prefetch, monkeypatch):
-    monkeypatch.setenv("MI_SDR_PREFETCH", prefetch)  # both gather forms (software-pipelined or not)
+def test_sdr_labeling_proofs_gather_vs_oracle(ctx, oracle, n_layers, nodes, count, prefetch, tune):
+    tune.set("sdr_prefetch", int(prefetch))  # both gather forms (software-pipelined or not)
     rng, labels, layers, chal, pidx = _layers_setup(n_layers, nodes, count, nodes + count)
     rid = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
     dev = torch.device("cuda:0")

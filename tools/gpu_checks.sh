@@ -27,7 +27,7 @@ for mode in "$@"; do
       done ;;
     msm20)
       timeout -k 10 200 python3 tools/msm_bench.py --log-rows 20 --reps 50 --table 20 2>&1 | grep "G1 MSM" || exit 1
-      MI_MSM_WT=0 timeout -k 10 200 python3 tools/msm_bench.py --log-rows 20 --reps 50 2>&1 | grep "G1 MSM" || exit 1 ;;
+      timeout -k 10 200 python3 tools/msm_bench.py --log-rows 20 --reps 50 --tune msm_wt=0 2>&1 | grep "G1 MSM" || exit 1 ;;
     trace)
       timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --hip-runtime-trace -d /tmp/wintrace -o run -- \
           $W --winning-reps 10 > $O/trace_bench.json 2> $O/trace_bench.err || exit 1

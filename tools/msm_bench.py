@@ -22,10 +22,15 @@ def main():
     ap.add_argument("--query", type=int, default=0, help="0 h, 1 l, 2 a, 3 b_g1, 4 b_g2")
     ap.add_argument("--table", type=int, default=-1, help="window-table bits (0 = library choice; -1 none)")
     ap.add_argument("--n", type=int, default=0, help="points (default: the whole query)")
+    ap.add_argument("--tune", action="append", default=[], metavar="NAME=VALUE", help="library A/B switch (mi_tune_set)")
     a = ap.parse_args()
     import numpy as np
     import torch
     import fil_groth16 as fg
+
+    for kv in a.tune:
+        k, _, v = kv.partition("=")
+        fg.tune_set(k, int(v))
     from fil_groth16 import synth
     from bench import TOXIC_SEED, splitmix_frs
 
