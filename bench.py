@@ -911,8 +911,9 @@ def main():
                     help="one GPU: the headline shape with a uniform witness, timed proofs (0 skips)")
     ap.add_argument("--stacked-log-nodes", type=int, default=30,
                     help="secondary (one GPU): the 32 GiB stacked-PoRep partition witness + prove (0 skips)")
-    ap.add_argument("--stacked-layers", type=int, default=11)
-    ap.add_argument("--stacked-challenges", type=int, default=18)
+    # default: the 32 GiB PoRep LayerChallenges from select_challenges (11 layers x 18 = ceil(176 / 10) challenges)
+    ap.add_argument("--stacked-layers", type=int, default=None)
+    ap.add_argument("--stacked-challenges", type=int, default=None)
     ap.add_argument("--stacked-reps", type=int, default=2)
     ap.add_argument("--post-sectors", type=int, default=2349,
                     help="Window-PoSt partition: sectors (0 skips the Window-PoSt / config-5 leg)")
@@ -933,6 +934,12 @@ def main():
     ap.add_argument("--tune", action="append", default=[], metavar="NAME=VALUE",
                     help="library A/B switch for the whole run (mi_tune_set, csrc/tune.h; tools' A/B runs only)")
     args = ap.parse_args()
+    if args.stacked_layers is None or args.stacked_challenges is None:
+        from fil_groth16.compound import SECTOR_SIZE_32GIB, porep_layer_challenges
+
+        lc = porep_layer_challenges(SECTOR_SIZE_32GIB)
+        args.stacked_layers = lc.layers if args.stacked_layers is None else args.stacked_layers
+        args.stacked_challenges = lc.max_count if args.stacked_challenges is None else args.stacked_challenges
 
     if "WORLD_SIZE" in os.environ:
         if int(os.environ["WORLD_SIZE"]) != args.gpus:

@@ -11,7 +11,7 @@ from .core import (FR_MODULUS, PROOF_BYTES, SHARE_BYTES, VK_BYTES, Circuit, Cont
                    get_groth_params, PARAMS, META, VK, prove_batch, prove_share, prove_share_ranges, h_coeffs_dev, trapdoor_dlogs, verify, verify_batch)
 from .compound import (MultiProof, partition_count, get_partitions_for_window_post,  # noqa: F401
                        circuit_proofs, seal_commit_phase2_proofs, generate_window_post_proofs,
-                       generate_winning_post_proof)
+                       generate_winning_post_proof, select_challenges, porep_layer_challenges, LayerChallenges)
 from . import tree  # noqa: F401  (Poseidon + tree C / tree R-last builders)
 from . import stacked  # noqa: F401  (stacked-PoRep circuit: R1CS + GPU witness)
 from . import sdr  # noqa: F401  (SDR labelling witness: SHA-256 labels of challenged nodes)

@@ -13,13 +13,52 @@
                                   count, FallbackPoStCompound::prove over them with post_config.priority
   generate_winning_post_proof     generate_winning_post (api/post.hpp:178-230): one partition
   shard_partitions                one process per GPU: partition k goes to rank k % world
+  select_challenges               proofs/parameters.hpp:90-99 (LayerChallenges, porep/stacked/vanilla/challenges.hpp:44-48)
+  porep_layer_challenges          setup_params' challenge selection for a sector size (parameters.hpp:78-88,
+                                  POREP_MINIMUM_CHALLENGES / POREP_PARTITIONS / LAYERS, constants.hpp:65-78)
 """
+from collections import namedtuple
+
 from .core import PROOF_BYTES, prove, prove_batch, verify_batch
 
 
 def partition_count(partitions: int) -> int:
     """core/partitions.hpp:36-38: -1 -> 1, 0 -> -1, p -> p."""
     return 1 if partitions == -1 else (-1 if partitions == 0 else partitions)
+
+
+# porep/stacked/vanilla/challenges.hpp:44-48: {layers, max_count}; challenges_count_all() is max_count (the
+# reference's test pins it: select_challenges(p, 12, 11).challenges_count_all() = 12 / 6 / 3 for p = 1 / 2 / 4,
+# libs/filecoin/test/parameters.cpp:35-43)
+LayerChallenges = namedtuple("LayerChallenges", ["layers", "max_count"])
+LayerChallenges.challenges_count_all = lambda self: self.max_count
+
+SECTOR_SIZE_32GIB = 1 << 35
+SECTOR_SIZE_64GIB = 1 << 36
+# constants.hpp:65-78 (every smaller sector size: 2 challenges, 1 partition, 2 layers)
+POREP_MINIMUM_CHALLENGES = {SECTOR_SIZE_32GIB: 176, SECTOR_SIZE_64GIB: 176}
+POREP_PARTITIONS = {SECTOR_SIZE_32GIB: 10, SECTOR_SIZE_64GIB: 10}
+LAYERS = {SECTOR_SIZE_32GIB: 11, SECTOR_SIZE_64GIB: 11}
+
+
+def select_challenges(partitions: int, minimum_total_challenges: int, layers: int) -> LayerChallenges:
+    """proofs/parameters.hpp:90-99: the smallest per-partition challenge count whose total over the partitions
+    reaches the minimum."""
+    if partitions < 1:
+        raise ValueError("select_challenges: partitions must be >= 1")
+    count = 1
+    guess = LayerChallenges(layers, count)
+    while partitions * guess.challenges_count_all() < minimum_total_challenges:
+        count += 1
+        guess = LayerChallenges(layers, count)
+    return guess
+
+
+def porep_layer_challenges(sector_bytes: int) -> LayerChallenges:
+    """The LayerChallenges setup_params derives for a sector size (parameters.hpp:78-88): 32 / 64 GiB -> 11 layers x
+    18 challenges per partition (176 over 10 partitions); the small test sizes -> 2 layers x 2 challenges."""
+    return select_challenges(POREP_PARTITIONS.get(sector_bytes, 1), POREP_MINIMUM_CHALLENGES.get(sector_bytes, 2),
+                             LAYERS.get(sector_bytes, 2))
 
 
 def get_partitions_for_window_post(total_sector_count: int, sector_count: int):

@@ -190,3 +190,19 @@ def test_tuning_switches_are_explicit_not_environment():
         assert fg.msm_window_bits(1 << 20) != 9
     finally:
         del os.environ["MI_MSM_C"]
+
+
+def test_select_challenges_reference_vectors():
+    """libs/filecoin/test/parameters.cpp:35-43 (partition_layer_challenges_test): select_challenges(p, 12, 11)
+    .challenges_count_all() is 12 / 6 / 3 for 1 / 2 / 4 partitions (and 6 for PoRepProofPartitions(2)); the
+    function is proofs/parameters.hpp:90-99.  The 32 / 64 GiB PoRep partitions take 11 layers x 18 challenges
+    (176 minimum over 10 partitions, constants.hpp:65-78); the small sizes 2 x 2."""
+    f = lambda p: compound.select_challenges(p, 12, 11).challenges_count_all()  # noqa: E731
+    assert (f(1), f(2), f(4)) == (12, 6, 3)
+    assert compound.select_challenges(2, 12, 11).layers == 11
+    assert compound.porep_layer_challenges(compound.SECTOR_SIZE_32GIB) == (11, 18)
+    assert compound.porep_layer_challenges(compound.SECTOR_SIZE_64GIB) == (11, 18)
+    assert compound.porep_layer_challenges(2048) == (2, 2)
+    assert compound.select_challenges(3, 10, 2).challenges_count_all() == 4  # the smallest count reaching 10
+    with pytest.raises(ValueError):
+        compound.select_challenges(0, 12, 11)

@@ -119,7 +119,11 @@ def test_builder_32gib_shape_counts():
     """32 GiB partition: 11 layers, 18 challenges (proofs/parameters.hpp:90-99), 2^30 nodes, tree C / R-last
     8-8 (SectorShape32GiB).  7,237,665 constraints per challenge + 571 shared: 130,278,541, i.e. the ~1.3e8 of
     BASELINE config 4, on a 2^27 domain; 328 inputs."""
-    c = stacked.StackedCircuit(11, 18, 1 << 30, 8, 8, 0, with_r1cs=False)
+    from fil_groth16.compound import SECTOR_SIZE_32GIB, porep_layer_challenges
+
+    lc = porep_layer_challenges(SECTOR_SIZE_32GIB)  # derived, not hard-coded: 176 challenges over 10 partitions
+    assert (lc.layers, lc.challenges_count_all()) == (11, 18)
+    c = stacked.StackedCircuit(lc.layers, lc.challenges_count_all(), 1 << 30, 8, 8, 0, with_r1cs=False)
     assert (c.num_constraints, c.num_inputs) == (130_278_541, 328)
     assert c.info["sha_blocks"] == 18 * (11 * 20 + 30 * 2)
     assert c.info["poseidon_hashes"] == 1 + 18 * (15 + 16 * 10)
