@@ -530,7 +530,8 @@ def window_post_leg(args, fg, ctx, device, rank, world, gdev, dist):
     from fil_groth16.compound import shard_partitions
     from fil_groth16.distributed import (agree_float, balanced_schedule, calibrate_hsplit, calibrate_lead_share,
                                          hsplit_fractions, hsplit_shares, latency_ranges, latency_ranges_hsplit,
-                                         lead_share_from_times, prove_partitions, prove_partitions_balanced)
+                                         lead_share_from_times, prove_partitions, prove_partitions_balanced,
+                                         destroy_group_broadcasters, group_broadcaster)
 
     S, C, nodes = args.post_sectors, args.post_challenges, 1 << args.post_log_nodes
     try:
@@ -656,6 +657,9 @@ def window_post_leg(args, fg, ctx, device, rank, world, gdev, dist):
         for p, rs in tail:
             if rank in rs:
                 share_fn(p, rs.index(rank), len(rs))
+    if dist and tail and latency == "h_split":
+        for p, rs in tail:  # every rank, in schedule order: the tail groups and their first broadcast, untimed
+            group_broadcaster(rs, gdev)
     ctx.synchronize()
     if dist:
         dist.barrier()
@@ -678,6 +682,8 @@ def window_post_leg(args, fg, ctx, device, rank, world, gdev, dist):
     dt = time.perf_counter() - t1
     mine_dt = dt
     st = ctx.stats()
+    if world > 1 and tail and latency == "h_split":
+        destroy_group_broadcasters()  # the tail groups' communicators (created once, at the warm-up step)
     # one GPU: the latency-mode shares the balanced config-5 schedule gives a tail partition, timed one after
     # another (slowest share = that group's tail on g GPUs), assembled and compared with the whole proof
     shares_res = None

@@ -16,6 +16,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <fcntl.h>
+#include <sys/file.h>
 #include <sys/random.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -199,6 +201,20 @@ int mi_get_groth_params(mi_ctx *ctx, const mi_circuit *circuit, const char *id, 
     if (generated) *generated = 0;
     const std::string pp = path_of(id, 0), vp = path_of(id, 2);
     if (!parent_exists(pp)) return fail(MI_ERR_ARG, pp + " has no parent directory");
+    // one reader-or-generator per file at a time: an exclusive lock on <params>.lock, so two processes that both
+    // find the file missing (or malformed) do not pair one's .params with the other's .vk
+    const std::string lp = pp + ".lock";
+    const int lfd = open(lp.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0644);
+    if (lfd < 0) return fail(MI_ERR_INTERNAL, "cannot open " + lp);
+    struct Unlock {
+        int fd;
+        ~Unlock() {
+            flock(fd, LOCK_UN);
+            close(fd);
+        }
+    } unlock{lfd};
+    while (flock(lfd, LOCK_EX) != 0)
+        if (errno != EINTR) return fail(MI_ERR_INTERNAL, "cannot lock " + lp);
     if (file_exists(pp)) {
         const int rc = mi_params_load(ctx, circuit, pp.c_str(), checked, out);
         if (rc == MI_OK) return MI_OK;
@@ -217,18 +233,19 @@ int mi_get_groth_params(mi_ctx *ctx, const mi_circuit *circuit, const char *id, 
     int rc = mi_srs_generate(ctx, circuit, tox, &srs);
     memset(tox, 0, sizeof tox);
     if (rc != MI_OK) return fail(rc, std::string("generating parameters: ") + mi_last_error());
-    // written under a temporary name and renamed, so a concurrent reader never maps a half-written file
-    const std::string tmp = pp + ".tmp" + std::to_string((unsigned long long)getpid());
+    // both files written under temporary names and renamed, so a reader never maps a half-written file; the vk is
+    // rewritten whenever the params are (a .vk left by earlier parameters would no longer verify their proofs)
+    const std::string tag = ".tmp" + std::to_string((unsigned long long)getpid());
+    const std::string tmp = pp + tag, vtmp = vp + tag;
     rc = mi_params_write(ctx, srs, tmp.c_str());
+    if (rc == MI_OK) rc = mi_vk_write(srs, vtmp.c_str());
     if (rc == MI_OK && rename(tmp.c_str(), pp.c_str()) != 0) rc = MI_ERR_INTERNAL;
+    if (rc == MI_OK && rename(vtmp.c_str(), vp.c_str()) != 0) rc = MI_ERR_INTERNAL;
     if (rc != MI_OK) {
         remove(tmp.c_str());
+        remove(vtmp.c_str());
         mi_srs_free(srs);
-        return fail(rc, "cannot write " + pp);
-    }
-    if (!file_exists(vp) && mi_vk_write(srs, vp.c_str()) != MI_OK) {
-        mi_srs_free(srs);
-        return fail(MI_ERR_INTERNAL, "cannot write " + vp);
+        return fail(rc, "cannot write " + pp + " / " + vp);
     }
     *out = srs;
     if (generated) *generated = 1;

@@ -121,15 +121,28 @@ def agree_blinding(count: int, rank: int, device="cpu"):
 MAX_SHARES = 2  # shares one rank contributes to a tail proof (H-split groups: its L/A/B slice, then its H slice)
 
 
+_GROUPS = {}  # (ranks, device) -> process subgroup, created once per schedule (group_broadcaster)
+
+
 def group_broadcaster(ranks, device="cpu"):
     """bcast(tensor) over the process subgroup ``ranks`` from its first rank (the group's lead), in place; every
     process must create the subgroups of a schedule in the same order (torch.distributed.new_group).  Without a
-    process group (one rank) it is the identity."""
+    process group (one rank) it is the identity.  The subgroup is created at the first call for these ranks and
+    reused after it (every step of a schedule asks for the same groups, and each new RCCL communicator holds
+    memory, streams and a lazy setup on its first broadcast); destroy_group_broadcasters frees them.  The first
+    call also runs one small broadcast, so that setup lands outside the caller's timed steps."""
+    import torch
     import torch.distributed as dist
 
     if not (dist.is_available() and dist.is_initialized()):
         return lambda t: (lambda: t)
-    pg = dist.new_group(ranks)
+    key = (tuple(ranks), str(device))
+    pg = _GROUPS.get(key)
+    if pg is None:
+        pg = dist.new_group(list(ranks))  # collective over the whole world: same order on every rank
+        if dist.get_rank() in ranks:
+            dist.broadcast(torch.zeros(1, dtype=torch.uint8, device=device), ranks[0], group=pg)  # warm-up
+        _GROUPS[key] = pg
 
     def bcast(t):
         """starts the broadcast of t (asynchronous: RCCL on its own stream); returns done() -> t, which waits for
@@ -143,6 +156,16 @@ def group_broadcaster(ranks, device="cpu"):
         return done
 
     return bcast
+
+
+def destroy_group_broadcasters():
+    """Frees the subgroups group_broadcaster created (collective: every rank calls it, in the same order)."""
+    import torch.distributed as dist
+
+    for key in list(_GROUPS):
+        pg = _GROUPS.pop(key)
+        if dist.is_available() and dist.is_initialized():
+            dist.destroy_process_group(pg)
 
 
 def prove_partitions_balanced(prove_fn, share_fn, assemble_fn, num_partitions: int, rank: int, world: int,

@@ -477,11 +477,21 @@ def _hsplit_worker(rank, world, port, num_partitions, outdir):
 
         return hsplit_shares(k, rg, h_coeffs, one, bcast)
 
-    buf = prove_partitions_balanced(lambda ids: [P.prove(zb, 300 + p, 400 + p)[0] for p in ids], share_fn,
-                                    lambda p, sh: fg.assemble(ex["vk"], sh, 300 + p, 400 + p), num_partitions, rank,
-                                    world, group_bcast=True)
+    run = lambda: prove_partitions_balanced(lambda ids: [P.prove(zb, 300 + p, 400 + p)[0] for p in ids],  # noqa: E731
+                                            share_fn, lambda p, sh: fg.assemble(ex["vk"], sh, 300 + p, 400 + p),
+                                            num_partitions, rank, world, group_bcast=True)
+    buf = run()
+    from_bcast = used["h_from_bcast"]
+    # the tail groups are created once per schedule, not per step, and freed by
+    # destroy_group_broadcasters
+    from fil_groth16 import distributed as fd
+
+    groups = dict(fd._GROUPS)
+    assert groups and run() == buf and fd._GROUPS == groups
+    fd.destroy_group_broadcasters()
+    assert not fd._GROUPS
     with open(os.path.join(outdir, f"r{rank}.bin"), "wb") as f:
-        f.write(buf + repr(used["h_from_bcast"]).encode())
+        f.write(buf + repr(from_bcast).encode())
     dist.barrier()
     dist.destroy_process_group()
 

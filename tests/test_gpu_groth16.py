@@ -622,6 +622,9 @@ def test_get_groth_params_read_or_generate(ctx, oracle, golden, tmp_path, monkey
     p.write_bytes(p.read_bytes()[:-5])
     pk3, gen3 = fg.get_groth_params(ctx, gc, cid)  # corrupt -> regenerated from OS randomness, valid proof
     assert gen3 and fg.params_inspect(str(p))["h"] == len(ex["h"]) // 96
+    # the stale .vk of the first parameters is replaced by the regenerated key's own
+    pk3.write_vk(str(tmp_path / "pk3.vk"))
+    assert (tmp_path / f"v28-{cid}.vk").read_bytes() == (tmp_path / "pk3.vk").read_bytes() != params_io.vk_bytes(ex)
     vk, ic = pk3.verifying_key()
     raw = fg.prove(ctx, pk3, gc, circuits.z_bytes(z), r, s, want_raw=True)[1]
     assert oracle.groth16_verify(vk, ic, circuits.z_bytes(z)[:32 * n_in], raw)
