@@ -90,6 +90,8 @@ struct mi_points {
     // fixed-base window table (mi_points_precompute) of caller-owned points; a key query's is the key's (Srs::wt)
     void *wt_own = nullptr;
     mi::WinTable wt_user;
+    // MSMs over these points hold it shared, mi_points_precompute exclusive while it swaps wt_own
+    mutable std::shared_mutex wt_mu;
     mi::WinTable wtab() const {
         if (wt_own || !srs) return wt_user;  // a table built on this point set first
         return srs->wt_of(which);
@@ -1158,6 +1160,7 @@ int mi_points_precompute(mi_ctx *ctx, mi_points *p, unsigned window_bits, uint64
             (void)hipFree(t);
             throw;
         }
+        std::unique_lock<std::shared_mutex> swap(p->wt_mu);  // no MSM over these points reads the old table now
         if (p->wt_own) (void)hipFree(p->wt_own);
         p->wt_own = t;
         p->wt_user.p = t;
@@ -1169,6 +1172,9 @@ int mi_points_precompute(mi_ctx *ctx, mi_points *p, unsigned window_bits, uint64
 int mi_points_table_info(const mi_points *p, uint64_t out[3]) {
     return guard([&] {
         need(p && out, "null argument");
+        std::shared_lock<std::shared_mutex> own(p->wt_mu);
+        std::shared_lock<std::shared_mutex> key;  // a key's tables may be released by another context's OOM retry
+        if (p->srs) key = std::shared_lock<std::shared_mutex>(p->srs->use_mu);
         const mi::WinTable t = p->wtab();
         out[0] = t.p ? t.c : 0;
         out[1] = t.p ? t.nwin : 0;
@@ -1183,6 +1189,7 @@ int mi_msm_g1_dev(mi_ctx *ctx, const mi_points *bases, const void *scalars_dev, 
         need(!bases->is_g2, "G2 bases passed to mi_msm_g1_dev");
         need(n <= bases->n, "n exceeds the number of bases");
         CtxLock l(ctx, 0, FENCE);
+        std::shared_lock<std::shared_mutex> own(bases->wt_mu);  // a precompute on these points waits for this MSM
         std::shared_lock<std::shared_mutex> in_use;  // a key's query: its split table stays while this MSM runs
         if (bases->srs) in_use = std::shared_lock<std::shared_mutex>(bases->srs->use_mu);
         mi::g1_xyzz_t r;
@@ -1198,6 +1205,7 @@ int mi_msm_g2_dev(mi_ctx *ctx, const mi_points *bases, const void *scalars_dev, 
         need(bases->is_g2, "G1 bases passed to mi_msm_g2_dev");
         need(n <= bases->n, "n exceeds the number of bases");
         CtxLock l(ctx, 0, FENCE);
+        std::shared_lock<std::shared_mutex> own(bases->wt_mu);  // a precompute on these points waits for this MSM
         std::shared_lock<std::shared_mutex> in_use;  // a key's query: its window table stays while this MSM runs
         if (bases->srs) in_use = std::shared_lock<std::shared_mutex>(bases->srs->use_mu);
         mi::g2_xyzz_t r;

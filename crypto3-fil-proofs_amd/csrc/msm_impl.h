@@ -133,10 +133,14 @@ __global__ void k_digits_wt(const fr_t *__restrict__ scalars, const uint32_t *__
     }
 }
 
+// The compacting digit kernels size their per-wave scratch as DIGITS_BLOCK / 64: gfx950 runs 64-wide waves
+// only (this library builds for gfx950 alone), and every launch of them passes DIGITS_BLOCK as its block size.
+constexpr unsigned DIGITS_BLOCK = 256;
+static_assert(DIGITS_BLOCK % 64 == 0 && DIGITS_BLOCK <= 1024, "whole 64-wide waves per digit block");
 // The same for sparse scalars (witness vectors: mostly 0 / 1, so most window digits are zero): only the non-zero
 // digits are written, compacted at [0, *count) in arbitrary order (per-thread counts, a wave prefix sum and one
 // atomic per wave).  The sort then runs over the entries alone.
-__global__ void __launch_bounds__(256) k_digits_wt_c(const fr_t *__restrict__ scalars, const uint32_t *__restrict__ idx,
+__global__ void __launch_bounds__(DIGITS_BLOCK) k_digits_wt_c(const fr_t *__restrict__ scalars, const uint32_t *__restrict__ idx,
                                                      uint32_t n, unsigned c, unsigned nwin, uint32_t stride,
                                                      uint32_t *__restrict__ count, uint32_t *__restrict__ keys,
                                                      uint32_t *__restrict__ vals) {
@@ -161,7 +165,7 @@ __global__ void __launch_bounds__(256) k_digits_wt_c(const fr_t *__restrict__ sc
     }
     // exclusive prefix over the wave, then over the block's four waves: one atomic per block (the counter is shared
     // by every block of the launch, so per-wave atomics queued behind each other)
-    __shared__ uint32_t wsum[4], bbase;
+    __shared__ uint32_t wsum[DIGITS_BLOCK / 64], bbase;
     const unsigned wave = threadIdx.x >> 6;
     uint32_t incl = mine;
     for (int o = 1; o < 64; o <<= 1) {
@@ -171,7 +175,8 @@ __global__ void __launch_bounds__(256) k_digits_wt_c(const fr_t *__restrict__ sc
     if (lane == 63) wsum[wave] = incl;
     __syncthreads();
     if (threadIdx.x == 0) {
-        const uint32_t t = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        uint32_t t = 0;
+        for (unsigned w = 0; w < DIGITS_BLOCK / 64; w++) t += wsum[w];
         bbase = t ? atomicAdd(count, t) : 0u;
     }
     __syncthreads();
@@ -1130,7 +1135,7 @@ inline bool msm_prepare_wt_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx
         if (sparse) {
             uint32_t *cnt_dev = dmax + 7;
             MI_HIP(hipMemsetAsync(cnt_dev, 0, 4, st));
-            k_digits_wt_c<<<grid_for(nscal, 256), 256, 0, st>>>(scalars, idx, (uint32_t)nscal, cb, nwin,
+            k_digits_wt_c<<<grid_for(nscal, DIGITS_BLOCK), DIGITS_BLOCK, 0, st>>>(scalars, idx, (uint32_t)nscal, cb, nwin,
                                                                 (uint32_t)stride, cnt_dev, keys, vals);
             MI_LAUNCHED(c, "k_digits_wt_c");
             uint32_t *pc = c.pin.as<uint32_t>(1);

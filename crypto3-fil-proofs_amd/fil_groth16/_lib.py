@@ -56,7 +56,10 @@ def torch_sync(ctx):
     the fill or copy that produced an input tensor, or an earlier reader of an output buffer -- with an event
     waited for on the device, not a host synchronisation (include/mi355x_groth16.h, "device pointers").  The
     entries return with their outputs written.  No-op without torch or before CUDA is initialised (the library's
-    default caller stream, the legacy NULL stream, then covers every blocking stream)."""
+    default caller stream, the legacy NULL stream, then covers every blocking stream).  The caller stream is a
+    property of the context, so a Context is meant to be driven from one Python thread (as the C ABI's threading
+    rule says); two threads on one context with different torch streams would race between this call and the
+    entry that follows it."""
     import sys
 
     t = sys.modules.get("torch")

@@ -113,7 +113,9 @@ const char *mi_last_error(void);
 /* stream handle (hipStream_t) the context launches on; external work may be ordered against it */
 int mi_ctx_stream(mi_ctx *ctx, void **stream_out);
 /* the caller stream of the "device pointers" rule above (a hipStream_t on this context's device; NULL = legacy
- * default stream); it stays set for every later call on the context */
+ * default stream); it stays set for every later call on the context.  The setting belongs to the context, not to
+ * the calling thread: a context shared by several host threads that use different caller streams must serialise
+ * each (set, entry) pair itself -- the "threading" rule above (one host thread per context) avoids the question */
 int mi_ctx_set_caller_stream(mi_ctx *ctx, void *stream);
 int mi_ctx_synchronize(mi_ctx *ctx);
 /* Page-locked host memory for witnesses.  The reference hands the prover host-side assignments

@@ -39,6 +39,7 @@ def main():
     ap.add_argument("db")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--md", action="store_true")
+    ap.add_argument("--top", type=int, default=0, help="also list the N kernels with the most device time per call")
     a = ap.parse_args()
     db = sqlite3.connect(a.db)
     rows = [(short(n), s, e) for n, s, e in db.execute("select name, start, end from kernels order by start")]
@@ -48,6 +49,7 @@ def main():
     calls = calls[-a.reps:]
     spans, busy = [], []
     cls = collections.OrderedDict()
+    per_kernel = collections.defaultdict(lambda: [0, 0.0])
     wit = []
     for lo, hi in calls:
         sel = rows[lo:hi]
@@ -59,6 +61,8 @@ def main():
         for n, s, e in sel:
             k = "witness (k_wit_*)" if "k_wit" in n else klass(n)
             cls[k] = cls.get(k, 0.0) + (e - s) / 1e6
+            per_kernel[n][0] += 1
+            per_kernel[n][1] += (e - s) / 1e6
     n = len(calls)
     out = {"calls": n, "span_ms_mean": sum(spans) / n, "busy_ms_mean": sum(busy) / n,
            "idle_ms_mean": (sum(spans) - sum(busy)) / n, "witness_busy_ms_mean": sum(wit) / n,
@@ -70,6 +74,10 @@ def main():
         print("| class | device ms per call (sum over streams) |\n|---|---|")
         for k, v in out["class_ms_per_call"].items():
             print(f"| {k} | {v:.3f} |")
+        if a.top:
+            print("\n| kernel | launches per call | device ms per call |\n|---|---|---|")
+            for name, (cnt, ms) in sorted(per_kernel.items(), key=lambda kv: -kv[1][1])[:a.top]:
+                print(f"| `{name[:70]}` | {cnt / n:g} | {ms / n:.2f} |")
     else:
         import json
 
