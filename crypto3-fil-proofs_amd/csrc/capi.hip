@@ -14,6 +14,20 @@
 #include <thread>
 
 #include "../../include/mi355x_groth16.h"
+
+#include <vector>
+#ifdef MI_FQ_CHECK
+namespace mi {
+// the Fq invariant counters of every translation unit (field.h FqCheckRegistrar; a function-local list, so the
+// registrations of other units' static initialisers never run before it exists)
+static std::vector<const void *> &fq_check_syms() {
+    static std::vector<const void *> v;
+    return v;
+}
+void fq_check_register(const void *symbol) { fq_check_syms().push_back(symbol); }
+static const std::vector<const void *> &fq_check_symbols() { return fq_check_syms(); }
+}  // namespace mi
+#endif
 #include "poseidon_math.h"
 #include "prover.h"
 #include "sdr.h"
@@ -660,6 +674,15 @@ int mi_srs_table_state(const mi_srs *srs, uint64_t out[3]) {
     });
 }
 
+int mi_srs_shared_la(const mi_srs *srs, int *present) {
+    return guard([&] {
+        need(srs && present, "null argument");
+        const mi::Srs &s = *srs->p;
+        std::shared_lock<std::shared_mutex> in_use(s.use_mu);
+        *present = s.a_aux ? 1 : 0;
+    });
+}
+
 int mi_srs_window_tables(const mi_srs *srs, uint64_t out[3]) {
     return guard([&] {
         need(srs && out, "null argument");
@@ -688,6 +711,28 @@ int mi_ctx_inject_oom(mi_ctx *ctx, int64_t count) {
         need(ctx != nullptr, "null ctx");
         CtxLock l(ctx);
         ctx->c.inject_oom = count;
+    });
+}
+
+int mi_fq_check_read(uint64_t out[2], int reset) {
+    return guard([&] {
+        need(out != nullptr, "null argument");
+        out[0] = out[1] = 0;
+#ifdef MI_FQ_CHECK
+        for (const void *sym : mi::fq_check_symbols()) {
+            unsigned int h[2] = {0, 0};
+            MI_HIP(hipMemcpyFromSymbol(h, sym, sizeof h, 0, hipMemcpyDeviceToHost));
+            out[0] += h[0];
+            out[1] += h[1];
+            if (reset) {
+                const unsigned int z[2] = {0, 0};
+                MI_HIP(hipMemcpyToSymbol(sym, z, sizeof z, 0, hipMemcpyHostToDevice));
+            }
+        }
+#else
+        (void)reset;
+        throw std::invalid_argument("library built without MI_FQ_CHECK (make fqcheck)");
+#endif
     });
 }
 
@@ -1482,6 +1527,13 @@ int mi_ctx_get_work(mi_ctx *ctx, uint64_t out[2]) {
         CtxLock l(ctx);
         out[0] = ctx->c.stats.madds_g1;
         out[1] = ctx->c.stats.madds_g2;
+    });
+}
+int mi_ctx_get_shared_plans(mi_ctx *ctx, uint64_t *out) {
+    return guard([&] {
+        need(ctx && out, "null argument");
+        CtxLock l(ctx);
+        *out = ctx->c.stats.shared_la;
     });
 }
 int mi_ctx_get_table_msms(mi_ctx *ctx, uint64_t out[2]) {

@@ -135,11 +135,13 @@ struct Stats {
     uint64_t oom_retries = 0;      // proofs re-run after an out-of-memory error (prover.hip groth16_sums)
     uint64_t oom_freed_bytes = 0;  // split tables + scratch released for those retries
     uint64_t wt_msms = 0, wt_msms_g2 = 0;  // G1 / G2 MSMs that ran over a window table (msm_run_wt)
+    uint64_t shared_la = 0;                // proofs whose L and A MSMs ran over one shared plan (Srs::a_aux)
     static constexpr int NK = 13;
     void merge(const Stats &o) {
         madds_g1 += o.madds_g1;
         wt_msms += o.wt_msms;
         wt_msms_g2 += o.wt_msms_g2;
+        shared_la += o.shared_la;
         madds_g2 += o.madds_g2;
         KStat *d[] = {&accum_g1, &accum_g2, &msm_g1, &msm_g2, &sort, &ntt, &prove, &h2d, &poseidon, &tree_h2d,
                       &wit_a, &wit_sha, &wit_pos};
@@ -313,6 +315,9 @@ struct MsmPlan {
 // false when every scalar is zero (the MSM is the identity).  split: plan the 2n half-scalar points of
 // the 2^128-shifted base table (msm_g1 with bases_hi); the plan then needs bases_hi too.
 bool msm_prepare(Ctx &c, const fr_t *scalars, const uint32_t *idx, uint64_t n, MsmPlan &plan, bool split = false);
+// the plan msm_g1 takes for subgroup bases without a 2^128 table: GLV split above the split threshold, plain below;
+// one plan serves several G1 base sets over the same scalars (msm_g1_planned), e.g. L and the aux part of A
+bool msm_prepare_g1_shared(Ctx &c, const fr_t *scalars, uint64_t n, MsmPlan &plan);
 void msm_g1_planned(Ctx &c, const MsmPlan &plan, const g1_affine_t *bases, g1_xyzz_t *result_host,
                     const g1_affine_t *bases_hi = nullptr);
 void msm_g2_planned(Ctx &c, const MsmPlan &plan, const g2_affine_t *bases, g2_xyzz_t *result_host);

@@ -23,6 +23,21 @@
 
 namespace mi {
 
+// MI_FQ_CHECK (a debug build, `make fqcheck`; off in release): the device group law counts violations of the Fq
+// magnitude invariant instead of trusting the comments -- [0] a normalised value with |top limb| > 2^24 (|V| beyond
+// ~9.8 p: fq_norm's host-only magnitude control would have been needed), [1] fq_is_zero with |round(V / p)| > 3 (the
+// group law's sums are argued to stay below 3 p).  Counters, not asserts: a device trap would fault the GPU.  Each
+// translation unit has its own counters and registers their host shadow at load (mi_fq_check_read sums them).
+#ifdef MI_FQ_CHECK
+__device__ static unsigned int g_fq_check[2];
+void fq_check_register(const void *symbol);
+struct FqCheckRegistrar {
+    FqCheckRegistrar() { fq_check_register((const void *)&g_fq_check); }
+};
+static FqCheckRegistrar g_fq_check_registrar;
+#define MI_FQ_CHECK_HIT(i) atomicAdd(&g_fq_check[i], 1u)
+#endif
+
 struct FqDesc {
     static constexpr int N = 12;
     static constexpr uint32_t INV = 0xfffcfffdu;  // -p^-1 mod 2^32
@@ -403,6 +418,9 @@ MI_HD bool fq_is_kp(const fq_t &a, int32_t k) {
 // register-light steps (an inlined 64-bit V - k p here cost the accumulation kernel 50 registers)
 MI_HD bool fq_is_zero(const fq_t &a) {
     int32_t k = fq_quot(a);
+#if defined(MI_FQ_CHECK) && defined(__HIP_DEVICE_COMPILE__)
+    if (k > 3 || k < -3) MI_FQ_CHECK_HIT(1);
+#endif
     if ((((uint32_t)a.v[0] - (uint32_t)k * (uint32_t)Fq30::P[0]) & Fq30::M) != 0) return false;
     fq_t x = a;
     while (k > 3) {  // only far-out representatives (never in the group law, whose values stay below 3 p)
@@ -434,6 +452,8 @@ MI_HD fq_t fq_norm(const int32_t *t) {
 #if !defined(__HIP_DEVICE_COMPILE__)
     const int32_t top = r.v[12] < 0 ? -r.v[12] : r.v[12];
     if (__builtin_expect(top > (1 << 24), 0)) r = fq_sub_kp(r, fq_quot(r));
+#elif defined(MI_FQ_CHECK)
+    if (r.v[12] > (1 << 24) || r.v[12] < -(1 << 24)) MI_FQ_CHECK_HIT(0);
 #endif
     return r;
 }

@@ -88,6 +88,11 @@ bool msm_prepare(Ctx &c, const fr_t *scalars, const uint32_t *idx, uint64_t n, M
     return msm_prepare_impl(c, scalars, idx, n, plan, split);
 }
 
+bool msm_prepare_g1_shared(Ctx &c, const fr_t *scalars, uint64_t n, MsmPlan &plan) {
+    const bool glv = msm_use_split(n) && msm_glv_mode() != 0;
+    return msm_prepare_impl(c, scalars, nullptr, n, plan, false, glv);
+}
+
 void msm_g1_planned(Ctx &c, const MsmPlan &plan, const g1_affine_t *bases, g1_xyzz_t *result_host,
                     const g1_affine_t *bases_hi) {
     if (!plan.total) {

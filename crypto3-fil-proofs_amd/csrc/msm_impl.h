@@ -561,25 +561,49 @@ __global__ void k_tree_count(const uint32_t *__restrict__ mlist, const uint32_t 
 
 // the first tree level's quotas before m is known on the host: over all nb slots, zero from *m_dev on; and every
 // level's partial count, totals[l] = sum_i ceil(ceil(n_i / L1^l) / L1) for the levels the largest bucket needs
-// (stride L1^l below ceil(*maxcnt / L0); wave sums, one atomic per wave and level), so the tree runs without a host
-// round trip per level.  L1 is a power of two (shifts, no division).
+// (stride L1^l below ceil(*maxcnt / L0)), so the tree runs without a host round trip per level.  L1 is a power of
+// two (shifts, no division).  TC_PER buckets per thread and one atomic per block and level: a wave-level atomic
+// put ~200 K same-address atomics per level into a 2^27-point plan (4 ms per launch in the Window-PoSt proof).
+constexpr unsigned TC_PER = 8;
 __global__ void __launch_bounds__(256) k_tree_count_l1(const uint32_t *__restrict__ mlist,
                                                        const uint32_t *__restrict__ ccnt,
                                                        const uint32_t *__restrict__ m_dev,
                                                        const uint32_t *__restrict__ maxcnt, uint32_t L0, uint32_t nb,
                                                        unsigned lg1, uint32_t *__restrict__ qcnt,
                                                        uint32_t *__restrict__ totals) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t n = i < nb && i < *m_dev ? ccnt[mlist[i]] : 0u;
+    __shared__ uint32_t part[TREE_MAXL][4];
+    const uint32_t m = *m_dev;
     const uint32_t mask1 = (1u << lg1) - 1;
-    if (i < nb) qcnt[i] = (n + mask1) >> lg1;
     const uint32_t maxchunks = (*maxcnt + L0 - 1) / L0;
-    unsigned s = 0;  // stride = 2^s
-    for (unsigned l = 0; l < TREE_MAXL && s < 32 && (1u << s) < maxchunks; l++, s += lg1) {
-        const uint32_t parts = n ? ((n - 1) >> s) + 1 : 0u;
-        uint32_t q = (parts + mask1) >> lg1;
-        for (int o = 32; o; o >>= 1) q += __shfl_xor(q, o);
-        if ((threadIdx.x & 63) == 0 && q) atomicAdd(&totals[l], q);
+    unsigned nlev = 0;  // levels with stride 2^(l lg1) below maxchunks
+    for (unsigned s = 0; nlev < TREE_MAXL && s < 32 && (1u << s) < maxchunks; s += lg1) nlev++;
+    uint32_t acc[TREE_MAXL];
+    MI_UNROLL for (unsigned l = 0; l < TREE_MAXL; l++) acc[l] = 0;
+    const uint32_t i0 = blockIdx.x * (256 * TC_PER) + threadIdx.x;
+    for (unsigned j = 0; j < TC_PER; j++) {
+        const uint32_t i = i0 + j * 256;
+        const uint32_t n = i < nb && i < m ? ccnt[mlist[i]] : 0u;
+        if (i < nb) qcnt[i] = (n + mask1) >> lg1;
+        MI_UNROLL for (unsigned l = 0; l < TREE_MAXL; l++) {
+            if (l < nlev) {
+                const unsigned s = l * lg1;
+                const uint32_t parts = n ? ((n - 1) >> s) + 1 : 0u;
+                acc[l] += (parts + mask1) >> lg1;
+            }
+        }
+    }
+    const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    MI_UNROLL for (unsigned l = 0; l < TREE_MAXL; l++) {
+        if (l < nlev) {
+            uint32_t q = acc[l];
+            for (int o = 32; o; o >>= 1) q += __shfl_xor(q, o);
+            if (lane == 0) part[l][wave] = q;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < nlev) {
+        const uint32_t t = part[threadIdx.x][0] + part[threadIdx.x][1] + part[threadIdx.x][2] + part[threadIdx.x][3];
+        if (t) atomicAdd(&totals[threadIdx.x], t);
     }
 }
 
@@ -920,7 +944,8 @@ inline void plan_counts(Ctx &c, MsmPlan &pl, const uint32_t *cntA, uint32_t *off
     MI_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, ids, flag, mlist, m_dev, nb, st));
     tmp = c.scratch[4].get(tb);
     MI_HIP(hipcub::DeviceSelect::Flagged(tmp, tb, ids, flag, mlist, m_dev, nb, st));
-    k_tree_count_l1<<<grid_for(nb, 256), 256, 0, st>>>(mlist, ccnt, m_dev, maxcnt_dev, L0, nb, lg1, qcnt, totals);
+    k_tree_count_l1<<<grid_for(nb, 256 * TC_PER), 256, 0, st>>>(mlist, ccnt, m_dev, maxcnt_dev, L0, nb, lg1, qcnt,
+                                                                 totals);
     MI_LAUNCHED(c, "k_tree_count_l1");
     tb = 0;
     MI_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, qcnt, qoff, nb, st));

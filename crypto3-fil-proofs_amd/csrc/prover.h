@@ -63,7 +63,11 @@ struct Srs {
         t.nwin = (256 + wt_c - 1) / wt_c;
         return t;
     }
-    bool has_tables() const { return h_hi || l_hi || a_hi || wt[0] || wt[1] || wt[2] || wt[3] || wt[4]; }
+    // the A query gathered into the aux index space (a_aux[v] = the A point of aux variable v, the affine infinity
+    // where v has no A density), built at load for subgroup-checked large keys: L and the aux part of A then share
+    // ONE GLV plan over z_aux (groth16_sums "shared L/A plan"); the inputs' part of A is a[0, n_in)
+    g1_affine_t *a_aux = nullptr;
+    bool has_tables() const { return h_hi || l_hi || a_hi || a_aux || wt[0] || wt[1] || wt[2] || wt[3] || wt[4]; }
     g2_affine_t *b_g2 = nullptr;
     g1_affine_t alpha_g1, beta_g1, delta_g1;
     g2_affine_t beta_g2, gamma_g2, delta_g2;
@@ -130,6 +134,9 @@ struct SrsStream {
     void *dst[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     uint64_t n[5] = {0, 0, 0, 0, 0}, filled[5] = {0, 0, 0, 0, 0};
     int *bad = nullptr;  // 5 queries x {malformed, infinity, outside subgroup}
+    // the circuit's A density (idx_a, copied at begin: the circuit may be freed before end) for Srs::a_aux
+    uint32_t *a_idx = nullptr;
+    uint64_t n_in = 0, n_aux = 0;
 };
 SrsStream *srs_stream_begin(Ctx &c, const Circuit *circ, const SrsHost &h, bool checked);
 void srs_stream_part(Ctx &c, SrsStream &st, int which, uint64_t first, const uint8_t *bytes, uint64_t n, bool on_device);

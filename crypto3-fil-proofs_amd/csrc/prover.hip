@@ -16,8 +16,10 @@
 
 #include <string.h>
 
+#include <atomic>
 #include <exception>
 #include <cstring>
+#include <future>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -232,6 +234,16 @@ __global__ void k_lc_scalars(const fr_t *__restrict__ at, const fr_t *__restrict
     uint64_t v = off + i;
     out[i] = from_mont((beta * at[v] + alpha * bt[v] + ct[v]) * inv);
 }
+// Srs::a_aux: A point j (an aux variable's, j >= n_in: idx[j] - n_in) moves to its aux position; the rest stays the
+// affine infinity (0, 0) of the zero-filled array
+__global__ void k_gather_a_aux(const g1_affine_t *__restrict__ a, const uint32_t *__restrict__ idx, uint64_t m,
+                               uint64_t n_in, uint64_t n_aux, g1_affine_t *__restrict__ out) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    const uint64_t v = (uint64_t)idx[j] - n_in;
+    if (v < n_aux) out[v] = a[j];
+}
+
 __global__ void k_gather_canon(const fr_t *__restrict__ src, const uint32_t *__restrict__ idx, uint64_t n,
                                fr_t *__restrict__ out) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -491,7 +503,7 @@ Srs::~Srs() {
                 break;
             }
     }
-    void *ps[] = {h_perm, l, a, b_g1, b_g2, at, bt, ct, h_hi, l_hi, a_hi, wt[0], wt[1], wt[2], wt[3], wt[4]};
+    void *ps[] = {h_perm, l, a, b_g1, b_g2, at, bt, ct, h_hi, l_hi, a_hi, a_aux, wt[0], wt[1], wt[2], wt[3], wt[4]};
     for (void *p : ps)
         if (p) hipFree(p);
 }
@@ -715,7 +727,7 @@ Circuit *circuit_load(Ctx &c, const R1csHost &cs) {
 // (staged through a bounded buffer) or from device memory (a received RCCL broadcast buffer: decoded in
 // place, no host copy).  Per query the chunks must arrive in order.
 namespace {
-void build_hi_tables(Ctx &c, Srs &S);
+void build_hi_tables(Ctx &c, Srs &S, const uint32_t *a_idx = nullptr, uint64_t n_in = 0, uint64_t n_aux = 0);
 const char *kQueryName[5] = {"h", "l", "a", "b_g1", "b_g2"};
 }
 
@@ -736,6 +748,12 @@ SrsStream *srs_stream_begin(Ctx &c, const Circuit *circ, const SrsHost &h, bool 
             if (h.n_b_g1 != circ->n_b || h.n_b_g2 != circ->n_b)
                 throw std::invalid_argument("|b_g1| / |b_g2| != B-density of the circuit");
             if (h.n_ic != circ->n_in) throw std::invalid_argument("|ic| != number of inputs");
+            if (circ->n_a > circ->n_in && circ->idx_a) {  // for Srs::a_aux at end (build_a_aux)
+                st->a_idx = dalloc<uint32_t>(circ->n_a);
+                MI_HIP(hipMemcpyAsync(st->a_idx, circ->idx_a, 4 * circ->n_a, hipMemcpyDeviceToDevice, c.stream));
+                st->n_in = circ->n_in;
+                st->n_aux = circ->n_aux;
+            }
         }
         if (h.n_b_g1 != h.n_b_g2) throw std::invalid_argument("|b_g1| != |b_g2|");
         S->n_h = h.n_h;
@@ -835,7 +853,7 @@ Srs *srs_stream_end(Ctx &c, SrsStream *st) {
         hipFree(st->hnat);
         st->hnat = nullptr;
         S->in_subgroup = st->checked;
-        build_hi_tables(c, *S);
+        build_hi_tables(c, *S, st->a_idx, st->n_in, st->n_aux);
     } catch (...) {
         srs_stream_abort(st);
         throw;
@@ -850,6 +868,7 @@ void srs_stream_abort(SrsStream *st) {
     if (!st) return;
     if (st->hnat) hipFree(st->hnat);
     if (st->bad) hipFree(st->bad);
+    if (st->a_idx) hipFree(st->a_idx);
     delete st->S;  // ~Srs frees the queries allocated so far
     delete st;
 }
@@ -1005,7 +1024,9 @@ void build_split_tables(Ctx &c, Srs &S) {
         const g1_affine_t *src;
         uint64_t n;
         g1_affine_t **dst;
-    } qs[] = {{S.h_perm, S.n_h, &S.h_hi}, {S.l, S.n_l, &S.l_hi}, {S.a, S.n_a, &S.a_hi}};
+    } qs[] = {{S.h_perm, S.n_h, &S.h_hi},
+              {S.a_aux ? nullptr : S.l, S.n_l, &S.l_hi},  // with a_aux, L and A run over one GLV plan: no table
+              {S.a_aux ? nullptr : S.a, S.n_a, &S.a_hi}};
     if (msm_glv_mode() == 2) {  // auto: tables only while they leave the prover its working set
         uint64_t need = 0;
         for (auto &q : qs) need += q.src && msm_use_split(q.n) ? q.n * sizeof(g1_affine_t) : 0;
@@ -1038,10 +1059,41 @@ void build_split_tables(Ctx &c, Srs &S) {
     }
 }
 
-// every MSM table of a key: the window tables of a small key, else the split tables
-void build_hi_tables(Ctx &c, Srs &S) {
+// Srs::a_aux (the shared L/A plan): for subgroup keys whose L MSM takes the split path, while the gathered query
+// leaves a proof its working set (the split tables' admission rule, counted before them).  a_idx = the circuit's A
+// density (bellman a_aux_density: every input, then the aux variables with A entries, ascending).
+void build_a_aux(Ctx &c, Srs &S, const uint32_t *a_idx, uint64_t n_in, uint64_t n_aux) {
+    if (!a_idx || !S.a || !S.in_subgroup || msm_glv_mode() == 0 || n_aux != S.n_l || S.n_a <= n_in ||
+        !msm_use_split(n_aux))
+        return;
+    size_t free_b = 0, total_b = 0;
+    MI_HIP(hipMemGetInfo(&free_b, &total_b));
+    const uint64_t need = n_aux * sizeof(g1_affine_t);
+    const uint64_t big = S.d > S.n_l ? S.d : S.n_l;
+    const uint64_t work = 32 * (S.n_l + 3 * S.d) + 2 * 360 * big;
+    if (need + work + work / 10 + (8ull << 30) > free_b) return;
+    try {
+        S.a_aux = dalloc<g1_affine_t>(n_aux);
+        MI_HIP(hipMemsetAsync(S.a_aux, 0, need, c.stream));
+        const uint64_t m = S.n_a - n_in;
+        k_gather_a_aux<<<grid1(m), 256, 0, c.stream>>>(S.a + n_in, a_idx + n_in, m, n_in, n_aux, S.a_aux);
+        MI_HIP(hipGetLastError());
+    } catch (const hip_error &e) {
+        if (e.code != hipErrorOutOfMemory) throw;
+        (void)hipStreamSynchronize(c.stream);
+        (void)hipGetLastError();
+        if (S.a_aux) (void)hipFree(S.a_aux);
+        S.a_aux = nullptr;
+    }
+}
+
+// every MSM table of a key: the window tables of a small key, else the gathered A query (when the circuit's A density
+// is given) and the split tables
+void build_hi_tables(Ctx &c, Srs &S, const uint32_t *a_idx, uint64_t n_in, uint64_t n_aux) {
     build_window_tables(c, S);
-    if (!S.has_tables()) build_split_tables(c, S);
+    if (S.has_tables()) return;
+    build_a_aux(c, S, a_idx, n_in, n_aux);
+    build_split_tables(c, S);
 }
 }  // namespace
 
@@ -1226,7 +1278,7 @@ Srs *srs_generate_once(Ctx &c, const Circuit &circ, const fr_t toxic_canonical[5
         S->beta_g2 = host_mul_affine(g2, toxic_canonical[2]);
         S->gamma_g2 = host_mul_affine(g2, toxic_canonical[3]);
         S->delta_g2 = host_mul_affine(g2, toxic_canonical[4]);
-        build_hi_tables(c, *S);
+        build_hi_tables(c, *S, circ.idx_a, circ.n_in, circ.n_aux);
     } catch (...) {
         (void)hipStreamSynchronize(st);  // no kernel may still write the buffers freed below
         delete S;
@@ -1379,6 +1431,45 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
                    srs.in_subgroup, &wt, a_lo);
             if (out.premul) out.sA = host::xyzz_mul(As, rg.premul_s->v, 8);
         };
+        // Shared L/A plan (Srs::a_aux, VERDICT r5 #1b).  L sums z_aux over l and A's aux part sums the same z_aux over
+        // a_aux (A's points in the aux index space, infinity where a variable has no A density), so ONE plan (digits,
+        // sort, bucket bounds, chunking: a GLV plan for these subgroup keys) serves both, and the input part of A,
+        // a[0, n_in) with z[0, n_in), is a small MSM of its own.  The auxiliary lane builds the plan after B and runs
+        // L's accumulation over it; the main lane runs A's accumulation over the same plan after H (a host handoff
+        // of the plan's counts plus a device event): one plan fewer per proof, the lanes' work as before.
+        const bool shared_la = !wide && srs.a_aux && rg.lo[1] == 0 && rg.cnt[1] == circ.n_aux && rg.lo[2] == 0 &&
+                               rg.cnt[2] == circ.n_a && circ.n_a > circ.n_in && msm_glv_mode() != 0;
+        std::promise<MsmPlan> la_plan;
+        std::future<MsmPlan> la_plan_f = la_plan.get_future();
+        std::atomic<bool> la_handed{false};
+        hipEvent_t la_ready = shared_la ? c.timer.get() : nullptr;
+        g1_xyzz_t A_aux = g1_xyzz_t::inf();
+        auto run_la_plan = [&](Ctx &x) {  // the shared plan, on the lane that runs L; handed to A's lane
+            MsmPlan pl;
+            msm_prepare_g1_shared(x, z_dev + circ.n_in, circ.n_aux, pl);  // pl.total == 0: every scalar zero
+            MI_HIP(hipEventRecord(la_ready, x.stream));
+            la_handed = true;
+            la_plan.set_value(pl);
+            return pl;
+        };
+        auto run_l_shared = [&](Ctx &x) {
+            const MsmPlan pl = run_la_plan(x);
+            msm_g1_planned(x, pl, srs.l, &Lq);
+            return pl;
+        };
+        auto finish_a = [&](Ctx &x) {  // A = A_aux + the inputs' part (idx_a starts with every input)
+            g1_xyzz_t A_in = g1_xyzz_t::inf();
+            msm_g1(x, srs.a, z_dev, nullptr, circ.n_in, &A_in, nullptr, srs.in_subgroup, nullptr, 0);
+            As = host::xyzz_add(A_aux, A_in);
+            if (out.premul) out.sA = host::xyzz_mul(As, rg.premul_s->v, 8);
+        };
+        auto run_a_shared = [&](Ctx &x) {  // A's lane: wait for the plan, accumulate A_aux over it
+            const MsmPlan pl = la_plan_f.get();
+            MI_HIP(hipStreamWaitEvent(x.stream, la_ready, 0));
+            msm_g1_planned(x, pl, srs.a_aux, &A_aux);
+            finish_a(x);
+        };
+        if (shared_la) c.stats.shared_la += 1;
         // aux-lane order: B before L (same-box A/B at 2^26: -2 ms per proof; tune::AUX_ORDER = 1
         // restores L first)
         const bool b_first = tune::get(tune::AUX_ORDER, 0) != 1;
@@ -1386,7 +1477,14 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
             try {
                 Ctx &x = *lane_ctx[k];
                 MI_HIP(hipSetDevice(c.device));
-                if (!wide) {
+                if (!wide && shared_la) {
+                    run_b(x);
+                    const MsmPlan pl = run_l_shared(x);
+                    if (one_lane) {  // the main lane is done: A over the same plan here, after L
+                        msm_g1_planned(x, pl, srs.a_aux, &A_aux);
+                        finish_a(x);
+                    }
+                } else if (!wide) {
                     if (b_first) run_b(x);
                     run_l(x);
                     if (!b_first) run_b(x);
@@ -1402,6 +1500,8 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
                 MI_HIP(hipEventRecord(done[k], x.stream));
             } catch (...) {
                 err[k] = std::current_exception();
+                // a lane that fails before handing over the shared plan must not leave A's lane waiting for it
+                if (shared_la && k == 0 && !la_handed.exchange(true)) la_plan.set_exception(err[k]);
             }
         };
         std::thread lanes[3];
@@ -1420,7 +1520,8 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
                        srs.in_subgroup, &wt_h, h_lo);
             else
                 H = g1_xyzz_t::inf();
-            if (!wide) run_a(c);
+            if (!wide && !shared_la) run_a(c);
+            if (shared_la && !one_lane) run_a_shared(c);
         } catch (...) {
             err_main = std::current_exception();
         }
@@ -1437,6 +1538,7 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
             lane_ctx[k]->timer.pool.push_back(done[k]);
         }
         c.timer.pool.push_back(ready);
+        if (la_ready) c.timer.pool.push_back(la_ready);
         if (!one_lane) {
             for (unsigned k = 0; k < nlanes; k++) {
                 Ctx &x = *lane_ctx[k];
@@ -1466,6 +1568,11 @@ uint64_t srs_drop_split_tables(Srs &S) {
             *t.p = nullptr;
             freed += t.n * sizeof(g1_affine_t);
         }
+    if (S.a_aux) {  // derived like the tables; an out-of-memory retry runs L and A over plans of their own
+        (void)hipFree(S.a_aux);
+        S.a_aux = nullptr;
+        freed += S.n_l * sizeof(g1_affine_t);
+    }
     for (int q = 0; q < 5; q++)
         if (S.wt[q]) {
             freed += S.wt_bytes(q);

@@ -38,7 +38,7 @@ EXPORTS = [
     "mi_stacked_build", "mi_post_build", "mi_stacked_info", "mi_stacked_r1cs", "mi_stacked_load", "mi_stacked_public_inputs", "mi_stacked_witness_dev",
     "mi_stacked_witness", "mi_stacked_free", "mi_circuit_check_dev",
     "mi_points_precompute", "mi_points_table_info", "mi_ctx_get_table_msms", "mi_srs_window_tables",
-    "mi_tune_set", "mi_tune_clear", "mi_tune_get",
+    "mi_tune_set", "mi_tune_clear", "mi_tune_get", "mi_fq_check_read", "mi_srs_shared_la", "mi_ctx_get_shared_plans",
 ]
 
 _lib = None
@@ -118,6 +118,7 @@ def lib():
         "mi_srs_readmit": ([vp, vp, vp], c_int),
         "mi_ctx_inject_oom": ([vp, ctypes.c_int64], c_int),
         "mi_tune_set": ([u8p, ctypes.c_int64], c_int),
+        "mi_fq_check_read": ([vp, c_int], c_int),
         "mi_tune_clear": ([u8p], c_int),
         "mi_tune_get": ([u8p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(c_int)], c_int),
         "mi_param_cache_id": ([u8p, u8p, vp, ctypes.c_size_t], c_int),
@@ -150,6 +151,8 @@ def lib():
         "mi_points_table_info": ([vp, vp], c_int),
         "mi_ctx_get_table_msms": ([vp, vp], c_int),
         "mi_srs_window_tables": ([vp, vp], c_int),
+        "mi_srs_shared_la": ([vp, ctypes.POINTER(c_int)], c_int),
+        "mi_ctx_get_shared_plans": ([vp, ctypes.POINTER(ctypes.c_uint64)], c_int),
         "mi_groth16_prove": ([vp, vp, vp, u8p, u8p, u8p, c_int, vp, vp], c_int),
         "mi_groth16_prove_dev": ([vp, vp, vp, vp, u8p, u8p, c_int, vp, vp], c_int),
         "mi_groth16_prove_batch": ([vp, vp, vp, u64, vp, u8p, c_int, vp], c_int),

@@ -101,6 +101,12 @@ class Context:
         check(lib().mi_ctx_get_fallbacks(self.h, w))
         return {"oom_retries": int(w[0]), "freed_bytes": int(w[1])}
 
+    def shared_plans(self) -> int:
+        """proofs since the last reset_stats whose L and A MSMs shared one plan (mi_ctx_get_shared_plans)"""
+        w = ctypes.c_uint64(0)
+        check(lib().mi_ctx_get_shared_plans(self.h, ctypes.byref(w)))
+        return int(w.value)
+
     def table_msms(self, g2: bool = False) -> int:
         """G1 (G2 with g2) MSMs that ran over a fixed-base window table since the last reset_stats
         (mi_ctx_get_table_msms)"""
@@ -354,6 +360,13 @@ class ProvingKey:
         out = (ctypes.c_uint64 * 3)()
         check(lib().mi_srs_table_state(self.h, out))
         return {"split_tables": bool(out[0]), "dropped": int(out[1]), "subgroup": bool(out[2])}
+
+    def shared_la(self) -> bool:
+        """True when the key holds its A query in the aux index space: whole proofs run L and A over one plan
+        (mi_srs_shared_la)"""
+        v = ctypes.c_int(0)
+        check(lib().mi_srs_shared_la(self.h, ctypes.byref(v)))
+        return bool(v.value)
 
     def window_tables(self):
         """{"window_bits", "windows", "queries"}: the fixed-base window tables of a small key (mi_srs_window_tables)"""

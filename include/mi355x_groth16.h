@@ -176,6 +176,13 @@ int mi_srs_table_state(const mi_srs *srs, uint64_t out[3]);
  * they fit; mi_points_precompute explains them): out[0] window bits, out[1] windows, out[2] queries with a table
  * (0..5: h, l, a, b_g1, b_g2).  Out-of-memory releases take them like the split tables, and mi_srs_readmit rebuilds them. */
 int mi_srs_window_tables(const mi_srs *srs, uint64_t out[3]);
+/* the shared L/A plan of large subgroup keys: *present = 1 when the key holds its A query gathered into the aux index
+ * space (built at load / generation when it fits, next to the split tables' admission rule), so a whole proof's L and
+ * A MSMs run over one plan (the inputs' part of A as a small MSM of its own); an out-of-memory release drops it like
+ * the tables (the retry runs L and A over plans of their own) and mi_srs_readmit does not rebuild it.  The MSM sums,
+ * and so the proof bytes, are those of separate plans.  No reference counterpart (bellman runs the L and A multiexps
+ * one after the other, over the same z). */
+int mi_srs_shared_la(const mi_srs *srs, int *present);
 int mi_srs_readmit(mi_ctx *ctx, mi_srs *srs, uint64_t *rebuilt_bytes);
 void mi_srs_free(mi_srs *srs);
 
@@ -441,6 +448,8 @@ int mi_ctx_get_fallbacks(mi_ctx *ctx, uint64_t out[2]);
 /* G1 (out[0]) and G2 (out[1]) MSMs run over a window table (mi_points_precompute, a small key's tables) since the
  * last reset */
 int mi_ctx_get_table_msms(mi_ctx *ctx, uint64_t out[2]);
+/* proofs since the last reset whose L and A MSMs ran over one shared plan (mi_srs_shared_la) */
+int mi_ctx_get_shared_plans(mi_ctx *ctx, uint64_t *out);
 /* TEST ONLY: the first attempt of each of the next `count` proofs on this context fails with a real out-of-memory
  * error after its NTT chain (count < 0: every proof until reset to 0), so the release-and-retry path runs at any
  * size.  Production code never calls it; nothing in the prove path reads the environment for it. */
@@ -453,6 +462,10 @@ int mi_ctx_inject_oom(mi_ctx *ctx, int64_t count);
  * default, mi_tune_clear(NULL) all of them; mi_tune_get reports whether a switch is set and its value.  No reference
  * counterpart (the reference has no GPU path to tune). */
 int mi_tune_set(const char *name, int64_t value);
+/* DEBUG BUILD ONLY (make fqcheck: -DMI_FQ_CHECK): violations of the device Fq magnitude invariant counted since load
+ * (or the last reset) -- out[0] normalised values with |top limb| > 2^24, out[1] zero tests with |round(V / p)| > 3
+ * (csrc/field.h).  A release build returns MI_ERR_ARG. */
+int mi_fq_check_read(uint64_t out[2], int reset);
 int mi_tune_clear(const char *name);
 int mi_tune_get(const char *name, int64_t *value, int *is_set);
 /* msm window size chosen for n points (exposed for tests / reports) */

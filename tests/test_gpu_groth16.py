@@ -133,6 +133,43 @@ def test_groth16_split_msm_vs_oracle(ctx, oracle, tune, split):
     assert fg.assemble(vk, shares, r, s) == op.prove(zb, r, s)[0]
 
 
+@pytest.mark.parametrize("n_in", [2, 6, 300])
+def test_groth16_shared_la_plan_vs_oracle(ctx, oracle, tune, n_in):
+    """VERDICT r5 #1b: a large subgroup key holds its A query in the aux index space (mi_srs_shared_la), so a whole
+    proof's L and A MSMs run over ONE GLV plan -- built on the auxiliary lane, L accumulated there, A's aux part on
+    the main lane after H, the inputs' part of A as a small MSM -- and the proof equals the oracle's byte for byte.
+    Forced at a size the oracle proves in seconds (split at any size, no window tables, the two-lane layout of large
+    proofs).  The aux variables without A density (random_circuit's later outputs) sit at infinity in the gathered
+    query.  One lane, latency-mode shares (separate plans over ranges) and an out-of-memory retry (which drops the
+    gathered query: separate plans again) give the same bytes."""
+    tune.set("msm_split", 2)
+    tune.set("msm_wt_max_log", 0)
+    tune.set("prove_wide_log", 0)
+    n_in_, n_aux, rws, z = circuits.random_circuit(37 + n_in, 4000, n_in=n_in, n_free=32)
+    oc, gc = _load(ctx, oracle, n_in_, n_aux, rws, z)
+    tox = circuits.toxic(37)
+    pk = fg.generate_random_parameters(ctx, gc, tox)
+    assert pk.shared_la()
+    op = oracle.OracleParams(oc, tox)
+    zb = circuits.z_bytes(z)
+    want = op.prove(zb, 5, 6)[0]
+    ctx.reset_stats()
+    assert fg.prove(ctx, pk, gc, zb, 5, 6) == want
+    assert ctx.shared_plans() == 1
+    tune.set("prove_lanes", 1)
+    assert fg.prove(ctx, pk, gc, zb, 5, 6) == want
+    tune.clear("prove_lanes")
+    assert ctx.shared_plans() == 2
+    vk, _ = pk.verifying_key()
+    assert fg.assemble(vk, [fg.prove_share(ctx, pk, gc, zb, k, 2) for k in range(2)], 5, 6) == want
+    assert ctx.shared_plans() == 2  # shares run over ranges: plans of their own
+    zeros = zb[:32 * n_in_] + bytes(32 * n_aux)  # every aux scalar zero: an empty shared plan
+    assert fg.prove(ctx, pk, gc, zeros, 5, 6) == op.prove(zeros, 5, 6)[0]
+    ctx.inject_oom(1)
+    assert fg.prove(ctx, pk, gc, zb, 7, 8) == op.prove(zb, 7, 8)[0]
+    assert not pk.shared_la() and ctx.fallbacks()["oom_retries"] == 1
+
+
 def test_prove_out_of_memory_degrades_to_glv(ctx, oracle, tune):
     """A proof whose scratch allocation fails (mi_ctx_inject_oom, a test-only entry: the main lane raises
     hipMalloc's out-of-memory error after the NTT chain while the auxiliary lane runs) is re-run in-process after

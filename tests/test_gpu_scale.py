@@ -8,6 +8,8 @@
   by the trapdoor discrete logs and by the pairing verifier.
 Bit-exact comparisons throughout.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -156,7 +158,52 @@ def test_groth16_2_27_config4_default_settings_verified(ctx, oracle, tune):
     assert oracle.groth16_verify(vk, ic, sc.z_array()[:32 * sc.n_in].tobytes(), raw)
     tune.set("msm_glv", int("1" if mode["split_tables"] else "0"))
     assert fg.prove(ctx, pk, gc, z.data_ptr(), r, s) == proof
-    del z, pk, gc
+    tune.clear("msm_glv")
+    # the production-size key load every prover process does once per shape (get_groth_params ->
+    # read_cached_params -> build_mapped_parameters, core/parameter_cache.hpp:124-128,185-200; mmap at
+    # core/crypto/mapped_scheme_params.hpp:50-60): this key written as a v28 params file (mi_params_write), freed,
+    # loaded back through mi_params_load unchecked and with every point subgroup-checked, and the loaded key proves
+    # the same bytes.  The file normally sits in the page cache right after being written, so the rates are the
+    # mmap + decode + upload (+ check) path's, not a cold disk's.
+    import gc as pygc
+    import json
+    import shutil
+    import tempfile
+    import time
+
+    counts = (pk.n_h, pk.n_l, pk.n_a, pk.n_b)
+    nbytes = 96 * sum(counts) + 192 * pk.n_b + 96 * (sc.n_in + 9)
+    tmpd = tempfile.mkdtemp(dir=os.environ.get("TMPDIR", "/tmp"))
+    rec = {"queries": dict(zip(("h", "l", "a", "b"), counts)), "file_bytes": nbytes,
+           "disk_free_bytes": shutil.disk_usage(tmpd).free}
+    try:
+        if rec["disk_free_bytes"] < 1.1 * nbytes:
+            rec["skipped"] = "scratch disk too small for the params file"
+        else:
+            path = os.path.join(tmpd, "config4.params")
+            t0 = time.perf_counter()
+            pk.write_params(path)
+            rec["write_s"] = time.perf_counter() - t0
+            del pk
+            pygc.collect()
+            torch.cuda.synchronize()
+            for checked in (False, True):
+                t0 = time.perf_counter()
+                pk2 = fg.ProvingKey.load_params(ctx, gc, path, checked=checked)
+                ctx.synchronize()
+                t = time.perf_counter() - t0
+                rec["load_checked_s" if checked else "load_s"] = t
+                rec["load_checked_GBps" if checked else "load_GBps"] = nbytes / t / 1e9
+                if checked:
+                    assert pk2.msm_info()["subgroup"]
+                    assert fg.prove(ctx, pk2, gc, z.data_ptr(), r, s) == proof
+                del pk2
+                pygc.collect()
+            rec["subgroup_check_s"] = rec["load_checked_s"] - rec["load_s"]
+    finally:
+        shutil.rmtree(tmpd, ignore_errors=True)
+    print("[params-2^27] " + json.dumps(rec), flush=True)
+    del z, gc
     torch.cuda.synchronize()
 
 

@@ -8,6 +8,7 @@
 #   post64    the 64 GiB Window-PoSt partition test with its record lines
 #   witness   the stacked / PoSt witness and Poseidon parity tests
 #   bench     the default bench line (python3 bench.py) into $O/bench.json
+#   wpab      the Window-PoSt leg, default and with each switch of WPAB="name=value ..." (--tune A/B)
 # usage: /usr/local/graft/bin/gpurun --timeout 1200 -- bash tools/gpu_checks.sh parity winning
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
@@ -46,6 +47,12 @@ for mode in "$@"; do
     bench)
       timeout -k 10 900 python3 bench.py > $O/bench.json 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
       tail -c 400 $O/bench.json ;;
+    wpab)  # the 32 GiB Window-PoSt leg (two lanes, as the driver bench runs it), default and with each WPAB switch
+      for v in default ${WPAB:-}; do
+        T=(); [ "$v" = default ] || T=(--tune "$v")
+        timeout -k 10 300 $W --post-sectors 2349 --post-reps 2 --post-share-groups "" --winning-log-nodes 0 "${T[@]}" > $O/wp_$v.json 2> $O/wp_$v.err || { tail -5 $O/wp_$v.err; exit 1; }
+        python3 -c "import json; w = json.load(open('$O/wp_$v.json'))['window_post_32gib']; print('window-post $v', round(w['ms_per_partition_rank0'], 1), w['verified'])"
+      done ;;
     post64)
       timeout -k 10 900 python3 -u -m pytest -x -q -s --timeout 800 --timeout-method thread tests/test_gpu_post.py -k 64gib > $O/post64.log 2>&1 || exit 1
       grep "window-post-64\|passed" $O/post64.log ;;
