@@ -1066,6 +1066,12 @@ void build_a_aux(Ctx &c, Srs &S, const uint32_t *a_idx, uint64_t n_in, uint64_t 
     if (!a_idx || !S.a || !S.in_subgroup || msm_glv_mode() == 0 || n_aux != S.n_l || S.n_a <= n_in ||
         !msm_use_split(n_aux))
         return;
+    // A's accumulation over the shared plan also adds the infinity points of the aux variables without A density
+    // (a full mixed addition each: a wave's lanes run in lockstep), so the plan it saves must outweigh them: a plan
+    // costs ~25 ps per entry against ~130 ps per mixed addition (profiles/r06_*), break-even near 84 % density.
+    // The Window-PoSt partition's A covers 99.6 % of its aux variables; the synthetic config-3 circuit's 66 %
+    // (measured there: 480 ms per proof shared, 461 ms with separate plans over the split tables).
+    if ((S.n_a - n_in) * 10 < n_aux * 9) return;
     size_t free_b = 0, total_b = 0;
     MI_HIP(hipMemGetInfo(&free_b, &total_b));
     const uint64_t need = n_aux * sizeof(g1_affine_t);
