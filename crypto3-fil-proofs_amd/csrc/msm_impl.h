@@ -57,7 +57,11 @@ namespace {
 #define MI_WAVES_RED MI_WAVES2  // the reduction kernels keep the two-wave cap (see g2pair.h LaneRed)
 #endif
 
-constexpr uint32_t L0_DEFAULT = 64;  // sorted entries per chunk at level 0 (mixed adds); tune::MSM_L0 overrides
+// sorted entries per chunk at level 0 (mixed adds); tune::MSM_L0 overrides.  Plans of >= 2^24 points per window take
+// L0_LARGE: round 6, same box, alternating, 128 against 64 took the 32 GiB Window-PoSt partition (128 entries per
+// bucket on average) from 1,514.9 to 1,483.7 ms and the config-3 proof (64 per bucket) from 469.5 to 468.4 ms (fewer
+// chunk-tree additions).  Smaller, latency-bound plans keep the shorter chains.
+constexpr uint32_t L0_DEFAULT = 64, L0_LARGE = 128;
 constexpr uint32_t L1_DEFAULT = 16;  // chunk partials summed per thread per tree level (full adds); tune::MSM_L1 overrides
 constexpr unsigned TREE_MAXL = 16;   // chunk-tree levels counted with the plan (L1 >= 4: up to 4^16 chunks a bucket)
 
@@ -918,8 +922,9 @@ inline void plan_counts(Ctx &c, MsmPlan &pl, const uint32_t *cntA, uint32_t *off
                         const uint32_t *maxcnt_dev, uint32_t *stage) {
     hipStream_t st = c.stream;
     // tune::MSM_L0 / MSM_L1 (tuning A/B): entries per level-0 chunk, partials per tree-level thread (a power of two)
-    const int64_t t0 = tune::get(tune::MSM_L0, L0_DEFAULT), t1 = tune::get(tune::MSM_L1, L1_DEFAULT);
-    uint32_t L0 = t0 >= 2 && t0 <= 1024 ? (uint32_t)t0 : L0_DEFAULT, L1 = t1 >= 4 && t1 <= 64 ? (uint32_t)t1 : L1_DEFAULT;
+    const uint32_t l0_auto = pl.n >= (1ull << 24) ? L0_LARGE : L0_DEFAULT;
+    const int64_t t0 = tune::get(tune::MSM_L0, l0_auto), t1 = tune::get(tune::MSM_L1, L1_DEFAULT);
+    uint32_t L0 = t0 >= 2 && t0 <= 1024 ? (uint32_t)t0 : l0_auto, L1 = t1 >= 4 && t1 <= 64 ? (uint32_t)t1 : L1_DEFAULT;
     if (L1 < 4 || L1 > 64 || (L1 & (L1 - 1))) L1 = L1_DEFAULT;
     unsigned lg1 = 0;
     while ((1u << lg1) < L1) lg1++;
