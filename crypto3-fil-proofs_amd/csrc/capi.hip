@@ -20,12 +20,16 @@
 namespace mi {
 // the Fq invariant counters of every translation unit (field.h FqCheckRegistrar; a function-local list, so the
 // registrations of other units' static initialisers never run before it exists)
-static std::vector<const void *> &fq_check_syms() {
-    static std::vector<const void *> v;
+struct FqCheckUnit {
+    const void *symbol;
+    const char *unit;
+};
+static std::vector<FqCheckUnit> &fq_check_syms() {
+    static std::vector<FqCheckUnit> v;
     return v;
 }
-void fq_check_register(const void *symbol) { fq_check_syms().push_back(symbol); }
-static const std::vector<const void *> &fq_check_symbols() { return fq_check_syms(); }
+void fq_check_register(const void *symbol, const char *unit) { fq_check_syms().push_back({symbol, unit}); }
+static const std::vector<FqCheckUnit> &fq_check_symbols() { return fq_check_syms(); }
 }  // namespace mi
 #endif
 #include "poseidon_math.h"
@@ -719,14 +723,18 @@ int mi_fq_check_read(uint64_t out[2], int reset) {
         need(out != nullptr, "null argument");
         out[0] = out[1] = 0;
 #ifdef MI_FQ_CHECK
-        for (const void *sym : mi::fq_check_symbols()) {
-            unsigned int h[2] = {0, 0};
-            MI_HIP(hipMemcpyFromSymbol(h, sym, sizeof h, 0, hipMemcpyDeviceToHost));
+        for (const auto &u : mi::fq_check_symbols()) {
+            unsigned int h[4] = {0, 0, 0, 0};
+            MI_HIP(hipMemcpyFromSymbol(h, u.symbol, sizeof h, 0, hipMemcpyDeviceToHost));
             out[0] += h[0];
             out[1] += h[1];
+            // debug build: where the counts come from (per translation unit), the largest |k| of a zero test and the
+            // largest |top limb| / 2^20 of a normalised value
+            fprintf(stderr, "[fq-check] %s: top-limb %u, zero-test |k| > 3 %u, max |k| %u, max |top| %u x 2^20\n",
+                    u.unit, h[0], h[1], h[2], h[3]);
             if (reset) {
-                const unsigned int z[2] = {0, 0};
-                MI_HIP(hipMemcpyToSymbol(sym, z, sizeof z, 0, hipMemcpyHostToDevice));
+                const unsigned int z[4] = {0, 0, 0, 0};
+                MI_HIP(hipMemcpyToSymbol(u.symbol, z, sizeof z, 0, hipMemcpyHostToDevice));
             }
         }
 #else

@@ -233,4 +233,71 @@ MI_HD bool in_prime_subgroup(const Affine<F> &a) {
     return xyzz_mul_inl(xyzz_from_affine(a), r, 8).is_inf();
 }
 
+// Endomorphism membership tests (the checked key load's kernel, round 6): ~70 group operations per point instead of
+// the ~384 of r P, the tests of Scott, "A note on group membership tests for G1, G2 and GT on BLS pairing-friendly
+// curves" (eprint 2021/1130, proof of correctness eprint 2022/352), as zkcrypto's bls12_381 is_torsion_free runs them:
+//   G1: sigma(P) == -[z^2] P,  sigma(x, y) = (beta^2 x, y), beta^2 the cube root of unity acting as -z^2 on G1 (the
+//       other root, glv.h's beta, acts as z^2 - 1);
+//   G2: psi(P) == [z] P,  psi(x, y) = (conj(x) cx, conj(y) cy), cx = (1 + u)^-((p - 1) / 3), cy = (1 + u)^-((p - 1) / 2)
+// with z = -0xd201000000010000.  tests/host/grouplaw_check.cpp compares both with r P == O on subgroup points, on
+// the non-subgroup points of the GPU tests and on cofactor-torsion and mixed points; the constants were derived and
+// the tests checked the same way over Python integers first.
+constexpr uint64_t BLS_Z_ABS = 0xd201000000010000ull;
+// canonical little-endian words: beta^2, cx (c0 = 0), cy
+constexpr uint32_t SUBGROUP_BETA2_RAW[12] = {0xfffefffeu, 0x2e01ffffu, 0x620a0002u, 0xde17d813u, 0xe6f89688u,
+                                             0xddb3a93bu, 0x6a0f77eau, 0xba69c607u, 0xdf76ce51u, 0x5f19672fu,
+                                             0x00000000u, 0x00000000u};
+constexpr uint32_t SUBGROUP_CX1_RAW[12] = {0x0000aaadu, 0x8bfd0000u, 0x4f49fffdu, 0x409427ebu, 0x0fb85f9bu,
+                                           0x897d2965u, 0x89759ad4u, 0xaa0d857du, 0x63d4de85u, 0xec024086u,
+                                           0x397fe699u, 0x1a0111eau};
+constexpr uint32_t SUBGROUP_CY0_RAW[12] = {0x121bdea2u, 0xf1ee7b04u, 0x3e67fa0au, 0x304466cfu, 0xf61eb45eu,
+                                           0xef396489u, 0x30b1cf60u, 0x1c3dedd9u, 0xd77a2cd9u, 0xe2e9c448u,
+                                           0x0180a68eu, 0x135203e6u};
+constexpr uint32_t SUBGROUP_CY1_RAW[12] = {0xede3cc09u, 0xc81084fbu, 0x72ec05f4u, 0xee67992fu, 0x009241c5u,
+                                           0x77f76e17u, 0xc2d3435eu, 0x48395dabu, 0x6bd17ffeu, 0x6831e36du,
+                                           0x37ff400bu, 0x06af0e04u};
+struct SubgroupConsts {
+    fq_t beta2;
+    fq2_t cx, cy;
+};
+inline SubgroupConsts subgroup_consts() {  // host: the Montgomery images, passed to the kernel
+    auto fq = [](const uint32_t *w) {
+        fq32_t raw;
+        for (int i = 0; i < 12; i++) raw.v[i] = w[i];
+        return fq_from_raw(raw);
+    };
+    SubgroupConsts s;
+    s.beta2 = fq(SUBGROUP_BETA2_RAW);
+    s.cx = {fq_t::zero(), fq(SUBGROUP_CX1_RAW)};
+    s.cy = {fq(SUBGROUP_CY0_RAW), fq(SUBGROUP_CY1_RAW)};
+    return s;
+}
+// [|z|] q by double-and-add over the 6 set bits of |z| (64 doublings)
+template <class F>
+MI_HD XYZZ<F> xyzz_mul_zabs_inl(const XYZZ<F> &q) {
+    XYZZ<F> r = q;  // bit 63
+#pragma unroll 1
+    for (int b = 62; b >= 0; b--) {
+        r = xyzz_dbl_inl(r);
+        if ((BLS_Z_ABS >> b) & 1) r = xyzz_add_inl(r, q);
+    }
+    return r;
+}
+// XYZZ q equals the affine (x, y): X = x ZZ and Y = y ZZZ (q finite)
+template <class F>
+MI_HD bool xyzz_eq_affine(const XYZZ<F> &q, const F &x, const F &y) {
+    return !q.is_inf() && q.X == x * q.ZZ && q.Y == y * q.ZZZ;
+}
+MI_HD bool in_prime_subgroup_fast(const Affine<fq_t> &a, const SubgroupConsts &s) {
+    if (a.is_inf()) return true;
+    const XYZZ<fq_t> z2 = xyzz_mul_zabs_inl(xyzz_mul_zabs_inl(xyzz_from_affine(a)));  // [z^2] P
+    return xyzz_eq_affine(z2, s.beta2 * a.x, -a.y);                                  // == -sigma(P)
+}
+MI_HD bool in_prime_subgroup_fast(const Affine<fq2_t> &a, const SubgroupConsts &s) {
+    if (a.is_inf()) return true;
+    const XYZZ<fq2_t> q = xyzz_mul_zabs_inl(xyzz_from_affine(a));  // [|z|] P = -[z] P
+    const fq2_t px = fq2_t{a.x.c0, -a.x.c1} * s.cx, py = fq2_t{a.y.c0, -a.y.c1} * s.cy;
+    return xyzz_eq_affine(q, px, -py);  // -[z] P == -psi(P)
+}
+
 }  // namespace mi

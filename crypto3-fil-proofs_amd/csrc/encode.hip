@@ -85,13 +85,14 @@ __global__ void k_g2_decode(const uint8_t *__restrict__ in, g2_affine_t *__restr
     out[i] = a;
 }
 
-// r * P == O for every decoded point (the checked load); bad[2] counts points outside the subgroup
+// prime-order-subgroup membership of every decoded point (the checked load; curve.h in_prime_subgroup_fast, the
+// endomorphism tests -- round 6; r P == O before, 4-5x the group operations); bad[2] counts points outside it
 template <class F>
 __global__ void __launch_bounds__(256) k_subgroup(const Affine<F> *__restrict__ pts, uint64_t n,
-                                                  int *__restrict__ bad) {
+                                                  int *__restrict__ bad, const SubgroupConsts sc) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    if (!in_prime_subgroup(pts[i])) atomicAdd(&bad[2], 1);
+    if (!in_prime_subgroup_fast(pts[i], sc)) atomicAdd(&bad[2], 1);
 }
 
 // entries >= r (not a valid Fr: core/fr32.hpp:36-40) -> *bad += 1
@@ -189,12 +190,14 @@ void g2_decode_uncompressed(Ctx &c, const uint8_t *dev_bytes, g2_affine_t *out, 
 }
 void g1_subgroup_check(Ctx &c, const g1_affine_t *pts, uint64_t n, int *bad_dev) {
     if (!n) return;
-    k_subgroup<fq_t><<<grid1(n), 256, 0, c.stream>>>(pts, n, bad_dev);
+    static const SubgroupConsts sc = subgroup_consts();
+    k_subgroup<fq_t><<<grid1(n), 256, 0, c.stream>>>(pts, n, bad_dev, sc);
     MI_HIP(hipGetLastError());
 }
 void g2_subgroup_check(Ctx &c, const g2_affine_t *pts, uint64_t n, int *bad_dev) {
     if (!n) return;
-    k_subgroup<fq2_t><<<grid1(n), 256, 0, c.stream>>>(pts, n, bad_dev);
+    static const SubgroupConsts sc = subgroup_consts();
+    k_subgroup<fq2_t><<<grid1(n), 256, 0, c.stream>>>(pts, n, bad_dev, sc);
     MI_HIP(hipGetLastError());
 }
 void fr_count_noncanonical(Ctx &c, const fr_t *d, uint64_t n, int *bad_dev, hipStream_t st) {

@@ -28,14 +28,21 @@ namespace mi {
 // ~9.8 p: fq_norm's host-only magnitude control would have been needed), [1] fq_is_zero with |round(V / p)| > 3 (the
 // group law's sums are argued to stay below 3 p).  Counters, not asserts: a device trap would fault the GPU.  Each
 // translation unit has its own counters and registers their host shadow at load (mi_fq_check_read sums them).
+// Round 6, the MSM / window-table / prove parity tests under the debug build (profiles/r06/fq_check_debug_build.log):
+// the top-limb bound held in every unit (largest |top limb| 11 x 2^20 of the 16 x 2^20 allowed); the MSM units never
+// zero-tested |k| > 3; prover.hip's key-table doubling chains (window / split tables, key generation) did so 1,694
+// times with |k| = 4, which fq_is_zero's reduction loop handles -- so |k| <= 3 is the MSM group law's property, not
+// a library-wide one, and the loop is what makes the zero test exact everywhere.
 #ifdef MI_FQ_CHECK
-__device__ static unsigned int g_fq_check[2];
-void fq_check_register(const void *symbol);
+// [0], [1] the two counts above, [2] the largest |round(V / p)| a zero test saw, [3] the largest |top limb| >> 20
+__device__ static unsigned int g_fq_check[4];
+void fq_check_register(const void *symbol, const char *unit);
 struct FqCheckRegistrar {
-    FqCheckRegistrar() { fq_check_register((const void *)&g_fq_check); }
+    FqCheckRegistrar() { fq_check_register((const void *)&g_fq_check, __BASE_FILE__); }
 };
 static FqCheckRegistrar g_fq_check_registrar;
 #define MI_FQ_CHECK_HIT(i) atomicAdd(&g_fq_check[i], 1u)
+#define MI_FQ_CHECK_MAX(i, v) atomicMax(&g_fq_check[i], (unsigned int)(v))
 #endif
 
 struct FqDesc {
@@ -419,7 +426,10 @@ MI_HD bool fq_is_kp(const fq_t &a, int32_t k) {
 MI_HD bool fq_is_zero(const fq_t &a) {
     int32_t k = fq_quot(a);
 #if defined(MI_FQ_CHECK) && defined(__HIP_DEVICE_COMPILE__)
-    if (k > 3 || k < -3) MI_FQ_CHECK_HIT(1);
+    if (k > 3 || k < -3) {
+        MI_FQ_CHECK_HIT(1);
+        MI_FQ_CHECK_MAX(2, k < 0 ? -k : k);
+    }
 #endif
     if ((((uint32_t)a.v[0] - (uint32_t)k * (uint32_t)Fq30::P[0]) & Fq30::M) != 0) return false;
     fq_t x = a;
@@ -454,6 +464,7 @@ MI_HD fq_t fq_norm(const int32_t *t) {
     if (__builtin_expect(top > (1 << 24), 0)) r = fq_sub_kp(r, fq_quot(r));
 #elif defined(MI_FQ_CHECK)
     if (r.v[12] > (1 << 24) || r.v[12] < -(1 << 24)) MI_FQ_CHECK_HIT(0);
+    MI_FQ_CHECK_MAX(3, (r.v[12] < 0 ? -r.v[12] : r.v[12]) >> 20);
 #endif
     return r;
 }

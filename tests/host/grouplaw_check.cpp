@@ -20,6 +20,7 @@
 #include "glv.h"
 #include "hostfield.h"
 #include "oracle.h"
+#include "subgroup_vectors.h"
 
 using namespace mi;
 
@@ -466,7 +467,48 @@ static void check_glv() {
     }
 }
 
+// the endomorphism membership tests of the checked key load (curve.h in_prime_subgroup_fast) against r P == O: on
+// random multiples of the generators (members), and on on-curve points outside the subgroup -- random ones,
+// cofactor-torsion points [r] Q and subgroup + torsion sums (subgroup_vectors.h)
+static void check_subgroup_tests() {
+    const SubgroupConsts sc = subgroup_consts();
+    auto unhex = [](const char *h, uint8_t *out, int n) {
+        for (int i = 0; i < n; i++) std::sscanf(h + 2 * i, "%2hhx", &out[i]);
+    };
+    auto g2from = [](const uint8_t *p) -> g2_affine_t {
+        if (p[0] & 0x40) return g2_affine_t::inf();
+        return {{fq_from_be(p + 48), fq_from_be(p)}, {fq_from_be(p + 144), fq_from_be(p + 96)}};
+    };
+    uint8_t g1g[96], g2g[192];
+    or_g1_generator(g1g);
+    or_g2_generator(g2g);
+    for (int it = 0; it < 12; it++) {
+        uint8_t s[32], p1[96], p2[192];
+        rand_scalar(s);
+        or_g1_mul(g1g, s, p1);
+        or_g2_mul(g2g, s, p2);
+        const g1_affine_t a1 = g1_from_bytes(p1);
+        const g2_affine_t a2 = g2from(p2);
+        CHECK(in_prime_subgroup(a1) && in_prime_subgroup_fast(a1, sc), "g1 member it=%d", it);
+        CHECK(in_prime_subgroup(a2) && in_prime_subgroup_fast(a2, sc), "g2 member it=%d", it);
+    }
+    CHECK(in_prime_subgroup_fast(g1_affine_t::inf(), sc) && in_prime_subgroup_fast(g2_affine_t::inf(), sc), "inf");
+    for (const char *h : G1_NON_SUBGROUP) {
+        uint8_t b[96];
+        unhex(h, b, 96);
+        const g1_affine_t a = g1_from_bytes(b);
+        CHECK(g1_on_curve(a) && !in_prime_subgroup(a) && !in_prime_subgroup_fast(a, sc), "g1 non-member %.16s", h + 80);
+    }
+    for (const char *h : G2_NON_SUBGROUP) {
+        uint8_t b[192];
+        unhex(h, b, 192);
+        const g2_affine_t a = g2from(b);
+        CHECK(g2_on_curve(a) && !in_prime_subgroup(a) && !in_prime_subgroup_fast(a, sc), "g2 non-member %.16s", h + 80);
+    }
+}
+
 int main() {
+    check_subgroup_tests();
     check_fields();
     check_growth();
     check_host_field();
