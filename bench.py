@@ -507,6 +507,46 @@ def stacked_leg(args, fg, ctx, device, world):
     return res
 
 
+def params_roundtrip(fg, ctx, circ, pk, zhost, rs):
+    """setup_s.params_load: the resident key written as a bellman/filecoin v28 params file under TMPDIR, loaded back
+    through mi_params_load unchecked (mmap + decode + upload) and checked (+ every point's subgroup test), and a proof
+    from the checked key compared byte for byte with the resident key's.  The file normally stays in the page cache
+    after the write, so the rates are the load path's, not a cold disk's (disk rate unmeasured)."""
+    import gc
+    import shutil
+    import tempfile
+
+    nbytes = 96 * (pk.n_h + pk.n_l + pk.n_a + pk.n_b) + 192 * pk.n_b + 96 * (circ.num_inputs + 9)
+    tmpd = tempfile.mkdtemp(dir=os.environ.get("TMPDIR", "/tmp"))
+    rec = {"file_bytes": nbytes, "disk_free_bytes": shutil.disk_usage(tmpd).free,
+           "note": "page-cache rates (the file was just written); cold-disk rate unmeasured"}
+    try:
+        if rec["disk_free_bytes"] < 1.1 * nbytes:
+            rec["skipped"] = "scratch disk too small for the params file"
+            return rec
+        path = os.path.join(tmpd, "key.params")
+        t0 = time.perf_counter()
+        pk.write_params(path)
+        rec["write_s"] = time.perf_counter() - t0
+        want = fg.prove_batch(ctx, pk, circ, [zhost], [rs])[0]
+        for checked in (False, True):
+            t0 = time.perf_counter()
+            pk2 = fg.ProvingKey.load_params(ctx, circ, path, checked=checked)
+            ctx.synchronize()
+            t = time.perf_counter() - t0
+            key = "load_checked" if checked else "load"
+            rec[key + "_s"] = t
+            rec[key + "_GBps"] = nbytes / t / 1e9
+            if checked:
+                rec["proof_equal"] = fg.prove_batch(ctx, pk2, circ, [zhost], [rs])[0] == want
+            del pk2
+            gc.collect()
+        rec["subgroup_check_s"] = rec["load_checked_s"] - rec["load_s"]
+    finally:
+        shutil.rmtree(tmpd, ignore_errors=True)
+    return rec
+
+
 def window_post_leg(args, fg, ctx, device, rank, world, gdev, dist):
     """The Window-PoSt circuit itself: partitions of --post-sectors 32 GiB sectors x
     --post-challenges challenges (2349 x 10 = 125,279,217 constraints, constants.hpp:85-89; domain 2^27).
@@ -937,6 +977,8 @@ def main():
                     help="secondary: tree C over 2^N columns x 11 layers (N a multiple of 3; 0 skips)")
     ap.add_argument("--sdr-log-labels", type=int, default=24,
                     help="secondary: SDR labelling-proof labels of 2^N challenges (0 skips)")
+    ap.add_argument("--params-roundtrip", type=int, default=1,
+                    help="1: write the main key as a params file and time its unchecked / checked load (setup_s)")
     ap.add_argument("--tune", action="append", default=[], metavar="NAME=VALUE",
                     help="library A/B switch for the whole run (mi_tune_set, csrc/tune.h; tools' A/B runs only)")
     args = ap.parse_args()
@@ -1152,6 +1194,18 @@ def main():
                  "ntt_fr_2e20_ms": n20 * 1e3, "ntt_fr_2e20_melems_per_s": m20 / n20 / 1e6}
         del x
     del sc_dev, pts
+
+    # the key load every prover process does once per shape (get_groth_params -> read_cached_params ->
+    # build_mapped_parameters, core/parameter_cache.hpp:124-128,185-200; mmap at mapped_scheme_params.hpp:50-60): the
+    # main key written as a v28 params file, loaded back unchecked and subgroup-checked (mi_params_load), and the
+    # loaded key's proof compared with the resident key's, outside every timer
+    params_load = None
+    if rank == 0 and world == 1 and args.params_roundtrip and not args.params:
+        try:
+            params_load = params_roundtrip(fg, ctx, circ, pk, zhost, blinding(0, 0))
+        except Exception as e:  # reported, never fatal
+            params_load = {"error": str(e)}
+        log(rank, f"params round trip: {params_load}")
 
     # tree C over one 2^tree_log_nodes-node sub-tree (device-resident labels), and the
     # oracle's CPU Poseidon on a sample of the same columns
@@ -1398,7 +1452,7 @@ def main():
         "window_post_32gib": post_res,
         "winning_post_32gib": winning,
         "timers_ms": {k: round(v["ms"], 3) for k, v in stats.items()},
-        "setup_s": {"synth": t_synth, "circuit_load": t_load, "srs": t_srs},
+        "setup_s": {"synth": t_synth, "circuit_load": t_load, "srs": t_srs, "params_load": params_load},
         "device_gb_after_setup": round(dev_used_gb, 2),
         "msm_split": {1: "glv", 0: "2^128 tables"}.get(fg.tune_get("msm_glv"),
                                                       "auto: 2^128 tables when they fit in HBM, else glv"),
