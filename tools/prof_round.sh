@@ -7,7 +7,7 @@
 set -e
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
 T=${1:-r2}
-B="python3 bench.py --msm-reps 1 --no-cpu-baseline --no-device-resident --tree-log-nodes 0 --config4-log-rows 0 --sdr-log-labels 0 --stacked-log-nodes 0 --post-sectors 0 --winning-log-nodes 0 --uniform-steps 0"
+B="python3 bench.py --msm-reps 1 --no-cpu-baseline --no-device-resident --tree-log-nodes 0 --config4-log-rows 0 --sdr-log-labels 0 --stacked-log-nodes 0 --post-sectors 0 --winning-log-nodes 0 --uniform-steps 0 --params-roundtrip 0"
 mkdir -p gpurun_out
 echo "$B" > gpurun_out/${T}_command.txt
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_trace -o run -- $B > gpurun_out/${T}_trace.json 2> gpurun_out/${T}_trace.err
