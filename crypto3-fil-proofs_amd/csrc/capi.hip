@@ -469,6 +469,9 @@ void mi_ctx_destroy(mi_ctx *ctx) {
     for (auto &b : ctx->c.scratch) b.release();
     if (ctx->normal) hipStreamDestroy(ctx->normal);
     if (ctx->high) hipStreamDestroy(ctx->high);
+    if (ctx->c.plan_stream) hipStreamDestroy(ctx->c.plan_stream);
+    for (auto e : ctx->c.plan_ev)
+        if (e) hipEventDestroy(e);
     if (ctx->fence) hipEventDestroy(ctx->fence);
     delete ctx;
 }

@@ -227,6 +227,10 @@ struct Ctx {
     // use; ctx_aux_free releases it.  An auxiliary lane's own `aux` is the next lane (small proofs run three).
     Ctx *aux = nullptr;
     hipStream_t aux_streams[2] = {nullptr, nullptr};  // (in the aux ctx) normal, high priority
+    // tune::PLAN_PRIO: this lane's MSM plans on a high-priority stream (created on first use, PlanStream in
+    // msm_impl.h), ordered after and before the lane's stream by two events
+    hipStream_t plan_stream = nullptr;
+    hipEvent_t plan_ev[2] = {nullptr, nullptr};
 };
 
 // the owner's auxiliary lane, its stream matched to the owner's current stream priority

@@ -997,12 +997,41 @@ inline bool plan_finish(Ctx &c, MsmPlan &pl, const uint32_t *offA, const uint32_
     return true;
 }
 
+// tune::PLAN_PRIO = 1 (A/B): the plan's kernels run on a high-priority stream of the lane, so that a plan built beside
+// the other lane's accumulation gets CUs as they free instead of queueing behind long accumulation workgroups.  RAII:
+// the lane's stream is swapped for the plan stream (after an event on it) and back (the lane waits for the plan).
+struct PlanStream {
+    Ctx &c;
+    hipStream_t saved = nullptr;
+    explicit PlanStream(Ctx &ctx) : c(ctx) {
+        if (tune::get(tune::PLAN_PRIO, 0) != 1) return;
+        if (!c.plan_stream) {
+            int lo = 0, hi = 0;
+            MI_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            MI_HIP(hipStreamCreateWithPriority(&c.plan_stream, hipStreamNonBlocking, hi));
+            MI_HIP(hipEventCreateWithFlags(&c.plan_ev[0], hipEventDisableTiming));
+            MI_HIP(hipEventCreateWithFlags(&c.plan_ev[1], hipEventDisableTiming));
+        }
+        saved = c.stream;
+        MI_HIP(hipEventRecord(c.plan_ev[0], saved));
+        MI_HIP(hipStreamWaitEvent(c.plan_stream, c.plan_ev[0], 0));
+        c.stream = c.plan_stream;
+    }
+    ~PlanStream() {  // also on unwinding: the lane's stream comes back ordered after the plan's work
+        if (!saved) return;
+        (void)hipEventRecord(c.plan_ev[1], c.plan_stream);
+        (void)hipStreamWaitEvent(saved, c.plan_ev[1], 0);
+        c.stream = saved;
+    }
+};
+
 // The plan's arrays live in scratch slots 3, 5-8, 16, 17 and stay valid until the next prepare on
 // this ctx; the accumulation phase only uses the other slots.
 inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, uint64_t nscal, MsmPlan &pl,
                              bool split = false, bool glv = false) {
     pl = MsmPlan();
     if (nscal == 0) return false;
+    PlanStream plan_stream(c);
     split = split || glv;
     pl.glv = glv;
     // split mode: 2 nscal points with 128-bit scalars (+1 carry bit), always on the compacted path
@@ -1145,6 +1174,7 @@ inline bool msm_prepare_wt_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx
                                 unsigned nwin, uint64_t stride, MsmPlan &pl, bool sparse = false) {
     pl = MsmPlan();
     if (nscal == 0) return false;
+    PlanStream plan_stream(c);
     const uint64_t np64 = (uint64_t)nwin * nscal;
     if (np64 >= 0xffffffffull || (uint64_t)nwin * stride >= 0x80000000ull || cb < 2 || cb > 24)
         throw std::runtime_error("msm: window-table instance too large for 32-bit sort indices");

@@ -1807,6 +1807,9 @@ void ctx_aux_free(Ctx &c) {
     for (auto &b : c.aux->scratch) b.release();
     for (auto s : c.aux->aux_streams)
         if (s) hipStreamDestroy(s);
+    if (c.aux->plan_stream) hipStreamDestroy(c.aux->plan_stream);
+    for (auto e : c.aux->plan_ev)
+        if (e) hipEventDestroy(e);
     delete c.aux;
     c.aux = nullptr;
 }

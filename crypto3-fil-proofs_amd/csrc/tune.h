@@ -20,7 +20,7 @@ enum Knob : int {
     MSM_WT,            // 0: ignore the keys' window tables
     MSM_WT_C,          // window bits of a window table (clamped to [8, 22])
     MSM_WT_MAX_LOG,    // keys with a domain <= 2^k build window tables (default 21; 0 = never)
-    MSM_L0,            // sorted entries per level-0 chunk (default 64)
+    MSM_L0,            // sorted entries per level-0 chunk (default 64, 128 for plans of >= 2^24 points a window)
     MSM_L1,            // chunk partials per tree-level thread (power of two, default 16)
     MSM_SORT,          // 1: the per-window sorted path (and digit compaction) at any size
     MSM_BITSUM,        // 0: one-window plans reduce through the running-sum kernels
@@ -41,7 +41,7 @@ enum Knob : int {
     POSEIDON_PAIR,     // 1 wave-pair kernel, 0 one thread per hash (default: pairs for arity 8, 11)
     TREE_BATCH,        // columns / leaves per upload batch of the host tree builders (default 2^21)
     DEBUG_SYNC,        // 1: synchronise and report after every debug_sync point
-    MSM_COUNTSORT,     // 0: rocPRIM onesweep for the per-window bucket sort instead of the counting sort
+    PLAN_PRIO,         // 1: MSM plans (digits, sort, bounds, chunking) on a high-priority stream of their lane
     NKNOBS
 };
 
@@ -52,7 +52,7 @@ inline constexpr const char *kNames[NKNOBS] = {
     "msm_wt_max_log", "msm_l0",         "msm_l1",         "msm_sort",      "msm_bitsum",     "msm_sega_log",
     "msm_segb_log",   "msm_bs_seg_log", "msm_bs_g0",      "g2_l2",         "g2_aff_k",       "qap_fused",
     "prove_lanes",    "prove_wide_log", "prove_b1_lane",  "aux_order",     "lane_prio",      "wit_pos_lanes",
-    "sdr_prefetch",   "poseidon_pair",  "tree_batch",     "debug_sync",    "msm_countsort"};
+    "sdr_prefetch",   "poseidon_pair",  "tree_batch",     "debug_sync",    "plan_prio"};
 
 inline std::atomic<int64_t> g_knobs[NKNOBS] = {};  // zero-initialised; reset() / first use mark them UNSET
 inline std::atomic<bool> g_init{false};

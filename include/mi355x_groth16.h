@@ -456,7 +456,7 @@ int mi_ctx_get_shared_plans(mi_ctx *ctx, uint64_t *out);
 int mi_ctx_inject_oom(mi_ctx *ctx, int64_t count);
 /* TEST / BENCHMARK ONLY: process-wide A/B switches (csrc/tune.h lists them with their meaning: "msm_c", "msm_split",
  * "msm_glv", "msm_wt", "msm_wt_max_log", "msm_sort", "g2_l2", "prove_lanes", "prove_b1_lane", "tree_batch",
- * "sdr_prefetch", "msm_countsort", ...).  Every switch defaults to the measured production choice, and the library
+ * "sdr_prefetch", "plan_prio", ...).  Every switch defaults to the measured production choice, and the library
  * reads no environment variable for them: a production prove runs the same windows, lanes and kernels whatever its
  * process environment holds.  mi_tune_set refuses an unknown name (MI_ERR_ARG); mi_tune_clear(name) restores one
  * default, mi_tune_clear(NULL) all of them; mi_tune_get reports whether a switch is set and its value.  No reference
