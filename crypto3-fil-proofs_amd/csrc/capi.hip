@@ -1547,6 +1547,13 @@ int mi_ctx_get_shared_plans(mi_ctx *ctx, uint64_t *out) {
         *out = ctx->c.stats.shared_la;
     });
 }
+int mi_ctx_get_derived_plans(mi_ctx *ctx, uint64_t *out) {
+    return guard([&] {
+        need(ctx && out, "null argument");
+        CtxLock l(ctx);
+        *out = ctx->c.stats.derived_a;
+    });
+}
 int mi_ctx_get_table_msms(mi_ctx *ctx, uint64_t out[2]) {
     return guard([&] {
         need(ctx && out, "null argument");

@@ -136,12 +136,14 @@ struct Stats {
     uint64_t oom_freed_bytes = 0;  // split tables + scratch released for those retries
     uint64_t wt_msms = 0, wt_msms_g2 = 0;  // G1 / G2 MSMs that ran over a window table (msm_run_wt)
     uint64_t shared_la = 0;                // proofs whose L and A MSMs ran over one shared plan (Srs::a_aux)
+    uint64_t derived_a = 0;                // proofs whose A plan was derived from L's (msm_derive_plan)
     static constexpr int NK = 13;
     void merge(const Stats &o) {
         madds_g1 += o.madds_g1;
         wt_msms += o.wt_msms;
         wt_msms_g2 += o.wt_msms_g2;
         shared_la += o.shared_la;
+        derived_a += o.derived_a;
         madds_g2 += o.madds_g2;
         KStat *d[] = {&accum_g1, &accum_g2, &msm_g1, &msm_g2, &sort, &ntt, &prove, &h2d, &poseidon, &tree_h2d,
                       &wit_a, &wit_sha, &wit_pos};
@@ -212,9 +214,10 @@ struct Ctx {
     hipStream_t stream = nullptr;
     std::recursive_mutex mu;
     NttTables tw;
-    DevBuf scratch[26];  // 0-19: MSM / NTT / upload temporaries (18-19: G2 second level), 20: prover vectors,
+    DevBuf scratch[34];  // 0-19: MSM / NTT / upload temporaries (18-19: G2 second level), 20: prover vectors,
                          // 21-22: witness slots (capi.hip uploader; 21 also building-block inputs),
-                         // 24-25: an MSM plan's multi-chunk bucket list and first chunk-tree level (msm_impl.h)
+                         // 24-25: an MSM plan's multi-chunk bucket list and first chunk-tree level (msm_impl.h),
+                         // 26-33: a derived plan's arrays (msm_derive_plan: they outlive the next msm_prepare)
     Stats stats;
     EventTimer timer;
     PinnedBuf pin;  // small readbacks (msm_impl.h); one lane's, reused call after call
@@ -301,6 +304,7 @@ void fr_from_mont_inplace(Ctx &c, fr_t *d, uint64_t n);
 // Scalar-side state of one MSM (digits sorted into buckets, chunked, chunk order): depends only on
 // the scalars, so MSMs over the same scalars with different bases (B_G1 and B_G2 of one prove)
 // share it.  Pointers are into the ctx scratch arena; valid until the next msm_prepare on the ctx.
+constexpr unsigned MSM_PLAN_MAXW = 16;  // windows of a split plan (msm_impl.h MAXW_S)
 struct MsmPlan {
     uint64_t n = 0;      // points of the plan (2 x the real points in split mode)
     uint64_t nreal = 0;  // split mode (non-zero): point j >= nreal is 2^128 * base[j - nreal], scalar halves
@@ -315,6 +319,10 @@ struct MsmPlan {
     uint32_t m = 0, l1_total = 0, L1 = 16;
     uint32_t level_total[16] = {};  // partials of tree level l (msm_impl.h TREE_MAXL)
     uint32_t *mlist = nullptr, *qcnt = nullptr, *qoff = nullptr;
+    // split plans: window w's entries are vals_s[w n, w n + wn[w]) (before the bucket bounds); marked: built with
+    // A's density in its entries (msm_prepare_marked), so msm_derive_plan can filter it
+    uint32_t wn[MSM_PLAN_MAXW] = {};
+    bool marked = false;
 };
 // false when every scalar is zero (the MSM is the identity).  split: plan the 2n half-scalar points of
 // the 2^128-shifted base table (msm_g1 with bases_hi); the plan then needs bases_hi too.
@@ -322,6 +330,14 @@ bool msm_prepare(Ctx &c, const fr_t *scalars, const uint32_t *idx, uint64_t n, M
 // the plan msm_g1 takes for subgroup bases without a 2^128 table: GLV split above the split threshold, plain below;
 // one plan serves several G1 base sets over the same scalars (msm_g1_planned), e.g. L and the aux part of A
 bool msm_prepare_g1_shared(Ctx &c, const fr_t *scalars, uint64_t n, MsmPlan &plan);
+// L's plan over the aux witness z_aux (n scalars, split through the 2^128 tables or, glv, the endomorphism) with A's
+// density marked in its entries (amark = Circuit::a_rank), then A's plan derived from it without a sort: the entries of
+// variables with A density, in L's bucket order, their point indices moved to A's (dst_base + the variable's rank in
+// rank_bits = Circuit::a_bits; the 2^128 / phi half at + nreal_dst).  The derived plan lives in scratch slots 26-33 of c (it survives the next msm_prepare on c,
+// so L's accumulation can follow); false when it has no entry.
+bool msm_prepare_marked(Ctx &c, const fr_t *scalars, uint64_t n, MsmPlan &plan, bool glv, const uint32_t *amark);
+bool msm_derive_plan(Ctx &c, const MsmPlan &src, const uint32_t *rank_bits, uint64_t nreal_dst, uint32_t dst_base,
+                     MsmPlan &plan);
 void msm_g1_planned(Ctx &c, const MsmPlan &plan, const g1_affine_t *bases, g1_xyzz_t *result_host,
                     const g1_affine_t *bases_hi = nullptr);
 void msm_g2_planned(Ctx &c, const MsmPlan &plan, const g2_affine_t *bases, g2_xyzz_t *result_host);

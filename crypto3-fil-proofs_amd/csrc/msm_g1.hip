@@ -93,6 +93,15 @@ bool msm_prepare_g1_shared(Ctx &c, const fr_t *scalars, uint64_t n, MsmPlan &pla
     return msm_prepare_impl(c, scalars, nullptr, n, plan, false, glv);
 }
 
+bool msm_prepare_marked(Ctx &c, const fr_t *scalars, uint64_t n, MsmPlan &plan, bool glv, const uint32_t *amark) {
+    return msm_prepare_impl(c, scalars, nullptr, n, plan, !glv, glv, amark);
+}
+
+bool msm_derive_plan(Ctx &c, const MsmPlan &src, const uint32_t *rank_bits, uint64_t nreal_dst, uint32_t dst_base,
+                     MsmPlan &plan) {
+    return msm_derive_plan_impl(c, src, rank_bits, nreal_dst, dst_base, plan);
+}
+
 void msm_g1_planned(Ctx &c, const MsmPlan &plan, const g1_affine_t *bases, g1_xyzz_t *result_host,
                     const g1_affine_t *bases_hi) {
     if (!plan.total) {

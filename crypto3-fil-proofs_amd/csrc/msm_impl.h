@@ -296,6 +296,10 @@ __global__ void __launch_bounds__(256) k_digits_c(const fr_t *__restrict__ scala
 // plain 12-window one (a thread per half-scalar point measured +2.3 ms per 2^26 MSM).  c >= 9 keeps
 // ceil(129 / c) <= MAXW_S windows.
 constexpr unsigned MAXW_S = 16;
+static_assert(MAXW_S == MSM_PLAN_MAXW, "MsmPlan::wn holds MAXW_S windows");
+// Entry values (sorted with the keys) are point index | sign << 31; bit 30 is A_MARK in plans built for
+// msm_derive_plan_impl, so every plan keeps its point indices below 2^30.
+constexpr uint32_t A_MARK = 1u << 30, IDX_MASK = A_MARK - 1;
 MI_HD uint32_t word4_of(const uint32_t *v, unsigned k) {
     uint32_t r = 0;
     MI_UNROLL for (int j = 0; j < 4; j++) r = (k == (unsigned)j) ? v[j] : r;
@@ -330,17 +334,23 @@ MI_HD void digits128(const uint32_t *v, unsigned c, unsigned nwin, uint32_t *dg)
 // GLV (glv.h): the halves are k1 = k mod lambda (over P_i) and k2 = k div lambda (over phi(P_i)), and the
 // key carries the half as its low bit -- sub-bucket 2 (digit - 1) + half -- so the entries over P and over
 // phi(P) of one bucket are accumulated apart and phi is applied once per bucket sum (k_glv_merge).
+// amark (optional, Circuit::a_rank): entries of scalar i with amark[i] != ~0 carry A_MARK (msm_derive_plan_impl).
 template <bool GLV>
 __global__ void __launch_bounds__(256) k_digits_split(const fr_t *__restrict__ scalars,
                                                       const uint32_t *__restrict__ idx, uint32_t nreal, unsigned c,
                                                       unsigned nwin, uint32_t *__restrict__ wcount,
-                                                      uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+                                                      uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
+                                                      const uint32_t *__restrict__ amark) {
     __shared__ uint32_t wc[4][MAXW_S];
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t n = 2ull * nreal;  // window stride of keys / vals
     fr_t s = fr_t::zero();
-    if (i < nreal) s = scalars[idx ? idx[i] : i];
+    uint32_t mark = 0;
+    if (i < nreal) {
+        s = scalars[idx ? idx[i] : i];
+        if (amark && amark[i] != 0xffffffffu) mark = A_MARK;
+    }
     uint32_t dlo[MAXW_S], dhi[MAXW_S];
     if constexpr (GLV) {
         uint32_t k1[4], k2[4];
@@ -379,11 +389,11 @@ __global__ void __launch_bounds__(256) k_digits_split(const fr_t *__restrict__ s
             const uint64_t o = (uint64_t)w * n + wc[wave][w];
             if (dlo[w]) {
                 keys[o + rlo[w]] = ((dlo[w] & 0x7fffffffu) - 1) << (GLV ? 1 : 0);
-                vals[o + rlo[w]] = i | (dlo[w] & 0x80000000u);
+                vals[o + rlo[w]] = i | mark | (dlo[w] & 0x80000000u);
             }
             if (dhi[w]) {
                 keys[o + rhi[w]] = GLV ? (((dhi[w] & 0x7fffffffu) - 1) << 1) | 1u : (dhi[w] & 0x7fffffffu) - 1;
-                vals[o + rhi[w]] = (i + nreal) | (dhi[w] & 0x80000000u);
+                vals[o + rhi[w]] = (i + nreal) | mark | (dhi[w] & 0x80000000u);
             }
         }
     }
@@ -496,7 +506,7 @@ __global__ void __launch_bounds__(256) MI_WAVES_ACC k_accum_level0(const uint32_
     // point j of the plan: bases[j], or in split mode bases_hi[j - nreal] from j = nreal on
     // (G1 only: split mode has no G2 table, and the select costs the G2 lane-pair kernel registers)
     auto src = [&](uint32_t v) {
-        const uint32_t j = v & 0x7fffffffu;
+        const uint32_t j = v & IDX_MASK;
         if constexpr (sizeof(F) == sizeof(fq_t))
             return j < nreal ? bases + j : bases_hi + (j - nreal);
         else
@@ -918,8 +928,14 @@ inline void sort_pairs_u32(void *tmp, size_t &bytes, const uint32_t *k_in, uint3
 // caller reads them after ITS one synchronisation (with its own bucket maxima) and plan_finish completes the plan:
 // chunk -> bucket map, length-sorted chunk order.  false when there is no entry at all.
 constexpr unsigned PLAN_PIN = 5 + TREE_MAXL;
+// scratch slots of the plan arrays that outlive plan_counts / plan_finish (the rest are temporaries): a plan's own, or
+// a derived plan's (msm_derive_plan_impl), which must survive the next plan on the same ctx
+struct PlanSlots {
+    unsigned mlist = 24, chunk_bucket = 17, order = 16;
+};
+constexpr PlanSlots DERIVED_SLOTS{31, 32, 33};
 inline void plan_counts(Ctx &c, MsmPlan &pl, const uint32_t *cntA, uint32_t *offB, uint32_t *cntB, uint32_t nb,
-                        const uint32_t *maxcnt_dev, uint32_t *stage) {
+                        const uint32_t *maxcnt_dev, uint32_t *stage, PlanSlots ps = {}) {
     hipStream_t st = c.stream;
     // tune::MSM_L0 / MSM_L1 (tuning A/B): entries per level-0 chunk, partials per tree-level thread (a power of two)
     const uint32_t l0_auto = pl.n >= (1ull << 24) ? L0_LARGE : L0_DEFAULT;
@@ -931,7 +947,7 @@ inline void plan_counts(Ctx &c, MsmPlan &pl, const uint32_t *cntA, uint32_t *off
     pl.L0 = L0;
     pl.L1 = L1;
     uint32_t *coff = offB, *ccnt = cntB;
-    uint32_t *mlist = c.scratch[24].as<uint32_t>(3 * (uint64_t)nb + 1 + TREE_MAXL), *m_dev = mlist + nb;
+    uint32_t *mlist = c.scratch[ps.mlist].as<uint32_t>(3 * (uint64_t)nb + 1 + TREE_MAXL), *m_dev = mlist + nb;
     uint32_t *qcnt = m_dev + 1, *qoff = qcnt + nb, *totals = qoff + nb;
     // level 0: buckets cut into chunks of <= L0 sorted entries; one mixed-add chain per chunk
     k_chunk_count<<<grid_for(nb > TREE_MAXL ? nb : TREE_MAXL, 256), 256, 0, st>>>(cntA, nb, L0, ccnt, totals, TREE_MAXL);
@@ -966,7 +982,7 @@ inline void plan_counts(Ctx &c, MsmPlan &pl, const uint32_t *cntA, uint32_t *off
 }
 
 inline bool plan_finish(Ctx &c, MsmPlan &pl, const uint32_t *offA, const uint32_t *cntA, uint32_t nb,
-                        const uint32_t *vals_s, const uint32_t *pin) {
+                        const uint32_t *vals_s, const uint32_t *pin, PlanSlots ps = {}) {
     hipStream_t st = c.stream;
     const uint32_t L0 = pl.L0;
     unsigned len_bits = 1;
@@ -978,11 +994,11 @@ inline bool plan_finish(Ctx &c, MsmPlan &pl, const uint32_t *offA, const uint32_
     for (unsigned l = 0; l < TREE_MAXL; l++) pl.level_total[l] = pin[5 + l];
     if (total == 0) return false;  // every scalar is zero
     const uint32_t *coff = pl.coff;
-    uint32_t *chunk_bucket = c.scratch[17].as<uint32_t>(total + 1);
+    uint32_t *chunk_bucket = c.scratch[ps.chunk_bucket].as<uint32_t>(total + 1);
     // chunk -> bucket (binary search over the chunk offsets) and the length-sorted chunk order (keys/vals scratch of
     // the main sort are free by now)
     uint32_t *lkeys = c.scratch[0].as<uint32_t>(total), *lids = c.scratch[1].as<uint32_t>(total);
-    uint32_t *lkeys_s = c.scratch[2].as<uint32_t>(total), *order = c.scratch[16].as<uint32_t>(total);
+    uint32_t *lkeys_s = c.scratch[2].as<uint32_t>(total), *order = c.scratch[ps.order].as<uint32_t>(total);
     k_chunk_len_keys<<<grid_for(total, 256), 256, 0, st>>>(coff, cntA, nb, total, L0, chunk_bucket, lkeys, lids);
     MI_LAUNCHED(c, "k_chunk_len_keys");
     size_t tb = 0;
@@ -1028,7 +1044,7 @@ struct PlanStream {
 // The plan's arrays live in scratch slots 3, 5-8, 16, 17 and stay valid until the next prepare on
 // this ctx; the accumulation phase only uses the other slots.
 inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, uint64_t nscal, MsmPlan &pl,
-                             bool split = false, bool glv = false) {
+                             bool split = false, bool glv = false, const uint32_t *amark = nullptr) {
     pl = MsmPlan();
     if (nscal == 0) return false;
     PlanStream plan_stream(c);
@@ -1046,7 +1062,7 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
     const uint32_t nbk = (glv ? 2u : 1u) << (cb - 1);
     const uint64_t nb64 = (uint64_t)nwin * nbk;
     const uint64_t np64 = (uint64_t)nwin * n;
-    if (np64 >= 0xffffffffull || nb64 >= 0x7fffffffull || n >= 0x80000000ull)
+    if (np64 >= 0xffffffffull || nb64 >= A_MARK || n >= A_MARK)
         throw std::runtime_error("msm: instance too large for 32-bit sort indices");
     const uint32_t nb = (uint32_t)nb64, np = (uint32_t)np64, invalid = nbk;  // window-local keys
     unsigned key_bits = 1;
@@ -1093,10 +1109,11 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
                 if (nwin > MAXW_S) throw std::logic_error("msm: split plan with more than MAXW_S windows");
                 if (glv)
                     k_digits_split<true><<<grid_for(nscal, 256), 256, 0, st>>>(scalars, idx, (uint32_t)nscal, cb, nwin,
-                                                                                wcount, keys, vals);
+                                                                                wcount, keys, vals, amark);
                 else
                     k_digits_split<false><<<grid_for(nscal, 256), 256, 0, st>>>(scalars, idx, (uint32_t)nscal, cb, nwin,
-                                                                                 wcount, keys, vals);
+                                                                                 wcount, keys, vals, amark);
+                pl.marked = amark != nullptr;
                 MI_LAUNCHED(c, "k_digits_split");
             } else {
                 k_digits_c<<<grid_for(n, 256), 256, 0, st>>>(scalars, idx, (uint32_t)n, cb, nwin, 0u, wcount, keys,
@@ -1107,6 +1124,7 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
             MI_HIP(hipMemcpyAsync(wn_pin, wcount, sizeof(uint32_t) * nwin, hipMemcpyDeviceToHost, st));
             MI_HIP(hipStreamSynchronize(st));
             std::copy(wn_pin, wn_pin + nwin, wn.begin());
+            if (nwin <= MAXW_S) std::copy(wn_pin, wn_pin + nwin, pl.wn);
             sort_pairs_u32(nullptr, tmp_bytes, keys, keys_s, vals, vals_s, (uint32_t)n, key_bits, st);
             void *tmp = c.scratch[4].get(tmp_bytes);
             for (unsigned w = 0; w < nwin; w++) {
@@ -1162,6 +1180,186 @@ inline bool msm_prepare_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx, u
     return plan_finish(c, pl, offA, cntA, nb, vals_s, pin + H);
 }
 
+// ---- a plan derived from a marked plan (msm_derive_plan): A's MSM over L's digits ----
+// L sums z_aux over l; the aux part of A sums the same z_aux over the A points of the variables with A density.  A
+// marked L plan (A_MARK on those entries) already holds A's digits, sorted into the same buckets: keeping the marked
+// entries of every bucket in order gives A's plan without a digit pass or a sort.  Three passes over L's entries in
+// tiles of DERIVE_T (window by window, only the valid entries): count the marked entries per tile; write them,
+// compacted, with their point index moved to A's (the compacted position of every source entry goes to `pref`); the
+// new bucket bounds from `pref` at each bucket's first and last entry.  Then the usual chunking (plan_counts,
+// plan_finish) into slots of their own.
+namespace {
+constexpr unsigned DERIVE_T = 2048;  // entries per tile: 256 threads x 8
+struct DeriveArgs {
+    uint64_t n;                        // window stride of the source entries
+    uint32_t nwin, nreal_src, nreal_dst, dst_base;
+    uint32_t wn[MAXW_S];               // valid source entries of window w
+    uint32_t tile0[MAXW_S + 1];        // first tile of window w
+    uint32_t vbase[MAXW_S + 1];        // first entry of window w in the windows' concatenation (pref's index)
+};
+MI_HD unsigned derive_window(const DeriveArgs &a, uint32_t tile) {
+    unsigned w = 0;
+    while (w + 1 < a.nwin && a.tile0[w + 1] <= tile) w++;
+    return w;
+}
+
+// Both passes read a tile as 8 rounds of 256 consecutive entries (one coalesced load per thread and round); a round's
+// marked entries keep their order through a ballot prefix within each wave and the waves' counts in LDS.
+__global__ void __launch_bounds__(256) k_derive_count(const uint32_t *__restrict__ vals, DeriveArgs a,
+                                                      uint32_t *__restrict__ tile_cnt) {
+    const uint32_t t = blockIdx.x;
+    const unsigned w = derive_window(a, t);
+    const uint32_t base = (t - a.tile0[w]) * DERIVE_T + threadIdx.x, lim = a.wn[w];
+    const uint32_t *src = vals + (uint64_t)w * a.n;
+    uint32_t cnt = 0;
+    MI_UNROLL for (int k = 0; k < 8; k++) {
+        const uint32_t i = base + 256 * k;
+        const bool f = i < lim && (src[i] & A_MARK);
+        cnt += (uint32_t)__popcll(__ballot(f));  // the wave's marked entries of this round
+    }
+    __shared__ uint32_t ws[4];
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) tile_cnt[t] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+__global__ void __launch_bounds__(256) k_derive_scatter(const uint32_t *__restrict__ vals,
+                                                        const uint2 *__restrict__ rbits, DeriveArgs a,
+                                                        const uint32_t *__restrict__ tile_base,
+                                                        uint32_t *__restrict__ out, uint32_t *__restrict__ pref) {
+    const uint32_t t = blockIdx.x;
+    const unsigned w = derive_window(a, t), lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t base = (t - a.tile0[w]) * DERIVE_T + threadIdx.x, lim = a.wn[w];
+    const uint32_t *src = vals + (uint64_t)w * a.n;
+    uint32_t *pr = pref + a.vbase[w];
+    const uint64_t below = (1ull << lane) - 1;
+    __shared__ uint32_t ws[2][4];
+    uint32_t run = tile_base[t];
+    MI_UNROLL for (int k = 0; k < 8; k++) {
+        const uint32_t i = base + 256 * k;
+        const bool valid = i < lim;
+        const uint32_t v = valid ? src[i] : 0u;
+        const bool f = (v & A_MARK) != 0;
+        const uint64_t m = __ballot(f);
+        if (lane == 0) ws[k & 1][wave] = (uint32_t)__popcll(m);
+        __syncthreads();  // double-buffered counts: one barrier a round
+        uint32_t off = 0, all = 0;
+        MI_UNROLL for (unsigned q = 0; q < 4; q++) {
+            const uint32_t c = ws[k & 1][q];
+            off += q < wave ? c : 0u;
+            all += c;
+        }
+        const uint32_t pos = run + off + (uint32_t)__popcll(m & below);
+        if (valid) pr[i] = pos;
+        if (f) {
+            const uint32_t j = v & IDX_MASK, hi = j >= a.nreal_src ? 1u : 0u;
+            const uint32_t var = hi ? j - a.nreal_src : j;
+            const uint2 g = rbits[var >> 5];  // (density bits, A points before them) of var's group of 32
+            const uint32_t r = g.y + __popc(g.x & ((1u << (var & 31)) - 1));
+            out[pos] = (a.dst_base + r + (hi ? a.nreal_dst : 0u)) | (v & 0x80000000u);
+        }
+        run += all;
+    }
+}
+
+// bucket b of the source plan (entries [off, off + cnt) of vals, window b / nbk) -> its marked entries' range
+__global__ void k_derive_bounds(const uint32_t *__restrict__ off, const uint32_t *__restrict__ cnt, uint32_t nb,
+                                uint32_t nbk, const uint32_t *__restrict__ vals, DeriveArgs a,
+                                const uint32_t *__restrict__ pref, uint32_t *__restrict__ off2,
+                                uint32_t *__restrict__ cnt2) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    const uint32_t c = cnt[b];
+    if (!c) {
+        off2[b] = cnt2[b] = 0;
+        return;
+    }
+    const uint32_t w = b / nbk, o = off[b];
+    const uint64_t v0 = a.vbase[w] + (o - (uint64_t)w * a.n), v1 = v0 + c - 1;
+    const uint32_t s = pref[v0], e = pref[v1] + ((vals[o + c - 1] & A_MARK) ? 1u : 0u);
+    off2[b] = s;
+    cnt2[b] = e - s;
+}
+
+}  // namespace
+
+// src: a marked split plan (msm_prepare_impl with amark) of nreal_src = src.nreal scalars; rank_bits = (bits, prefix)
+// per 32 variables (Circuit::a_bits): the destination point of marked variable v is dst_base + its rank.  The derived plan (pl) is a split plan of nreal_dst
+// points: entry point j < nreal_src -> dst_base + rank[j], j >= nreal_src -> nreal_dst + dst_base + rank[j -
+// nreal_src].  src's arrays must still be valid (no prepare on their ctx since); false: no marked entry.
+inline bool msm_derive_plan_impl(Ctx &c, const MsmPlan &src, const uint32_t *rank_bits, uint64_t nreal_dst,
+                                 uint32_t dst_base, MsmPlan &pl) {
+    pl = MsmPlan();
+    if (!src.total) return false;
+    if (!src.marked || !src.nreal || src.nwin > MAXW_S || 2 * (nreal_dst + dst_base) >= A_MARK)
+        throw std::logic_error("msm_derive_plan: the source is not a marked split plan");
+    PlanStream plan_stream(c);
+    hipStream_t st = c.stream;
+    DeriveArgs a{};
+    a.n = src.n;
+    a.nwin = src.nwin;
+    a.nreal_src = (uint32_t)src.nreal;
+    a.nreal_dst = (uint32_t)nreal_dst;
+    a.dst_base = dst_base;
+    uint64_t ntiles = 0, ent = 0;
+    for (unsigned w = 0; w < src.nwin; w++) {
+        a.wn[w] = src.wn[w];
+        a.tile0[w] = (uint32_t)ntiles;
+        a.vbase[w] = (uint32_t)ent;
+        ntiles += (src.wn[w] + DERIVE_T - 1) / DERIVE_T;
+        ent += src.wn[w];
+    }
+    a.tile0[src.nwin] = (uint32_t)ntiles;
+    a.vbase[src.nwin] = (uint32_t)ent;
+    if (ent >= 0xffffffffull) throw std::runtime_error("msm_derive_plan: too many entries");
+    pl.n = 2 * nreal_dst;
+    pl.nreal = nreal_dst;
+    pl.cb = src.cb;
+    pl.nwin = src.nwin;
+    pl.nbk = src.nbk;
+    pl.nb = src.nb;
+    pl.glv = src.glv;
+    const uint32_t nb = src.nb;
+    uint32_t *pref = c.scratch[0].as<uint32_t>(ent ? ent : 1);
+    uint32_t *tile_cnt = c.scratch[1].as<uint32_t>(2 * (ntiles + 1)), *tile_base = tile_cnt + ntiles + 1;
+    uint32_t *vals2 = c.scratch[26].as<uint32_t>(ent ? ent : 1);
+    uint32_t *off2 = c.scratch[27].as<uint32_t>(nb), *cnt2 = c.scratch[28].as<uint32_t>(nb);
+    uint32_t *coff2 = c.scratch[29].as<uint32_t>(nb), *ccnt2 = c.scratch[30].as<uint32_t>(nb);
+    uint32_t *dmax = c.scratch[9].as<uint32_t>(4 + PLAN_PIN);  // [max bucket, marked entries, pad x 2, counts]
+    {
+        ScopedTimer tsort(c, &c.stats.sort, nreal_dst);
+        MI_HIP(hipMemsetAsync(tile_cnt + ntiles, 0, 4, st));
+        if (ntiles) {
+            k_derive_count<<<(unsigned)ntiles, 256, 0, st>>>(src.vals_s, a, tile_cnt);
+            MI_LAUNCHED(c, "k_derive_count");
+        }
+        size_t tb = 0;
+        MI_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, tile_cnt, tile_base, ntiles + 1, st));
+        void *tmp = c.scratch[4].get(tb);
+        MI_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, tile_cnt, tile_base, ntiles + 1, st));
+        if (ntiles) {
+            k_derive_scatter<<<(unsigned)ntiles, 256, 0, st>>>(src.vals_s, reinterpret_cast<const uint2 *>(rank_bits), a,
+                                                               tile_base, vals2, pref);
+            MI_LAUNCHED(c, "k_derive_scatter");
+        }
+        k_derive_bounds<<<grid_for(nb, 256), 256, 0, st>>>(src.off, src.cnt, nb, src.nbk, src.vals_s, a, pref, off2,
+                                                           cnt2);
+        MI_LAUNCHED(c, "k_derive_bounds");
+        tb = 0;
+        MI_HIP(hipcub::DeviceReduce::Max(nullptr, tb, cnt2, dmax, nb, st));
+        tmp = c.scratch[4].get(tb);
+        MI_HIP(hipcub::DeviceReduce::Max(tmp, tb, cnt2, dmax, nb, st));
+        MI_HIP(hipMemcpyAsync(dmax + 1, tile_base + ntiles, 4, hipMemcpyDeviceToDevice, st));
+    }
+    uint32_t *pin = c.pin.as<uint32_t>(4 + PLAN_PIN);
+    plan_counts(c, pl, cnt2, coff2, ccnt2, nb, dmax, dmax + 4, DERIVED_SLOTS);
+    MI_HIP(hipMemcpyAsync(pin, dmax, sizeof(uint32_t) * (4 + PLAN_PIN), hipMemcpyDeviceToHost, st));
+    MI_HIP(hipStreamSynchronize(st));
+    pl.maxcnt = pin[0];
+    pl.entries = pin[1];
+    return plan_finish(c, pl, off2, cnt2, nb, vals2, pin + 4, DERIVED_SLOTS);
+}
+
 // tune::MSM_BITSUM = 0 sends one-window plans through reduce_windows (A/B, tests)
 inline bool bitsum_enabled() { return tune::get(tune::MSM_BITSUM, 1) != 0; }
 
@@ -1176,7 +1374,7 @@ inline bool msm_prepare_wt_impl(Ctx &c, const fr_t *scalars, const uint32_t *idx
     if (nscal == 0) return false;
     PlanStream plan_stream(c);
     const uint64_t np64 = (uint64_t)nwin * nscal;
-    if (np64 >= 0xffffffffull || (uint64_t)nwin * stride >= 0x80000000ull || cb < 2 || cb > 24)
+    if (np64 >= 0xffffffffull || (uint64_t)nwin * stride >= A_MARK || cb < 2 || cb > 24)
         throw std::runtime_error("msm: window-table instance too large for 32-bit sort indices");
     hipStream_t st = c.stream;
     const uint32_t nbk = 1u << (cb - 1), invalid = nbk;

@@ -29,6 +29,12 @@ struct Circuit {
     // density index lists into z (bellman a_aux_density / b_input_density / b_aux_density)
     uint32_t *idx_a = nullptr, *idx_b = nullptr;
     uint64_t n_a = 0, n_b = 0, n_b_in = 0;
+    // a_rank[v] = r when aux variable v is A point n_in + r (idx_a[n_in + r] = n_in + v), ~0 without A density: maps
+    // the entries of L's MSM plan onto A's points (msm_derive_plan, groth16_sums "A plan derived from L's")
+    uint32_t *a_rank = nullptr;
+    // the same map in 8 bytes per 32 variables (a MALL-resident 16 MB at 2^26): word 2g = the A-density bits of
+    // variables 32g.., word 2g + 1 = the A points before them; rank(v) = prefix + popcount(bits below v)
+    uint32_t *a_bits = nullptr;
     ~Circuit();
 };
 

@@ -244,6 +244,33 @@ __global__ void k_gather_a_aux(const g1_affine_t *__restrict__ a, const uint32_t
     if (v < n_aux) out[v] = a[j];
 }
 
+// Circuit::a_rank: a_rank[idx[r] - n_in] = r over the aux part of the A density (idx = idx_a + n_in, m entries)
+__global__ void k_a_rank(const uint32_t *__restrict__ idx, uint64_t m, uint64_t n_in, uint64_t n_aux,
+                         uint32_t *__restrict__ rank) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= m) return;
+    const uint64_t v = (uint64_t)idx[r] - n_in;
+    if (v < n_aux) rank[v] = (uint32_t)r;
+}
+
+// Circuit::a_bits from a_rank: group g's density bits (word 2g) and their count (cnt[g], scanned into word 2g + 1)
+__global__ void k_a_bits(const uint32_t *__restrict__ rank, uint64_t n_aux, uint64_t ng, uint32_t *__restrict__ bits,
+                         uint32_t *__restrict__ cnt) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= ng) return;
+    uint32_t m = 0;
+    for (unsigned k = 0; k < 32; k++) {
+        const uint64_t v = 32 * g + k;
+        if (v < n_aux && rank[v] != 0xffffffffu) m |= 1u << k;
+    }
+    bits[2 * g] = m;
+    cnt[g] = __popc(m);
+}
+__global__ void k_a_bits_prefix(const uint32_t *__restrict__ pre, uint64_t ng, uint32_t *__restrict__ bits) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g < ng) bits[2 * g + 1] = pre[g];
+}
+
 __global__ void k_gather_canon(const fr_t *__restrict__ src, const uint32_t *__restrict__ idx, uint64_t n,
                                fr_t *__restrict__ out) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -478,6 +505,8 @@ Circuit::~Circuit() {
     if (ctab) hipFree(ctab);
     if (idx_a) hipFree(idx_a);
     if (idx_b) hipFree(idx_b);
+    if (a_rank) hipFree(a_rank);
+    if (a_bits) hipFree(a_bits);
 }
 namespace {
 std::mutex g_keys_mu;
@@ -618,6 +647,24 @@ Circuit *circuit_load_compact(Ctx &c, const R1csCompact &cs) {
         C->n_b = ib.size();
         C->idx_a = dalloc<uint32_t>(ia.size());
         MI_HIP(hipMemcpy(C->idx_a, ia.data(), 4 * ia.size(), hipMemcpyHostToDevice));
+        if (C->n_a > cs.n_in && cs.n_aux) {
+            C->a_rank = dalloc<uint32_t>(cs.n_aux);
+            MI_HIP(hipMemsetAsync(C->a_rank, 0xff, 4 * cs.n_aux, c.stream));
+            const uint64_t m = C->n_a - cs.n_in;
+            k_a_rank<<<grid1(m), 256, 0, c.stream>>>(C->idx_a + cs.n_in, m, cs.n_in, cs.n_aux, C->a_rank);
+            MI_HIP(hipGetLastError());
+            const uint64_t ng = (cs.n_aux + 31) / 32;
+            C->a_bits = dalloc<uint32_t>(2 * ng);
+            uint32_t *cnt = c.scratch[0].as<uint32_t>(2 * ng), *pre = cnt + ng;
+            k_a_bits<<<grid1(ng), 256, 0, c.stream>>>(C->a_rank, cs.n_aux, ng, C->a_bits, cnt);
+            MI_HIP(hipGetLastError());
+            size_t tb = 0;
+            MI_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, pre, ng, c.stream));
+            void *tmp = c.scratch[4].get(tb);
+            MI_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, pre, ng, c.stream));
+            k_a_bits_prefix<<<grid1(ng), 256, 0, c.stream>>>(pre, ng, C->a_bits);
+            MI_HIP(hipGetLastError());
+        }
         if (!ib.empty()) {
             C->idx_b = dalloc<uint32_t>(ib.size());
             MI_HIP(hipMemcpy(C->idx_b, ib.data(), 4 * ib.size(), hipMemcpyHostToDevice));
@@ -1445,10 +1492,25 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
         // of the plan's counts plus a device event): one plan fewer per proof, the lanes' work as before.
         const bool shared_la = !wide && srs.a_aux && rg.lo[1] == 0 && rg.cnt[1] == circ.n_aux && rg.lo[2] == 0 &&
                                rg.cnt[2] == circ.n_a && circ.n_a > circ.n_in && msm_glv_mode() != 0;
+        // A plan derived from L's (msm_derive_plan): keys below the shared plan's density rule (the synthetic config-3
+        // circuit: A covers 66 % of the aux variables) keep A's own query, but A's digits are L's digits of the
+        // variables with A density, already sorted into L's buckets.  The lane that runs L builds L's plan with those
+        // entries marked (Circuit::a_rank), derives A's plan from it by filtering (no digit pass, no sort) into plan
+        // slots of its own, hands it to the main lane and accumulates L; A's accumulation runs after H over A's points
+        // and tables.  Both plans need the same split: the 2^128 tables of l and a, or GLV for both.
+        const int glv_mode = msm_glv_mode();
+        auto glv_for = [&](const g1_affine_t *hi) { return glv_mode == 1 || (glv_mode == 2 && !hi && srs.in_subgroup); };
+        const bool la_glv = glv_for(srs.l_hi);
+        const bool derive_a = !wide && !shared_la && circ.a_rank && circ.a_bits && tune::get(tune::A_FROM_L, 1) != 0 &&
+                              rg.lo[1] == 0 && rg.cnt[1] == circ.n_aux && rg.lo[2] == 0 && rg.cnt[2] == circ.n_a &&
+                              circ.n_a > circ.n_in && msm_use_split(circ.n_aux) && !srs.wt[1] && !srs.wt[2] &&
+                              la_glv == glv_for(srs.a_hi) && (la_glv || (srs.l_hi && srs.a_hi)) &&
+                              2 * (circ.n_aux + circ.n_a) < (1ull << 30);
+        const bool hand_a = shared_la || derive_a;  // A's plan comes from the auxiliary lane
         std::promise<MsmPlan> la_plan;
         std::future<MsmPlan> la_plan_f = la_plan.get_future();
         std::atomic<bool> la_handed{false};
-        hipEvent_t la_ready = shared_la ? c.timer.get() : nullptr;
+        hipEvent_t la_ready = hand_a ? c.timer.get() : nullptr;
         g1_xyzz_t A_aux = g1_xyzz_t::inf();
         auto run_la_plan = [&](Ctx &x) {  // the shared plan, on the lane that runs L; handed to A's lane
             MsmPlan pl;
@@ -1475,7 +1537,23 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
             msm_g1_planned(x, pl, srs.a_aux, &A_aux);
             finish_a(x);
         };
+        // derived: L's marked plan, A's plan from it (handed over), L's accumulation; returns A's plan
+        auto run_l_derive = [&](Ctx &x) {
+            MsmPlan pl, pa;
+            const bool any = msm_prepare_marked(x, z_dev + circ.n_in, circ.n_aux, pl, la_glv, circ.a_rank);
+            if (any) msm_derive_plan(x, pl, circ.a_bits, circ.n_a, (uint32_t)circ.n_in, pa);
+            MI_HIP(hipEventRecord(la_ready, x.stream));
+            la_handed = true;
+            la_plan.set_value(pa);
+            if (any) msm_g1_planned(x, pl, srs.l, &Lq, la_glv ? nullptr : srs.l_hi);
+            return pa;
+        };
+        auto run_a_derived = [&](Ctx &x, const MsmPlan &pa) {  // A_aux over A's own points, then the inputs' part
+            msm_g1_planned(x, pa, srs.a, &A_aux, la_glv ? nullptr : srs.a_hi);
+            finish_a(x);
+        };
         if (shared_la) c.stats.shared_la += 1;
+        if (derive_a) c.stats.derived_a += 1;
         // aux-lane order: B before L (same-box A/B at 2^26: -2 ms per proof; tune::AUX_ORDER = 1
         // restores L first)
         const bool b_first = tune::get(tune::AUX_ORDER, 0) != 1;
@@ -1490,6 +1568,11 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
                         msm_g1_planned(x, pl, srs.a_aux, &A_aux);
                         finish_a(x);
                     }
+                } else if (!wide && derive_a) {
+                    if (b_first) run_b(x);
+                    const MsmPlan pa = run_l_derive(x);
+                    if (!b_first) run_b(x);
+                    if (one_lane) run_a_derived(x, pa);  // the main lane is done: A here, after L
                 } else if (!wide) {
                     if (b_first) run_b(x);
                     run_l(x);
@@ -1507,7 +1590,7 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
             } catch (...) {
                 err[k] = std::current_exception();
                 // a lane that fails before handing over the shared plan must not leave A's lane waiting for it
-                if (shared_la && k == 0 && !la_handed.exchange(true)) la_plan.set_exception(err[k]);
+                if (hand_a && k == 0 && !la_handed.exchange(true)) la_plan.set_exception(err[k]);
             }
         };
         std::thread lanes[3];
@@ -1526,8 +1609,13 @@ ProofSums groth16_sums_once(Ctx &c, const Srs &srs, const Circuit &circ, const f
                        srs.in_subgroup, &wt_h, h_lo);
             else
                 H = g1_xyzz_t::inf();
-            if (!wide && !shared_la) run_a(c);
+            if (!wide && !hand_a) run_a(c);
             if (shared_la && !one_lane) run_a_shared(c);
+            if (derive_a && !one_lane) {
+                const MsmPlan pa = la_plan_f.get();
+                MI_HIP(hipStreamWaitEvent(c.stream, la_ready, 0));
+                run_a_derived(c, pa);
+            }
         } catch (...) {
             err_main = std::current_exception();
         }

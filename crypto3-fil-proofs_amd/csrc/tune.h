@@ -42,6 +42,7 @@ enum Knob : int {
     TREE_BATCH,        // columns / leaves per upload batch of the host tree builders (default 2^21)
     DEBUG_SYNC,        // 1: synchronise and report after every debug_sync point
     PLAN_PRIO,         // 1: MSM plans (digits, sort, bounds, chunking) on a high-priority stream of their lane
+    A_FROM_L,          // 0: A's plan sorted on its own instead of derived from L's (below the shared-plan density)
     NKNOBS
 };
 
@@ -52,7 +53,8 @@ inline constexpr const char *kNames[NKNOBS] = {
     "msm_wt_max_log", "msm_l0",         "msm_l1",         "msm_sort",      "msm_bitsum",     "msm_sega_log",
     "msm_segb_log",   "msm_bs_seg_log", "msm_bs_g0",      "g2_l2",         "g2_aff_k",       "qap_fused",
     "prove_lanes",    "prove_wide_log", "prove_b1_lane",  "aux_order",     "lane_prio",      "wit_pos_lanes",
-    "sdr_prefetch",   "poseidon_pair",  "tree_batch",     "debug_sync",    "plan_prio"};
+    "sdr_prefetch",   "poseidon_pair",  "tree_batch",     "debug_sync",    "plan_prio",
+    "a_from_l"};
 
 inline std::atomic<int64_t> g_knobs[NKNOBS] = {};  // zero-initialised; reset() / first use mark them UNSET
 inline std::atomic<bool> g_init{false};

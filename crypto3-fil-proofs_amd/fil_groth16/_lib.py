@@ -39,6 +39,7 @@ EXPORTS = [
     "mi_stacked_witness", "mi_stacked_free", "mi_circuit_check_dev",
     "mi_points_precompute", "mi_points_table_info", "mi_ctx_get_table_msms", "mi_srs_window_tables",
     "mi_tune_set", "mi_tune_clear", "mi_tune_get", "mi_fq_check_read", "mi_srs_shared_la", "mi_ctx_get_shared_plans",
+    "mi_ctx_get_derived_plans",
 ]
 
 _lib = None
@@ -153,6 +154,7 @@ def lib():
         "mi_srs_window_tables": ([vp, vp], c_int),
         "mi_srs_shared_la": ([vp, ctypes.POINTER(c_int)], c_int),
         "mi_ctx_get_shared_plans": ([vp, ctypes.POINTER(ctypes.c_uint64)], c_int),
+        "mi_ctx_get_derived_plans": ([vp, ctypes.POINTER(ctypes.c_uint64)], c_int),
         "mi_groth16_prove": ([vp, vp, vp, u8p, u8p, u8p, c_int, vp, vp], c_int),
         "mi_groth16_prove_dev": ([vp, vp, vp, vp, u8p, u8p, c_int, vp, vp], c_int),
         "mi_groth16_prove_batch": ([vp, vp, vp, u64, vp, u8p, c_int, vp], c_int),

@@ -107,6 +107,12 @@ class Context:
         check(lib().mi_ctx_get_shared_plans(self.h, ctypes.byref(w)))
         return int(w.value)
 
+    def derived_plans(self) -> int:
+        """proofs since the last reset_stats whose A plan was filtered out of L's (mi_ctx_get_derived_plans)"""
+        w = ctypes.c_uint64(0)
+        check(lib().mi_ctx_get_derived_plans(self.h, ctypes.byref(w)))
+        return int(w.value)
+
     def table_msms(self, g2: bool = False) -> int:
         """G1 (G2 with g2) MSMs that ran over a fixed-base window table since the last reset_stats
         (mi_ctx_get_table_msms)"""

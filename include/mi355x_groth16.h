@@ -450,13 +450,16 @@ int mi_ctx_get_fallbacks(mi_ctx *ctx, uint64_t out[2]);
 int mi_ctx_get_table_msms(mi_ctx *ctx, uint64_t out[2]);
 /* proofs since the last reset whose L and A MSMs ran over one shared plan (mi_srs_shared_la) */
 int mi_ctx_get_shared_plans(mi_ctx *ctx, uint64_t *out);
+/* proofs since the last reset whose A plan was derived from L's (keys below the shared plan's density rule: L's plan
+ * carries A's density in its entries and A's plan is filtered out of it, without a digit pass or a sort of its own) */
+int mi_ctx_get_derived_plans(mi_ctx *ctx, uint64_t *out);
 /* TEST ONLY: the first attempt of each of the next `count` proofs on this context fails with a real out-of-memory
  * error after its NTT chain (count < 0: every proof until reset to 0), so the release-and-retry path runs at any
  * size.  Production code never calls it; nothing in the prove path reads the environment for it. */
 int mi_ctx_inject_oom(mi_ctx *ctx, int64_t count);
 /* TEST / BENCHMARK ONLY: process-wide A/B switches (csrc/tune.h lists them with their meaning: "msm_c", "msm_split",
  * "msm_glv", "msm_wt", "msm_wt_max_log", "msm_sort", "g2_l2", "prove_lanes", "prove_b1_lane", "tree_batch",
- * "sdr_prefetch", "plan_prio", ...).  Every switch defaults to the measured production choice, and the library
+ * "sdr_prefetch", "plan_prio", "a_from_l", ...).  Every switch defaults to the measured production choice, and the library
  * reads no environment variable for them: a production prove runs the same windows, lanes and kernels whatever its
  * process environment holds.  mi_tune_set refuses an unknown name (MI_ERR_ARG); mi_tune_clear(name) restores one
  * default, mi_tune_clear(NULL) all of them; mi_tune_get reports whether a switch is set and its value.  No reference

@@ -177,6 +177,56 @@ def test_groth16_shared_la_plan_vs_oracle(ctx, oracle, tune, n_in, cover):
     assert not pk.shared_la() and ctx.fallbacks()["oom_retries"] == 1
 
 
+@pytest.mark.parametrize("mode", ["tables", "glv"])
+def test_groth16_derived_a_plan_vs_oracle(ctx, oracle, tune, mode):
+    """Keys below the shared plan's density rule: L's plan carries A's density in its entries and A's plan is filtered
+    out of it (msm_derive_plan: no digit pass, no sort of its own), on the lane that runs L, then accumulated over A's
+    own points on the main lane.  Over the 2^128 split tables and over GLV; both auxiliary-lane orders, one lane, an
+    all-zero aux witness (empty plans), A's own plan (a_from_l = 0), and latency-mode shares (ranges: plans of their
+    own) give the oracle's bytes."""
+    tune.set("msm_split", 2)
+    tune.set("msm_wt_max_log", 0)
+    tune.set("prove_wide_log", 0)
+    if mode == "glv":
+        tune.set("msm_glv", 1)
+    n_in, n_aux, rws, z = circuits.random_circuit(41, 3000, n_in=3, n_free=32)
+    in_a = {c for row in rws for c, _ in row[0]}
+    assert sum(1 for v in range(n_in, n_in + n_aux) if v in in_a) * 10 < n_aux * 9  # below the shared-plan rule
+    oc, gc = _load(ctx, oracle, n_in, n_aux, rws, z)
+    tox = circuits.toxic(41)
+    pk = fg.generate_random_parameters(ctx, gc, tox)
+    assert not pk.shared_la()
+    op = oracle.OracleParams(oc, tox)
+    zb = circuits.z_bytes(z)
+    want = op.prove(zb, 5, 6)[0]
+    ctx.reset_stats()
+    assert fg.prove(ctx, pk, gc, zb, 5, 6) == want
+    assert ctx.derived_plans() == 1 and ctx.shared_plans() == 0
+    tune.set("aux_order", 1)  # L (and the derived plan) before B on the auxiliary lane
+    assert fg.prove(ctx, pk, gc, zb, 5, 6) == want
+    tune.clear("aux_order")
+    tune.set("prove_lanes", 1)
+    assert fg.prove(ctx, pk, gc, zb, 5, 6) == want
+    tune.clear("prove_lanes")
+    assert ctx.derived_plans() == 3
+    tune.set("a_from_l", 0)
+    assert fg.prove(ctx, pk, gc, zb, 5, 6) == want
+    tune.clear("a_from_l")
+    assert ctx.derived_plans() == 3
+    vk, _ = pk.verifying_key()
+    assert fg.assemble(vk, [fg.prove_share(ctx, pk, gc, zb, k, 2) for k in range(2)], 5, 6) == want
+    assert ctx.derived_plans() == 3
+    zeros = zb[:32 * n_in] + bytes(32 * n_aux)
+    assert fg.prove(ctx, pk, gc, zeros, 5, 6) == op.prove(zeros, 5, 6)[0]
+    # only the inputs and the variables without A density non-zero: A's derived plan is empty, L's is not
+    zl = bytearray(zb)
+    for v in range(n_in, n_in + n_aux):
+        if v in in_a:
+            zl[32 * v:32 * v + 32] = bytes(32)
+    assert fg.prove(ctx, pk, gc, bytes(zl), 5, 6) == op.prove(bytes(zl), 5, 6)[0]
+    assert ctx.derived_plans() == 5
+
+
 def test_prove_out_of_memory_degrades_to_glv(ctx, oracle, tune):
     """A proof whose scratch allocation fails (mi_ctx_inject_oom, a test-only entry: the main lane raises
     hipMalloc's out-of-memory error after the NTT chain while the auxiliary lane runs) is re-run in-process after

@@ -50,14 +50,14 @@ for mode in "$@"; do
       tail -c 400 $O/bench.json ;;
     wpab)  # the 32 GiB Window-PoSt leg (two lanes, as the driver bench runs it), default and with each WPAB switch
       for v in default ${WPAB:-}; do
-        T=(); [ "$v" = default ] || T=(--tune "$v")
+        T=(); [ "$v" = default ] || for kv in ${v//,/ }; do T+=(--tune "$kv"); done
         timeout -k 10 300 $W --post-sectors 2349 --post-reps 2 --post-share-groups "" --winning-log-nodes 0 "${T[@]}" > $O/wp_$v.json 2> $O/wp_$v.err || { tail -5 $O/wp_$v.err; exit 1; }
         python3 -c "import json; w = json.load(open('$O/wp_$v.json'))['window_post_32gib']; print('window-post $v', round(w['ms_per_partition_rank0'], 1), w['verified'])"
       done ;;
     c3ab)  # config-3 main leg (5 timed proofs), default and each C3AB switch, alternated twice (same box)
       for rep in 1 2; do
         for v in default ${C3AB:-}; do
-          T=(); [ "$v" = default ] || T=(--tune "$v")
+          T=(); [ "$v" = default ] || for kv in ${v//,/ }; do T+=(--tune "$kv"); done
           timeout -k 10 300 python3 bench.py --steps 5 --warmup 1 --msm-reps 1 --no-cpu-baseline --no-device-resident --tree-log-nodes 0 --sdr-log-labels 0 --config4-log-rows 0 --stacked-log-nodes 0 --post-sectors 0 --uniform-steps 0 --winning-log-nodes 0 "${T[@]}" > $O/c3_$v.json 2> $O/c3_$v.err || { tail -5 $O/c3_$v.err; exit 1; }
           python3 -c "import json; d = json.load(open('$O/c3_$v.json')); print('config3 $v', round(d['ms_per_step'], 2), round(d['value'] / 1e6, 2), 'Mc/s')"
         done

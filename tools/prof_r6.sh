@@ -14,7 +14,7 @@ while [ $# -gt 0 ]; do
   modes+=("$1"); shift
 done
 QUIET=(--no-cpu-baseline --no-device-resident --tree-log-nodes 0 --sdr-log-labels 0 --config4-log-rows 0
-       --stacked-log-nodes 0 --uniform-steps 0 --winning-log-nodes 0 --tune prove_lanes=1)
+       --stacked-log-nodes 0 --uniform-steps 0 --winning-log-nodes 0 --params-roundtrip 0 --tune prove_lanes=1)
 for mode in "${modes[@]}"; do
   case $mode in
     winpost)
