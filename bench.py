@@ -1362,7 +1362,7 @@ def main():
         o_madds = o.get("madds", 0) / o["launches"]
         o_rate = o_madds / (o_ms * 1e-3) / 1e9 if o_ms > 0 else None
         one_lane_res = {
-            "mode": "one lane (MI_PROVE_LANES=1, one proof): the kernel alone on the chip",
+            "mode": "one lane (prove_lanes=1, one proof): the kernel alone on the chip",
             "avg_launch_ms": o_ms, "launches": o["launches"], "madds_per_launch": o_madds, "gmadd_per_s": o_rate,
             "hbm_frac": (bytes_per_unit * o["units"] / o["launches"] / (o_ms * 1e-3) / 1e9) / HBM_PEAK_GBS
             if o_ms > 0 else None,

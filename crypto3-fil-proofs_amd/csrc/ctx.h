@@ -263,7 +263,7 @@ struct ScopedTimer {
     }
 };
 
-// Opt-in launch checking (env MI_DEBUG_SYNC=1): synchronise after each launch and name the kernel
+// Opt-in launch checking (tune debug_sync=1, tests only): synchronise after each launch and name the kernel
 // that faulted.  Off by default (no synchronisation in the hot path).
 void debug_sync(Ctx &c, const char *what);
 #define MI_LAUNCHED(ctx, name)          \

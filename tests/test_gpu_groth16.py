@@ -273,7 +273,7 @@ def test_prove_out_of_memory_degrades_to_glv(ctx, oracle, tune):
 def test_prove_window_tables(ctx, oracle, tune):
     """A small key builds fixed-base window tables for h, l, a, b_g1 and b_g2 at generation (domain <= 2^21): its
     proofs run those five MSMs over one bucket set each and equal the oracle's, as do latency-mode shares (table slices at
-    an offset); MI_MSM_WT=0 (the plain path) gives the same bytes.  An out-of-memory retry releases the tables like
+    an offset); msm_wt=0 (the plain path) gives the same bytes.  An out-of-memory retry releases the tables like
     the split tables, and mi_srs_readmit rebuilds them."""
     tune.clear("msm_wt_max_log")
     tune.clear("msm_wt")
@@ -320,7 +320,7 @@ def test_prove_batch_and_priority(ctx, oracle):
 
 
 def test_prove_lane_layouts_identical(ctx, oracle, tune):
-    """Small proofs (domain <= 2^MI_PROVE_WIDE_LOG, default 2^21) run B, L and A on three auxiliary lanes of their
+    """Small proofs (domain <= 2^prove_wide_log, default 2^21) run B, L and A on three auxiliary lanes of their
     own; large ones keep the two-lane layout (prover.hip groth16_sums_once).  Both layouts give the oracle's
     proof, for several witnesses in a row on the same context (the lanes' scratch arenas are reused)."""
     n_in, n_aux, rws, z = circuits.random_circuit(43, 5000)
@@ -333,7 +333,7 @@ def test_prove_lane_layouts_identical(ctx, oracle, tune):
         tune.set("prove_wide_log", int(wide_log))
         tune.set("prove_b1_lane", int(b1_lane))
         got = [fg.prove(ctx, pk, gc, zb, r, s) for r, s in [(7, 8), (9, 10)]]
-        assert got == want, f"MI_PROVE_WIDE_LOG={wide_log} MI_PROVE_B1_LANE={b1_lane}"
+        assert got == want, f"prove_wide_log={wide_log} prove_b1_lane={b1_lane}"
 
 
 def test_prove_rejects_mismatched_srs(ctx):

@@ -83,7 +83,7 @@ def test_msm_g1_random(ctx, oracle, n):
 @pytest.fixture(params=["0", "2"])
 def g2_level2(request, tune):
     """G2 bucket reduction: "0" the running-sum kernels, "2" the second-level MSM over affine buckets
-    (forced at every size; by default it takes over from 2^20 level-1 buckets, MI_G2_L2)."""
+    (forced at every size; by default it takes over from 2^20 level-1 buckets, g2_l2)."""
     tune.set("g2_l2", int(request.param))
     return request.param
 
@@ -138,7 +138,7 @@ def test_msm_rejects_bad_points(ctx, oracle):
 @pytest.fixture(params=["auto", "windowed"])
 def sort_mode(request, tune):
     """auto: 2^20 sorts every window in one call; windowed: the per-window sort with zero-digit
-    compaction that MSMs of 2^22+ points take (MI_MSM_SORT, read at every MSM)."""
+    compaction that MSMs of 2^22+ points take (msm_sort, read at every MSM)."""
     tune.set("msm_sort", 1 if request.param == "windowed" else 0)
     return request.param
 
@@ -215,9 +215,9 @@ def _split_scalars(n, seed):
 
 @pytest.mark.parametrize("split", ["0", "2", "glv"])
 def test_msm_split_tables_vs_oracle(ctx, oracle, tune, split):
-    """Split mode (MI_MSM_SPLIT=2 forces it at any size): the l and a queries' MSMs over their 2^128
+    """Split mode (msm_split=2 forces it at any size): the l and a queries' MSMs over their 2^128
     tables, against the oracle's MSM over the same points; "glv": keys generated and MSMs run with
-    MI_MSM_GLV=1 (no tables)."""
+    msm_glv=1 (no tables)."""
     import torch
 
     tune.set("msm_split", int("2" if split == "glv" else split))
@@ -270,7 +270,7 @@ def _glv_scalars(n, seed):
 
 @pytest.mark.parametrize("n,c", [(1, ""), (13, ""), (5000, ""), (5000, "12"), (5000, "22")])
 def test_msm_glv_vs_oracle(ctx, oracle, tune, n, c):
-    """G1 split mode through the GLV endomorphism (MI_MSM_GLV=1; MI_MSM_SPLIT=2 forces split at any size)
+    """G1 split mode through the GLV endomorphism (msm_glv=1; msm_split=2 forces split at any size)
     over caller-uploaded bases, which have no 2^128 table: edge scalars of the k = k1 + lambda k2
     decomposition, at the default window, c = 12 and the production c = 22 (2^22 sub-buckets per window)."""
     tune.set("msm_glv", 1)
@@ -333,8 +333,8 @@ def test_msm_glv_boolean_heavy_2_20(ctx, oracle, tune):
 
 
 def test_msm_glv_auto_uploaded_bases(ctx, oracle, tune):
-    """Default policy (MI_MSM_GLV unset): caller-uploaded bases have no 2^128 table, so a split-size G1 MSM
-    takes the GLV split; the same MSM with MI_MSM_GLV=0 runs the plain 256-bit path."""
+    """Default policy (msm_glv unset): caller-uploaded bases have no 2^128 table, so a split-size G1 MSM
+    takes the GLV split; the same MSM with msm_glv=0 runs the plain 256-bit path."""
     tune.clear("msm_glv")
     tune.set("msm_split", 2)
     n = 3001
@@ -373,7 +373,7 @@ def test_msm_window_table_vs_oracle(ctx, oracle, n, c):
 def test_msm_window_table_linearity_2_20(ctx, oracle, tune, bitsum):
     """BASELINE config-2 size over a window table at the library's window choice and at c = 20 (2^19 buckets in
     one window): MSM(k_i G, s_i) == (sum s_i k_i) G.  bitsum "0" reduces the one window with the running-sum
-    kernels instead of the bit-row sums (MI_MSM_BITSUM)."""
+    kernels instead of the bit-row sums (msm_bitsum)."""
     import torch
 
     tune.set("msm_bitsum", int(bitsum))

@@ -1,7 +1,7 @@
 """GPU parity at the production settings the bench runs (VERDICT r1 "verify what you time").
 
 * The window sizes the cost model picks at 2^26 / 2^27 (c = 20..22: 12-13 windows plain, 6-7 windows in
-  split mode, 2^19-2^21 buckets per window) forced through MI_MSM_C onto 2^16-2^17-point MSMs the
+  split mode, 2^19-2^21 buckets per window) forced through msm_c onto 2^16-2^17-point MSMs the
   oracle checks in about a second, G1 plain and split, G2 with both bucket-reduction modes, and one
   full prove at c = 22.
 * One default-settings 2^26-constraint proof (BASELINE config 3, exactly what bench.py times) checked
@@ -129,7 +129,7 @@ def test_groth16_2_27_config4_default_settings_verified(ctx, oracle, tune):
     """BASELINE config 4 shape (2^27 domain, ~1.3e8 constraints: the 32 GiB PoRep partition size) with
     default settings, as bench.py's config4 leg times it.  The trapdoor discrete logs and both pairing
     verifiers check the proof.  Then the G1 split mode the auto policy did NOT pick is forced on the same
-    key (MI_MSM_GLV=1 over resident 2^128 tables, or MI_MSM_GLV=0 = the plain 256-bit path when the
+    key (msm_glv=1 over resident 2^128 tables, or msm_glv=0 = the plain 256-bit path when the
     tables were skipped for HBM), and the proof bytes must be identical."""
     import torch
 
