@@ -1128,6 +1128,7 @@ def main():
     # main lane's, on the same stream), so k_accum_level0's launch times are the kernel's own and not stretched by
     # the other lane's sorts and NTTs (the timed proofs' two-lane figure is reported beside it)
     one_lane = None
+    a_plan = None  # how this key's proofs plan A's MSM: "own", "shared" (one plan with L) or "derived" (from L's)
     if rank == 0:
         try:
             with fg.tuned(prove_lanes=1):
@@ -1135,6 +1136,7 @@ def main():
                 fg.prove_batch(ctx, pk, circ, [zhost], [blinding(0, 0)], priority=prio)
                 ctx.synchronize()
             one_lane = ctx.stats()
+            a_plan = "derived" if ctx.derived_plans() else "shared" if ctx.shared_plans() else "own"
         except Exception as e:  # reported, never fatal
             one_lane = {"error": str(e)}
 
@@ -1390,7 +1392,7 @@ def main():
         "config": {"workload": workload_name(args.log_rows, P, world),
                    "constraints": n, "domain": shape["d"], "num_inputs": shape["n_in"], "num_aux": shape["n_aux"],
                    "a_query": shape["n_a"], "b_query": shape["n_b"], "proofs_per_step": P if P else world,
-                   "partitions_per_rank": per_step,
+                   "partitions_per_rank": per_step, "a_plan": a_plan,
                    "parallelism": f"partition-sharded x{world}"},
         "verified": verified,
         "verified_proofs": len(proofs),

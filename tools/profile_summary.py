@@ -20,6 +20,7 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+A_PLAN = "own"  # set by main(): how the profiled proofs planned A (g1_launch_points)
 
 
 def _one(path, pattern):
@@ -65,6 +66,9 @@ def g1_launch_points(bench):
     valu_roofline.one_lane when the line has it); then the standalone MSM (1 warm + msm_reps)."""
     cfg = bench["config"]
     per_prove = [cfg["domain"] - 1, cfg["num_aux"], cfg["a_query"], cfg["b_query"]]
+    if A_PLAN in ("derived", "shared"):  # A as its aux part over L's plan plus a small MSM over the inputs' points
+        per_prove = [cfg["domain"] - 1, cfg["num_aux"], cfg["a_query"] - cfg["num_inputs"], cfg["b_query"],
+                     cfg["num_inputs"]]
     one_lane = (bench.get("valu_roofline") or {}).get("one_lane") or {}
     proves = bench["warmup"] + bench["steps"] + (1 if "avg_launch_ms" in one_lane else 0)
     msm = [bench["msm_g1_points"]] * (1 + bench.get("msm_reps", 1))
@@ -80,8 +84,12 @@ def main():
     ap.add_argument("--bench-json", required=True)
     ap.add_argument("--kernel", default="k_accum_level0<mi::fq_t>")
     ap.add_argument("--command-file", help="the profiled bench command (tools/prof_round.sh writes <tag>_command.txt)")
+    ap.add_argument("--a-plan", choices=["own", "shared", "derived"],
+                    help="A's plan in the profiled proofs (default: the bench line's config.a_plan, else own)")
     args = ap.parse_args()
     bench = json.loads(open(args.bench_json).read().strip().splitlines()[-1])
+    global A_PLAN
+    A_PLAN = args.a_plan or bench["config"].get("a_plan") or "own"
     bench.setdefault("msm_reps", 1)
     cmd = open(args.command_file).read().strip() if args.command_file else "python3 bench.py (see tools/prof_round.sh)"
     out = {"tag": args.tag, "command": "rocprofv3 --kernel-trace --stats / --pmc FETCH_SIZE / --pmc WRITE_SIZE -- " + cmd,
