@@ -177,7 +177,7 @@ def test_groth16_shared_la_plan_vs_oracle(ctx, oracle, tune, n_in, cover):
     assert not pk.shared_la() and ctx.fallbacks()["oom_retries"] == 1
 
 
-@pytest.mark.parametrize("mode", ["tables", "glv"])
+@pytest.mark.parametrize("mode", ["tables", "glv", "short_chunks"])
 def test_groth16_derived_a_plan_vs_oracle(ctx, oracle, tune, mode):
     """Keys below the shared plan's density rule: L's plan carries A's density in its entries and A's plan is filtered
     out of it (msm_derive_plan: no digit pass, no sort of its own), on the lane that runs L, then accumulated over A's
@@ -189,6 +189,9 @@ def test_groth16_derived_a_plan_vs_oracle(ctx, oracle, tune, mode):
     tune.set("prove_wide_log", 0)
     if mode == "glv":
         tune.set("msm_glv", 1)
+    if mode == "short_chunks":  # level-0 chunks of 2 entries, 4 partials per tree thread: every derived bucket of
+        tune.set("msm_l0", 2)   # 3+ entries goes through the multi-chunk list and chunk-tree levels of its own slots
+        tune.set("msm_l1", 4)
     n_in, n_aux, rws, z = circuits.random_circuit(41, 3000, n_in=3, n_free=32)
     in_a = {c for row in rws for c, _ in row[0]}
     assert sum(1 for v in range(n_in, n_in + n_aux) if v in in_a) * 10 < n_aux * 9  # below the shared-plan rule
